@@ -1,0 +1,142 @@
+/*
+ * tbdk.h — C ABI of the MI355X-native TBD/KLT hot path (libtbdk.so).
+ *
+ * This is the drop-in boundary for the per-frame tracking-by-detection path of
+ * the reference (tkortz/opencv, OpenCV 3.4.7 fork).  Each entry point names the
+ * reference interface it replaces.  Conventions:
+ *   - plain pointers and sizes; every image/point buffer is DEVICE memory owned
+ *     by the caller (hipMalloc / torch), except where a parameter says "host";
+ *   - every call is asynchronous on the given HIP stream (passed as void*,
+ *     NULL = the legacy default stream); no hidden host sync, no device
+ *     globals, so contexts on different devices/threads are independent;
+ *   - every call returns an int status (TBDK_OK or a negative TBDK_E*);
+ *     n == 0 is a no-op returning TBDK_OK (reference: pyrlk.cpp:221-227
+ *     releases the outputs on empty input).
+ */
+#ifndef TBDK_H
+#define TBDK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TBDK_OK 0
+#define TBDK_EINVAL (-1)   /* bad argument (reference: CV_Assert -> cv::Exception)   */
+#define TBDK_EHIP (-2)     /* HIP runtime error (reference: cudaSafeCall)             */
+#define TBDK_ENOMEM (-3)   /* device allocation failed                                */
+#define TBDK_ENODEV (-4)   /* no such device / no GPU (reference: throw_no_cuda())    */
+
+#define TBDK_MAX_LEVELS 8
+
+/* flags, same values as the reference (video/include/opencv2/video/tracking.hpp:56-57) */
+#define TBDK_OPTFLOW_USE_INITIAL_FLOW 4
+#define TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS 8
+
+typedef struct tbdk_ctx tbdk_ctx;
+
+/* One pyramid level in device memory.  Interior pixel (x, y) is at
+ * data[(y + pad) * pitch + x + pad]; the `pad`-wide frame around it holds
+ * BORDER_REFLECT_101 values, as cv::buildOpticalFlowPyramid's padded levels do
+ * (video/src/lkpyramid.cpp:726-762). */
+typedef struct tbdk_level {
+    uint8_t* data;
+    int32_t width, height, pitch, pad;
+} tbdk_level;
+
+typedef struct tbdk_pyr {
+    int32_t nlevels;                 /* levels built = maxLevel used + 1 */
+    int32_t win_w, win_h;            /* window the level count was derived for */
+    tbdk_level lv[TBDK_MAX_LEVELS];
+    void* storage;                   /* owned by the library; free with tbdk_pyr_destroy */
+} tbdk_pyr;
+
+/* cv::TermCriteria(COUNT+EPS, maxCount, epsilon) + flags + minEigThreshold of
+ * cv::calcOpticalFlowPyrLK (video/include/opencv2/video/tracking.hpp:178-183) */
+typedef struct tbdk_lk_params {
+    int32_t win_w, win_h;            /* default 21, 21 */
+    int32_t max_level;               /* default 3 (clamped to the pyramids) */
+    int32_t max_count;               /* default 30, clamped to [0, 100] */
+    double epsilon;                  /* default 0.01, clamped to [0, 10] then squared */
+    int32_t flags;                   /* TBDK_OPTFLOW_* */
+    float min_eig_threshold;         /* default 1e-4 */
+} tbdk_lk_params;
+
+/* ---- context ------------------------------------------------------------ */
+
+/* Creates a context bound to HIP device `device` (one per thread x device). */
+int tbdk_ctx_create(int device, tbdk_ctx** out);
+int tbdk_ctx_destroy(tbdk_ctx* ctx);
+/* device ordinal of the context */
+int tbdk_ctx_device(const tbdk_ctx* ctx);
+
+/* Per-kernel timing with HIP events recorded on the launch stream.
+ * enable != 0 starts recording (clears previous records). */
+int tbdk_timing_enable(tbdk_ctx* ctx, int enable);
+/* Synchronises the recorded events and returns, for kernel `name`
+ * ("pyr_build", "lk_sparse", ...), the number of launches and the summed
+ * device milliseconds. */
+int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
+
+/* ---- pyramids ------------------------------------------------------------ */
+
+/* Allocates a padded pyramid for width x height u8 frames.  The level count
+ * follows cv::buildOpticalFlowPyramid's stop rule for window (win_w, win_h)
+ * (video/src/lkpyramid.cpp:782-787).  Not for the hot path (hipMalloc). */
+int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level,
+                    int win_w, int win_h, tbdk_pyr* pyr);
+int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr);
+
+/* Builds every level of `pyr` from the device u8 image `img` (row pitch in
+ * bytes).  Replaces cv::buildOpticalFlowPyramid (video/src/lkpyramid.cpp:697)
+ * and, level by level, cv::cuda::pyrDown
+ * (modules/cudawarping/include/opencv2/cudawarping.hpp:201) — bit-exact with
+ * the CPU pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857). */
+int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream);
+
+/* Synchronous copy of level `level` to host memory (GpuMat::download
+ * analogue; not for the hot path).  with_border != 0 copies the padded frame
+ * ((height+2*pad) rows of (width+2*pad) bytes), else the interior. */
+int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
+                      int with_border);
+
+/* Single-level cv::cuda::pyrDown replacement: dst = pyrDown(src),
+ * dst size ((w+1)/2, (h+1)/2), plain (unpadded) device images. */
+int tbdk_pyr_down_u8(tbdk_ctx* ctx, const uint8_t* src, int width, int height, int src_pitch,
+                     uint8_t* dst, int dst_pitch, void* stream);
+
+/* ---- sparse pyramidal Lucas-Kanade -------------------------------------- */
+
+/* Replaces cv::cuda::SparsePyrLKOpticalFlow::calc
+ * (modules/cudaoptflow/include/opencv2/cudaoptflow.hpp:160-180, impl
+ * modules/cudaoptflow/src/pyrlk.cpp:326-349) with the numerics of the CPU
+ * cv::calcOpticalFlowPyrLK (video/src/lkpyramid.cpp:1207-1377, 178-695).
+ *   prev_pts / next_pts : n x float2 (x, y); next_pts is read as the initial
+ *                         guess when TBDK_OPTFLOW_USE_INITIAL_FLOW is set
+ *   status              : n x u8 (1 = tracked)
+ *   err                 : n x f32 or NULL (L1 patch error / 32 at level 0; the
+ *                         minimum eigenvalue with LK_GET_MIN_EIGENVALS; 0 where
+ *                         status is 0 and the reference leaves it unset)
+ *   iters               : n x i32 or NULL (Newton iterations over all levels)
+ * All levels run in one launch; one wave64 per point. */
+int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
+                   const float* prev_pts, float* next_pts, uint8_t* status, float* err,
+                   int32_t* iters, int n, const tbdk_lk_params* params, void* stream);
+
+/* ---- synthetic sequences (bench / test input) ----------------------------- */
+
+/* Renders frames [t0, t0+nframes) of the deterministic synthetic sequence of
+ * opencv_amd/csrc/synth_spec.h into `out` (device, nframes x height x pitch).
+ * gt_boxes (host, may be NULL): nframes x nobj x 5 int32 {valid, x, y, w, h}. */
+int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int nobj,
+                      int t0, int nframes, uint8_t* out, int pitch, int32_t* gt_boxes,
+                      void* stream);
+
+/* Library version string */
+const char* tbdk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TBDK_H */

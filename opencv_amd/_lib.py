@@ -1,0 +1,113 @@
+"""ctypes binding of libtbdk.so (the C ABI declared in include/tbdk.h).
+
+The product path is the HIP library; there is no CPU fallback.  If the shared
+object is missing the import fails loudly (`TbdkError`), and every call that
+returns a negative status raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtbdk.so")
+
+TBDK_OK = 0
+TBDK_EINVAL = -1
+TBDK_EHIP = -2
+TBDK_ENOMEM = -3
+TBDK_ENODEV = -4
+TBDK_MAX_LEVELS = 8
+OPTFLOW_USE_INITIAL_FLOW = 4
+OPTFLOW_LK_GET_MIN_EIGENVALS = 8
+
+_ERRNAMES = {
+    TBDK_EINVAL: "TBDK_EINVAL (bad argument)",
+    TBDK_EHIP: "TBDK_EHIP (HIP runtime error)",
+    TBDK_ENOMEM: "TBDK_ENOMEM (device allocation failed)",
+    TBDK_ENODEV: "TBDK_ENODEV (no such device)",
+}
+
+
+class TbdkError(RuntimeError):
+    """Raised for a negative TBDK_* status (the reference throws cv::Exception)."""
+
+
+class Level(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("pitch", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+class Pyr(C.Structure):
+    _fields_ = [
+        ("nlevels", C.c_int32),
+        ("win_w", C.c_int32),
+        ("win_h", C.c_int32),
+        ("lv", Level * TBDK_MAX_LEVELS),
+        ("storage", C.c_void_p),
+    ]
+
+
+class LkParams(C.Structure):
+    _fields_ = [
+        ("win_w", C.c_int32),
+        ("win_h", C.c_int32),
+        ("max_level", C.c_int32),
+        ("max_count", C.c_int32),
+        ("epsilon", C.c_double),
+        ("flags", C.c_int32),
+        ("min_eig_threshold", C.c_float),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/tbdk.h declares
+SIGNATURES = {
+    "tbdk_version": (C.c_char_p, []),
+    "tbdk_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "tbdk_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "tbdk_ctx_device": (C.c_int, [C.c_void_p]),
+    "tbdk_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
+    "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
+    "tbdk_pyr_download": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int, C.c_int]),
+    "tbdk_pyr_down_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                   C.c_void_p]),
+    "tbdk_lk_sparse": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.POINTER(Pyr), C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_int, C.POINTER(LkParams), C.c_void_p]),
+    "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libtbdk.so (once).  Raises TbdkError if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise TbdkError(
+            f"libtbdk.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP path has no CPU fallback)")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "tbdk call") -> None:
+    if status != TBDK_OK:
+        raise TbdkError(f"{what} failed: {_ERRNAMES.get(status, status)}")

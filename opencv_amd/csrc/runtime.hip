@@ -1,0 +1,305 @@
+// runtime.hip — the C ABI of include/tbdk.h: contexts, pyramids, launches,
+// per-kernel HIP-event timing.  Host code, compiled by hipcc for gfx950.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "synth_spec.h"
+#include "tbdk_internal.hpp"
+
+namespace tbdk {
+
+static hipEvent_t take_event(tbdk_ctx* ctx)
+{
+    if (!ctx->free_events.empty()) {
+        hipEvent_t e = ctx->free_events.back();
+        ctx->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
+{
+    if (!ctx->timing) return -1;
+    TimingRec r{name, take_event(ctx), take_event(ctx)};
+    if (!r.begin || !r.end) return -1;
+    (void)hipEventRecord(r.begin, s);
+    ctx->recs.push_back(r);
+    return (int)ctx->recs.size() - 1;
+}
+
+void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s)
+{
+    if (rec < 0) return;
+    (void)hipEventRecord(ctx->recs[rec].end, s);
+}
+
+static int map_err(hipError_t e)
+{
+    if (e == hipSuccess) return TBDK_OK;
+    if (e == hipErrorOutOfMemory) return TBDK_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TBDK_ENODEV;
+    return TBDK_EHIP;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace tbdk
+
+using namespace tbdk;
+
+extern "C" {
+
+const char* tbdk_version(void) { return "tbdk 0.1 (gfx950)"; }
+
+int tbdk_ctx_create(int device, tbdk_ctx** out)
+{
+    if (!out) return TBDK_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return TBDK_ENODEV;
+    if (device < 0 || device >= n) return TBDK_ENODEV;
+    tbdk_ctx* c = new (std::nothrow) tbdk_ctx();
+    if (!c) return TBDK_ENOMEM;
+    c->device = device;
+    *out = c;
+    return TBDK_OK;
+}
+
+int tbdk_ctx_destroy(tbdk_ctx* ctx)
+{
+    if (!ctx) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    for (auto& r : ctx->recs) {
+        (void)hipEventDestroy(r.begin);
+        (void)hipEventDestroy(r.end);
+    }
+    for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    delete ctx;
+    return TBDK_OK;
+}
+
+int tbdk_ctx_device(const tbdk_ctx* ctx) { return ctx ? ctx->device : TBDK_EINVAL; }
+
+int tbdk_timing_enable(tbdk_ctx* ctx, int enable)
+{
+    if (!ctx) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    for (auto& r : ctx->recs) {
+        ctx->free_events.push_back(r.begin);
+        ctx->free_events.push_back(r.end);
+    }
+    ctx->recs.clear();
+    ctx->timing = enable != 0;
+    return TBDK_OK;
+}
+
+int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double* total_ms)
+{
+    if (!ctx || !name) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    int64_t cnt = 0;
+    double tot = 0.0;
+    for (auto& r : ctx->recs) {
+        if (std::strcmp(r.name, name) != 0) continue;
+        hipError_t e = hipEventSynchronize(r.end);
+        if (e != hipSuccess) return map_err(e);
+        float ms = 0.f;
+        e = hipEventElapsedTime(&ms, r.begin, r.end);
+        if (e != hipSuccess) return map_err(e);
+        cnt++;
+        tot += ms;
+    }
+    if (launches) *launches = cnt;
+    if (total_ms) *total_ms = tot;
+    return TBDK_OK;
+}
+
+int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+{
+    if (!ctx || !pyr || width <= 0 || height <= 0 || max_level < 0 || win_w <= 2 || win_h <= 2 || win_w > 63 ||
+        win_h > 63)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    std::memset(pyr, 0, sizeof(*pyr));
+    if (max_level >= TBDK_MAX_LEVELS) max_level = TBDK_MAX_LEVELS - 1;
+    const int pad = level_pad(win_w, win_h);
+    // level sizes and the buildOpticalFlowPyramid stop rule (lkpyramid.cpp:782-787)
+    int w = width, h = height, nlev = 0;
+    size_t offs[TBDK_MAX_LEVELS], total = 0;
+    for (int level = 0; level <= max_level; ++level) {
+        tbdk_level& L = pyr->lv[level];
+        L.width = w;
+        L.height = h;
+        L.pad = pad;
+        L.pitch = align_up(w + 2 * pad, 256);
+        offs[level] = total;
+        total += (size_t)L.pitch * (h + 2 * pad);
+        total = (total + 255) & ~(size_t)255;
+        nlev = level + 1;
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+        if (w <= win_w || h <= win_h) break;
+    }
+    void* mem = nullptr;
+    hipError_t e = hipMalloc(&mem, total);
+    if (e != hipSuccess) return map_err(e);
+    pyr->storage = mem;
+    pyr->nlevels = nlev;
+    pyr->win_w = win_w;
+    pyr->win_h = win_h;
+    for (int level = 0; level < nlev; ++level) pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
+    return TBDK_OK;
+}
+
+int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr)
+{
+    if (!ctx || !pyr) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (pyr->storage) (void)hipFree(pyr->storage);
+    std::memset(pyr, 0, sizeof(*pyr));
+    return TBDK_OK;
+}
+
+int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream)
+{
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pitch < pyr->lv[0].width) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "pyr_build", s);
+    hipError_t e = launch_pad_copy(img, pitch, pyr->lv[0], s);
+    for (int level = 1; e == hipSuccess && level < pyr->nlevels; ++level)
+        e = launch_pyr_down_padded(pyr->lv[level - 1], pyr->lv[level], s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
+                      int with_border)
+{
+    if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
+    const tbdk_level& L = pyr->lv[level];
+    const int w = with_border ? L.width + 2 * L.pad : L.width;
+    const int h = with_border ? L.height + 2 * L.pad : L.height;
+    if (host_pitch < w) return TBDK_EINVAL;
+    const uint8_t* src = with_border ? L.data : L.data + (size_t)L.pad * L.pitch + L.pad;
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipMemcpy2D(host, host_pitch, src, L.pitch, w, h, hipMemcpyDeviceToHost);
+    return map_err(e);
+}
+
+int tbdk_pyr_down_u8(tbdk_ctx* ctx, const uint8_t* src, int width, int height, int src_pitch, uint8_t* dst,
+                     int dst_pitch, void* stream)
+{
+    if (!ctx || !src || !dst || width <= 0 || height <= 0 || src_pitch < width || dst_pitch < (width + 1) / 2)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "pyr_down", s);
+    hipError_t e = launch_pyr_down_plain(src, width, height, src_pitch, dst, dst_pitch, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts,
+                   float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
+                   void* stream)
+{
+    if (!ctx || !prev || !next || !p || n < 0) return TBDK_EINVAL;
+    if (n == 0) return TBDK_OK;
+    if (!prev_pts || !next_pts || !status) return TBDK_EINVAL;
+    if (p->win_w <= 2 || p->win_h <= 2 || p->win_w > 63 || p->win_h > 63 || p->max_level < 0) return TBDK_EINVAL;
+    if (prev->nlevels <= 0 || next->nlevels <= 0) return TBDK_EINVAL;
+    const int pad_needed = p->win_w > p->win_h ? p->win_w + 2 : p->win_h + 2;
+    int max_level = p->max_level;
+    if (prev->nlevels - 1 < max_level) max_level = prev->nlevels - 1;
+    if (next->nlevels - 1 < max_level) max_level = next->nlevels - 1;
+    LkArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int l = 0; l <= max_level; ++l) {
+        const tbdk_level& I = prev->lv[l];
+        const tbdk_level& J = next->lv[l];
+        if (I.width != J.width || I.height != J.height) return TBDK_EINVAL;
+        if (I.pad < pad_needed || J.pad < pad_needed) return TBDK_EINVAL;
+        a.lv[l] = LkLevel{I.data, J.data, I.width, I.height, I.pitch, J.pitch, I.pad, J.pad};
+    }
+    a.max_level = max_level;
+    a.win_w = p->win_w;
+    a.win_h = p->win_h;
+    a.max_count = p->max_count < 0 ? 0 : (p->max_count > 100 ? 100 : p->max_count);
+    double eps = p->epsilon < 0. ? 0. : (p->epsilon > 10. ? 10. : p->epsilon);
+    a.eps2 = eps * eps;
+    a.flags = p->flags;
+    a.min_eig = p->min_eig_threshold;
+    a.prev_pts = prev_pts;
+    a.next_pts = next_pts;
+    a.status = status;
+    a.err = err;
+    a.iters = iters;
+    a.n = n;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "lk_sparse", s);
+    hipError_t e = launch_lk_sparse(a, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int nobj, int t0, int nframes,
+                      uint8_t* out, int pitch, int32_t* gt_boxes, void* stream)
+{
+    if (!ctx || !out || width <= 0 || height <= 0 || nobj < 0 || nobj > SYN_MAX_OBJECTS || nframes <= 0 ||
+        pitch < width)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nob = nobj > 0 ? nobj : 1;
+    syn_object* objs = static_cast<syn_object*>(std::malloc(sizeof(syn_object) * nob));
+    syn_pose* poses = static_cast<syn_pose*>(std::malloc(sizeof(syn_pose) * (size_t)nob * nframes));
+    if (!objs || !poses) {
+        std::free(objs);
+        std::free(poses);
+        return TBDK_ENOMEM;
+    }
+    syn_make_objects(seed, width, height, nobj, objs);
+    for (int f = 0; f < nframes; ++f)
+        for (int o = 0; o < nobj; ++o) {
+            syn_pose* p = &poses[(size_t)f * nobj + o];
+            syn_pose_at(&objs[o], width, height, t0 + f, p);
+            if (gt_boxes) {
+                int32_t* gb = gt_boxes + ((size_t)f * nobj + o) * 5;
+                gb[0] = syn_gt_box(p, width, height, gb + 1);
+                if (!gb[0]) gb[1] = gb[2] = gb[3] = gb[4] = 0;
+            }
+        }
+    void* dposes = nullptr;
+    hipError_t e = hipMalloc(&dposes, sizeof(syn_pose) * (size_t)nob * nframes);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(dposes, poses, sizeof(syn_pose) * (size_t)nob * nframes, hipMemcpyHostToDevice, s);
+    uint32_t bgseed = syn_hash(seed ^ 0xB6A5EEDU);
+    if (e == hipSuccess) e = launch_synth(dposes, nobj, bgseed, width, height, nframes, out, pitch, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (dposes) (void)hipFree(dposes);
+    std::free(objs);
+    std::free(poses);
+    return map_err(e);
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// tbdk_internal.hpp — shared declarations of the HIP kernels and the C-ABI runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/tbdk.h"
+
+namespace tbdk {
+
+__host__ __device__ inline int align_up(int v, int a) { return (v + a - 1) / a * a; }
+
+// Border width of every padded level: >= win + 1 so the LK window plus its
+// bilinear/Scharr neighbours never leaves the allocation.
+inline int level_pad(int win_w, int win_h)
+{
+    int m = win_w > win_h ? win_w : win_h;
+    int p = align_up(m + 2, 16);
+    return p < 32 ? 32 : p;
+}
+
+struct TimingRec {
+    const char* name;
+    hipEvent_t begin, end;
+};
+
+}  // namespace tbdk
+
+struct tbdk_ctx {
+    int device = 0;
+    bool timing = false;
+    std::vector<tbdk::TimingRec> recs;
+    std::vector<hipEvent_t> free_events;
+};
+
+namespace tbdk {
+
+// RAII-free helpers used by the C-ABI around each launch.
+int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s);
+void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s);
+
+// ---- kernels (klt_pyr.hip) ----
+hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& dst, hipStream_t s);
+hipError_t launch_pyr_down_padded(const tbdk_level& src, const tbdk_level& dst, hipStream_t s);
+hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, uint8_t* dst, int dpitch,
+                                 hipStream_t s);
+
+// ---- kernels (klt_lk.hip) ----
+struct LkLevel {
+    const uint8_t* I;
+    const uint8_t* J;
+    int w, h, ipitch, jpitch, ipad, jpad;
+};
+
+struct LkArgs {
+    LkLevel lv[TBDK_MAX_LEVELS];
+    int max_level, win_w, win_h, max_count, flags, n;
+    double eps2;
+    float min_eig;
+    const float* prev_pts;
+    float* next_pts;
+    uint8_t* status;
+    float* err;
+    int32_t* iters;
+};
+
+size_t lk_smem_bytes(int win_w, int win_h);
+hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);
+
+// ---- synthetic renderer (synth.hip) ----
+struct SynPoseDev;  // == syn_pose
+hipError_t launch_synth(const void* poses_dev, int nobj, uint32_t bgseed, int W, int H, int nframes,
+                        uint8_t* out, int pitch, hipStream_t s);
+
+}  // namespace tbdk

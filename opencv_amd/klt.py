@@ -1,0 +1,247 @@
+"""Host-side mirror of the reference's KLT operator interfaces over libtbdk.
+
+Device memory is plain torch tensors on a HIP device (plumbing only; every
+computation runs in the HIP kernels of libtbdk.so).  The classes keep the
+shape of the reference's CUDA interfaces:
+
+  * SparsePyrLKOpticalFlow  <- cv::cuda::SparsePyrLKOpticalFlow
+        (modules/cudaoptflow/include/opencv2/cudaoptflow.hpp:160-180)
+  * Pyramid / build_pyramid <- cv::buildOpticalFlowPyramid
+        (modules/video/src/lkpyramid.cpp:697-793)
+  * pyr_down                <- cv::cuda::pyrDown
+        (modules/cudawarping/include/opencv2/cudawarping.hpp:201)
+
+Argument meaning and error behaviour follow the reference: `calc` accepts
+images or prebuilt pyramids, empty point sets return empty outputs
+(pyrlk.cpp:221-227), invalid arguments raise (CV_Assert -> TbdkError).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+_ctx_cache: dict[int, "Context"] = {}
+
+
+def _stream_ptr(stream) -> C.c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+class Context:
+    """One tbdk_ctx per HIP device (the C ABI allows one per thread x device)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        _lib.check(self.lib.tbdk_ctx_create(int(device), C.byref(h)), "tbdk_ctx_create")
+        self.handle = h
+        self.device = int(device)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and h.value:
+            try:
+                self.lib.tbdk_ctx_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    @staticmethod
+    def get(device: int = 0) -> "Context":
+        c = _ctx_cache.get(device)
+        if c is None:
+            c = Context(device)
+            _ctx_cache[device] = c
+        return c
+
+    def timing_enable(self, on: bool = True) -> None:
+        _lib.check(self.lib.tbdk_timing_enable(self.handle, int(bool(on))), "tbdk_timing_enable")
+
+    def timing_query(self, name: str) -> tuple[int, float]:
+        n = C.c_int64()
+        ms = C.c_double()
+        _lib.check(self.lib.tbdk_timing_query(self.handle, name.encode(), C.byref(n), C.byref(ms)),
+                   "tbdk_timing_query")
+        return int(n.value), float(ms.value)
+
+
+class Pyramid:
+    """A padded u8 pyramid in device memory (tbdk_pyr)."""
+
+    def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21)):
+        self.ctx = ctx
+        self.pyr = _lib.Pyr()
+        _lib.check(ctx.lib.tbdk_pyr_create(ctx.handle, int(width), int(height), int(max_level), int(win[0]),
+                                           int(win[1]), C.byref(self.pyr)), "tbdk_pyr_create")
+        self.width, self.height = int(width), int(height)
+
+    @property
+    def nlevels(self) -> int:
+        return int(self.pyr.nlevels)
+
+    def build(self, img: torch.Tensor, stream=None) -> "Pyramid":
+        if img.dtype != torch.uint8 or img.dim() != 2 or not img.is_cuda:
+            raise _lib.TbdkError("Pyramid.build expects a 2-D uint8 device tensor")
+        if img.shape[0] != self.height or img.shape[1] != self.width or img.stride(1) != 1:
+            raise _lib.TbdkError("image size / layout does not match the pyramid")
+        _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
+                                               C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
+        return self
+
+    def level(self, i: int, with_border: bool = False):
+        """Host copy of level i as a (H, W) uint8 numpy array (test / download helper)."""
+        import numpy as np
+        L = self.pyr.lv[i]
+        h = L.height + (2 * L.pad if with_border else 0)
+        w = L.width + (2 * L.pad if with_border else 0)
+        out = np.empty((h, w), dtype=np.uint8)
+        _lib.check(self.ctx.lib.tbdk_pyr_download(self.ctx.handle, C.byref(self.pyr), int(i),
+                                                  out.ctypes.data_as(C.c_void_p), w, int(bool(with_border))),
+                   "tbdk_pyr_download")
+        return out
+
+    def __del__(self):
+        if getattr(self, "pyr", None) is not None and self.pyr.storage:
+            try:
+                self.ctx.lib.tbdk_pyr_destroy(self.ctx.handle, C.byref(self.pyr))
+            except Exception:
+                pass
+
+
+def build_pyramid(img: torch.Tensor, win=(21, 21), max_level: int = 3, ctx: Context | None = None,
+                  stream=None) -> Pyramid:
+    ctx = ctx or Context.get(img.device.index or 0)
+    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win).build(img, stream)
+
+
+def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torch.Tensor:
+    """cv::cuda::pyrDown for CV_8UC1: ((w+1)/2, (h+1)/2), bit-exact with the CPU pyrDown."""
+    if src.dtype != torch.uint8 or src.dim() != 2 or not src.is_cuda or src.stride(1) != 1:
+        raise _lib.TbdkError("pyr_down expects a 2-D uint8 device tensor")
+    ctx = ctx or Context.get(src.device.index or 0)
+    h, w = src.shape
+    dst = torch.empty(((h + 1) // 2, (w + 1) // 2), dtype=torch.uint8, device=src.device)
+    _lib.check(ctx.lib.tbdk_pyr_down_u8(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
+                                        C.c_void_p(dst.data_ptr()), dst.stride(0), _stream_ptr(stream)),
+               "tbdk_pyr_down_u8")
+    return dst
+
+
+@dataclass
+class LkResult:
+    next_pts: torch.Tensor
+    status: torch.Tensor
+    err: torch.Tensor | None
+    iters: torch.Tensor | None
+
+
+class SparsePyrLKOpticalFlow:
+    """cv::cuda::SparsePyrLKOpticalFlow with the CPU calcOpticalFlowPyrLK numerics.
+
+    create(winSize=(21,21), maxLevel=3, iters=30, useInitialFlow=False) mirrors
+    cudaoptflow.hpp:175-179; epsilon / minEigThreshold / getMinEigenVals are the
+    CPU calcOpticalFlowPyrLK parameters (video/include/opencv2/video/tracking.hpp:178-183).
+    """
+
+    def __init__(self, winSize=(21, 21), maxLevel: int = 3, iters: int = 30, useInitialFlow: bool = False,
+                 epsilon: float = 0.01, minEigThreshold: float = 1e-4, getMinEigenVals: bool = False,
+                 device: int = 0):
+        self.win = (int(winSize[0]), int(winSize[1]))
+        self.max_level = int(maxLevel)
+        self.iters = int(iters)
+        self.use_initial_flow = bool(useInitialFlow)
+        self.epsilon = float(epsilon)
+        self.min_eig = float(minEigThreshold)
+        self.get_min_eig = bool(getMinEigenVals)
+        self.ctx = Context.get(device)
+
+    @staticmethod
+    def create(winSize=(21, 21), maxLevel: int = 3, iters: int = 30, useInitialFlow: bool = False, **kw):
+        return SparsePyrLKOpticalFlow(winSize, maxLevel, iters, useInitialFlow, **kw)
+
+    # getters / setters of cudaoptflow.hpp:163-173
+    def getWinSize(self):
+        return self.win
+
+    def setWinSize(self, win):
+        self.win = (int(win[0]), int(win[1]))
+
+    def getMaxLevel(self):
+        return self.max_level
+
+    def setMaxLevel(self, v):
+        self.max_level = int(v)
+
+    def getNumIters(self):
+        return self.iters
+
+    def setNumIters(self, v):
+        self.iters = int(v)
+
+    def getUseInitialFlow(self):
+        return self.use_initial_flow
+
+    def setUseInitialFlow(self, v):
+        self.use_initial_flow = bool(v)
+
+    def params(self) -> _lib.LkParams:
+        flags = 0
+        if self.use_initial_flow:
+            flags |= _lib.OPTFLOW_USE_INITIAL_FLOW
+        if self.get_min_eig:
+            flags |= _lib.OPTFLOW_LK_GET_MIN_EIGENVALS
+        return _lib.LkParams(self.win[0], self.win[1], self.max_level, self.iters, self.epsilon, flags,
+                             self.min_eig)
+
+    def _as_pyr(self, img) -> Pyramid:
+        if isinstance(img, Pyramid):
+            return img
+        return build_pyramid(img, self.win, self.max_level, self.ctx)
+
+    def calc(self, prevImg, nextImg, prevPts: torch.Tensor, nextPts: torch.Tensor | None = None,
+             want_err: bool = True, want_iters: bool = False, stream=None) -> LkResult:
+        if prevPts.dtype != torch.float32 or not prevPts.is_cuda:
+            raise _lib.TbdkError("prevPts must be a float32 device tensor of shape (N, 2)")
+        pts = prevPts.reshape(-1, 2).contiguous()
+        n = pts.shape[0]
+        dev = pts.device
+        if n == 0:
+            return LkResult(torch.empty((0, 2), dtype=torch.float32, device=dev),
+                            torch.empty((0,), dtype=torch.uint8, device=dev), None, None)
+        P, N = self._as_pyr(prevImg), self._as_pyr(nextImg)
+        if self.use_initial_flow:
+            if nextPts is None or nextPts.numel() != 2 * n:
+                raise _lib.TbdkError("useInitialFlow requires nextPts of the same size as prevPts")
+            out = nextPts.reshape(-1, 2).to(torch.float32).contiguous().clone()
+        else:
+            out = torch.empty((n, 2), dtype=torch.float32, device=dev)
+        status = torch.empty((n,), dtype=torch.uint8, device=dev)
+        err = torch.empty((n,), dtype=torch.float32, device=dev) if want_err else None
+        iters = torch.empty((n,), dtype=torch.int32, device=dev) if want_iters else None
+        prm = self.params()
+        _lib.check(self.ctx.lib.tbdk_lk_sparse(
+            self.ctx.handle, C.byref(P.pyr), C.byref(N.pyr), C.c_void_p(pts.data_ptr()), C.c_void_p(out.data_ptr()),
+            C.c_void_p(status.data_ptr()), C.c_void_p(err.data_ptr()) if err is not None else None,
+            C.c_void_p(iters.data_ptr()) if iters is not None else None, n, C.byref(prm), _stream_ptr(stream)),
+            "tbdk_lk_sparse")
+        return LkResult(out, status, err, iters)
+
+
+def synth_render(seed: int, width: int, height: int, nobj: int, t0: int, nframes: int, device: int = 0,
+                 ctx: Context | None = None, stream=None):
+    """Render frames [t0, t0+nframes) of the synthetic sequence into HBM.
+
+    Returns (frames uint8 (nframes, H, W) device tensor, gt int32 (nframes, nobj, 5) host tensor)."""
+    ctx = ctx or Context.get(device)
+    frames = torch.empty((nframes, height, width), dtype=torch.uint8, device=f"cuda:{device}")
+    gt = torch.zeros((nframes, max(nobj, 1), 5), dtype=torch.int32)
+    _lib.check(ctx.lib.tbdk_synth_render(ctx.handle, seed, width, height, nobj, t0, nframes,
+                                         C.c_void_p(frames.data_ptr()), width, C.c_void_p(gt.data_ptr()),
+                                         _stream_ptr(stream)), "tbdk_synth_render")
+    return frames, gt[:, :nobj]

@@ -1,0 +1,201 @@
+"""ctypes binding of oracle/liboracle.so — the CPU checker (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+ACCUM_SSE2 = 0
+ACCUM_EXACT = 1
+MAX_LEVELS = 8
+
+
+class Plane(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("pitch", C.c_int), ("pad", C.c_int)]
+
+
+class OPyr(C.Structure):
+    _fields_ = [("nlevels", C.c_int), ("lv", Plane * MAX_LEVELS)]
+
+
+class LkParams(C.Structure):
+    _fields_ = [
+        ("winW", C.c_int), ("winH", C.c_int), ("maxLevel", C.c_int), ("maxCount", C.c_int),
+        ("epsilon", C.c_double), ("flags", C.c_int), ("minEigThreshold", C.c_float), ("accum", C.c_int),
+        ("nthreads", C.c_int),
+    ]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_LIB):
+        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+    lib = C.CDLL(ORACLE_LIB)
+    lib.orc_build_pyramid.restype = C.c_int
+    lib.orc_build_pyramid.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.POINTER(OPyr)]
+    lib.orc_free_pyramid.argtypes = [C.POINTER(OPyr)]
+    lib.orc_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    lib.orc_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    lib.orc_lk.restype = C.c_int
+    lib.orc_lk.argtypes = [C.POINTER(OPyr), C.POINTER(OPyr), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                           C.POINTER(LkParams), C.c_void_p]
+    lib.orc_synth_frames.restype = C.c_int
+    lib.orc_synth_frames.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                     C.c_void_p]
+    lib.orc_reflect101.restype = C.c_int
+    lib.orc_reflect101.argtypes = [C.c_int, C.c_int]
+    lib.orc_now.restype = C.c_double
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Pyramid:
+    """Oracle pyramid (host memory), freed on GC."""
+
+    def __init__(self, img: np.ndarray, win=(21, 21), max_level=3, pad=32):
+        lib = load()
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        self.p = OPyr()
+        lib.orc_build_pyramid(_ptr(img), img.shape[1], img.shape[0], img.strides[0], win[0], win[1], max_level, pad,
+                              C.byref(self.p))
+        self.nlevels = self.p.nlevels
+
+    def level(self, i: int, with_border=False) -> np.ndarray:
+        L = self.p.lv[i]
+        full = np.ctypeslib.as_array(C.cast(L.data, C.POINTER(C.c_uint8)), shape=(L.h + 2 * L.pad, L.pitch)).copy()
+        if with_border:
+            return full[:, :L.w + 2 * L.pad]
+        return full[L.pad:L.pad + L.h, L.pad:L.pad + L.w]
+
+    def __del__(self):
+        if _lib is not None and getattr(self, "p", None) is not None:
+            _lib.orc_free_pyramid(C.byref(self.p))
+            self.p = None
+
+
+def pyr_down(img: np.ndarray) -> np.ndarray:
+    lib = load()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.empty(((h + 1) // 2, (w + 1) // 2), dtype=np.uint8)
+    lib.orc_pyr_down(_ptr(img), w, h, img.strides[0], _ptr(out), out.shape[1], out.shape[0], out.strides[0])
+    return out
+
+
+def scharr(img: np.ndarray) -> np.ndarray:
+    lib = load()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.empty((h, w, 2), dtype=np.int16)
+    lib.orc_scharr(_ptr(img), w, h, img.strides[0], _ptr(out), 2 * w)
+    return out
+
+
+def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01, flags=0,
+       min_eig=1e-4, accum=ACCUM_SSE2, nthreads=8, init: np.ndarray | None = None):
+    lib = load()
+    pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 2)
+    n = pts.shape[0]
+    nxt_pts = np.zeros((n, 2), dtype=np.float32) if init is None else np.ascontiguousarray(init, np.float32).copy()
+    status = np.zeros(n, dtype=np.uint8)
+    err = np.zeros(n, dtype=np.float32)
+    iters = np.zeros(n, dtype=np.int32)
+    prm = LkParams(win[0], win[1], max_level, max_count, eps, flags, min_eig, accum, nthreads)
+    if n:
+        lib.orc_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status), _ptr(err), n,
+                   C.byref(prm), _ptr(iters))
+    return nxt_pts, status, err, iters
+
+
+def synth(seed: int, W: int, H: int, nobj: int, t0: int, nframes: int):
+    lib = load()
+    out = np.zeros((nframes, H, W), dtype=np.uint8)
+    gt = np.zeros((nframes, max(nobj, 1), 5), dtype=np.int32)
+    rc = lib.orc_synth_frames(seed, W, H, nobj, t0, nframes, _ptr(out), W, _ptr(gt))
+    assert rc == 0
+    return out, gt[:, :nobj]
+
+
+def read_png_gray(path: str) -> np.ndarray:
+    """Minimal PNG decoder (8-bit gray / RGB / RGBA, non-interlaced) -> uint8 gray.
+
+    Gray conversion (RGB) uses cv::cvtColor's integer BGR2GRAY weights
+    (R*4899 + G*9617 + B*1868 + 8192) >> 14 (imgproc/src/color_rgb.simd.hpp).
+    """
+    import struct
+    import zlib
+
+    with open(path, "rb") as f:
+        data = f.read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n", "not a PNG"
+    pos, idat, hdr = 8, b"", None
+    while pos < len(data):
+        ln, = struct.unpack(">I", data[pos:pos + 4])
+        typ = data[pos + 4:pos + 8]
+        body = data[pos + 8:pos + 8 + ln]
+        if typ == b"IHDR":
+            hdr = struct.unpack(">IIBBBBB", body)
+        elif typ == b"IDAT":
+            idat += body
+        elif typ == b"IEND":
+            break
+        pos += 12 + ln
+    w, h, depth, ctype, _, _, interlace = hdr
+    assert depth == 8 and interlace == 0, "unsupported PNG"
+    ch = {0: 1, 2: 3, 4: 2, 6: 4}[ctype]
+    raw = zlib.decompress(idat)
+    stride = w * ch
+    out = np.zeros((h, stride), dtype=np.int32)
+    prev = np.zeros(stride, dtype=np.int32)
+    p = 0
+    for y in range(h):
+        ft = raw[p]
+        line = np.frombuffer(raw[p + 1:p + 1 + stride], dtype=np.uint8).astype(np.int32)
+        p += 1 + stride
+        cur = np.zeros(stride, dtype=np.int32)
+        if ft == 0:
+            cur = line
+        elif ft == 1:
+            for x in range(stride):
+                cur[x] = (line[x] + (cur[x - ch] if x >= ch else 0)) & 255
+        elif ft == 2:
+            cur = (line + prev) & 255
+        elif ft == 3:
+            for x in range(stride):
+                cur[x] = (line[x] + (((cur[x - ch] if x >= ch else 0) + prev[x]) >> 1)) & 255
+        elif ft == 4:
+            for x in range(stride):
+                a = cur[x - ch] if x >= ch else 0
+                b = prev[x]
+                c = prev[x - ch] if x >= ch else 0
+                pa, pb, pc = abs(b - c), abs(a - c), abs(a + b - 2 * c)
+                pr = a if (pa <= pb and pa <= pc) else (b if pb <= pc else c)
+                cur[x] = (line[x] + pr) & 255
+        out[y] = cur
+        prev = cur
+    img = out.reshape(h, w, ch)
+    if ch == 1:
+        return img[:, :, 0].astype(np.uint8)
+    if ch == 2:
+        return img[:, :, 0].astype(np.uint8)
+    r, g, b = img[:, :, 0], img[:, :, 1], img[:, :, 2]
+    return ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)

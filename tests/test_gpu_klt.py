@@ -1,0 +1,177 @@
+"""GPU parity tests proper: the HIP path (through the C ABI) against the CPU oracle.
+
+Bars:
+  * synthetic frames, pyramid levels (interior + reflect-101 frame): bit-exact
+  * LK vs oracle in ORC_ACCUM_EXACT mode (same integer sums, one rounding):
+    bit-exact next_pts / status / err / iteration counts
+  * LK vs oracle in the reference's SSE2 accumulation order: |dp| <= 1e-2 px for
+    >= 99.5 % of tracked points and status agreement >= 99.5 %,
+    plus the reference's own GPU-vs-CPU rule (test_optflow.cpp:241-264: int-truncated
+    positions within 1 px, mismatch <= 1 %).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_DATA = "/root/reference/samples/data"
+
+
+def klt():
+    from opencv_amd import klt as K
+
+    return K
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def grid_points(h, w, step, margin):
+    ys, xs = np.mgrid[margin:h - margin:step, margin:w - margin:step]
+    return np.stack([xs.ravel(), ys.ravel()], 1).astype(np.float32)
+
+
+def basketball_pair():
+    p1 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "basketball_pair.npz")
+    if os.path.exists(p1):
+        d = np.load(p1)
+        return d["a"], d["b"]
+    a = O.read_png_gray(os.path.join(REF_DATA, "basketball1.png"))
+    b = O.read_png_gray(os.path.join(REF_DATA, "basketball2.png"))
+    return a, b
+
+
+def test_synth_render_matches_oracle(gpu):
+    K = klt()
+    fr, gt = K.synth_render(20261015, 640, 480, 32, 0, 3, ctx=gpu)
+    ofr, ogt = O.synth(20261015, 640, 480, 32, 0, 3)
+    assert np.array_equal(fr.cpu().numpy(), ofr)
+    assert np.array_equal(gt.numpy(), ogt)
+    golden = json.load(open(os.path.join(GOLDEN, "synth_hashes.json")))
+    fr2, gt2 = K.synth_render(20261015, 1920, 1080, 128, 0, 2, ctx=gpu)
+    f2 = fr2.cpu().numpy()
+    assert [hashlib.sha256(f2[i].tobytes()).hexdigest() for i in range(2)] == golden["1920x1080x128"]
+    assert hashlib.sha256(gt2.numpy().tobytes()).hexdigest() == golden["1920x1080x128_gt"]
+
+
+@pytest.mark.parametrize("shape,maxlev,win", [((480, 640), 3, 21), ((1080, 1920), 2, 21), ((375, 1242), 3, 21),
+                                             ((61, 93), 4, 7), ((2160, 3840), 3, 21), ((37, 29), 3, 15)])
+def test_pyramid_bit_exact(gpu, shape, maxlev, win):
+    K = klt()
+    img = np.random.default_rng(shape[0]).integers(0, 256, shape, dtype=np.uint8)
+    P = K.build_pyramid(to_dev(img), (win, win), maxlev, ctx=gpu)
+    torch.cuda.synchronize()
+    R = O.Pyramid(img, (win, win), maxlev, pad=P.pyr.lv[0].pad)
+    assert P.nlevels == R.nlevels
+    for lvl in range(P.nlevels):
+        assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"level {lvl}"
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (480, 640), (1079, 1919), (375, 1242)])
+def test_pyr_down_plain_bit_exact(gpu, shape):
+    K = klt()
+    img = np.random.default_rng(3).integers(0, 256, shape, dtype=np.uint8)
+    got = K.pyr_down(to_dev(img), ctx=gpu).cpu().numpy()
+    assert np.array_equal(got, O.pyr_down(img))
+
+
+def run_pair(gpu, a, b, pts, win=(21, 21), maxlev=3, iters=30, eps=0.01, flags=0, init=None):
+    K = klt()
+    lk = K.SparsePyrLKOpticalFlow(win, maxlev, iters, bool(flags & 4), epsilon=eps,
+                                  getMinEigenVals=bool(flags & 8))
+    Pa = K.build_pyramid(to_dev(a), win, maxlev, ctx=gpu)
+    Pb = K.build_pyramid(to_dev(b), win, maxlev, ctx=gpu)
+    r = lk.calc(Pa, Pb, to_dev(pts), None if init is None else to_dev(init), want_iters=True)
+    torch.cuda.synchronize()
+    g = (r.next_pts.cpu().numpy(), r.status.cpu().numpy(), r.err.cpu().numpy(), r.iters.cpu().numpy())
+    pad = Pa.pyr.lv[0].pad
+    Ra, Rb = O.Pyramid(a, win, maxlev, pad), O.Pyramid(b, win, maxlev, pad)
+    ex = O.lk(Ra, Rb, pts, win, maxlev, iters, eps, flags, accum=O.ACCUM_EXACT, init=init)
+    sse = O.lk(Ra, Rb, pts, win, maxlev, iters, eps, flags, accum=O.ACCUM_SSE2, init=init)
+    return g, ex, sse
+
+
+def assert_exact(g, ex):
+    nx, st, er, it = g
+    assert np.array_equal(st, ex[1]), f"status mismatch {np.flatnonzero(st != ex[1])[:10]}"
+    ok = st == 1
+    assert np.array_equal(nx[ok].view(np.uint32), ex[0][ok].view(np.uint32)), \
+        f"next_pts mismatch: max {np.abs(nx - ex[0])[ok].max()}"
+    assert np.array_equal(er[ok].view(np.uint32), ex[2][ok].view(np.uint32))
+    assert np.array_equal(it, ex[3])
+
+
+def assert_tolerance(g, sse, frac=0.995, tol=1e-2):
+    nx, st = g[0], g[1]
+    assert (st == sse[1]).mean() >= frac
+    ok = (st == 1) & (sse[1] == 1)
+    d = np.abs(nx - sse[0]).max(1)[ok]
+    assert (d <= tol).mean() >= frac, f"only {(d <= tol).mean():.4f} within {tol}"
+    # reference GPU-vs-CPU rule (cudaoptflow/test/test_optflow.cpp:241-264)
+    bad = (np.abs(np.trunc(nx) - np.trunc(sse[0])).max(1) > 1) | (st != sse[1])
+    assert bad.mean() <= 0.01
+
+
+def test_lk_synthetic_640(gpu):
+    fr, _ = O.synth(20261015, 640, 480, 32, 0, 2)
+    pts = grid_points(480, 640, 6, 2)
+    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts)
+    assert_exact(g, ex)
+    assert_tolerance(g, sse)
+
+
+def test_lk_basketball_pair(gpu):
+    a, b = basketball_pair()
+    pts = grid_points(a.shape[0], a.shape[1], 5, 0)
+    g, ex, sse = run_pair(gpu, a, b, pts)
+    assert_exact(g, ex)
+    assert_tolerance(g, sse)
+
+
+@pytest.mark.parametrize("win,maxlev,iters", [((7, 7), 2, 7), ((11, 11), 2, 30), ((15, 9), 4, 30),
+                                              ((31, 31), 3, 30), ((41, 41), 4, 30), ((21, 21), 0, 1)])
+def test_lk_window_and_level_variants(gpu, win, maxlev, iters):
+    fr, _ = O.synth(77, 320, 240, 12, 3, 2)
+    pts = grid_points(240, 320, 7, 0) + np.float32([0.37, 0.61])
+    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters)
+    assert_exact(g, ex)
+
+
+def test_lk_edge_points_and_flags(gpu):
+    fr, _ = O.synth(9, 200, 150, 6, 0, 2)
+    pts = np.array([[-100, -100], [1e4, 5], [0, 0], [199.9, 149.9], [-21.0, 50.0], [-20.5, 3.0], [210.0, 160.0],
+                    [100.5, 75.5], [3.2, 147.9]], np.float32)
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts)
+    assert_exact(g, ex)
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=8)  # OPTFLOW_LK_GET_MIN_EIGENVALS
+    assert_exact(g, ex)
+    init = pts + np.float32([1.5, -0.5])
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=4, init=init)  # OPTFLOW_USE_INITIAL_FLOW
+    assert_exact(g, ex)
+
+
+def test_lk_empty_input(gpu):
+    K = klt()
+    lk = K.SparsePyrLKOpticalFlow()
+    img = torch.zeros((64, 64), dtype=torch.uint8, device="cuda")
+    r = lk.calc(img, img, torch.zeros((0, 2), dtype=torch.float32, device="cuda"))
+    assert r.next_pts.shape == (0, 2) and r.status.shape == (0,)
+
+
+def test_lk_1080p_full_size(gpu):
+    # config 2: 1080p pair, 64 boxes x 256 corners-like point count, 3-level PyrLK
+    fr, gt = O.synth(20261015, 1920, 1080, 128, 0, 2)
+    rng = np.random.default_rng(1)
+    pts = np.stack([rng.uniform(0, 1920, 16384), rng.uniform(0, 1080, 16384)], 1).astype(np.float32)
+    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, maxlev=2)
+    assert_exact(g, ex)
+    assert_tolerance(g, sse)
