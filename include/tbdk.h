@@ -45,10 +45,16 @@ typedef struct tbdk_level {
     int32_t width, height, pitch, pad;
 } tbdk_level;
 
+/* A pyramid with derivatives, the layout of
+ * cv::buildOpticalFlowPyramid(..., withDerivatives=true) (lkpyramid.cpp:765-780):
+ * lv[i] are the u8 levels; dv[i] the Scharr derivative planes of calcSharrDeriv
+ * (lkpyramid.cpp:55-144), CV_16SC2 interleaved (Ix, Iy) per pixel (4 bytes; pitch
+ * in bytes) with a zero (BORDER_CONSTANT) frame of `pad` pixels. */
 typedef struct tbdk_pyr {
     int32_t nlevels;                 /* levels built = maxLevel used + 1 */
     int32_t win_w, win_h;            /* window the level count was derived for */
     tbdk_level lv[TBDK_MAX_LEVELS];
+    tbdk_level dv[TBDK_MAX_LEVELS];
     void* storage;                   /* owned by the library; free with tbdk_pyr_destroy */
 } tbdk_pyr;
 
@@ -61,6 +67,7 @@ typedef struct tbdk_lk_params {
     double epsilon;                  /* default 0.01, clamped to [0, 10] then squared */
     int32_t flags;                   /* TBDK_OPTFLOW_* */
     float min_eig_threshold;         /* default 1e-4 */
+    int32_t impl;                    /* 0 auto; 1 register-strip kernel; 2 generic LDS kernel */
 } tbdk_lk_params;
 
 /* ---- context ------------------------------------------------------------ */
@@ -88,8 +95,8 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level,
                     int win_w, int win_h, tbdk_pyr* pyr);
 int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr);
 
-/* Builds every level of `pyr` from the device u8 image `img` (row pitch in
- * bytes).  Replaces cv::buildOpticalFlowPyramid (video/src/lkpyramid.cpp:697)
+/* Builds every level of `pyr` (and its derivative planes) from the device u8
+ * image `img` (row pitch in bytes).  Replaces cv::buildOpticalFlowPyramid (video/src/lkpyramid.cpp:697)
  * and, level by level, cv::cuda::pyrDown
  * (modules/cudawarping/include/opencv2/cudawarping.hpp:201) — bit-exact with
  * the CPU pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857). */
@@ -100,6 +107,8 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
  * ((height+2*pad) rows of (width+2*pad) bytes), else the interior. */
 int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
                       int with_border);
+/* Same for the derivative plane of `level` (interior, CV_16SC2, host_pitch in bytes). */
+int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16_t* host, int host_pitch);
 
 /* Single-level cv::cuda::pyrDown replacement: dst = pyrDown(src),
  * dst size ((w+1)/2, (h+1)/2), plain (unpadded) device images. */

@@ -49,6 +49,7 @@ class Pyr(C.Structure):
         ("win_w", C.c_int32),
         ("win_h", C.c_int32),
         ("lv", Level * TBDK_MAX_LEVELS),
+        ("dv", Level * TBDK_MAX_LEVELS),
         ("storage", C.c_void_p),
     ]
 
@@ -62,6 +63,7 @@ class LkParams(C.Structure):
         ("epsilon", C.c_double),
         ("flags", C.c_int32),
         ("min_eig_threshold", C.c_float),
+        ("impl", C.c_int32),
     ]
 
 
@@ -77,6 +79,7 @@ SIGNATURES = {
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
     "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_download": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int, C.c_int]),
+    "tbdk_pyr_download_deriv": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int]),
     "tbdk_pyr_down_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                    C.c_void_p]),
     "tbdk_lk_sparse": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.POINTER(Pyr), C.c_void_p, C.c_void_p, C.c_void_p,

@@ -94,6 +94,67 @@ __global__ void pyr_down_plain_kernel(const uint8_t* __restrict__ src, int sw, i
     dst[(size_t)y * dpitch + x] = (uint8_t)((sum + 128) >> 8);
 }
 
+// calcSharrDeriv (lkpyramid.cpp:55-144) of every level into its int16x2 plane.
+// Rows/columns outside the level come from the level's reflect-101 frame, which
+// is exactly the reference's row (:78-80) and column (:111-116) reflection.
+struct ScharrLevels {
+    const uint8_t* src[TBDK_MAX_LEVELS];
+    uint8_t* dst[TBDK_MAX_LEVELS];
+    int w[TBDK_MAX_LEVELS], h[TBDK_MAX_LEVELS], spitch[TBDK_MAX_LEVELS], spad[TBDK_MAX_LEVELS];
+    int dpitch[TBDK_MAX_LEVELS], dpad[TBDK_MAX_LEVELS];
+};
+
+__global__ void scharr_levels_kernel(ScharrLevels a)
+{
+    const int lvl = blockIdx.z;
+    const int y = blockIdx.y;
+    const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int w = a.w[lvl], h = a.h[lvl];
+    if (y >= h || x0 >= w) return;
+    const int sp = a.spitch[lvl];
+    const uint8_t* r1 = a.src[lvl] + (size_t)(y + a.spad[lvl]) * sp + a.spad[lvl] + x0;
+    const uint8_t* r0 = r1 - sp;
+    const uint8_t* r2 = r1 + sp;
+    int t0[6], t1[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int c = k - 1;
+        t0[k] = (r0[c] + r2[c]) * 3 + r1[c] * 10;
+        t1[k] = r2[c] - r0[c];
+    }
+    int32_t out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ix = t0[k + 2] - t0[k];
+        const int iy = (t1[k + 2] + t1[k]) * 3 + t1[k + 1] * 10;
+        out[k] = (int32_t)(((uint32_t)ix & 0xffffu) | ((uint32_t)iy << 16));
+    }
+    int32_t* d = reinterpret_cast<int32_t*>(a.dst[lvl] + (size_t)(y + a.dpad[lvl]) * a.dpitch[lvl]) + a.dpad[lvl] + x0;
+    const int n = w - x0 < 4 ? w - x0 : 4;
+    for (int k = 0; k < n; ++k) d[k] = out[k];
+}
+
+hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s)
+{
+    ScharrLevels a;
+    int maxw = 0, maxh = 0;
+    for (int l = 0; l < pyr.nlevels; ++l) {
+        a.src[l] = pyr.lv[l].data;
+        a.dst[l] = pyr.dv[l].data;
+        a.w[l] = pyr.lv[l].width;
+        a.h[l] = pyr.lv[l].height;
+        a.spitch[l] = pyr.lv[l].pitch;
+        a.spad[l] = pyr.lv[l].pad;
+        a.dpitch[l] = pyr.dv[l].pitch;
+        a.dpad[l] = pyr.dv[l].pad;
+        maxw = a.w[l] > maxw ? a.w[l] : maxw;
+        maxh = a.h[l] > maxh ? a.h[l] : maxh;
+    }
+    dim3 block(256), grid(((maxw + 3) / 4 + 255) / 256, maxh, pyr.nlevels);
+    hipLaunchKernelGGL(scharr_levels_kernel, grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& d, hipStream_t s)
 {
     const int wp = d.width + 2 * d.pad, hp = d.height + 2 * d.pad;

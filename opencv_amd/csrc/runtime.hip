@@ -143,7 +143,7 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win
     const int pad = level_pad(win_w, win_h);
     // level sizes and the buildOpticalFlowPyramid stop rule (lkpyramid.cpp:782-787)
     int w = width, h = height, nlev = 0;
-    size_t offs[TBDK_MAX_LEVELS], total = 0;
+    size_t offs[TBDK_MAX_LEVELS], doffs[TBDK_MAX_LEVELS], total = 0;
     for (int level = 0; level <= max_level; ++level) {
         tbdk_level& L = pyr->lv[level];
         L.width = w;
@@ -151,7 +151,15 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win
         L.pad = pad;
         L.pitch = align_up(w + 2 * pad, 256);
         offs[level] = total;
-        total += (size_t)L.pitch * (h + 2 * pad);
+        total += (size_t)L.pitch * (h + 2 * pad) + 256;  // +256: aligned over-reads of the last row
+        total = (total + 255) & ~(size_t)255;
+        tbdk_level& D = pyr->dv[level];
+        D.width = w;
+        D.height = h;
+        D.pad = pad;
+        D.pitch = align_up((w + 2 * pad) * 4, 256);
+        doffs[level] = total;
+        total += (size_t)D.pitch * (h + 2 * pad) + 256;
         total = (total + 255) & ~(size_t)255;
         nlev = level + 1;
         w = (w + 1) / 2;
@@ -161,11 +169,20 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win
     void* mem = nullptr;
     hipError_t e = hipMalloc(&mem, total);
     if (e != hipSuccess) return map_err(e);
+    // the derivative planes' BORDER_CONSTANT frame is zero once and never rewritten
+    e = hipMemset(mem, 0, total);
+    if (e != hipSuccess) {
+        (void)hipFree(mem);
+        return map_err(e);
+    }
     pyr->storage = mem;
     pyr->nlevels = nlev;
     pyr->win_w = win_w;
     pyr->win_h = win_h;
-    for (int level = 0; level < nlev; ++level) pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
+    for (int level = 0; level < nlev; ++level) {
+        pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
+        pyr->dv[level].data = static_cast<uint8_t*>(mem) + doffs[level];
+    }
     return TBDK_OK;
 }
 
@@ -187,6 +204,7 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     hipError_t e = launch_pad_copy(img, pitch, pyr->lv[0], s);
     for (int level = 1; e == hipSuccess && level < pyr->nlevels; ++level)
         e = launch_pyr_down_padded(pyr->lv[level - 1], pyr->lv[level], s);
+    if (e == hipSuccess) e = launch_scharr_levels(*pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }
@@ -202,6 +220,17 @@ int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* ho
     const uint8_t* src = with_border ? L.data : L.data + (size_t)L.pad * L.pitch + L.pad;
     DeviceGuard g(ctx->device);
     hipError_t e = hipMemcpy2D(host, host_pitch, src, L.pitch, w, h, hipMemcpyDeviceToHost);
+    return map_err(e);
+}
+
+int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16_t* host, int host_pitch)
+{
+    if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
+    const tbdk_level& D = pyr->dv[level];
+    if (host_pitch < D.width * 4) return TBDK_EINVAL;
+    const uint8_t* src = D.data + (size_t)D.pad * D.pitch + (size_t)D.pad * 4;
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipMemcpy2D(host, host_pitch, src, D.pitch, (size_t)D.width * 4, D.height, hipMemcpyDeviceToHost);
     return map_err(e);
 }
 
@@ -238,7 +267,8 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
         const tbdk_level& J = next->lv[l];
         if (I.width != J.width || I.height != J.height) return TBDK_EINVAL;
         if (I.pad < pad_needed || J.pad < pad_needed) return TBDK_EINVAL;
-        a.lv[l] = LkLevel{I.data, J.data, I.width, I.height, I.pitch, J.pitch, I.pad, J.pad};
+        const tbdk_level& D = prev->dv[l];
+        a.lv[l] = LkLevel{I.data, J.data, D.data, I.width, I.height, I.pitch, J.pitch, I.pad, J.pad, D.pitch, D.pad};
     }
     a.max_level = max_level;
     a.win_w = p->win_w;
@@ -256,8 +286,13 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
     a.n = n;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    bool have_d = true;
+    for (int l = 0; l <= max_level; ++l)
+        if (!a.lv[l].D || a.lv[l].dpad < pad_needed) have_d = false;
+    const bool strip = p->impl != 2 && have_d && lk_strip_supported(p->win_w, p->win_h);
+    if (p->impl == 1 && !strip) return TBDK_EINVAL;
     int rec = timing_begin(ctx, "lk_sparse", s);
-    hipError_t e = launch_lk_sparse(a, s);
+    hipError_t e = strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }

@@ -46,12 +46,15 @@ hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& dst
 hipError_t launch_pyr_down_padded(const tbdk_level& src, const tbdk_level& dst, hipStream_t s);
 hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, uint8_t* dst, int dpitch,
                                  hipStream_t s);
+// Scharr derivative planes (interior only; the zero frame is written once at allocation)
+hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s);
 
 // ---- kernels (klt_lk.hip) ----
 struct LkLevel {
     const uint8_t* I;
     const uint8_t* J;
-    int w, h, ipitch, jpitch, ipad, jpad;
+    const uint8_t* D;   // derivative plane of I (int16x2 per pixel), may be null
+    int w, h, ipitch, jpitch, ipad, jpad, dpitch, dpad;
 };
 
 struct LkArgs {
@@ -68,6 +71,10 @@ struct LkArgs {
 
 size_t lk_smem_bytes(int win_w, int win_h);
 hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);
+// register-strip kernel (klt_lk_strip.hip); returns hipErrorNotSupported for
+// windows without an instantiation (caller falls back to launch_lk_sparse)
+bool lk_strip_supported(int win_w, int win_h);
+hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 
 // ---- synthetic renderer (synth.hip) ----
 struct SynPoseDev;  // == syn_pose

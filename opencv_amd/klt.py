@@ -106,6 +106,16 @@ class Pyramid:
                    "tbdk_pyr_download")
         return out
 
+    def deriv(self, i: int):
+        """Host copy of the Scharr derivative plane of level i: (H, W, 2) int16 (Ix, Iy)."""
+        import numpy as np
+        L = self.pyr.dv[i]
+        out = np.empty((L.height, L.width, 2), dtype=np.int16)
+        _lib.check(self.ctx.lib.tbdk_pyr_download_deriv(self.ctx.handle, C.byref(self.pyr), int(i),
+                                                        out.ctypes.data_as(C.c_void_p), L.width * 4),
+                   "tbdk_pyr_download_deriv")
+        return out
+
     def __del__(self):
         if getattr(self, "pyr", None) is not None and self.pyr.storage:
             try:
@@ -151,7 +161,7 @@ class SparsePyrLKOpticalFlow:
 
     def __init__(self, winSize=(21, 21), maxLevel: int = 3, iters: int = 30, useInitialFlow: bool = False,
                  epsilon: float = 0.01, minEigThreshold: float = 1e-4, getMinEigenVals: bool = False,
-                 device: int = 0):
+                 device: int = 0, impl: int = 0):
         self.win = (int(winSize[0]), int(winSize[1]))
         self.max_level = int(maxLevel)
         self.iters = int(iters)
@@ -159,6 +169,7 @@ class SparsePyrLKOpticalFlow:
         self.epsilon = float(epsilon)
         self.min_eig = float(minEigThreshold)
         self.get_min_eig = bool(getMinEigenVals)
+        self.impl = int(impl)
         self.ctx = Context.get(device)
 
     @staticmethod
@@ -197,7 +208,7 @@ class SparsePyrLKOpticalFlow:
         if self.get_min_eig:
             flags |= _lib.OPTFLOW_LK_GET_MIN_EIGENVALS
         return _lib.LkParams(self.win[0], self.win[1], self.max_level, self.iters, self.epsilon, flags,
-                             self.min_eig)
+                             self.min_eig, self.impl)
 
     def _as_pyr(self, img) -> Pyramid:
         if isinstance(img, Pyramid):

@@ -74,6 +74,7 @@ def test_pyramid_bit_exact(gpu, shape, maxlev, win):
     assert P.nlevels == R.nlevels
     for lvl in range(P.nlevels):
         assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"level {lvl}"
+        assert np.array_equal(P.deriv(lvl), O.scharr(R.level(lvl))), f"deriv level {lvl}"
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (3, 5), (480, 640), (1079, 1919), (375, 1242)])
@@ -84,10 +85,10 @@ def test_pyr_down_plain_bit_exact(gpu, shape):
     assert np.array_equal(got, O.pyr_down(img))
 
 
-def run_pair(gpu, a, b, pts, win=(21, 21), maxlev=3, iters=30, eps=0.01, flags=0, init=None):
+def run_pair(gpu, a, b, pts, win=(21, 21), maxlev=3, iters=30, eps=0.01, flags=0, init=None, impl=0):
     K = klt()
     lk = K.SparsePyrLKOpticalFlow(win, maxlev, iters, bool(flags & 4), epsilon=eps,
-                                  getMinEigenVals=bool(flags & 8))
+                                  getMinEigenVals=bool(flags & 8), impl=impl)
     Pa = K.build_pyramid(to_dev(a), win, maxlev, ctx=gpu)
     Pb = K.build_pyramid(to_dev(b), win, maxlev, ctx=gpu)
     r = lk.calc(Pa, Pb, to_dev(pts), None if init is None else to_dev(init), want_iters=True)
@@ -121,41 +122,52 @@ def assert_tolerance(g, sse, frac=0.995, tol=1e-2):
     assert bad.mean() <= 0.01
 
 
-def test_lk_synthetic_640(gpu):
+IMPLS = [pytest.param(1, id="strip"), pytest.param(2, id="generic")]
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+def test_lk_synthetic_640(gpu, impl):
     fr, _ = O.synth(20261015, 640, 480, 32, 0, 2)
     pts = grid_points(480, 640, 6, 2)
-    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts)
+    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, impl=impl)
     assert_exact(g, ex)
     assert_tolerance(g, sse)
 
 
-def test_lk_basketball_pair(gpu):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_lk_basketball_pair(gpu, impl):
     a, b = basketball_pair()
     pts = grid_points(a.shape[0], a.shape[1], 5, 0)
-    g, ex, sse = run_pair(gpu, a, b, pts)
+    g, ex, sse = run_pair(gpu, a, b, pts, impl=impl)
     assert_exact(g, ex)
     assert_tolerance(g, sse)
 
 
-@pytest.mark.parametrize("win,maxlev,iters", [((7, 7), 2, 7), ((11, 11), 2, 30), ((15, 9), 4, 30),
-                                              ((31, 31), 3, 30), ((41, 41), 4, 30), ((21, 21), 0, 1)])
+@pytest.mark.parametrize("win,maxlev,iters", [((7, 7), 2, 7), ((9, 9), 3, 30), ((11, 11), 2, 30), ((15, 9), 4, 30),
+                                              ((15, 15), 3, 30), ((19, 19), 3, 30), ((23, 23), 3, 30),
+                                              ((29, 29), 3, 30), ((31, 31), 3, 30), ((41, 41), 4, 30),
+                                              ((21, 21), 0, 1)])
 def test_lk_window_and_level_variants(gpu, win, maxlev, iters):
     fr, _ = O.synth(77, 320, 240, 12, 3, 2)
     pts = grid_points(240, 320, 7, 0) + np.float32([0.37, 0.61])
     g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters)
     assert_exact(g, ex)
+    if win[0] == win[1] and win[0] <= 31:  # both kernels must agree bit for bit
+        g2, _, _ = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters, impl=2)
+        assert_exact(g2, ex)
 
 
-def test_lk_edge_points_and_flags(gpu):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_lk_edge_points_and_flags(gpu, impl):
     fr, _ = O.synth(9, 200, 150, 6, 0, 2)
     pts = np.array([[-100, -100], [1e4, 5], [0, 0], [199.9, 149.9], [-21.0, 50.0], [-20.5, 3.0], [210.0, 160.0],
-                    [100.5, 75.5], [3.2, 147.9]], np.float32)
-    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts)
+                    [100.5, 75.5], [3.2, 147.9], [-10.0, -10.0], [219.0, 169.0], [-31.0, 80.0]], np.float32)
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, impl=impl)
     assert_exact(g, ex)
-    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=8)  # OPTFLOW_LK_GET_MIN_EIGENVALS
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=8, impl=impl)  # OPTFLOW_LK_GET_MIN_EIGENVALS
     assert_exact(g, ex)
     init = pts + np.float32([1.5, -0.5])
-    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=4, init=init)  # OPTFLOW_USE_INITIAL_FLOW
+    g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=4, init=init, impl=impl)  # OPTFLOW_USE_INITIAL_FLOW
     assert_exact(g, ex)
 
 
@@ -167,11 +179,12 @@ def test_lk_empty_input(gpu):
     assert r.next_pts.shape == (0, 2) and r.status.shape == (0,)
 
 
-def test_lk_1080p_full_size(gpu):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_lk_1080p_full_size(gpu, impl):
     # config 2: 1080p pair, 64 boxes x 256 corners-like point count, 3-level PyrLK
     fr, gt = O.synth(20261015, 1920, 1080, 128, 0, 2)
     rng = np.random.default_rng(1)
     pts = np.stack([rng.uniform(0, 1920, 16384), rng.uniform(0, 1080, 16384)], 1).astype(np.float32)
-    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, maxlev=2)
+    g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, maxlev=2, impl=impl)
     assert_exact(g, ex)
     assert_tolerance(g, sse)
