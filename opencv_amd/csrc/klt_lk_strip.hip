@@ -8,12 +8,16 @@
 //   * lane = one window column x, G = 64 / WW column groups, each lane owns a
 //     vertical strip of R = ceil(WH / G) patch rows (win 21: 3 x 21 lanes x 7 rows);
 //   * the I patch and the interpolated Scharr derivatives stay in VGPRs for all
-//     Newton iterations (no LDS at all); derivatives come from the pyramid's
+//     Newton iterations (no LDS); derivatives come from the pyramid's
 //     precomputed int16x2 planes (withDerivatives layout, lkpyramid.cpp:765-780);
-//   * each J row pair is one aligned dwordx2 load + v_alignbyte per lane; the
-//     lane's R+1 rows feed R bilinear samples (row reuse in registers);
-//   * b / G reductions: DPP within 16-lane rows on 16-bit halves (exact), then
-//     four v_readlane into SGPRs -> wave-uniform scalars.
+//   * buffer loads with 32-bit lane offsets and the row offset in an SGPR
+//     (soffset); one aligned dwordx2 per row, v_perm_b32 picks the two pixels
+//     as an int16 pair, v_dot2_i32_i16 does the 14-bit fixed-point bilinear
+//     (same int16 x int16 products as the reference's _mm_madd_epi16, :288-303);
+//   * the J strip is re-loaded only when the integer window origin moves (near
+//     convergence the Newton steps are sub-pixel, so most iterations are pure VALU);
+//   * G / b sums: DPP over 8-lane groups in int32 (cannot overflow), eight
+//     v_readlane into SGPRs, int64 scalar sum -> exact, wave-uniform.
 #include "tbdk_internal.hpp"
 
 namespace tbdk {
@@ -22,18 +26,17 @@ namespace {
 
 constexpr int W_BITS = 14, W_BITS1 = 14;
 
-__device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-struct __attribute__((aligned(4))) u32x2 {
-    uint32_t lo, hi;
-};
-
-// 4 bytes starting at byte address p (any alignment) from two aligned dwords
-__device__ __forceinline__ uint32_t load_u8x4(const uint8_t* p)
+__device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
 {
-    const uint32_t off = (uint32_t)reinterpret_cast<uintptr_t>(p) & 3u;
-    const u32x2 v = *reinterpret_cast<const u32x2*>(p - off);  // keeps the global address space
-    return __builtin_amdgcn_alignbyte(v.hi, v.lo, off);
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), c, false);
+}
+
+// bilinear of a packed pixel pair on two rows: (p0 . w0 + p1 . w1 + round) >> shift
+__device__ __forceinline__ int bilin(uint32_t p0, uint32_t p1, uint32_t w0, uint32_t w1, int shift)
+{
+    return sdot2(p0, w0, sdot2(p1, w1, 1 << (shift - 1))) >> shift;
 }
 
 template <int CTRL>
@@ -42,41 +45,57 @@ __device__ __forceinline__ int dpp(int v)
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
 
-// sum over each 16-lane row, result in every lane of the row
-__device__ __forceinline__ int row_sum16(int v)
+// exact wave-wide sums of N int32 lane values: DPP inside GROUP-lane groups in
+// int32, then an int64 scalar sum of the 64/GROUP group totals.  The caller
+// picks GROUP so that GROUP * (max |lane partial|) < 2^31 (lane partial of a
+// strip of R rows: R * 8160 * 4081 for b, R * 4081^2 for G).  Result is
+// uniform (SGPR).
+template <int GROUP, int N>
+__device__ __forceinline__ void wave_sum_exact(int (&v)[N], long long (&out)[N])
 {
-    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-    v += dpp<0x141>(v);  // row_half_mirror
-    v += dpp<0x140>(v);  // row_mirror
-    return v;
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] += dpp<0xB1>(v[k]);  // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] += dpp<0x4E>(v[k]);  // quad_perm [2,3,0,1]
+    if constexpr (GROUP >= 8) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] += dpp<0x141>(v[k]);  // row_half_mirror
+    }
+    if constexpr (GROUP >= 16) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] += dpp<0x140>(v[k]);  // row_mirror
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        long long s = 0;
+#pragma unroll
+        for (int g = 0; g < 64 / GROUP; ++g) s += (long long)__builtin_amdgcn_readlane(v[k], GROUP * g);
+        out[k] = s;
+    }
 }
 
-__device__ __forceinline__ int sum_rows(int v)
+__device__ __forceinline__ void bilinear_weights(float fa, float fb, uint32_t& w0, uint32_t& w1)
 {
-    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
-           __builtin_amdgcn_readlane(v, 48);
+    const int w00 = __float2int_rn((1.f - fa) * (1.f - fb) * (1 << W_BITS));
+    const int w01 = __float2int_rn(fa * (1.f - fb) * (1 << W_BITS));
+    const int w10 = __float2int_rn((1.f - fa) * fb * (1 << W_BITS));
+    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+    w0 = ((uint32_t)w00 & 0xFFFFu) | ((uint32_t)w01 << 16);
+    w1 = ((uint32_t)w10 & 0xFFFFu) | ((uint32_t)w11 << 16);
 }
 
-// exact wave-wide sum of int32 lane values (|v| < 2^31) as int64, uniform
-__device__ __forceinline__ long long wave_sum_exact(int v)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes)
 {
-    const int lo = v & 0xFFFF;  // v = hi * 65536 + lo, lo in [0, 65535]
-    const int hi = v >> 16;
-    const int slo = sum_rows(row_sum16(lo));
-    const int shi = sum_rows(row_sum16(hi));
-    return (long long)shi * 65536 + (long long)slo;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
 
-// wave-wide sum when the total provably fits int32
-__device__ __forceinline__ int wave_sum_small(int v) { return sum_rows(row_sum16(v)); }
-
-__device__ __forceinline__ void bilinear_weights(float fa, float fb, int& w00, int& w01, int& w10, int& w11)
+// (pixel off, pixel off+1) of the 8 bytes at aligned offset, as an int16 pair
+__device__ __forceinline__ uint32_t load_pair_u8(__amdgpu_buffer_rsrc_t rs, uint32_t aligned, int soff,
+                                                 uint32_t sel)
 {
-    w00 = __float2int_rn((1.f - fa) * (1.f - fb) * (1 << W_BITS));
-    w01 = __float2int_rn(fa * (1.f - fb) * (1 << W_BITS));
-    w10 = __float2int_rn((1.f - fa) * fb * (1 << W_BITS));
-    w11 = (1 << W_BITS) - w00 - w01 - w10;
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned, soff, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned + 4, soff, 0);
+    return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
 }  // namespace
@@ -84,8 +103,9 @@ __device__ __forceinline__ void bilinear_weights(float fa, float fb, int& w00, i
 template <int WW, int WH>
 __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
 {
-    constexpr int G = 64 / WW;              // column groups per wave
-    constexpr int R = (WH + G - 1) / G;     // patch rows per lane
+    constexpr int G = 64 / WW;           // column groups per wave
+    constexpr int R = (WH + G - 1) / G;  // patch rows per lane
+    constexpr int GRP = R <= 4 ? 16 : (R <= 8 ? 8 : 4);  // exact-reduction group (see wave_sum_exact)
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;  // wave-uniform
@@ -94,7 +114,6 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
     const int x = lane - grp * WW;
     const bool lane_on = grp < G;
     const int row0 = lane_on ? grp * R : 0;
-    // number of valid rows of this lane's strip
     const int nrows = lane_on ? (WH - row0 < R ? WH - row0 : R) : 0;
 
     const float FLT_SCALE = 1.f / (1 << 20);
@@ -138,96 +157,109 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
             }
             continue;
         }
-        int iw00, iw01, iw10, iw11;
-        bilinear_weights(prevx - ipx, prevy - ipy, iw00, iw01, iw10, iw11);
+        uint32_t w0, w1;
+        bilinear_weights(prevx - ipx, prevy - ipy, w0, w1);
 
-        // ---- strip of I (2 columns) and of the derivative plane (2 columns), R+1 rows
+        const int hp = L.h + 2 * L.ipad;
+        const __amdgpu_buffer_rsrc_t rI = make_rsrc(L.I, L.ipitch * hp + 256);
+        const __amdgpu_buffer_rsrc_t rD = make_rsrc(L.D, L.dpitch * (L.h + 2 * L.dpad) + 256);
+        const __amdgpu_buffer_rsrc_t rJ = make_rsrc(L.J, L.jpitch * (L.h + 2 * L.jpad) + 256);
+
+        // ---- I strip (2 columns) and derivative strip (2 columns), R+1 rows
         int ival[R], gx[R], gy[R];
-        int a11 = 0, a12 = 0, a22 = 0;
         {
-            const uint8_t* ib = L.I + (size_t)(ipy + row0 + L.ipad) * L.ipitch + (ipx + x + L.ipad);
-            const uint8_t* db = L.D + (size_t)(ipy + row0 + L.dpad) * L.dpitch + (size_t)(ipx + x + L.dpad) * 4;
-            uint32_t ir[R + 1];
-            u32x2 dr[R + 1];
+            const uint32_t ioff = (uint32_t)((ipy + row0 + L.ipad) * L.ipitch + ipx + x + L.ipad);
+            const uint32_t isel = 0x0C000C00u | ((ioff & 3u) + (((ioff & 3u) + 1u) << 16));
+            const uint32_t ialn = ioff & ~3u;
+            const uint32_t doff = (uint32_t)((ipy + row0 + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4);
+            uint32_t ip[R + 1], dxp[R + 1], dyp[R + 1];
 #pragma unroll
             for (int r = 0; r <= R; ++r) {
-                ir[r] = load_u8x4(ib + (size_t)r * L.ipitch);
-                dr[r] = *reinterpret_cast<const u32x2*>(db + (size_t)r * L.dpitch);
+                ip[r] = load_pair_u8(rI, ialn, r * L.ipitch, isel);
+                const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);
+                const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);
+                dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
+                dyp[r] = __builtin_amdgcn_perm(d1, d0, 0x07060302u);  // (Iy(x), Iy(x+1))
             }
+            int acc[3] = {0, 0, 0};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int i00 = ir[r] & 255, i01 = (ir[r] >> 8) & 255;
-                const int i10 = ir[r + 1] & 255, i11 = (ir[r + 1] >> 8) & 255;
-                const int iv = descale(i00 * iw00 + i01 * iw01 + i10 * iw10 + i11 * iw11, W_BITS1 - 5);
-                const int d00 = (int)dr[r].lo, d01 = (int)dr[r].hi, d10 = (int)dr[r + 1].lo, d11 = (int)dr[r + 1].hi;
-                const int ix = descale((int16_t)d00 * iw00 + (int16_t)d01 * iw01 + (int16_t)d10 * iw10 +
-                                           (int16_t)d11 * iw11, W_BITS1);
-                const int iy = descale((d00 >> 16) * iw00 + (d01 >> 16) * iw01 + (d10 >> 16) * iw10 +
-                                           (d11 >> 16) * iw11, W_BITS1);
                 const bool on = r < nrows;
-                ival[r] = iv;
+                ival[r] = bilin(ip[r], ip[r + 1], w0, w1, W_BITS1 - 5);
+                const int ix = bilin(dxp[r], dxp[r + 1], w0, w1, W_BITS1);
+                const int iy = bilin(dyp[r], dyp[r + 1], w0, w1, W_BITS1);
                 gx[r] = on ? ix : 0;
                 gy[r] = on ? iy : 0;
-                a11 += gx[r] * gx[r];
-                a12 += gx[r] * gy[r];
-                a22 += gy[r] * gy[r];
+                acc[0] += gx[r] * gx[r];
+                acc[1] += gx[r] * gy[r];
+                acc[2] += gy[r] * gy[r];
             }
-        }
-        const float A11 = (float)wave_sum_exact(a11) * FLT_SCALE;
-        const float A12 = (float)wave_sum_exact(a12) * FLT_SCALE;
-        const float A22 = (float)wave_sum_exact(a22) * FLT_SCALE;
+            long long s[3];
+            wave_sum_exact<GRP, 3>(acc, s);
+            // A = float(exact sum) * 2^-20   (lkpyramid.cpp:438-440)
+            const float A11 = (float)s[0] * FLT_SCALE;
+            const float A12 = (float)s[1] * FLT_SCALE;
+            const float A22 = (float)s[2] * FLT_SCALE;
 
-        float D = A11 * A22 - A12 * A12;
-        const float minEig =
-            (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
-        if (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS) errv = minEig;
-        if (minEig < a.min_eig || D < 1.19209290e-07F /*FLT_EPSILON*/) {
-            if (level == 0) status = 0;
-            continue;
-        }
-        D = 1.f / D;
-
-        nextx -= halfx;
-        nexty -= halfy;
-        float pdx = 0.f, pdy = 0.f;
-        for (int j = 0; j < a.max_count; ++j) {
-            const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
-            if (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h) {
+            float D = A11 * A22 - A12 * A12;
+            const float minEig =
+                (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+            if (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS) errv = minEig;
+            if (minEig < a.min_eig || D < 1.19209290e-07F /*FLT_EPSILON*/) {
                 if (level == 0) status = 0;
-                break;
+                continue;
             }
-            nit++;
-            bilinear_weights(nextx - inx, nexty - iny, iw00, iw01, iw10, iw11);
-            const uint8_t* jb = L.J + (size_t)(iny + row0 + L.jpad) * L.jpitch + (inx + x + L.jpad);
-            uint32_t jr[R + 1];
+            D = 1.f / D;
+
+            nextx -= halfx;
+            nexty -= halfy;
+            float pdx = 0.f, pdy = 0.f;
+            int pinx = 0x7fffffff, piny = 0;
+            uint32_t jp[R + 1];
 #pragma unroll
-            for (int r = 0; r <= R; ++r) jr[r] = load_u8x4(jb + (size_t)r * L.jpitch);
-            int b1 = 0, b2 = 0;
+            for (int r = 0; r <= R; ++r) jp[r] = 0;
+            for (int j = 0; j < a.max_count; ++j) {
+                const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
+                if (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h) {
+                    if (level == 0) status = 0;
+                    break;
+                }
+                nit++;
+                if (inx != pinx || iny != piny) {  // uniform: reload the J strip
+                    const uint32_t joff = (uint32_t)((iny + row0 + L.jpad) * L.jpitch + inx + x + L.jpad);
+                    const uint32_t jsel = 0x0C000C00u | ((joff & 3u) + (((joff & 3u) + 1u) << 16));
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int j00 = jr[r] & 255, j01 = (jr[r] >> 8) & 255;
-                const int j10 = jr[r + 1] & 255, j11 = (jr[r + 1] >> 8) & 255;
-                const int diff =
-                    descale(j00 * iw00 + j01 * iw01 + j10 * iw10 + j11 * iw11, W_BITS1 - 5) - ival[r];
-                b1 += diff * gx[r];
-                b2 += diff * gy[r];
+                    for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8(rJ, joff & ~3u, r * L.jpitch, jsel);
+                    pinx = inx;
+                    piny = iny;
+                }
+                bilinear_weights(nextx - inx, nexty - iny, w0, w1);
+                int b[2] = {0, 0};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int diff = bilin(jp[r], jp[r + 1], w0, w1, W_BITS1 - 5) - ival[r];
+                    b[0] += diff * gx[r];
+                    b[1] += diff * gy[r];
+                }
+                long long sb[2];
+                wave_sum_exact<GRP, 2>(b, sb);
+                const float fb1 = (float)sb[0] * FLT_SCALE;
+                const float fb2 = (float)sb[1] * FLT_SCALE;
+                const float ddx = (A12 * fb2 - A22 * fb1) * D;
+                const float ddy = (A12 * fb1 - A11 * fb2) * D;
+                nextx += ddx;
+                nexty += ddy;
+                outx = nextx + halfx;
+                outy = nexty + halfy;
+                if ((double)ddx * ddx + (double)ddy * ddy <= a.eps2) break;
+                if (j > 0 && (double)fabsf(ddx + pdx) < 0.01 && (double)fabsf(ddy + pdy) < 0.01) {
+                    outx -= ddx * 0.5f;
+                    outy -= ddy * 0.5f;
+                    break;
+                }
+                pdx = ddx;
+                pdy = ddy;
             }
-            const float fb1 = (float)wave_sum_exact(b1) * FLT_SCALE;
-            const float fb2 = (float)wave_sum_exact(b2) * FLT_SCALE;
-            const float ddx = (A12 * fb2 - A22 * fb1) * D;
-            const float ddy = (A12 * fb1 - A11 * fb2) * D;
-            nextx += ddx;
-            nexty += ddy;
-            outx = nextx + halfx;
-            outy = nexty + halfy;
-            if ((double)ddx * ddx + (double)ddy * ddy <= a.eps2) break;
-            if (j > 0 && (double)fabsf(ddx + pdx) < 0.01 && (double)fabsf(ddy + pdy) < 0.01) {
-                outx -= ddx * 0.5f;
-                outy -= ddy * 0.5f;
-                break;
-            }
-            pdx = ddx;
-            pdy = ddy;
         }
 
         if (level == 0 && status && a.err && (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS) == 0) {
@@ -236,21 +268,21 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
             if (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h) {
                 status = 0;
             } else {
-                bilinear_weights(npx - inx, npy - iny, iw00, iw01, iw10, iw11);
-                const uint8_t* jb = L.J + (size_t)(iny + row0 + L.jpad) * L.jpitch + (inx + x + L.jpad);
-                uint32_t jr[R + 1];
+                bilinear_weights(npx - inx, npy - iny, w0, w1);
+                const uint32_t joff = (uint32_t)((iny + row0 + L.jpad) * L.jpitch + inx + x + L.jpad);
+                const uint32_t jsel = 0x0C000C00u | ((joff & 3u) + (((joff & 3u) + 1u) << 16));
+                uint32_t jp[R + 1];
 #pragma unroll
-                for (int r = 0; r <= R; ++r) jr[r] = load_u8x4(jb + (size_t)r * L.jpitch);
-                int e = 0;
+                for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8(rJ, joff & ~3u, r * L.jpitch, jsel);
+                int e[1] = {0};
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const int j00 = jr[r] & 255, j01 = (jr[r] >> 8) & 255;
-                    const int j10 = jr[r + 1] & 255, j11 = (jr[r + 1] >> 8) & 255;
-                    const int diff =
-                        descale(j00 * iw00 + j01 * iw01 + j10 * iw10 + j11 * iw11, W_BITS1 - 5) - ival[r];
-                    e += r < nrows ? (diff < 0 ? -diff : diff) : 0;
+                    const int diff = bilin(jp[r], jp[r + 1], w0, w1, W_BITS1 - 5) - ival[r];
+                    e[0] += r < nrows ? (diff < 0 ? -diff : diff) : 0;
                 }
-                const float errval = (float)wave_sum_small(e);
+                long long se[1];
+                wave_sum_exact<GRP, 1>(e, se);
+                const float errval = (float)se[0];
                 errv = errval * 1.f / (float)(32 * WW * WH);
             }
         }
@@ -284,9 +316,9 @@ hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s)
 {
     const dim3 grid((a.n + 3) / 4), block(256);
     switch (a.win_w) {
-#define TBDK_CASE(W)                                                             \
-    case W:                                                                      \
-        hipLaunchKernelGGL((lk_strip_kernel<W, W>), grid, block, 0, s, a);       \
+#define TBDK_CASE(W)                                                       \
+    case W:                                                                \
+        hipLaunchKernelGGL((lk_strip_kernel<W, W>), grid, block, 0, s, a); \
         break;
         TBDK_STRIP_WINDOWS(TBDK_CASE)
 #undef TBDK_CASE
