@@ -133,6 +133,38 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
                    const float* prev_pts, float* next_pts, uint8_t* status, float* err,
                    int32_t* iters, int n, const tbdk_lk_params* params, void* stream);
 
+/* ---- good features to track over box ROIs --------------------------------- */
+
+typedef struct tbdk_roi {
+    int32_t x, y, width, height;     /* must lie inside the image */
+} tbdk_roi;
+
+/* cv::cuda::createGoodFeaturesToTrackDetector(CV_8UC1, maxCorners, qualityLevel,
+ * minDistance, blockSize=3, useHarrisDetector=false)
+ * (modules/cudaimgproc/include/opencv2/cudaimgproc.hpp:603-604) */
+typedef struct tbdk_gftt_params {
+    int32_t max_corners;             /* > 0 */
+    double quality_level;            /* > 0 */
+    double min_distance;             /* >= 0 */
+    int32_t block_size;              /* 3 (the only supported value) */
+} tbdk_gftt_params;
+
+/* Replaces CornersDetector::detect (modules/cudaimgproc/src/gftt.cpp:98-213)
+ * applied to each ROI as an isolated image, with the CPU goodFeaturesToTrack
+ * semantics (imgproc/src/featureselect.cpp:361-516: max over the ROI,
+ * deterministic value/address ordering, greedy min-distance) — all ROIs of a
+ * frame in one batch and with no host synchronisation.
+ *   img        : device u8 image (width x height, row pitch in bytes)
+ *   rois       : HOST array of nroi ROIs (copied during the call)
+ *   corners    : device, nroi x max_corners x float2, frame coordinates
+ *   counts     : device, nroi int32 (corners found; -1 if a ROI produced more
+ *                candidates than the on-chip buffer holds — never truncated)
+ * Scratch grows on demand (tbdk_gftt_reserve avoids allocation in the call). */
+int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch,
+                   const tbdk_roi* rois, int nroi, const tbdk_gftt_params* params,
+                   float* corners, int32_t* counts, void* stream);
+int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
+
 /* ---- synthetic sequences (bench / test input) ----------------------------- */
 
 /* Renders frames [t0, t0+nframes) of the deterministic synthetic sequence of

@@ -67,6 +67,19 @@ class LkParams(C.Structure):
     ]
 
 
+class Roi(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class GfttParams(C.Structure):
+    _fields_ = [
+        ("max_corners", C.c_int32),
+        ("quality_level", C.c_double),
+        ("min_distance", C.c_double),
+        ("block_size", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/tbdk.h declares
 SIGNATURES = {
     "tbdk_version": (C.c_char_p, []),
@@ -84,6 +97,9 @@ SIGNATURES = {
                                    C.c_void_p]),
     "tbdk_lk_sparse": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.POINTER(Pyr), C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_int, C.POINTER(LkParams), C.c_void_p]),
+    "tbdk_gftt_rois": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Roi), C.c_int,
+                                 C.POINTER(GfttParams), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tbdk_gftt_reserve": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
 }

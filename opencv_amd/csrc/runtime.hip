@@ -92,6 +92,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
         (void)hipEventDestroy(r.end);
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
+    if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
+    if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
     delete ctx;
     return TBDK_OK;
 }
@@ -293,6 +296,82 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
     if (p->impl == 1 && !strip) return TBDK_EINVAL;
     int rec = timing_begin(ctx, "lk_sparse", s);
     hipError_t e = strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
+{
+    if (!ctx || max_rois < 0 || max_total_pixels < 0) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (max_rois > ctx->gftt_cap_rois) {
+        if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
+        if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
+        ctx->gftt_rois = nullptr;
+        ctx->gftt_max = nullptr;
+        ctx->gftt_cap_rois = 0;
+        hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)max_rois);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_max), sizeof(int) * (size_t)max_rois);
+        if (e != hipSuccess) return map_err(e);
+        ctx->gftt_cap_rois = max_rois;
+    }
+    if (max_total_pixels > ctx->gftt_cap_px) {
+        if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
+        ctx->gftt_planes = nullptr;
+        ctx->gftt_cap_px = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_planes), sizeof(float) * 4 * (size_t)max_total_pixels);
+        if (e != hipSuccess) return map_err(e);
+        ctx->gftt_cap_px = max_total_pixels;
+    }
+    return TBDK_OK;
+}
+
+int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, const tbdk_roi* rois,
+                   int nroi, const tbdk_gftt_params* p, float* corners, int32_t* counts, void* stream)
+{
+    if (!ctx || !p || nroi < 0) return TBDK_EINVAL;
+    if (nroi == 0) return TBDK_OK;
+    if (!img || !rois || !corners || !counts || width <= 0 || height <= 0 || pitch < width) return TBDK_EINVAL;
+    if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
+        return TBDK_EINVAL;
+    std::vector<GfttRoi> tab((size_t)nroi);
+    int64_t total = 0;
+    int max_area = 0, max_w = 0;
+    for (int i = 0; i < nroi; ++i) {
+        const tbdk_roi& r = rois[i];
+        if (r.x < 0 || r.y < 0 || r.width <= 0 || r.height <= 0 || r.x + r.width > width || r.y + r.height > height)
+            return TBDK_EINVAL;
+        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total};
+        total += (int64_t)r.width * r.height;
+        max_area = r.width * r.height > max_area ? r.width * r.height : max_area;
+        max_w = r.width > max_w ? r.width : max_w;
+    }
+    if (total > INT32_MAX) return TBDK_EINVAL;
+    int rc = tbdk_gftt_reserve(ctx, nroi > ctx->gftt_cap_rois ? nroi : ctx->gftt_cap_rois,
+                               total > ctx->gftt_cap_px ? total : ctx->gftt_cap_px);
+    if (rc != TBDK_OK) return rc;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "gftt", s);
+    hipError_t e = hipMemcpyAsync(ctx->gftt_rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
+    GfttArgs a;
+    a.img = img;
+    a.pitch = pitch;
+    a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
+    a.nroi = nroi;
+    a.cov0 = ctx->gftt_planes;
+    a.cov1 = ctx->gftt_planes + ctx->gftt_cap_px;
+    a.cov2 = ctx->gftt_planes + 2 * ctx->gftt_cap_px;
+    a.eig = ctx->gftt_planes + 3 * ctx->gftt_cap_px;
+    a.roi_max = ctx->gftt_max;
+    a.cap = 16384;
+    a.max_corners = p->max_corners;
+    a.quality = p->quality_level;
+    a.min_distance = p->min_distance;
+    a.corners = reinterpret_cast<float2*>(corners);
+    a.counts = counts;
+    if (gftt_select_smem(a.cap, a.max_corners) > 160 * 1024) return TBDK_EINVAL;
+    if (e == hipSuccess) e = launch_gftt(a, max_area, max_w, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }

@@ -33,6 +33,12 @@ struct tbdk_ctx {
     bool timing = false;
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
+    // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
+    void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
+    int* gftt_max = nullptr;     // int[cap_rois]
+    float* gftt_planes = nullptr;  // 4 x cap_px floats: cov0, cov1, cov2, eig
+    int gftt_cap_rois = 0;
+    int64_t gftt_cap_px = 0;
 };
 
 namespace tbdk {
@@ -81,4 +87,30 @@ struct SynPoseDev;  // == syn_pose
 hipError_t launch_synth(const void* poses_dev, int nobj, uint32_t bgseed, int W, int H, int nframes,
                         uint8_t* out, int pitch, hipStream_t s);
 
+}  // namespace tbdk
+
+namespace tbdk {
+// ---- GFTT over ROIs (klt_gftt.hip) ----
+struct GfttRoi {
+    int x, y, w, h;
+    int off;  // first pixel of this ROI in the scratch planes
+};
+struct GfttArgs {
+    const uint8_t* img;
+    int pitch;
+    const GfttRoi* rois;
+    int nroi;
+    float* cov0;
+    float* cov1;
+    float* cov2;
+    float* eig;
+    int* roi_max;
+    int cap;  // LDS candidate capacity per ROI (power of two)
+    int max_corners;
+    double quality, min_distance;
+    float2* corners;  // nroi x max_corners
+    int32_t* counts;  // nroi (-1: candidate overflow)
+};
+size_t gftt_select_smem(int cap, int max_corners);
+hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s);
 }  // namespace tbdk

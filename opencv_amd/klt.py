@@ -244,6 +244,43 @@ class SparsePyrLKOpticalFlow:
         return LkResult(out, status, err, iters)
 
 
+class GoodFeaturesToTrackDetector:
+    """cv::cuda::createGoodFeaturesToTrackDetector(CV_8UC1, maxCorners, qualityLevel,
+    minDistance, blockSize=3) (cudaimgproc.hpp:603-604) with the CPU
+    goodFeaturesToTrack semantics, applied to a batch of box ROIs of one image."""
+
+    def __init__(self, maxCorners: int = 1000, qualityLevel: float = 0.01, minDistance: float = 0.0,
+                 blockSize: int = 3, useHarrisDetector: bool = False, device: int = 0):
+        if useHarrisDetector:
+            raise _lib.TbdkError("Harris response is not implemented (min-eigenvalue only)")
+        self.prm = _lib.GfttParams(int(maxCorners), float(qualityLevel), float(minDistance), int(blockSize))
+        self.ctx = Context.get(device)
+
+    def detect_rois(self, image: torch.Tensor, rois, stream=None):
+        """rois: iterable of (x, y, w, h).  Returns (corners (nroi, maxCorners, 2) f32,
+        counts (nroi,) i32) device tensors; corners are in image coordinates."""
+        if image.dtype != torch.uint8 or image.dim() != 2 or not image.is_cuda or image.stride(1) != 1:
+            raise _lib.TbdkError("detect expects a 2-D uint8 device tensor")
+        rois = list(rois)
+        n = len(rois)
+        arr = (_lib.Roi * max(n, 1))(*[_lib.Roi(int(x), int(y), int(w), int(h)) for (x, y, w, h) in rois])
+        corners = torch.zeros((n, self.prm.max_corners, 2), dtype=torch.float32, device=image.device)
+        counts = torch.zeros((n,), dtype=torch.int32, device=image.device)
+        _lib.check(self.ctx.lib.tbdk_gftt_rois(self.ctx.handle, C.c_void_p(image.data_ptr()), image.shape[1],
+                                               image.shape[0], image.stride(0), arr, n, C.byref(self.prm),
+                                               C.c_void_p(corners.data_ptr()), C.c_void_p(counts.data_ptr()),
+                                               _stream_ptr(stream)), "tbdk_gftt_rois")
+        return corners, counts
+
+    def detect(self, image: torch.Tensor, stream=None) -> torch.Tensor:
+        """Whole image as one ROI -> (K, 2) corners (CornersDetector::detect without mask)."""
+        c, n = self.detect_rois(image, [(0, 0, image.shape[1], image.shape[0])], stream)
+        k = int(n[0].item())
+        if k < 0:
+            raise _lib.TbdkError("candidate buffer overflow (image too large for one ROI)")
+        return c[0, :k]
+
+
 def synth_render(seed: int, width: int, height: int, nobj: int, t0: int, nframes: int, device: int = 0,
                  ctx: Context | None = None, stream=None):
     """Render frames [t0, t0+nframes) of the synthetic sequence into HBM.

@@ -90,3 +90,18 @@ double orc_now(void);
 }
 #endif
 #endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* cv::goodFeaturesToTrack(image, corners, maxCorners, qualityLevel, minDistance,
+ * noArray(), blockSize=3, gradientSize=3, useHarris=false) on an isolated u8
+ * image (imgproc/src/featureselect.cpp:361-516, corner.cpp:52-101,237-326).
+ * Returns the corner count; corners: maxCorners x float2 (x, y). */
+int orc_gftt(const uint8_t* img, int w, int h, int pitch, int maxCorners, double qualityLevel,
+             double minDistance, float* corners);
+/* cornerMinEigenVal(blockSize=3, ksize=3, BORDER_REFLECT_101) -> eig (w x h float) */
+void orc_min_eig(const uint8_t* img, int w, int h, int pitch, float* eig);
+#ifdef __cplusplus
+}
+#endif

@@ -199,3 +199,33 @@ def read_png_gray(path: str) -> np.ndarray:
         return img[:, :, 0].astype(np.uint8)
     r, g, b = img[:, :, 0], img[:, :, 1], img[:, :, 2]
     return ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+def gftt(img: np.ndarray, max_corners=1000, quality=0.01, min_distance=0.0) -> np.ndarray:
+    lib = load()
+    lib.orc_gftt.restype = C.c_int
+    lib.orc_gftt.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros((max(max_corners, 1), 2), dtype=np.float32)
+    n = lib.orc_gftt(_ptr(img), w, h, img.strides[0], max_corners, quality, min_distance, _ptr(out))
+    return out[:n]
+
+
+def min_eig(img: np.ndarray) -> np.ndarray:
+    lib = load()
+    lib.orc_min_eig.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), dtype=np.float32)
+    lib.orc_min_eig(_ptr(img), w, h, img.strides[0], _ptr(out))
+    return out
+
+
+def gftt_rois(frame: np.ndarray, rois, max_corners=256, quality=0.01, min_distance=3.0):
+    """Per-ROI goodFeaturesToTrack on isolated ROIs; corners in frame coordinates."""
+    res = []
+    for (x, y, w, h) in rois:
+        c = gftt(frame[y:y + h, x:x + w], max_corners, quality, min_distance)
+        res.append(c + np.float32([x, y]))
+    return res

@@ -1,0 +1,58 @@
+"""GPU GFTT over box ROIs vs the CPU oracle: identical corner lists (bit-exact
+positions, same order, same count) per ROI."""
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def detect(gpu, frame, rois, maxc, q, md):
+    from opencv_amd import klt
+
+    det = klt.GoodFeaturesToTrackDetector(maxc, q, md)
+    c, n = det.detect_rois(torch.from_numpy(np.ascontiguousarray(frame)).cuda(), rois)
+    torch.cuda.synchronize()
+    return c.cpu().numpy(), n.cpu().numpy()
+
+
+def check(frame, rois, c, n, maxc, q, md):
+    ref = O.gftt_rois(frame, rois, maxc, q, md)
+    for i, r in enumerate(ref):
+        assert n[i] == len(r), f"roi {i}: count {n[i]} vs {len(r)}"
+        assert np.array_equal(c[i, :n[i]], r), f"roi {i}: corners differ"
+
+
+@pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (1000, 0.01, 0.0), (64, 0.05, 8.0), (32, 0.3, 1.0)])
+def test_gftt_rois_match_oracle(gpu, maxc, q, md):
+    fr, gt = O.synth(20261015, 640, 480, 32, 0, 1)
+    rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]
+    c, n = detect(gpu, fr[0], rois, maxc, q, md)
+    check(fr[0], rois, c, n, maxc, q, md)
+
+
+def test_gftt_basketball_and_edge_rois(gpu):
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "basketball_pair.npz"))
+    img = d["a"]
+    rois = [(0, 0, 640, 480)[:2] + (160, 120), (600, 440, 40, 40), (0, 0, 3, 3), (5, 5, 2, 50), (100, 100, 1, 1),
+            (300, 200, 77, 33), (0, 0, 320, 240)]
+    c, n = detect(gpu, img, rois, 500, 0.01, 2.0)
+    check(img, rois, c, n, 500, 0.01, 2.0)
+
+
+def test_gftt_flat_and_empty(gpu):
+    img = np.full((100, 100), 77, np.uint8)
+    c, n = detect(gpu, img, [(0, 0, 100, 100), (10, 10, 20, 20)], 100, 0.01, 0.0)
+    assert (n == 0).all()
+    c, n = detect(gpu, img, [], 100, 0.01, 0.0)
+    assert n.shape == (0,)
+
+
+def test_gftt_1080p_128_boxes(gpu):
+    fr, gt = O.synth(20261015, 1920, 1080, 128, 0, 1)
+    rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]
+    c, n = detect(gpu, fr[0], rois, 256, 0.01, 3.0)
+    check(fr[0], rois, c, n, 256, 0.01, 3.0)
+    assert (n > 0).all()
