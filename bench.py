@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py — tracked frames/sec of the 1080p x 128-object TBD loop on MI355X.
+
+Workload (BASELINE.json configs[2]): one synthetic 1920x1080 sequence of
+`warmup + steps` frames with 128 moving textured objects per GPU, rendered
+into HBM before timing (tbdk_synth_render).  A "step" is one frame through the
+full loop of libtbdk (tbdk_tbd_step): 3-level pyramid + Scharr planes, GFTT in
+the boxes of new / re-detect tracks, sparse PyrLK (win 21) over every track's
+corners, per-track similarity fit (KLT box propagation), and the native
+cv::tbd::Tracker step on the frame's ground-truth detections.
+
+Multi-GPU: one process per GPU (torchrun), one independent sequence per GPU
+(seed + rank), no data-path collective; value = frames of all ranks / max
+wall time over ranks ("scaling": "weak").
+
+Prints ONE JSON line on rank 0 (contract in the task description), including
+"roofline" for the dominant kernel (lk_sparse, VALU-bound -> TFLOP/s against
+the 157.3 TF f32 peak) and "cpu_baseline" (the CPU oracle restatement of the
+same per-frame KLT work, timed on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "tracked frames/sec, 1080p×128-object TBD loop @ 1/2/4/8 MI355X"
+PEAK_F32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 (vector == f32 MFMA)
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def lk_flops(points_levels: float, iters: float, win: int) -> float:
+    """per point per level 441*30 (I / dI bilinear + G) plus,
+    per Newton iteration, 441*13 (J bilinear, diff, 2 FMA) for win 21."""
+    area = win * win
+    return points_levels * area * 30.0 + iters * area * 13.0
+
+
+def pyr_bytes(w: int, h: int, nlevels: int) -> int:
+    """B_pyr = sum_{L<n-1} (|L| + |L+1|) for the new frame."""
+    sizes = []
+    for _ in range(nlevels):
+        sizes.append(w * h)
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return sum(sizes[i] + sizes[i + 1] for i in range(nlevels - 1))
+
+
+def cpu_baseline(frames_host, gt, args, seconds: float):
+    """The oracle (CPU restatement of the reference path) running the same
+    per-frame KLT work: pyramid, GFTT in every box every `redetect` frames
+    (single-threaded, as the reference's goodFeaturesToTrack), multithreaded
+    LK over the tracked corners (the reference's parallel_for_ over points).
+    The host tracker step (~1 ms, identical code on both sides) is excluded."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import _oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    pts = None
+    prev = None
+    done = 0
+    t0 = time.perf_counter()
+    n = frames_host.shape[0]
+    for f in range(n):
+        img = frames_host[f]
+        P = O.Pyramid(img, (args.win, args.win), args.max_level)
+        if prev is not None and pts is not None and len(pts):
+            nxt, st, _, _ = O.lk(prev, P, pts, (args.win, args.win), args.max_level, 30, 0.01, 0, 1e-4,
+                                 O.ACCUM_SSE2, threads)
+            pts = nxt[st == 1]
+        if f % args.redetect == 0 or pts is None:
+            rois = [tuple(int(v) for v in g[1:]) for g in gt[f] if g[0]]
+            got = O.gftt_rois(img, rois, 256, 0.01, 3.0)
+            pts = np.concatenate(got).astype(np.float32) if got else np.zeros((0, 2), np.float32)
+        prev = P
+        done += 1
+        if time.perf_counter() - t0 > seconds and done >= 3:
+            break
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} frames of the rank-0 sequence, {args.width}x{args.height}x{args.objects} "
+                      f"objects: oracle pyramid + GFTT(256/box, every {args.redetect} frames, 1 thread) + "
+                      f"PyrLK win {args.win} SSE2-order ({threads} threads); tracker step excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--objects", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--win", type=int, default=21)
+    ap.add_argument("--max-level", type=int, default=2)
+    ap.add_argument("--redetect", type=int, default=5)
+    ap.add_argument("--bounds", choices=["reference", "frame"], default="reference",
+                    help="reference: the tracker's hard-coded 1280x720 filter (tbd.cpp:218); frame: W x H")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from opencv_amd import klt, tbd
+
+    ctx = klt.Context.get(dev)
+    nframes = args.warmup + args.steps
+    frames, gt = klt.synth_render(args.seed + rank, args.width, args.height, args.objects, 0, nframes,
+                                  device=dev, ctx=ctx)
+    gtn = gt.numpy()
+    dets = [tbd.detections_from_gt(gtn[f]) for f in range(nframes)]
+    over = {}
+    if args.bounds == "frame":
+        over = dict(bounds_xmax=args.width, bounds_ymax=args.height)
+    cfg = tbd.default_config(args.width, args.height, win=args.win, max_level=args.max_level,
+                             redetect_every=args.redetect, **over)
+    loop = tbd.TbdLoop(cfg, ctx=ctx)
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    for f in range(args.warmup):
+        loop.step(frames[f], f, dets[f], stream)
+
+    ctx.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lk_pts = lk_it = klt_pts = ntr = redet = 0
+    for f in range(args.warmup, nframes):
+        m = loop.step(frames[f], f, dets[f], stream)
+        lk_pts += m.lk_points
+        lk_it += m.lk_iters
+        klt_pts += m.klt_points
+        ntr += m.ntracks
+        redet += m.redetected
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    kstats = {}
+    for name in ("pyr_build", "lk_sparse", "gftt", "tbd_fit"):
+        c, ms = ctx.timing_query(name)
+        kstats[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "total_ms": ms}
+    ctx.timing_enable(False)
+
+    lk = kstats["lk_sparse"]
+    nlev = args.max_level + 1
+    if lk["launches"]:
+        flops_per_launch = lk_flops(lk_pts * nlev, lk_it, args.win) / lk["launches"]
+        achieved = flops_per_launch / (lk["avg_us"] * 1e-6) / 1e12
+    else:
+        flops_per_launch, achieved = 0.0, 0.0
+    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": None, "kernel": "lk_sparse",
+                "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA use; peak = fp32 vector rate; "
+                        "algorithmic flops per SURVEY.md §8(d) with the measured iteration count",
+                "flops_per_launch": flops_per_launch,
+                "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
+                "mean_iters_per_point": lk_it / max(1, lk_pts)}
+    pb = pyr_bytes(args.width, args.height, nlev)
+    pyr = kstats["pyr_build"]
+    pyr_gbs = pb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
+    roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build"}
+
+    steps_all = args.steps * world
+    out = {
+        "metric": METRIC,
+        "value": round(steps_all / el, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1000.0, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (deterministic in-repo generator, opencv_amd/csrc/synth_spec.h)",
+        "config": {"workload": f"TBD loop {args.width}x{args.height} x {args.objects} objects "
+                               f"(BASELINE configs[2]), {nframes}-frame sequence per GPU",
+                   "levels": nlev, "win": args.win, "gftt": f"256/box, q 0.01, minDist 3, every {args.redetect}",
+                   "tracker_bounds": args.bounds, "parallelism": f"replicas x{world} (one sequence per GPU)"},
+        "roofline": roofline,
+        "roofline_pyramid": roof_pyr,
+        "kernels": kstats,
+        "per_frame": {"lk_points": lk_pts / args.steps, "tracked_points": klt_pts / args.steps,
+                      "tracks": ntr / args.steps, "gftt_rois": redet / args.steps},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nb = min(nframes, 40)
+        out["cpu_baseline"] = cpu_baseline(frames[:nb].cpu().numpy(), gtn[:nb], args, args.cpu_baseline_seconds)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -165,6 +165,72 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
                    float* corners, int32_t* counts, void* stream);
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
 
+/* ---- tracking-by-detection loop (one video stream per context) ------------ */
+
+/* Per-stream TBD loop: pyramid -> (GFTT on new / re-detect tracks) -> PyrLK over
+ * every track's corners -> per-track similarity fit (KLT box propagation, the
+ * Track::motionModel hook of modules/trackingbydetection/include/opencv2/tbd.hpp:111)
+ * -> cv::tbd::Tracker::performTrackingStep (modules/trackingbydetection/src/tbd.cpp:210-286)
+ * restated natively.  Replaces the tracking section of samples/gpu/tbd.cpp:624-706. */
+typedef struct tbdk_tbd tbdk_tbd;
+
+typedef struct tbdk_tbd_config {
+    int32_t width, height;
+    /* PyrLK (cv::calcOpticalFlowPyrLK defaults except maxLevel: "3-level" = 2) */
+    int32_t win, max_level, lk_iters;
+    double lk_epsilon;
+    float min_eig_threshold;
+    /* GFTT per track box */
+    int32_t max_corners;             /* <= 256 */
+    double quality_level, min_distance;
+    int32_t redetect_every;          /* re-detect corners every N frames (5) */
+    int32_t min_points;              /* ... or when fewer points survive (32) */
+    int32_t min_fit_points;          /* points needed for the box fit (4) */
+    /* cv::tbd::TbdArgs (samples/gpu/tbd.cpp:249-254 defaults) */
+    double cost_of_non_assignment;
+    int32_t time_window_size, track_age_threshold;
+    double track_visibility_threshold, track_confidence_threshold;
+    /* filterTracksOutOfBounds window; the reference hard-codes 0,1280,0,720 */
+    int32_t bounds_xmin, bounds_xmax, bounds_ymin, bounds_ymax;
+    int32_t max_tracks;              /* point-set slots on the device */
+    int32_t use_klt;                 /* 0: reference constant-velocity prediction only */
+} tbdk_tbd_config;
+
+typedef struct tbdk_detection {      /* cv::tbd::Detection (tbd.hpp:69-83) */
+    int32_t id, x, y, width, height;
+    double confidence;
+} tbdk_detection;
+
+typedef struct tbdk_frame_metrics {  /* per-frame TP/FN/FP/GT/c/sum d (tbd.hpp:145-151) */
+    int32_t tp, fn, fp, gt, matches;
+    double bbox_overlap;
+    int32_t ntracks;
+    int32_t lk_points;               /* corners that entered PyrLK this frame */
+    int32_t klt_points;              /* ... of which tracked (status 1) */
+    int32_t klt_predicted;           /* tracks predicted by the KLT fit */
+    int32_t redetected;              /* GFTT ROIs this frame */
+    int32_t pad_;
+    int64_t lk_iters;                /* Newton iterations over all levels (flop accounting) */
+} tbdk_frame_metrics;
+
+typedef struct tbdk_track_info {
+    uint32_t id;
+    int32_t x, y, width, height;             /* last box */
+    int32_t pred_x, pred_y, pred_w, pred_h;  /* predPosition */
+    int32_t age, total_visible;
+    int32_t npoints;                         /* tracked corners after this frame */
+    double max_confidence, bbox_overlap;
+} tbdk_track_info;
+
+int tbdk_tbd_default_config(int width, int height, tbdk_tbd_config* cfg);
+int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out);
+int tbdk_tbd_destroy(tbdk_tbd* tbd);
+/* One frame through the loop.  frame: device u8 (width x height, pitch);
+ * dets: HOST array.  Synchronises the stream once (predictions -> host tracker). */
+int tbdk_tbd_step(tbdk_tbd* tbd, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
+                  int ndets, tbdk_frame_metrics* metrics, void* stream);
+int tbdk_tbd_tracks(tbdk_tbd* tbd, tbdk_track_info* out, int cap, int* n);
+
 /* ---- synthetic sequences (bench / test input) ----------------------------- */
 
 /* Renders frames [t0, t0+nframes) of the deterministic synthetic sequence of

@@ -80,6 +80,41 @@ class GfttParams(C.Structure):
     ]
 
 
+class TbdConfig(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32),
+        ("win", C.c_int32), ("max_level", C.c_int32), ("lk_iters", C.c_int32),
+        ("lk_epsilon", C.c_double), ("min_eig_threshold", C.c_float),
+        ("max_corners", C.c_int32), ("quality_level", C.c_double), ("min_distance", C.c_double),
+        ("redetect_every", C.c_int32), ("min_points", C.c_int32), ("min_fit_points", C.c_int32),
+        ("cost_of_non_assignment", C.c_double),
+        ("time_window_size", C.c_int32), ("track_age_threshold", C.c_int32),
+        ("track_visibility_threshold", C.c_double), ("track_confidence_threshold", C.c_double),
+        ("bounds_xmin", C.c_int32), ("bounds_xmax", C.c_int32), ("bounds_ymin", C.c_int32),
+        ("bounds_ymax", C.c_int32),
+        ("max_tracks", C.c_int32), ("use_klt", C.c_int32),
+    ]
+
+
+class Detection(C.Structure):
+    _fields_ = [("id", C.c_int32), ("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("confidence", C.c_double)]
+
+
+class FrameMetrics(C.Structure):
+    _fields_ = [("tp", C.c_int32), ("fn", C.c_int32), ("fp", C.c_int32), ("gt", C.c_int32),
+                ("matches", C.c_int32), ("bbox_overlap", C.c_double), ("ntracks", C.c_int32),
+                ("lk_points", C.c_int32), ("klt_points", C.c_int32), ("klt_predicted", C.c_int32),
+                ("redetected", C.c_int32), ("pad_", C.c_int32), ("lk_iters", C.c_int64)]
+
+
+class TrackInfo(C.Structure):
+    _fields_ = [("id", C.c_uint32), ("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("pred_x", C.c_int32), ("pred_y", C.c_int32), ("pred_w", C.c_int32),
+                ("pred_h", C.c_int32), ("age", C.c_int32), ("total_visible", C.c_int32),
+                ("npoints", C.c_int32), ("max_confidence", C.c_double), ("bbox_overlap", C.c_double)]
+
+
 # name -> (restype, argtypes); every symbol include/tbdk.h declares
 SIGNATURES = {
     "tbdk_version": (C.c_char_p, []),
@@ -100,6 +135,12 @@ SIGNATURES = {
     "tbdk_gftt_rois": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Roi), C.c_int,
                                  C.POINTER(GfttParams), C.c_void_p, C.c_void_p, C.c_void_p]),
     "tbdk_gftt_reserve": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
+    "tbdk_tbd_default_config": (C.c_int, [C.c_int, C.c_int, C.POINTER(TbdConfig)]),
+    "tbdk_tbd_create": (C.c_int, [C.c_void_p, C.POINTER(TbdConfig), C.POINTER(C.c_void_p)]),
+    "tbdk_tbd_destroy": (C.c_int, [C.c_void_p]),
+    "tbdk_tbd_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(Detection), C.c_int,
+                                C.POINTER(FrameMetrics), C.c_void_p]),
+    "tbdk_tbd_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
 }

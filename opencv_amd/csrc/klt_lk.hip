@@ -47,6 +47,7 @@ __global__ __launch_bounds__(64) void lk_sparse_kernel(LkArgs a)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int i = blockIdx.x;
     if (i >= a.n) return;
+    if (a.seg_counts && i % a.seg_stride >= a.seg_counts[i / a.seg_stride]) return;
     const int lane = threadIdx.x;
     const int winW = a.win_w, winH = a.win_h, area = winW * winH;
     const int SW = winW + 3, SH = winH + 3, DW = winW + 1;

@@ -109,6 +109,7 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;  // wave-uniform
+    if (a.seg_counts && i % a.seg_stride >= a.seg_counts[i / a.seg_stride]) return;
 
     const int grp = lane / WW;
     const int x = lane - grp * WW;

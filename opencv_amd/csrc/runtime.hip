@@ -60,6 +60,8 @@ struct DeviceGuard {
     }
 };
 
+int map_status(hipError_t e) { return map_err(e); }
+
 }  // namespace tbdk
 
 using namespace tbdk;
@@ -254,6 +256,15 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
                    float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
                    void* stream)
 {
+    return tbdk::lk_internal(ctx, prev, next, prev_pts, next_pts, status, err, iters, n, p, nullptr, 0, stream);
+}
+
+}  // extern "C"
+
+int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts,
+                      float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
+                      const int32_t* seg_counts, int seg_stride, void* stream)
+{
     if (!ctx || !prev || !next || !p || n < 0) return TBDK_EINVAL;
     if (n == 0) return TBDK_OK;
     if (!prev_pts || !next_pts || !status) return TBDK_EINVAL;
@@ -287,6 +298,9 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
     a.err = err;
     a.iters = iters;
     a.n = n;
+    a.seg_counts = seg_counts;
+    a.seg_stride = seg_stride > 0 ? seg_stride : 1;
+    if (seg_counts && seg_stride <= 0) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     bool have_d = true;
@@ -299,6 +313,8 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
     timing_end(ctx, rec, s);
     return map_err(e);
 }
+
+extern "C" {
 
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
 {

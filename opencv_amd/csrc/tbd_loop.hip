@@ -1,0 +1,510 @@
+// tbd_loop.hip — the per-stream tracking-by-detection loop (C ABI tbdk_tbd_*).
+//
+// Per frame (one HIP stream, one host thread per stream / GPU):
+//   1. pyramid (+ Scharr planes) of the new frame                       [HIP]
+//   2. sparse PyrLK of every live track's corners, prev -> new frame     [HIP, one launch,
+//      segmented layout: slot s owns points s*256 .. s*256+count[s]-1]
+//   3. tbd_fit_kernel, one wave per live track: ballot-compaction of the
+//      tracked points (they become next frame's corners) and the 4-DOF
+//      similarity fit of getRTMatrix (video/src/lkpyramid.cpp:1436-1468),
+//      giving the KLT-propagated centroid                                [HIP]
+//   4. predictions -> host (the single stream sync of the frame)
+//   5. cv::tbd::Tracker::performTrackingStep restated natively, with the
+//      KLT centroid as Track::motionModel (tbd.hpp:111)                 [host C++]
+//   6. GFTT in the boxes of new tracks and of tracks due for re-detection
+//      (every `redetect_every` frames or < min_points corners), written
+//      straight into their point slots                                   [HIP]
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <new>
+#include <queue>
+#include <unordered_map>
+#include <vector>
+
+#include "tbd_tracker.hpp"
+#include "tbdk_internal.hpp"
+
+namespace tbdk {
+
+constexpr int kSlotPts = 256;  // corner capacity per track
+
+struct FitEntry {
+    int slot;
+    int x, y, w, h;  // the track's last box (centroid convention of tbd.cpp:1064-1065)
+};
+
+struct FitOut {
+    double cx, cy;  // KLT-propagated centroid
+    double scale;
+    int valid;
+    int n;          // corners still tracked (kept in the slot)
+    int npts;       // corners that entered LK this frame
+    int iters;      // Newton iterations of those corners over all levels (flop accounting)
+};
+
+// One wave per live track.  Fit terms follow getRTMatrix's non-full-affine
+// branch: float products summed in double, in point order (one lane, so the
+// double rounding sequence is fixed and matches the oracle).
+__global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict__ ents, int nents,
+                                                     float2* __restrict__ slot_pts,
+                                                     const float2* __restrict__ slot_next,
+                                                     const uint8_t* __restrict__ slot_status,
+                                                     const int32_t* __restrict__ slot_iters,
+                                                     int32_t* __restrict__ slot_counts, FitOut* __restrict__ out,
+                                                     int min_fit)
+{
+    __shared__ float2 sa[kSlotPts], sb[kSlotPts];
+    const int e = blockIdx.x;
+    if (e >= nents) return;
+    const int lane = threadIdx.x;
+    const FitEntry E = ents[e];
+    const int cnt = slot_counts[E.slot];
+    const size_t base = (size_t)E.slot * kSlotPts;
+    int m = 0, it = 0;
+    for (int j0 = 0; j0 < kSlotPts; j0 += 64) {
+        const int j = j0 + lane;
+        const bool ok = j < cnt && slot_status[base + j];
+        it += j < cnt ? slot_iters[base + j] : 0;
+        const unsigned long long bal = __ballot(ok);
+        if (ok) {
+            const int pos = m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+            sa[pos] = slot_pts[base + j];
+            sb[pos] = slot_next[base + j];
+        }
+        m += __popcll(bal);
+    }
+    __syncthreads();
+    for (int j = lane; j < m; j += 64) slot_pts[base + j] = sb[j];
+    for (int off = 32; off >= 1; off >>= 1) it += __shfl_xor(it, off, 64);
+    if (lane == 0) {
+        slot_counts[E.slot] = m;
+        double s00 = 0, s02 = 0, s03 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+        for (int i = 0; i < m; ++i) {
+            const float ax = sa[i].x, ay = sa[i].y, bx = sb[i].x, by = sb[i].y;
+            s00 += ax * ax + ay * ay;
+            s02 += ax;
+            s03 += ay;
+            b0 += ax * bx + ay * by;
+            b1 += ax * by - ay * bx;
+            b2 += bx;
+            b3 += by;
+        }
+        FitOut o;
+        o.n = m;
+        o.npts = cnt;
+        o.iters = it;
+        o.valid = 0;
+        o.cx = o.cy = 0.0;
+        o.scale = 0.0;
+        if (m >= min_fit && m > 0) {
+            const double n = (double)m;
+            const double den = s00 - (s02 * s02 + s03 * s03) / n;
+            if (den > 1e-9) {
+                const double p = (b0 - (s02 * b2 + s03 * b3) / n) / den;
+                const double q = (b1 + (s03 * b2 - s02 * b3) / n) / den;
+                const double tx = (b2 - s02 * p + s03 * q) / n;
+                const double ty = (b3 - s03 * p - s02 * q) / n;
+                const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
+                o.cx = p * cx0 - q * cy0 + tx;
+                o.cy = q * cx0 + p * cy0 + ty;
+                o.scale = sqrt(p * p + q * q);
+                o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
+            }
+        }
+        out[e] = o;
+    }
+}
+
+// point sets of deleted tracks: count = 0 (keeps later LK launches from
+// working on stale slots)
+__global__ void tbd_clear_kernel(const int* __restrict__ slots, int n, int32_t* __restrict__ slot_counts)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) slot_counts[slots[k]] = 0;
+}
+
+// GFTT staging -> point slots
+__global__ void tbd_scatter_kernel(const float2* __restrict__ corners, const int32_t* __restrict__ counts,
+                                   const int* __restrict__ roi_slot, int maxc, float2* __restrict__ slot_pts,
+                                   int32_t* __restrict__ slot_counts)
+{
+    const int r = blockIdx.x;
+    const int n = counts[r] < 0 ? 0 : counts[r];
+    const int s = roi_slot[r];
+    for (int j = threadIdx.x; j < n; j += blockDim.x)
+        slot_pts[(size_t)s * kSlotPts + j] = corners[(size_t)r * maxc + j];
+    if (threadIdx.x == 0) slot_counts[s] = n;
+}
+
+}  // namespace tbdk
+
+using namespace tbdk;
+
+struct tbdk_tbd {
+    tbdk_ctx* ctx = nullptr;
+    tbdk_tbd_config cfg;
+    tbdk_pyr pyr[2];
+    int cur = 0;
+    bool have_prev = false;
+    tbd::Tracker* tracker = nullptr;
+    // device
+    float2* slot_pts = nullptr;
+    float2* slot_next = nullptr;
+    uint8_t* slot_status = nullptr;
+    int32_t* slot_iters = nullptr;
+    int32_t* slot_counts = nullptr;
+    FitEntry* d_ents = nullptr;
+    FitOut* d_fit = nullptr;
+    float2* d_corners = nullptr;
+    int32_t* d_ccounts = nullptr;
+    int* d_roi_slot = nullptr;
+    int* d_clear = nullptr;
+    // pinned host (rewritten only after h2d_done has completed)
+    FitEntry* h_ents = nullptr;
+    FitOut* h_fit = nullptr;
+    int* h_roi_slot = nullptr;
+    int* h_clear = nullptr;
+    hipEvent_t h2d_done = nullptr;
+    // host bookkeeping; slots are handed out lowest-first so the LK launch
+    // covers only [0, max live slot] x 256 points
+    std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
+    std::unordered_map<unsigned, int> slot_of;     // track id -> slot
+    std::unordered_map<unsigned, int> npts_of;     // track id -> corners after last fit
+    std::vector<tbd::Detection> dets;
+    std::vector<tbd::Prediction> preds;
+    std::vector<tbdk_roi> rois;
+};
+
+namespace {
+
+int release(tbdk_tbd* t)
+{
+    if (!t) return TBDK_OK;
+    for (int i = 0; i < 2; ++i)
+        if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_ents,
+                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_roi_slot, t->d_clear};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    if (t->h2d_done) (void)hipEventDestroy(t->h2d_done);
+    void* host[] = {t->h_ents, t->h_fit, t->h_roi_slot, t->h_clear};
+    for (void* p : host)
+        if (p) (void)hipHostFree(p);
+    delete t->tracker;
+    delete t;
+    return TBDK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tbdk_tbd_default_config(int width, int height, tbdk_tbd_config* c)
+{
+    if (!c || width <= 0 || height <= 0) return TBDK_EINVAL;
+    std::memset(c, 0, sizeof(*c));
+    c->width = width;
+    c->height = height;
+    c->win = 21;
+    c->max_level = 2;  // "3-level PyrLK" (levels - 1)
+    c->lk_iters = 30;
+    c->lk_epsilon = 0.01;
+    c->min_eig_threshold = 1e-4f;
+    c->max_corners = 256;
+    c->quality_level = 0.01;
+    c->min_distance = 3.0;
+    c->redetect_every = 5;
+    c->min_points = 32;
+    c->min_fit_points = 4;
+    c->cost_of_non_assignment = 10.0;
+    c->time_window_size = 16;
+    c->track_age_threshold = 4;
+    c->track_visibility_threshold = 0.3;
+    c->track_confidence_threshold = 0.2;
+    c->bounds_xmin = 0;
+    c->bounds_xmax = 1280;
+    c->bounds_ymin = 0;
+    c->bounds_ymax = 720;
+    c->max_tracks = 1024;
+    c->use_klt = 1;
+    return TBDK_OK;
+}
+
+int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
+{
+    if (!ctx || !cfg || !out) return TBDK_EINVAL;
+    *out = nullptr;
+    if (cfg->max_corners <= 0 || cfg->max_corners > kSlotPts || cfg->max_tracks <= 0 || cfg->win < 3 ||
+        cfg->win > 31 || cfg->redetect_every <= 0)
+        return TBDK_EINVAL;
+    tbdk_tbd* t = new (std::nothrow) tbdk_tbd();
+    if (!t) return TBDK_ENOMEM;
+    t->ctx = ctx;
+    t->cfg = *cfg;
+    std::memset(t->pyr, 0, sizeof(t->pyr));
+    int rc = TBDK_OK;
+    for (int i = 0; i < 2 && rc == TBDK_OK; ++i)
+        rc = tbdk_pyr_create(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i]);
+    if (rc != TBDK_OK) {
+        release(t);
+        return rc;
+    }
+    const size_t S = (size_t)cfg->max_tracks;
+    hipError_t e = hipSuccess;
+    auto dm = [&](void** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc(p, bytes);
+        if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
+    };
+    auto hm = [&](void** p, size_t bytes) {
+        if (e == hipSuccess) e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+    };
+    dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_status), S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * S);
+    dm(reinterpret_cast<void**>(&t->d_ents), sizeof(FitEntry) * S);
+    dm(reinterpret_cast<void**>(&t->d_fit), sizeof(FitOut) * S);
+    dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
+    dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
+    dm(reinterpret_cast<void**>(&t->d_roi_slot), sizeof(int) * S);
+    dm(reinterpret_cast<void**>(&t->d_clear), sizeof(int) * S);
+    hm(reinterpret_cast<void**>(&t->h_ents), sizeof(FitEntry) * S);
+    hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
+    hm(reinterpret_cast<void**>(&t->h_roi_slot), sizeof(int) * S);
+    hm(reinterpret_cast<void**>(&t->h_clear), sizeof(int) * S);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->h2d_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        release(t);
+        return map_status(e);
+    }
+    tbd::TbdArgs a;
+    a.costOfNonAssignment = cfg->cost_of_non_assignment;
+    a.timeWindowSize = (unsigned)cfg->time_window_size;
+    a.trackAgeThreshold = (unsigned)cfg->track_age_threshold;
+    a.trackVisibilityThreshold = cfg->track_visibility_threshold;
+    a.trackConfidenceThreshold = cfg->track_confidence_threshold;
+    a.shouldStoreMetrics = true;
+    a.boundsXmin = cfg->bounds_xmin;
+    a.boundsXmax = cfg->bounds_xmax;
+    a.boundsYmin = cfg->bounds_ymin;
+    a.boundsYmax = cfg->bounds_ymax;
+    t->tracker = new (std::nothrow) tbd::Tracker(a);
+    if (!t->tracker) {
+        release(t);
+        return TBDK_ENOMEM;
+    }
+    for (int s = 0; s < cfg->max_tracks; ++s) t->free_slots.push(s);
+    rc = tbdk_gftt_reserve(ctx, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
+    if (rc != TBDK_OK) {
+        release(t);
+        return rc;
+    }
+    *out = t;
+    return TBDK_OK;
+}
+
+int tbdk_tbd_destroy(tbdk_tbd* t) { return release(t); }
+
+int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets, int ndets,
+                  tbdk_frame_metrics* metrics, void* stream)
+{
+    if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width) return TBDK_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const tbdk_tbd_config& c = t->cfg;
+    tbdk_pyr& P = t->pyr[t->cur];
+    tbdk_pyr& Pprev = t->pyr[t->cur ^ 1];
+    int rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, stream);
+    if (rc != TBDK_OK) return rc;
+    (void)hipSetDevice(t->ctx->device);
+
+    // pinned staging buffers are rewritten below: the previous frame's uploads must be done
+    hipError_t ew = hipEventSynchronize(t->h2d_done);
+    if (ew != hipSuccess) return map_status(ew);
+
+    // ---- KLT propagation of every live track
+    std::vector<tbd::Track>& tracks = t->tracker->getTracks();
+    int nents = 0, klt_points = 0, klt_pred = 0, hi_slot = 0, lk_points = 0;
+    int64_t lk_iters = 0;
+    for (const auto& kv : t->slot_of) hi_slot = std::max(hi_slot, kv.second + 1);
+    t->preds.clear();
+    if (c.use_klt && t->have_prev && !tracks.empty()) {
+        for (const auto& tr : tracks) {
+            auto it = t->slot_of.find(tr.id);
+            if (it == t->slot_of.end()) continue;
+            const tbd::Rect& b = tr.bboxes.back();
+            t->h_ents[nents++] = FitEntry{it->second, b.x, b.y, b.width, b.height};
+        }
+        tbdk_lk_params lp;
+        lp.win_w = lp.win_h = c.win;
+        lp.max_level = c.max_level;
+        lp.max_count = c.lk_iters;
+        lp.epsilon = c.lk_epsilon;
+        lp.flags = 0;
+        lp.min_eig_threshold = c.min_eig_threshold;
+        lp.impl = 0;
+        rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
+                         reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                         hi_slot * kSlotPts, &lp, t->slot_counts, kSlotPts, stream);
+        if (rc != TBDK_OK) return rc;
+        hipError_t e = hipMemcpyAsync(t->d_ents, t->h_ents, sizeof(FitEntry) * nents, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return map_status(e);
+        int rec = timing_begin(t->ctx, "tbd_fit", s);
+        hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
+                           t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
+        timing_end(t->ctx, rec, s);
+        e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return map_status(e);
+        for (int k = 0; k < nents; ++k) {
+            const FitOut& o = t->h_fit[k];
+            // map back: entries were filled in track order, skipping slotless tracks
+            klt_points += o.n;
+            lk_points += o.npts;
+            lk_iters += o.iters;
+        }
+        int k = 0;
+        for (const auto& tr : tracks) {
+            if (t->slot_of.find(tr.id) == t->slot_of.end()) continue;
+            const FitOut& o = t->h_fit[k++];
+            t->npts_of[tr.id] = o.n;
+            if (o.valid) {
+                t->preds.push_back(tbd::Prediction{tr.id, 1, o.cx, o.cy});
+                klt_pred++;
+            }
+        }
+    }
+
+    // ---- host tracker step (cv::tbd::Tracker::performTrackingStep)
+    t->dets.resize((size_t)ndets);
+    for (int i = 0; i < ndets; ++i) {
+        tbd::Detection& d = t->dets[i];
+        d.id = dets[i].id;
+        d.frame_id = frame_id;
+        d.bbox = tbd::Rect(dets[i].x, dets[i].y, dets[i].width, dets[i].height);
+        d.confidence = dets[i].confidence;
+    }
+    t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size());
+    int nclear = 0;
+    for (unsigned id : t->tracker->deletedIds) {
+        auto it = t->slot_of.find(id);
+        if (it != t->slot_of.end()) {
+            t->free_slots.push(it->second);
+            t->h_clear[nclear++] = it->second;
+            t->slot_of.erase(it);
+        }
+        t->npts_of.erase(id);
+    }
+    if (nclear > 0) {
+        hipError_t e = hipMemcpyAsync(t->d_clear, t->h_clear, sizeof(int) * nclear, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return map_status(e);
+        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, s, t->d_clear, nclear,
+                           t->slot_counts);
+    }
+
+    // ---- corners for new tracks and tracks due for re-detection
+    t->rois.clear();
+    int nroi = 0;
+    if (c.use_klt) {
+        for (const auto& tr : t->tracker->getTracks()) {
+            auto it = t->slot_of.find(tr.id);
+            bool is_new = it == t->slot_of.end();
+            int slot;
+            if (is_new) {
+                if (t->free_slots.empty()) continue;  // slot pool exhausted: track runs on the motion model
+                slot = t->free_slots.top();
+                t->free_slots.pop();
+                t->slot_of[tr.id] = slot;
+            } else {
+                slot = it->second;
+                auto np = t->npts_of.find(tr.id);
+                const int n = np == t->npts_of.end() ? 0 : np->second;
+                if (frame_id % c.redetect_every != 0 && n >= c.min_points) continue;
+            }
+            const tbd::Rect& b = tr.bboxes.back();
+            int x0 = std::max(b.x, 0), y0 = std::max(b.y, 0);
+            int x1 = std::min(b.x + b.width, c.width), y1 = std::min(b.y + b.height, c.height);
+            if (x1 - x0 < 3 || y1 - y0 < 3) {  // nothing to detect in: empty point set
+                t->rois.push_back(tbdk_roi{0, 0, 1, 1});
+            } else {
+                t->rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+            }
+            t->h_roi_slot[nroi++] = slot;
+            t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
+        }
+    }
+    if (nroi > 0) {
+        tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
+        const tbdk_level& L0 = P.lv[0];
+        rc = tbdk_gftt_rois(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, c.width, c.height, L0.pitch,
+                            t->rois.data(), nroi, &gp, reinterpret_cast<float*>(t->d_corners), t->d_ccounts, stream);
+        if (rc != TBDK_OK) return rc;
+        hipError_t e = hipMemcpyAsync(t->d_roi_slot, t->h_roi_slot, sizeof(int) * nroi, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return map_status(e);
+        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, s, t->d_corners, t->d_ccounts,
+                           t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
+        e = hipGetLastError();
+        if (e != hipSuccess) return map_status(e);
+    }
+    {
+        hipError_t e = hipEventRecord(t->h2d_done, s);
+        if (e != hipSuccess) return map_status(e);
+    }
+    t->cur ^= 1;
+    t->have_prev = true;
+
+    if (metrics) {
+        const tbd::Tracker& tk = *t->tracker;
+        metrics->tp = tk.truePositives.back();
+        metrics->fn = tk.falseNegatives.back();
+        metrics->fp = tk.falsePositives.back();
+        metrics->gt = tk.groundTruths.back();
+        metrics->matches = tk.numMatches.back();
+        metrics->bbox_overlap = tk.bboxOverlap.back();
+        metrics->ntracks = (int)t->tracker->getTracks().size();
+        metrics->klt_points = klt_points;
+        metrics->lk_points = lk_points;
+        metrics->lk_iters = lk_iters;
+        metrics->pad_ = 0;
+        metrics->klt_predicted = klt_pred;
+        metrics->redetected = nroi;
+    }
+    return TBDK_OK;
+}
+
+int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
+{
+    if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
+    const auto& tracks = t->tracker->getTracks();
+    std::vector<int32_t> counts((size_t)t->cfg.max_tracks);
+    hipError_t e = hipMemcpy(counts.data(), t->slot_counts, sizeof(int32_t) * counts.size(), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return map_status(e);
+    int k = 0;
+    for (const auto& tr : tracks) {
+        if (k >= cap) break;
+        tbdk_track_info& o = out[k++];
+        const tbd::Rect& b = tr.bboxes.back();
+        o.id = tr.id;
+        o.x = b.x;
+        o.y = b.y;
+        o.width = b.width;
+        o.height = b.height;
+        o.pred_x = tr.predPosition.x;
+        o.pred_y = tr.predPosition.y;
+        o.pred_w = tr.predPosition.width;
+        o.pred_h = tr.predPosition.height;
+        o.age = (int32_t)tr.age;
+        o.total_visible = (int32_t)tr.totalVisibleCount;
+        auto it = t->slot_of.find(tr.id);
+        o.npoints = it == t->slot_of.end() ? 0 : counts[(size_t)it->second];
+        o.max_confidence = tr.maxConfidence;
+        o.bbox_overlap = tr.bboxOverlap;
+    }
+    *n = (int)tracks.size();
+    return TBDK_OK;
+}
+
+}  // extern "C"

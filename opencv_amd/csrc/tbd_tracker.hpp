@@ -1,0 +1,116 @@
+// tbd_tracker.hpp — native restatement of the reference's cv::tbd tracker
+// (modules/trackingbydetection/include/opencv2/tbd.hpp:25-184,
+//  modules/trackingbydetection/src/tbd.cpp:52-1106).
+//
+// The bookkeeping is bit-exact with the reference (Rect rounding, integer
+// box averaging, the padded-square assignment solver with its 1e-8 zero test,
+// lifecycle thresholds, the 1280x720 out-of-bounds filter), but the data
+// layout is built for a per-frame hot loop: per-track history is kept as the
+// bounded windows the algorithm reads (last 4 boxes, last 2 frames, last
+// timeWindowSize scores) instead of ever-growing vectors, tracks are not
+// copied every frame, and the cost matrix is one flat array.
+//
+// Track::motionModel (tbd.hpp:111) is the hook the KLT path plugs into: a
+// per-track predicted centroid computed on the GPU (affine fit of the track's
+// tracked corners) replaces the constant-velocity model when it is valid.
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <vector>
+
+namespace tbdk {
+namespace tbd {
+
+struct Rect {
+    int x = 0, y = 0, width = 0, height = 0;
+    Rect() = default;
+    Rect(int x_, int y_, int w_, int h_) : x(x_), y(y_), width(w_), height(h_) {}
+    int area() const { return width * height; }
+};
+
+// cv::Rect(Point2d, Size): the point is converted with cvRound (round half to
+// even, core/include/opencv2/core/types.hpp:1175-1178, fast_math.hpp:101-106)
+Rect rect_from_point2d(double px, double py, int w, int h);
+
+struct TbdArgs {  // cv::tbd::TbdArgs (tbd.hpp:25-41); defaults of samples/gpu/tbd.cpp:249-254
+    double costOfNonAssignment = 10.0;
+    unsigned timeWindowSize = 16;
+    unsigned trackAgeThreshold = 4;
+    double trackVisibilityThreshold = 0.3;
+    double trackConfidenceThreshold = 0.2;
+    bool shouldStoreMetrics = true;
+    // filterTracksOutOfBounds(0, 1280, 0, 720) is hard-coded in the reference
+    // (tbd.cpp:218, "TAMERT HACK" :317); kept as the default for bit-exactness
+    int boundsXmin = 0, boundsXmax = 1280, boundsYmin = 0, boundsYmax = 720;
+};
+
+struct Detection {  // cv::tbd::Detection (tbd.hpp:69-83)
+    int id = -1;
+    int frame_id = 0;
+    Rect bbox;
+    double confidence = 1.0;
+};
+
+struct Track {  // cv::tbd::Track (tbd.hpp:89-114) with bounded history
+    unsigned id = 0;
+    std::deque<Rect> bboxes;    // last <= 4 boxes (updateAssignedTracks reads 4)
+    std::deque<int> frames;     // last <= 2 frame ids (motion model reads 2)
+    std::deque<double> scores;  // last <= timeWindowSize scores
+    unsigned age = 1, totalVisibleCount = 1;
+    double maxConfidence = 0, avgConfidence = 0;
+    Rect predPosition;
+    double bboxOverlap = 1.0;
+    int64_t historyLength = 1;  // number of boxes the reference vector would hold
+    int slot = -1;              // GPU point-set slot (product bookkeeping, not in the reference)
+};
+
+// predicted centroid supplied by the KLT box propagation (per track id)
+struct Prediction {
+    unsigned id;
+    int valid;
+    double cx, cy;
+};
+
+class Tracker {
+public:
+    explicit Tracker(const TbdArgs& args);
+    void reset();
+    unsigned getNextTrackId() { return nextTrackId++; }
+    std::vector<Track>& getTracks() { return tracks; }
+
+    // Tracker::performTrackingStep (tbd.cpp:210-286).  preds (may be null)
+    // override the motion model for the tracks they name.
+    void performTrackingStep(std::vector<Detection>& dets, int frame_id, const Prediction* preds = nullptr,
+                             int npreds = 0);
+
+    // per-frame metrics (tbd.hpp:145-151)
+    std::vector<int> truePositives, falseNegatives, falsePositives, groundTruths, numMatches;
+    std::vector<double> bboxOverlap;
+    // product-side bookkeeping of the last step (for the GPU point sets)
+    std::vector<unsigned> createdIds;  // tracks created this step
+    std::vector<unsigned> deletedIds;  // tracks removed this step (filtered or lost)
+    std::vector<int> lastAssignments;  // per track (after filtering), -1 unassigned
+
+private:
+    TbdArgs args;
+    unsigned nextTrackId = 0;
+    std::vector<Track> tracks;
+    std::vector<double> cost;  // flat n x n cost matrix
+    std::vector<unsigned> assignmentPerRow;
+
+    void predictNewLocationsOfTracks(int frame_id, const Prediction* preds, int npreds);
+    void filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax);
+    void solveAssignment(std::vector<Detection>& dets, std::vector<int>& assignments,
+                         std::vector<unsigned>& unassignedTracks, std::vector<unsigned>& unassignedDetections);
+    void updateAssignedTracks(std::vector<Detection>& dets, const std::vector<int>& assignments);
+    void updateUnassignedTracks(const std::vector<unsigned>& unassignedTracks, int frame_id);
+    void deleteLostTracks();
+    void createNewTracks(std::vector<Detection>& dets, const std::vector<unsigned>& unassignedDetections);
+    void updateTrackConfidence(Track& t);
+};
+
+double computeBoundingBoxOverlap(const Rect& a, const Rect& b);  // tbd.cpp:1085-1106
+
+}  // namespace tbd
+}  // namespace tbdk

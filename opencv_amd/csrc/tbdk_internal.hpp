@@ -65,6 +65,10 @@ struct LkLevel {
 
 struct LkArgs {
     LkLevel lv[TBDK_MAX_LEVELS];
+    // optional segmented layout: point i = seg * seg_stride + j is valid iff
+    // j < seg_counts[seg]; invalid points are skipped (outputs untouched)
+    const int32_t* seg_counts;
+    int seg_stride;
     int max_level, win_w, win_h, max_count, flags, n;
     double eps2;
     float min_eig;
@@ -74,6 +78,12 @@ struct LkArgs {
     float* err;
     int32_t* iters;
 };
+
+// argument checking + kernel choice shared by tbdk_lk_sparse and the TBD loop
+int lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts, float* next_pts,
+                uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
+                const int32_t* seg_counts, int seg_stride, void* stream);
+int map_status(hipError_t e);
 
 size_t lk_smem_bytes(int win_w, int win_h);
 hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);

@@ -1,0 +1,80 @@
+"""Host mirror of the reference's tracking-by-detection loop over libtbdk.
+
+`TbdLoop` is one video stream on one GPU: the tracking section of
+samples/gpu/tbd.cpp:624-706 (cv::tbd::Tracker::performTrackingStep,
+modules/trackingbydetection/src/tbd.cpp:210-286) with the KLT box
+propagation (pyramid, GFTT, PyrLK, similarity fit) feeding Track::motionModel
+(tbd.hpp:111).  Everything runs in libtbdk.so: HIP kernels for the image work,
+native C++ for the tracker bookkeeping.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .klt import Context, _stream_ptr
+
+
+def default_config(width: int, height: int, **overrides) -> _lib.TbdConfig:
+    lib = _lib.load()
+    cfg = _lib.TbdConfig()
+    _lib.check(lib.tbdk_tbd_default_config(int(width), int(height), C.byref(cfg)), "tbdk_tbd_default_config")
+    for k, v in overrides.items():
+        if not hasattr(cfg, k):
+            raise _lib.TbdkError(f"unknown TBD config field {k}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+def detections_from_gt(gt_frame) -> list[tuple]:
+    """GT rows {valid, x, y, w, h} -> detections (id = object index, confidence 1.0),
+    as parseDetections builds them from a ground-truth file (samples/gpu/tbd.cpp:1297-1340)."""
+    out = []
+    for oid, row in enumerate(gt_frame.tolist()):
+        if row[0]:
+            out.append((oid, row[1], row[2], row[3], row[4], 1.0))
+    return out
+
+
+class TbdLoop:
+    def __init__(self, cfg: _lib.TbdConfig, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or Context.get(device)
+        self.cfg = cfg
+        h = C.c_void_p()
+        _lib.check(self.ctx.lib.tbdk_tbd_create(self.ctx.handle, C.byref(cfg), C.byref(h)), "tbdk_tbd_create")
+        self.handle = h
+        self._dets = (_lib.Detection * 4096)()
+
+    def step(self, frame: torch.Tensor, frame_id: int, dets, stream=None) -> _lib.FrameMetrics:
+        if frame.dtype != torch.uint8 or frame.dim() != 2 or not frame.is_cuda or frame.stride(1) != 1:
+            raise _lib.TbdkError("frame must be a 2-D uint8 device tensor")
+        n = len(dets)
+        if n > len(self._dets):
+            self._dets = (_lib.Detection * (2 * n))()
+        for i, (oid, x, y, w, h, conf) in enumerate(dets):
+            d = self._dets[i]
+            d.id, d.x, d.y, d.width, d.height, d.confidence = oid, x, y, w, h, conf
+        m = _lib.FrameMetrics()
+        _lib.check(self.ctx.lib.tbdk_tbd_step(self.handle, C.c_void_p(frame.data_ptr()), int(frame.stride(0)),
+                                              int(frame_id), self._dets, n, C.byref(m), _stream_ptr(stream)),
+                   "tbdk_tbd_step")
+        return m
+
+    def tracks(self):
+        cap = 4096
+        arr = (_lib.TrackInfo * cap)()
+        n = C.c_int()
+        _lib.check(self.ctx.lib.tbdk_tbd_tracks(self.handle, arr, cap, C.byref(n)), "tbdk_tbd_tracks")
+        keys = [f[0] for f in _lib.TrackInfo._fields_]
+        return [{k: getattr(arr[i], k) for k in keys} for i in range(min(n.value, cap))]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.ctx.lib.tbdk_tbd_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
