@@ -7,18 +7,24 @@
 // evaluation order documented in oracle/gftt_oracle.c; built with
 // -ffp-contract=off so every expression rounds exactly as written.
 //
-// Three launches, all ROIs batched in each (one frame's re-detect set):
-//   1. gftt_cov   : one thread per ROI pixel: Sobel 3x3 (reflect-101 inside the
-//                   ROI) -> cov = (Dx^2, DxDy, Dy^2), three float planes
-//   2. gftt_eig   : one thread per ROI column: boxFilter 3x3 with the reference's
-//                   double row sums and running column sum walked top to bottom,
-//                   min eigenvalue, per-ROI max (ordered-int atomicMax)
+// Three launches, all ROIs of a frame batched in each:
+//   1. gftt_rowsum: one thread per ROI pixel: Sobel 3x3 (reflect-101 inside
+//                   the ROI) at x-1, x, x+1 -> cov = (Dx^2, DxDy, Dy^2) ->
+//                   the boxFilter's horizontal sums in double (RowSum ksize 3,
+//                   box_filter.simd.hpp:84-89), three double planes
+//   2. gftt_eig   : one thread per ROI column: the reference's running column
+//                   sum (ColumnSum, box_filter.simd.hpp:176-273) walked top to
+//                   bottom — loads of 8 rows are issued ahead of the dependent
+//                   add chain — then the min eigenvalue and a per-ROI max
 //   3. gftt_select: one 256-thread workgroup per ROI: threshold-to-zero at
 //                   max*q, 3x3 non-max test, candidates compacted into LDS,
-//                   bitonic sort by (value desc, address desc) — the reference's
-//                   deterministic tie-break (featureselect.cpp:56-64) — then the
-//                   greedy min-distance walk by one wave with wave-parallel
-//                   distance tests against the accepted set.
+//                   bitonic sort by (value desc, address desc) — the
+//                   reference's deterministic tie-break (featureselect.cpp:56-64)
+//                   — then the greedy min-distance walk (:421-503) by one wave,
+//                   64 candidates per step: each lane tests its candidate
+//                   against the accepted list, in-batch conflicts become a
+//                   64-bit mask, and a scalar pass over the lanes in order
+//                   accepts exactly what the sequential walk would.
 #include <cfloat>
 
 #include "tbdk_internal.hpp"
@@ -46,22 +52,20 @@ __device__ __forceinline__ int fkey(float f)
 }
 __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
-}  // namespace
+struct Cov {
+    float c0, c1, c2;
+};
 
-__global__ __launch_bounds__(256) void gftt_cov_kernel(GfttArgs a)
+// Sobel (deriv.cpp:414-465 -> sepFilter2D) of ROI column x, row y, then cov
+__device__ __forceinline__ Cov sobel_cov(const uint8_t* img, int pitch, const GfttRoi& R, int x, int y)
 {
-    const int r = blockIdx.y;
-    const GfttRoi R = a.rois[r];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= R.w * R.h) return;
-    const int y = p / R.w, x = p - y * R.w;
     const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
     const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
     const int xl = refl(x - 1, R.w), xr = refl(x + 1, R.w);
     float rx[3], ry[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const uint8_t* s = a.img + (size_t)(R.y + refl(y + j - 1, R.h)) * a.pitch + R.x;
+        const uint8_t* s = img + (size_t)(R.y + refl(y + j - 1, R.h)) * pitch + R.x;
         const float s0 = s[xl], s1 = s[x], s2 = s[xr];
         float t = -1.f * s0;
         t = t + 0.f * s1;
@@ -74,66 +78,94 @@ __global__ __launch_bounds__(256) void gftt_cov_kernel(GfttArgs a)
     }
     const float dx = (rx[0] + rx[2]) * k + (rx[1] * k2 + 0.f);
     const float dy = (ry[2] - ry[0]) + 0.f;
+    return Cov{dx * dx, dx * dy, dy * dy};
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void gftt_rowsum_kernel(GfttArgs a)
+{
+    const int r = blockIdx.y;
+    const GfttRoi R = a.rois[r];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= R.w * R.h) return;
+    const int y = p / R.w, x = p - y * R.w;
+    const Cov l = sobel_cov(a.img, a.pitch, R, refl(x - 1, R.w), y);
+    const Cov c = sobel_cov(a.img, a.pitch, R, x, y);
+    const Cov q = sobel_cov(a.img, a.pitch, R, refl(x + 1, R.w), y);
     const size_t o = (size_t)R.off + p;
-    a.cov0[o] = dx * dx;
-    a.cov1[o] = dx * dy;
-    a.cov2[o] = dy * dy;
+    a.rs0[o] = (double)l.c0 + (double)c.c0 + (double)q.c0;
+    a.rs1[o] = (double)l.c1 + (double)c.c1 + (double)q.c1;
+    a.rs2[o] = (double)l.c2 + (double)c.c2 + (double)q.c2;
 }
 
 __global__ __launch_bounds__(256) void gftt_eig_kernel(GfttArgs a)
 {
+    constexpr int CH = 8;  // rows loaded ahead of the add chain
     const int r = blockIdx.y;
     const GfttRoi R = a.rois[r];
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= R.w) return;
-    const int xl = refl(x - 1, R.w), xr = refl(x + 1, R.w);
-    const float* c0 = a.cov0 + R.off;
-    const float* c1 = a.cov1 + R.off;
-    const float* c2 = a.cov2 + R.off;
-    auto rowsum = [&](int yy, double& s0, double& s1, double& s2) {
-        const size_t b = (size_t)refl(yy, R.h) * R.w;
-        s0 = (double)c0[b + xl] + (double)c0[b + x] + (double)c0[b + xr];
-        s1 = (double)c1[b + xl] + (double)c1[b + x] + (double)c1[b + xr];
-        s2 = (double)c2[b + xl] + (double)c2[b + x] + (double)c2[b + xr];
-    };
-    double m0, m1, m2, n0, n1, n2, S0, S1, S2;
-    rowsum(-1, m0, m1, m2);
-    S0 = 0.0 + m0;
-    S1 = 0.0 + m1;
-    S2 = 0.0 + m2;
-    rowsum(0, n0, n1, n2);
-    S0 = S0 + n0;
-    S1 = S1 + n1;
-    S2 = S2 + n2;
+    const double* p0 = a.rs0 + R.off + x;
+    const double* p1 = a.rs1 + R.off + x;
+    const double* p2 = a.rs2 + R.off + x;
+    float* E = a.eig + R.off + x;
+    const size_t W = (size_t)R.w;
+    // ColumnSum: SUM = 0 + row(-1), SUM += row(0); per output y:
+    // s = SUM + row(y+1); out = (float)s; SUM = s - row(y-1)
+    const int rm1 = refl(-1, R.h);
+    double m1_0 = p0[rm1 * W], m1_1 = p1[rm1 * W], m1_2 = p2[rm1 * W];  // row y-1
+    double m0_0 = p0[0], m0_1 = p1[0], m0_2 = p2[0];                    // row y
+    double S0 = 0.0 + m1_0, S1 = 0.0 + m1_1, S2 = 0.0 + m1_2;
+    S0 = S0 + m0_0;
+    S1 = S1 + m0_1;
+    S2 = S2 + m0_2;
     int best = INT_MIN;
-    for (int y = 0; y < R.h; ++y) {
-        double p0, p1, p2;
-        rowsum(y + 1, p0, p1, p2);  // entering row
-        double q0, q1, q2;
-        rowsum(y - 1, q0, q1, q2);  // leaving row
-        const double t0 = S0 + p0, t1 = S1 + p1, t2 = S2 + p2;
-        const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
-        S0 = t0 - q0;
-        S1 = t1 - q1;
-        S2 = t2 - q2;
-        const float t = aa - cc;
-        const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-        a.eig[(size_t)R.off + (size_t)y * R.w + x] = e;
-        const int kk = fkey(e);
-        best = kk > best ? kk : best;
+    for (int y0 = 0; y0 < R.h; y0 += CH) {
+        double q0[CH], q1[CH], q2[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {  // independent loads of rows y0+1 .. y0+CH
+            const int yy = y0 + k + 1;
+            const size_t row = (size_t)refl(yy < R.h + 1 ? yy : R.h, R.h) * W;
+            q0[k] = p0[row];
+            q1[k] = p1[row];
+            q2[k] = p2[row];
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int y = y0 + k;
+            if (y < R.h) {
+                const double t0 = S0 + q0[k], t1 = S1 + q1[k], t2 = S2 + q2[k];
+                S0 = t0 - m1_0;
+                S1 = t1 - m1_1;
+                S2 = t2 - m1_2;
+                m1_0 = m0_0;
+                m1_1 = m0_1;
+                m1_2 = m0_2;
+                m0_0 = q0[k];
+                m0_1 = q1[k];
+                m0_2 = q2[k];
+                const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
+                const float t = aa - cc;
+                const float e = (aa + cc) - sqrtf(bb * bb + t * t);
+                E[(size_t)y * W] = e;
+                const int kk = fkey(e);
+                best = kk > best ? kk : best;
+            }
+        }
     }
     atomicMax(&a.roi_max[r], best);
 }
 
 struct Cand {
     float v;
-    int idx;
+    int key;  // (y << 16) | x : same order as the reference's address tie-break
 };
 
 // a before b in the reference order: value desc, then address desc
 __device__ __forceinline__ bool cand_before(const Cand& a, const Cand& b)
 {
-    return a.v > b.v || (a.v == b.v && a.idx > b.idx);
+    return a.v > b.v || (a.v == b.v && a.key > b.key);
 }
 
 __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
@@ -150,8 +182,7 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
     const float maxv = fkey_inv(a.roi_max[r]);
     const float thr = (float)((double)maxv * a.quality);
     const float* E = a.eig + R.off;
-    // threshold-to-zero + 3x3 dilate-equal test on interior pixels
-    auto ev = [&](int yy, int xx) {
+    auto ev = [&](int yy, int xx) {  // threshold-to-zero (THRESH_TOZERO)
         const float v = E[(size_t)yy * R.w + xx];
         return v > thr ? v : 0.f;
     };
@@ -168,9 +199,9 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
                 const float q = ev(y + dy, x + dx);
                 m = q > m ? q : m;
             }
-        if (v == m) {
+        if (v == m) {  // dilate(3x3) equality
             const int slot = atomicAdd(&s_count, 1);
-            if (slot < a.cap) cand[slot] = Cand{v, y * R.w + x};
+            if (slot < a.cap) cand[slot] = Cand{v, (y << 16) | x};
         }
     }
     __syncthreads();
@@ -183,14 +214,13 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
     while (np2 < total) np2 <<= 1;
     for (int i = total + tid; i < np2; i += blockDim.x) cand[i] = Cand{-FLT_MAX, -1};
     __syncthreads();
-    // bitonic sort, "before" order first
-    for (int k = 2; k <= np2; k <<= 1) {
+    for (int k = 2; k <= np2; k <<= 1) {  // bitonic sort, "before" order first
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = tid; i < np2; i += blockDim.x) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
                     const bool up = (i & k) == 0;
-                    Cand ci = cand[i], cj = cand[ixj];
+                    const Cand ci = cand[i], cj = cand[ixj];
                     const bool swap = up ? cand_before(cj, ci) : cand_before(ci, cj);
                     if (swap) {
                         cand[i] = cj;
@@ -201,38 +231,60 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
             __syncthreads();
         }
     }
-    // greedy selection (featureselect.cpp:421-503) by wave 0
-    if (tid < 64) {
-        const int lane = tid;
-        int n = 0;
-        const bool use_dist = a.min_distance >= 1.0;
-        const double md2 = a.min_distance * a.min_distance;
-        float2* out = a.corners + (size_t)r * a.max_corners;
-        for (int i = 0; i < total; ++i) {
-            const int idx = cand[i].idx;
-            const int y = idx / R.w, x = idx - y * R.w;
-            bool good = true;
-            if (use_dist) {
-                bool conflict = false;
-                for (int q = lane; q < n; q += 64) {
-                    const float dx = (float)x - acc[q].x, dy = (float)y - acc[q].y;
-                    conflict |= (double)(dx * dx + dy * dy) < md2;
-                }
-                good = __ballot(conflict) == 0ull;
+    if (tid >= 64) return;
+    // ---- greedy walk in sorted order, 64 candidates per step (wave 0)
+    const int lane = tid;
+    const bool use_dist = a.min_distance >= 1.0;
+    const double md2 = a.min_distance * a.min_distance;
+    const int maxc = a.max_corners;
+    float2* out = a.corners + (size_t)r * maxc;
+    int n = 0;
+    bool done = false;
+    for (int i0 = 0; i0 < total && !done; i0 += 64) {
+        const int i = i0 + lane;
+        const bool valid = i < total;
+        const int key = valid ? cand[i].key : 0;
+        const float fx = (float)(key & 0xFFFF), fy = (float)(key >> 16);
+        bool good = valid;
+        unsigned long long cm = 0ull;
+        if (use_dist) {
+            for (int q = 0; q < n; ++q) {  // vs corners accepted in earlier steps
+                const float2 p = acc[q];
+                const float dx = fx - p.x, dy = fy - p.y;
+                good = good && !((double)(dx * dx + dy * dy) < md2);
             }
-            if (good) {
-                if (lane == 0) {
-                    acc[n] = make_float2((float)x, (float)y);
-                    out[n] = make_float2((float)(x + R.x), (float)(y + R.y));
-                }
-                n++;
-                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): acc[n-1] visible to all lanes
-                __builtin_amdgcn_wave_barrier();
-                if (a.max_corners > 0 && n == a.max_corners) break;
+            for (int j = 0; j < 64; ++j) {  // vs earlier candidates of this step
+                const float xj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(fx), j));
+                const float yj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(fy), j));
+                const float dx = fx - xj, dy = fy - yj;
+                if (j < lane && (double)(dx * dx + dy * dy) < md2) cm |= 1ull << j;
             }
         }
-        if (lane == 0) a.counts[r] = n;
+        const unsigned long long goodm = __ballot(good);
+        unsigned long long accm = 0ull;
+        int cnt = n;
+        for (int k = 0; k < 64; ++k) {  // uniform scalar pass: the sequential acceptance
+            if (!((goodm >> k) & 1ull)) continue;
+            const unsigned long long ck =
+                ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(cm >> 32), k) << 32) |
+                (unsigned)__builtin_amdgcn_readlane((int)(unsigned)cm, k);
+            if (ck & accm) continue;
+            accm |= 1ull << k;
+            if (++cnt == maxc) {
+                done = true;
+                break;
+            }
+        }
+        if ((accm >> lane) & 1ull) {
+            const int pos = n + __popcll(accm & ((1ull << lane) - 1ull));
+            acc[pos] = make_float2(fx, fy);
+            out[pos] = make_float2(fx + (float)R.x, fy + (float)R.y);
+        }
+        n = cnt;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): acc[] visible to the next step
+        __builtin_amdgcn_wave_barrier();
     }
+    if (lane == 0) a.counts[r] = n;
 }
 
 size_t gftt_select_smem(int cap, int max_corners)
@@ -242,10 +294,10 @@ size_t gftt_select_smem(int cap, int max_corners)
 
 hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(a.roi_max, 0x80, sizeof(int) * a.nroi, s);  // INT_MIN-ish keys
+    hipError_t e = hipMemsetAsync(a.roi_max, 0x80, sizeof(int) * a.nroi, s);  // very negative keys
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gftt_cov_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3((max_w + 255) / 256, a.nroi), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gftt_rowsum_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gftt_eig_kernel, dim3((max_w + 63) / 64, a.nroi), dim3(64), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),

@@ -335,7 +335,7 @@ int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
         if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
         ctx->gftt_planes = nullptr;
         ctx->gftt_cap_px = 0;
-        hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_planes), sizeof(float) * 4 * (size_t)max_total_pixels);
+        hipError_t e = hipMalloc(&ctx->gftt_planes, (sizeof(double) * 3 + sizeof(float)) * (size_t)max_total_pixels);
         if (e != hipSuccess) return map_err(e);
         ctx->gftt_cap_px = max_total_pixels;
     }
@@ -375,10 +375,10 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     a.pitch = pitch;
     a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
     a.nroi = nroi;
-    a.cov0 = ctx->gftt_planes;
-    a.cov1 = ctx->gftt_planes + ctx->gftt_cap_px;
-    a.cov2 = ctx->gftt_planes + 2 * ctx->gftt_cap_px;
-    a.eig = ctx->gftt_planes + 3 * ctx->gftt_cap_px;
+    a.rs0 = static_cast<double*>(ctx->gftt_planes);
+    a.rs1 = a.rs0 + ctx->gftt_cap_px;
+    a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
+    a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
     a.roi_max = ctx->gftt_max;
     a.cap = 16384;
     a.max_corners = p->max_corners;

@@ -36,7 +36,7 @@ struct tbdk_ctx {
     // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
     void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
     int* gftt_max = nullptr;     // int[cap_rois]
-    float* gftt_planes = nullptr;  // 4 x cap_px floats: cov0, cov1, cov2, eig
+    void* gftt_planes = nullptr;  // 3 x cap_px doubles (row sums) + cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
 };
@@ -110,9 +110,9 @@ struct GfttArgs {
     int pitch;
     const GfttRoi* rois;
     int nroi;
-    float* cov0;
-    float* cov1;
-    float* cov2;
+    double* rs0;  // boxFilter horizontal sums of (Dx^2, DxDy, Dy^2), per ROI pixel
+    double* rs1;
+    double* rs2;
     float* eig;
     int* roi_max;
     int cap;  // LDS candidate capacity per ROI (power of two)
