@@ -174,10 +174,17 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
     int& s_count = *reinterpret_cast<int*>(smem);  // all LDS in the one dynamic region
     Cand* cand = reinterpret_cast<Cand*>(smem + 16);
     float2* acc = reinterpret_cast<float2*>(smem + 16 + sizeof(Cand) * a.cap);
+    uint32_t* occ = reinterpret_cast<uint32_t*>(smem + 16 + sizeof(Cand) * a.cap +
+                                                sizeof(float2) * (size_t)a.max_corners);
     const int r = blockIdx.x;
     const GfttRoi R = a.rois[r];
     const int tid = threadIdx.x;
+    // occupancy bitmap of accepted corners (1 bit per ROI pixel), if it fits
+    const int ow = (R.w + 31) / 32 + 1;  // words per row (+1: two-word window reads)
+    const bool use_occ = (size_t)ow * R.h * 4 <= (size_t)a.occ_bytes;
     if (tid == 0) s_count = 0;
+    if (use_occ)
+        for (int i = tid; i < ow * R.h; i += blockDim.x) occ[i] = 0u;
     __syncthreads();
     const float maxv = fkey_inv(a.roi_max[r]);
     const float thr = (float)((double)maxv * a.quality);
@@ -186,22 +193,23 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
         const float v = E[(size_t)yy * R.w + xx];
         return v > thr ? v : 0.f;
     };
-    const int iw = R.w - 2, ih = R.h - 2;
-    for (int p = tid; p < (iw > 0 && ih > 0 ? iw * ih : 0); p += blockDim.x) {
-        const int y = p / iw + 1, x = p % iw + 1;
-        const float v = ev(y, x);
-        if (v == 0.f) continue;
-        float m = v;
+    // interior 3x3 local maxima (dilate-equal), row by row: no integer division
+    for (int y = 1; y < R.h - 1; ++y) {
+        for (int x = 1 + tid; x < R.w - 1; x += blockDim.x) {
+            const float v = ev(y, x);
+            if (v == 0.f) continue;
+            float m = v;
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
+            for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                const float q = ev(y + dy, x + dx);
-                m = q > m ? q : m;
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const float q = ev(y + dy, x + dx);
+                    m = q > m ? q : m;
+                }
+            if (v == m) {
+                const int slot = atomicAdd(&s_count, 1);
+                if (slot < a.cap) cand[slot] = Cand{v, (y << 16) | x};
             }
-        if (v == m) {  // dilate(3x3) equality
-            const int slot = atomicAdd(&s_count, 1);
-            if (slot < a.cap) cand[slot] = Cand{v, (y << 16) | x};
         }
     }
     __syncthreads();
@@ -236,6 +244,9 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
     const int lane = tid;
     const bool use_dist = a.min_distance >= 1.0;
     const double md2 = a.min_distance * a.min_distance;
+    int rad = (int)ceil(a.min_distance) - 1;  // |d| <= rad can be closer than min_distance
+    if ((double)(rad + 1) * (rad + 1) < md2) rad++;
+    const bool occ_ok = use_occ && rad <= 31;
     const int maxc = a.max_corners;
     float2* out = a.corners + (size_t)r * maxc;
     int n = 0;
@@ -244,14 +255,35 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
         const int i = i0 + lane;
         const bool valid = i < total;
         const int key = valid ? cand[i].key : 0;
-        const float fx = (float)(key & 0xFFFF), fy = (float)(key >> 16);
+        const int ix = key & 0xFFFF, iy = key >> 16;
+        const float fx = (float)ix, fy = (float)iy;
         bool good = valid;
         unsigned long long cm = 0ull;
         if (use_dist) {
-            for (int q = 0; q < n; ++q) {  // vs corners accepted in earlier steps
-                const float2 p = acc[q];
-                const float dx = fx - p.x, dy = fy - p.y;
-                good = good && !((double)(dx * dx + dy * dy) < md2);
+            if (occ_ok) {  // accepted corners within the window, exact distance test
+                for (int dy = -rad; dy <= rad && good; ++dy) {
+                    const int yy = iy + dy;
+                    if (yy < 0 || yy >= R.h) continue;
+                    const int x0 = ix - rad < 0 ? 0 : ix - rad;
+                    const int x1 = ix + rad >= R.w ? R.w - 1 : ix + rad;
+                    for (int wx = x0 >> 5; wx <= (x1 >> 5) && good; ++wx) {
+                        uint32_t bits = occ[yy * ow + wx];
+                        while (bits && good) {
+                            const int b = __builtin_ctz(bits);
+                            bits &= bits - 1u;
+                            const int xx = (wx << 5) + b;
+                            if (xx < x0 || xx > x1) continue;
+                            const float ddx = fx - (float)xx, ddy = fy - (float)yy;
+                            if ((double)(ddx * ddx + ddy * ddy) < md2) good = false;
+                        }
+                    }
+                }
+            } else {
+                for (int q = 0; q < n; ++q) {  // vs corners accepted in earlier steps
+                    const float2 p = acc[q];
+                    const float dx = fx - p.x, dy = fy - p.y;
+                    good = good && !((double)(dx * dx + dy * dy) < md2);
+                }
             }
             for (int j = 0; j < 64; ++j) {  // vs earlier candidates of this step
                 const float xj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(fx), j));
@@ -279,17 +311,19 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
             const int pos = n + __popcll(accm & ((1ull << lane) - 1ull));
             acc[pos] = make_float2(fx, fy);
             out[pos] = make_float2(fx + (float)R.x, fy + (float)R.y);
+            if (occ_ok) atomicOr(&occ[iy * ow + (ix >> 5)], 1u << (ix & 31));
         }
         n = cnt;
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): acc[] visible to the next step
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): acc[] / occ[] visible to the next step
         __builtin_amdgcn_wave_barrier();
     }
     if (lane == 0) a.counts[r] = n;
 }
 
-size_t gftt_select_smem(int cap, int max_corners)
+size_t gftt_select_smem(int cap, int max_corners, int occ_bytes)
 {
-    return 16 + sizeof(Cand) * (size_t)cap + sizeof(float2) * (size_t)(max_corners > 0 ? max_corners : cap);
+    return 16 + sizeof(Cand) * (size_t)cap + sizeof(float2) * (size_t)(max_corners > 0 ? max_corners : cap) +
+           (size_t)occ_bytes;
 }
 
 hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s)
@@ -298,7 +332,7 @@ hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_rowsum_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
     hipLaunchKernelGGL(gftt_eig_kernel, dim3((max_w + 63) / 64, a.nroi), dim3(64), 0, s, a);
-    const size_t smem = gftt_select_smem(a.cap, a.max_corners);
+    const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.occ_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);

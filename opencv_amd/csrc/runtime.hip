@@ -386,7 +386,11 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     a.min_distance = p->min_distance;
     a.corners = reinterpret_cast<float2*>(corners);
     a.counts = counts;
-    if (gftt_select_smem(a.cap, a.max_corners) > 160 * 1024) return TBDK_EINVAL;
+    {
+        const long budget = 160L * 1024 - (long)gftt_select_smem(a.cap, a.max_corners, 0);
+        if (budget < 0) return TBDK_EINVAL;
+        a.occ_bytes = (int)(budget & ~15L);
+    }
     if (e == hipSuccess) e = launch_gftt(a, max_area, max_w, s);
     timing_end(ctx, rec, s);
     return map_err(e);

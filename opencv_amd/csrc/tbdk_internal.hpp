@@ -115,12 +115,13 @@ struct GfttArgs {
     double* rs2;
     float* eig;
     int* roi_max;
-    int cap;  // LDS candidate capacity per ROI (power of two)
+    int cap;        // LDS candidate capacity per ROI (power of two)
+    int occ_bytes;  // LDS for the accepted-corner occupancy bitmap
     int max_corners;
     double quality, min_distance;
     float2* corners;  // nroi x max_corners
     int32_t* counts;  // nroi (-1: candidate overflow)
 };
-size_t gftt_select_smem(int cap, int max_corners);
+size_t gftt_select_smem(int cap, int max_corners, int occ_bytes);
 hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s);
 }  // namespace tbdk
