@@ -211,6 +211,8 @@ typedef struct tbdk_frame_metrics {  /* per-frame TP/FN/FP/GT/c/sum d (tbd.hpp:1
     int32_t redetected;              /* GFTT ROIs this frame */
     int32_t pad_;
     int64_t lk_iters;                /* Newton iterations over all levels (flop accounting) */
+    float host_wait_us;              /* host time blocked on the device this step */
+    float host_tracker_us;           /* host time in the tracker step (assignment + bookkeeping) */
 } tbdk_frame_metrics;
 
 typedef struct tbdk_track_info {

@@ -168,71 +168,104 @@ __device__ __forceinline__ bool cand_before(const Cand& a, const Cand& b)
     return a.v > b.v || (a.v == b.v && a.key > b.key);
 }
 
-__global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
+// threshold-to-zero at max*q + 3x3 dilate-equality on interior pixels, one
+// thread per ROI pixel; candidates appended to the ROI's global list (the
+// append order is irrelevant: the list is sorted by (value, address) next)
+__global__ __launch_bounds__(256) void gftt_nms_kernel(GfttArgs a)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int& s_count = *reinterpret_cast<int*>(smem);  // all LDS in the one dynamic region
-    Cand* cand = reinterpret_cast<Cand*>(smem + 16);
-    float2* acc = reinterpret_cast<float2*>(smem + 16 + sizeof(Cand) * a.cap);
-    uint32_t* occ = reinterpret_cast<uint32_t*>(smem + 16 + sizeof(Cand) * a.cap +
-                                                sizeof(float2) * (size_t)a.max_corners);
-    const int r = blockIdx.x;
+    __shared__ int lcount, lbase;
+    const int r = blockIdx.y;
     const GfttRoi R = a.rois[r];
-    const int tid = threadIdx.x;
-    // occupancy bitmap of accepted corners (1 bit per ROI pixel), if it fits
-    const int ow = (R.w + 31) / 32 + 1;  // words per row (+1: two-word window reads)
-    const bool use_occ = (size_t)ow * R.h * 4 <= (size_t)a.occ_bytes;
-    if (tid == 0) s_count = 0;
-    if (use_occ)
-        for (int i = tid; i < ow * R.h; i += blockDim.x) occ[i] = 0u;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iw = R.w - 2, ih = R.h - 2;
+    if (iw <= 0 || ih <= 0 || (int)(blockIdx.x * blockDim.x) >= iw * ih) return;  // block-uniform
+    if (threadIdx.x == 0) lcount = 0;
     __syncthreads();
-    const float maxv = fkey_inv(a.roi_max[r]);
-    const float thr = (float)((double)maxv * a.quality);
-    const float* E = a.eig + R.off;
-    auto ev = [&](int yy, int xx) {  // threshold-to-zero (THRESH_TOZERO)
-        const float v = E[(size_t)yy * R.w + xx];
-        return v > thr ? v : 0.f;
-    };
-    // interior 3x3 local maxima (dilate-equal), row by row: no integer division
-    for (int y = 1; y < R.h - 1; ++y) {
-        for (int x = 1 + tid; x < R.w - 1; x += blockDim.x) {
-            const float v = ev(y, x);
-            if (v == 0.f) continue;
+    bool keep = false;
+    float v = 0.f;
+    int key = 0;
+    if (p < iw * ih) {
+        const int y = p / iw + 1, x = p - (y - 1) * iw + 1;
+        const float thr = (float)((double)fkey_inv(a.roi_max[r]) * a.quality);
+        const float* E = a.eig + R.off + (size_t)y * R.w + x;
+        const float v0 = E[0];
+        v = v0 > thr ? v0 : 0.f;
+        if (v != 0.f) {
             float m = v;
 #pragma unroll
             for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
                 for (int dx = -1; dx <= 1; ++dx) {
-                    const float q = ev(y + dy, x + dx);
+                    const float q0 = E[dy * R.w + dx];
+                    const float q = q0 > thr ? q0 : 0.f;
                     m = q > m ? q : m;
                 }
-            if (v == m) {
-                const int slot = atomicAdd(&s_count, 1);
-                if (slot < a.cap) cand[slot] = Cand{v, (y << 16) | x};
-            }
+            keep = v == m;
+            key = (y << 16) | x;
         }
     }
+    // block-aggregated append: one global atomic per block, not per candidate
+    int li = 0;
+    if (keep) li = atomicAdd(&lcount, 1);
     __syncthreads();
-    const int total = s_count;
+    if (threadIdx.x == 0) lbase = lcount ? atomicAdd(&a.cand_count[r], lcount) : 0;
+    __syncthreads();
+    const int slot = lbase + li;
+    if (keep && slot < a.cap) reinterpret_cast<Cand*>(a.cand)[(size_t)r * a.cap + slot] = Cand{v, key};
+}
+
+constexpr int kSelThreads = 512;
+
+__global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Cand* cand = reinterpret_cast<Cand*>(smem);  // all LDS in the one dynamic region
+    float2* acc = reinterpret_cast<float2*>(smem + sizeof(Cand) * a.cap);
+    float2* bxy = acc + a.max_corners;  // this step's 64 candidate positions
+    uint32_t* occ = reinterpret_cast<uint32_t*>(bxy + 64);
+    const int r = blockIdx.x;
+    const GfttRoi R = a.rois[r];
+    const int tid = threadIdx.x;
+    const int total = a.cand_count[r];
     if (total > a.cap) {  // candidate buffer overflow: report, never silently truncate
         if (tid == 0) a.counts[r] = -1;
         return;
     }
+    // occupancy bitmap of accepted corners (1 bit per ROI pixel), if it fits
+    const int ow = (R.w + 31) / 32 + 1;  // words per row (+1: two-word window reads)
+    const bool use_occ = (size_t)ow * R.h * 4 <= (size_t)a.occ_bytes;
+    if (use_occ)
+        for (int i = tid; i < ow * R.h; i += kSelThreads) occ[i] = 0u;
     int np2 = 1;
     while (np2 < total) np2 <<= 1;
-    for (int i = total + tid; i < np2; i += blockDim.x) cand[i] = Cand{-FLT_MAX, -1};
+    const Cand* src = reinterpret_cast<const Cand*>(a.cand) + (size_t)r * a.cap;
+    for (int i = tid; i < np2; i += kSelThreads) cand[i] = i < total ? src[i] : Cand{-FLT_MAX, -1};
     __syncthreads();
-    for (int k = 2; k <= np2; k <<= 1) {  // bitonic sort, "before" order first
+    // bitonic sort, "before" order first; every thread owns np2/2/threads
+    // compare-exchange pairs per stage (branch-free indexing, loads batched)
+    const int npairs = np2 >> 1;
+    for (int k = 2; k <= np2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & k) == 0;
-                    const Cand ci = cand[i], cj = cand[ixj];
-                    const bool swap = up ? cand_before(cj, ci) : cand_before(ci, cj);
+            for (int pb = 0; pb < npairs; pb += kSelThreads * 4) {
+                int ii[4];
+                Cand ci[4], cj[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int pidx = pb + u * kSelThreads + tid;
+                    ii[u] = pidx < npairs ? ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)) : -1;
+                    if (ii[u] >= 0) {
+                        ci[u] = cand[ii[u]];
+                        cj[u] = cand[ii[u] + j];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (ii[u] < 0) continue;
+                    const bool up = (ii[u] & k) == 0;
+                    const bool swap = up ? cand_before(cj[u], ci[u]) : cand_before(ci[u], cj[u]);
                     if (swap) {
-                        cand[i] = cj;
-                        cand[ixj] = ci;
+                        cand[ii[u]] = cj[u];
+                        cand[ii[u] + j] = ci[u];
                     }
                 }
             }
@@ -240,7 +273,7 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
         }
     }
     if (tid >= 64) return;
-    // ---- greedy walk in sorted order, 64 candidates per step (wave 0)
+    // ---- greedy walk in sorted order (featureselect.cpp:421-503), 64 candidates per step
     const int lane = tid;
     const bool use_dist = a.min_distance >= 1.0;
     const double md2 = a.min_distance * a.min_distance;
@@ -260,6 +293,7 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
         bool good = valid;
         unsigned long long cm = 0ull;
         if (use_dist) {
+            bxy[lane] = make_float2(fx, fy);
             if (occ_ok) {  // accepted corners within the window, exact distance test
                 for (int dy = -rad; dy <= rad && good; ++dy) {
                     const int yy = iy + dy;
@@ -280,15 +314,17 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
                 }
             } else {
                 for (int q = 0; q < n; ++q) {  // vs corners accepted in earlier steps
-                    const float2 p = acc[q];
-                    const float dx = fx - p.x, dy = fy - p.y;
+                    const float2 pq = acc[q];
+                    const float dx = fx - pq.x, dy = fy - pq.y;
                     good = good && !((double)(dx * dx + dy * dy) < md2);
                 }
             }
-            for (int j = 0; j < 64; ++j) {  // vs earlier candidates of this step
-                const float xj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(fx), j));
-                const float yj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(fy), j));
-                const float dx = fx - xj, dy = fy - yj;
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll 8
+            for (int j = 0; j < 64; ++j) {  // vs earlier candidates of this step (LDS broadcast reads)
+                const float2 pj = bxy[j];
+                const float dx = fx - pj.x, dy = fy - pj.y;
                 if (j < lane && (double)(dx * dx + dy * dy) < md2) cm |= 1ull << j;
             }
         }
@@ -322,22 +358,23 @@ __global__ __launch_bounds__(256) void gftt_select_kernel(GfttArgs a)
 
 size_t gftt_select_smem(int cap, int max_corners, int occ_bytes)
 {
-    return 16 + sizeof(Cand) * (size_t)cap + sizeof(float2) * (size_t)(max_corners > 0 ? max_corners : cap) +
-           (size_t)occ_bytes;
+    return sizeof(Cand) * (size_t)cap + sizeof(float2) * (size_t)(max_corners + 64) + (size_t)occ_bytes;
 }
 
 hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(a.roi_max, 0x80, sizeof(int) * a.nroi, s);  // very negative keys
+    if (e == hipSuccess) e = hipMemsetAsync(a.cand_count, 0, sizeof(int) * a.nroi, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_rowsum_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
     hipLaunchKernelGGL(gftt_eig_kernel, dim3((max_w + 63) / 64, a.nroi), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(gftt_nms_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.occ_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gftt_select_kernel, dim3(a.nroi), dim3(256), smem, s, a);
+    hipLaunchKernelGGL(gftt_select_kernel, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
     return hipGetLastError();
 }
 

@@ -97,6 +97,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
     if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
     if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
+    if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
     delete ctx;
     return TBDK_OK;
 }
@@ -323,11 +324,16 @@ int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
     if (max_rois > ctx->gftt_cap_rois) {
         if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
         if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
+        if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
         ctx->gftt_rois = nullptr;
         ctx->gftt_max = nullptr;
+        ctx->gftt_cand = nullptr;
         ctx->gftt_cap_rois = 0;
         hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)max_rois);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_max), sizeof(int) * (size_t)max_rois);
+        // roi_max and the candidate counters share one allocation
+        if (e == hipSuccess)
+            e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_max), 2 * sizeof(int) * (size_t)max_rois);
+        if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, kGfttCandBytes * (size_t)max_rois);
         if (e != hipSuccess) return map_err(e);
         ctx->gftt_cap_rois = max_rois;
     }
@@ -380,7 +386,9 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
     a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
     a.roi_max = ctx->gftt_max;
-    a.cap = 16384;
+    a.cand_count = ctx->gftt_max + ctx->gftt_cap_rois;
+    a.cand = ctx->gftt_cand;
+    a.cap = kGfttCap;
     a.max_corners = p->max_corners;
     a.quality = p->quality_level;
     a.min_distance = p->min_distance;

@@ -15,6 +15,7 @@
 //      (every `redetect_every` frames or < min_points corners), written
 //      straight into their point slots                                   [HIP]
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -238,7 +239,8 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (!ctx || !cfg || !out) return TBDK_EINVAL;
     *out = nullptr;
     if (cfg->max_corners <= 0 || cfg->max_corners > kSlotPts || cfg->max_tracks <= 0 || cfg->win < 3 ||
-        cfg->win > 31 || cfg->redetect_every <= 0)
+        cfg->win > 31 || cfg->redetect_every <= 0 || cfg->time_window_size <= 0 ||
+        cfg->time_window_size > (int)tbd::kMaxTimeWindow)
         return TBDK_EINVAL;
     tbdk_tbd* t = new (std::nothrow) tbdk_tbd();
     if (!t) return TBDK_ENOMEM;
@@ -322,7 +324,10 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     (void)hipSetDevice(t->ctx->device);
 
     // pinned staging buffers are rewritten below: the previous frame's uploads must be done
+    using clk = std::chrono::steady_clock;
+    auto tw0 = clk::now();
     hipError_t ew = hipEventSynchronize(t->h2d_done);
+    double wait_us = std::chrono::duration<double, std::micro>(clk::now() - tw0).count();
     if (ew != hipSuccess) return map_status(ew);
 
     // ---- KLT propagation of every live track
@@ -357,7 +362,9 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
         timing_end(t->ctx, rec, s);
         e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
+        auto ts0 = clk::now();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
+        wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);
         for (int k = 0; k < nents; ++k) {
             const FitOut& o = t->h_fit[k];
@@ -387,7 +394,9 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         d.bbox = tbd::Rect(dets[i].x, dets[i].y, dets[i].width, dets[i].height);
         d.confidence = dets[i].confidence;
     }
+    auto tt0 = clk::now();
     t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size());
+    const double tracker_us = std::chrono::duration<double, std::micro>(clk::now() - tt0).count();
     int nclear = 0;
     for (unsigned id : t->tracker->deletedIds) {
         auto it = t->slot_of.find(id);
@@ -471,6 +480,8 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         metrics->pad_ = 0;
         metrics->klt_predicted = klt_pred;
         metrics->redetected = nroi;
+        metrics->host_wait_us = (float)wait_us;
+        metrics->host_tracker_us = (float)tracker_us;
     }
     return TBDK_OK;
 }

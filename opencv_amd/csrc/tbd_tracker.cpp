@@ -71,15 +71,19 @@ static void constant_velocity(const Track& t, int frame_id, double& cx, double& 
 // predictNewLocationsOfTracks (tbd.cpp:288-304) with the KLT hook
 void Tracker::predictNewLocationsOfTracks(int frame_id, const Prediction* preds, int npreds)
 {
+    // first valid prediction per id, looked up by binary search
+    predIndex.clear();
+    for (int k = 0; preds && k < npreds; ++k)
+        if (preds[k].valid) predIndex.push_back(k);
+    std::stable_sort(predIndex.begin(), predIndex.end(),
+                     [&](int a, int b) { return preds[a].id < preds[b].id; });
     for (auto& t : tracks) {
         const Rect& bbox = t.bboxes.back();
         double cx, cy;
         const Prediction* p = nullptr;
-        for (int k = 0; preds && k < npreds; ++k)
-            if (preds[k].id == t.id && preds[k].valid) {
-                p = &preds[k];
-                break;
-            }
+        auto it = std::lower_bound(predIndex.begin(), predIndex.end(), t.id,
+                                   [&](int k, unsigned id) { return preds[k].id < id; });
+        if (it != predIndex.end() && preds[*it].id == t.id) p = &preds[*it];
         if (p) {
             cx = p->cx;
             cy = p->cy;
@@ -93,20 +97,25 @@ void Tracker::predictNewLocationsOfTracks(int frame_id, const Prediction* preds,
 // filterTracksOutOfBounds (tbd.cpp:306-331)
 void Tracker::filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax)
 {
-    std::vector<Track> kept;
-    kept.reserve(tracks.size());
-    for (auto& t : tracks) {
-        const Rect& r = t.predPosition;
+    size_t k = 0;
+    for (size_t i = 0; i < tracks.size(); ++i) {
+        const Rect& r = tracks[i].predPosition;
         if (r.x + r.width < xmin || r.x >= xmax || r.y + r.height < ymin || r.y >= ymax)
-            deletedIds.push_back(t.id);
-        else
-            kept.push_back(std::move(t));
+            deletedIds.push_back(tracks[i].id);
+        else if (k++ != i)
+            tracks[k - 1] = tracks[i];
     }
-    tracks.swap(kept);
+    tracks.resize(k);
 }
 
 // calculateCostMatrix + solveAssignmentProblem + classifyAssignments
-// (tbd.cpp:333-891), flat n x n matrix, zero pattern cached per outer round
+// (tbd.cpp:333-891) on a flat n x n matrix.  The reference's operation order
+// on every matrix entry is kept (row minima, column minima, the step-4
+// subtract/add of mu), so every comparison sees the same doubles; only the
+// loop nests are reorganised for the cache and the vector units: column
+// minima are accumulated row by row (same r order per column), the zero
+// pattern and its row/column counts are rebuilt in one pass, and the
+// "row assigned to column c" lookup of the cover step is an inverse map.
 void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& assignments,
                               std::vector<unsigned>& unassignedTracks, std::vector<unsigned>& unassignedDetections)
 {
@@ -114,56 +123,106 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
     const unsigned n = std::max(nT, nD);
     const double huge = 10000000.0;
     const double pad = args.costOfNonAssignment * 2;
-    cost.assign((size_t)n * n, pad);
-    for (unsigned i = 0; i < nT; ++i)
-        for (unsigned j = 0; j < nD; ++j)
-            cost[(size_t)i * n + j] = 1.0 - computeBoundingBoxOverlap(tracks[i].predPosition, dets[j].bbox);
+    cost.resize((size_t)n * n);
+    // detections as SoA for a branch-free, vectorisable IoU row
+    detX0.resize(nD); detY0.resize(nD); detX1.resize(nD); detY1.resize(nD); detArea.resize(nD);
+    for (unsigned j = 0; j < nD; ++j) {
+        const Rect& b = dets[j].bbox;
+        detX0[j] = b.x; detY0[j] = b.y; detX1[j] = b.x + b.width; detY1[j] = b.y + b.height;
+        detArea[j] = b.area();
+    }
     assignmentPerRow.assign(n, n);
-    auto C = [&](unsigned r, unsigned c) -> double& { return cost[(size_t)r * n + c]; };
-
-    if (n > 0) {
-        // step 1: row minima (tbd.cpp:494-516)
+    if (n == 0) return;
+    // calculateCostMatrix (:333-351) fused with step 1, the row minima (:494-516)
+    for (unsigned r = 0; r < n; ++r) {
+        double* row = &cost[(size_t)r * n];
+        unsigned c0 = 0;
+        if (r < nT) {
+            const Rect& p = tracks[r].predPosition;
+            const int px0 = p.x, py0 = p.y, px1 = p.x + p.width, py1 = p.y + p.height, pa = p.area();
+            for (unsigned j = 0; j < nD; ++j) {  // computeBoundingBoxOverlap, branch-free
+                const int xl = std::max(px0, detX0[j]), xr = std::min(px1, detX1[j]);
+                const int yt = std::max(py0, detY0[j]), yb = std::min(py1, detY1[j]);
+                const double inter = (double)(xr - xl) * (double)(yb - yt);
+                const double uni = (double)(pa + detArea[j]) - inter;
+                const double iou = (xr < xl || yb < yt) ? 0.0 : inter / uni;
+                row[j] = 1.0 - iou;
+            }
+            c0 = nD;
+        }
+        for (unsigned c = c0; c < n; ++c) row[c] = pad;
+        // the reference's sequential min; the value is order independent (no NaN
+        // can be selected by `<`), so four interleaved partial minima are used
+        double m0 = huge, m1 = huge, m2 = huge, m3 = huge;
+        unsigned c = 0;
+        for (; c + 4 <= n; c += 4) {
+            m0 = (row[c] < m0) ? row[c] : m0;
+            m1 = (row[c + 1] < m1) ? row[c + 1] : m1;
+            m2 = (row[c + 2] < m2) ? row[c + 2] : m2;
+            m3 = (row[c + 3] < m3) ? row[c + 3] : m3;
+        }
+        for (; c < n; ++c) m0 = (row[c] < m0) ? row[c] : m0;
+        m0 = (m1 < m0) ? m1 : m0;
+        m2 = (m3 < m2) ? m3 : m2;
+        const double m = (m2 < m0) ? m2 : m0;
+        for (unsigned k = 0; k < n; ++k) row[k] -= m;
+    }
+    {
+        // step 2: column minima (:539-561), scanned in the same r order per column
+        colMin.assign(n, huge);
         for (unsigned r = 0; r < n; ++r) {
-            double m = huge;
-            for (unsigned c = 0; c < n; ++c) m = (C(r, c) < m) ? C(r, c) : m;
-            for (unsigned c = 0; c < n; ++c) C(r, c) -= m;
+            const double* row = &cost[(size_t)r * n];
+            for (unsigned c = 0; c < n; ++c) colMin[c] = (row[c] < colMin[c]) ? row[c] : colMin[c];
         }
-        // step 2: column minima (:539-561)
-        for (unsigned c = 0; c < n; ++c) {
-            double m = huge;
-            for (unsigned r = 0; r < n; ++r) m = (C(r, c) < m) ? C(r, c) : m;
-            for (unsigned r = 0; r < n; ++r) C(r, c) -= m;
+        for (unsigned r = 0; r < n; ++r) {
+            double* row = &cost[(size_t)r * n];
+            for (unsigned c = 0; c < n; ++c) row[c] -= colMin[c];
         }
-        std::vector<uint8_t> zero((size_t)n * n);
-        std::vector<unsigned> rowZeros(n), colZeros(n);
-        std::vector<char> rowA(n), colA(n), rowM(n), colM(n), rowCov(n), colCov(n);
+        zero.resize((size_t)n * n);
+        rowZeros.resize(n);
+        colZeros.resize(n);
+        colRow.resize(n);
+        rowA.resize(n);
+        colA.resize(n);
+        rowM.resize(n);
+        colM.resize(n);
         while (true) {  // (:585-887)
-            for (size_t k = 0; k < zero.size(); ++k) zero[k] = equalsZero(cost[k]) ? 1 : 0;
-            std::fill(rowZeros.begin(), rowZeros.end(), 0u);
             std::fill(colZeros.begin(), colZeros.end(), 0u);
-            for (unsigned r = 0; r < n; ++r)
-                for (unsigned c = 0; c < n; ++c)
-                    if (zero[(size_t)r * n + c]) {
-                        rowZeros[r]++;
-                        colZeros[c]++;
-                    }
+            for (unsigned r = 0; r < n; ++r) {
+                const double* row = &cost[(size_t)r * n];
+                uint8_t* z = &zero[(size_t)r * n];
+                unsigned cnt = 0;
+                for (unsigned c = 0; c < n; ++c) {
+                    const uint8_t b = std::fabs(row[c]) < 0.00000001 ? 1 : 0;  // == equalsZero
+                    z[c] = b;
+                    cnt += b;
+                    colZeros[c] += b;
+                }
+                rowZeros[r] = cnt;
+            }
             std::fill(rowA.begin(), rowA.end(), 0);
             std::fill(colA.begin(), colA.end(), 0);
+            std::fill(colRow.begin(), colRow.end(), n);
             unsigned numAssigned = 0;
             assignmentPerRow.assign(n, n);
+            auto assign = [&](unsigned r, unsigned c) {
+                rowA[r] = colA[c] = 1;
+                assignmentPerRow[r] = c;
+                colRow[c] = r;
+                numAssigned++;
+            };
             bool made = true;
             while (made) {
                 made = false;
                 // rows with exactly one zero (:607-636)
                 for (unsigned r = 0; r < n; ++r) {
                     if (rowA[r] || rowZeros[r] != 1) continue;
+                    const uint8_t* z = &zero[(size_t)r * n];
                     unsigned c = 0;
-                    while (!zero[(size_t)r * n + c]) ++c;
+                    while (!z[c]) ++c;
                     if (!colA[c]) {
-                        rowA[r] = colA[c] = 1;
-                        assignmentPerRow[r] = c;
+                        assign(r, c);
                         made = true;
-                        numAssigned++;
                     }
                 }
                 // columns with exactly one zero (:639-668)
@@ -172,22 +231,19 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
                     unsigned r = 0;
                     while (!zero[(size_t)r * n + c]) ++r;
                     if (!rowA[r]) {
-                        rowA[r] = colA[c] = 1;
-                        assignmentPerRow[r] = c;
+                        assign(r, c);
                         made = true;
-                        numAssigned++;
                     }
                 }
                 // otherwise: first free zero of every unassigned row (:672-714)
                 if (!made) {
                     for (unsigned r = 0; r < n; ++r) {
                         if (rowA[r]) continue;
+                        const uint8_t* z = &zero[(size_t)r * n];
                         for (unsigned c = 0; c < n; ++c) {
-                            if (zero[(size_t)r * n + c] && !colA[c]) {
-                                rowA[r] = colA[c] = 1;
-                                assignmentPerRow[r] = c;
+                            if (z[c] && !colA[c]) {
+                                assign(r, c);
                                 made = true;
-                                numAssigned++;
                                 break;
                             }
                         }
@@ -202,40 +258,41 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
                 unsigned newly = 0;
                 for (unsigned r = 0; r < n; ++r) {
                     if (!rowM[r]) continue;
+                    const uint8_t* z = &zero[(size_t)r * n];
                     for (unsigned c = 0; c < n; ++c)
-                        if (zero[(size_t)r * n + c] && !colM[c]) {
+                        if (z[c] && !colM[c]) {
                             colM[c] = 1;
                             newly++;
                         }
                 }
-                for (unsigned c = 0; c < n; ++c) {
-                    if (!colM[c]) continue;
-                    for (unsigned r2 = 0; r2 < n; ++r2)
-                        if (assignmentPerRow[r2] == c) rowM[r2] = 1;
-                }
+                for (unsigned c = 0; c < n; ++c)
+                    if (colM[c] && colRow[c] < n) rowM[colRow[c]] = 1;
                 if (newly == 0) break;
             }
             bool allMarked = true;
-            for (unsigned r = 0; r < n; ++r) {
-                rowCov[r] = !rowM[r];
+            for (unsigned r = 0; r < n; ++r)
                 if (!rowM[r]) allMarked = false;
-            }
             if (allMarked) break;
-            for (unsigned c = 0; c < n; ++c) colCov[c] = colM[c];
-            // step 4 (:853-886)
+            // step 4 (:853-886): covered rows are the unmarked ones, covered columns the marked ones
             double mu = huge;
             for (unsigned r = 0; r < n; ++r) {
-                if (rowCov[r]) continue;
+                if (!rowM[r]) continue;
+                const double* row = &cost[(size_t)r * n];
                 for (unsigned c = 0; c < n; ++c) {
-                    if (colCov[c]) continue;
-                    mu = (C(r, c) < mu) ? C(r, c) : mu;
+                    if (colM[c]) continue;
+                    mu = (row[c] < mu) ? row[c] : mu;
                 }
             }
-            for (unsigned r = 0; r < n; ++r)
-                for (unsigned c = 0; c < n; ++c) {
-                    if (!rowCov[r] && !colCov[c]) C(r, c) -= mu;
-                    else if (rowCov[r] && colCov[c]) C(r, c) += mu;
+            for (unsigned r = 0; r < n; ++r) {
+                double* row = &cost[(size_t)r * n];
+                if (rowM[r]) {
+                    for (unsigned c = 0; c < n; ++c)
+                        if (!colM[c]) row[c] -= mu;
+                } else {
+                    for (unsigned c = 0; c < n; ++c)
+                        if (colM[c]) row[c] += mu;
                 }
+            }
         }
     }
     // classifyAssignments (:353-379)
@@ -259,7 +316,7 @@ void Tracker::updateTrackConfidence(Track& t)
     const unsigned num = (unsigned)t.scores.size() < args.timeWindowSize ? (unsigned)t.scores.size()
                                                                           : args.timeWindowSize;
     double maxScore = 0.0, sum = 0.0;
-    for (unsigned k = (unsigned)t.scores.size() - num; k < t.scores.size(); ++k) {
+    for (unsigned k = t.scores.size() - num; k < t.scores.size(); ++k) {
         const double s = t.scores[k];
         sum += s;
         if (s > maxScore) maxScore = s;
@@ -268,14 +325,13 @@ void Tracker::updateTrackConfidence(Track& t)
     t.avgConfidence = sum / num;
 }
 
-static void push_box(Track& t, const Rect& r, int frame, double score, unsigned window)
+// the windows keep at least what the reference reads of its ever-growing
+// vectors: 4 boxes, 2 frame ids, timeWindowSize (<= kMaxTimeWindow) scores
+static void push_box(Track& t, const Rect& r, int frame, double score)
 {
     t.bboxes.push_back(r);
-    if (t.bboxes.size() > 4) t.bboxes.pop_front();
     t.frames.push_back(frame);
-    if (t.frames.size() > 2) t.frames.pop_front();
     t.scores.push_back(score);
-    if (t.scores.size() > window) t.scores.pop_front();
     t.historyLength++;
 }
 
@@ -288,7 +344,7 @@ void Tracker::updateAssignedTracks(std::vector<Detection>& dets, const std::vect
         const Detection& d = dets[(size_t)assignments[i]];
         const unsigned nprior = t.historyLength < 4 ? (unsigned)t.historyLength : 4u;
         unsigned wsum = 0, hsum = 0;
-        for (size_t k = t.bboxes.size() - nprior; k < t.bboxes.size(); ++k) {
+        for (unsigned k = t.bboxes.size() - nprior; k < t.bboxes.size(); ++k) {
             wsum += t.bboxes[k].width;
             hsum += t.bboxes[k].height;
         }
@@ -298,7 +354,7 @@ void Tracker::updateAssignedTracks(std::vector<Detection>& dets, const std::vect
         cx += (d.bbox.width / 2) - (w / 2);
         cy += (d.bbox.height / 2) - (h / 2);
         t.bboxOverlap = computeBoundingBoxOverlap(d.bbox, t.predPosition);
-        push_box(t, rect_from_point2d(cx, cy, w, h), d.frame_id, d.confidence, args.timeWindowSize);
+        push_box(t, rect_from_point2d(cx, cy, w, h), d.frame_id, d.confidence);
         t.age++;
         t.totalVisibleCount++;
         updateTrackConfidence(t);
@@ -311,7 +367,7 @@ void Tracker::updateUnassignedTracks(const std::vector<unsigned>& un, int frame_
     for (unsigned idx : un) {
         Track& t = tracks[idx];
         t.age++;
-        push_box(t, t.predPosition, frame_id, 0.0, args.timeWindowSize);
+        push_box(t, t.predPosition, frame_id, 0.0);
         t.bboxOverlap = 0.0;
         updateTrackConfidence(t);
     }
@@ -320,17 +376,17 @@ void Tracker::updateUnassignedTracks(const std::vector<unsigned>& un, int frame_
 // deleteLostTracks (tbd.cpp:1011-1037)
 void Tracker::deleteLostTracks()
 {
-    std::vector<Track> kept;
-    kept.reserve(tracks.size());
-    for (auto& t : tracks) {
+    size_t k = 0;
+    for (size_t i = 0; i < tracks.size(); ++i) {
+        const Track& t = tracks[i];
         const double visibility = ((double)t.totalVisibleCount) / t.age;
         if ((t.age <= args.trackAgeThreshold && visibility <= args.trackVisibilityThreshold) ||
             (t.maxConfidence >= 0.0 && t.maxConfidence <= args.trackConfidenceThreshold))
             deletedIds.push_back(t.id);
-        else
-            kept.push_back(std::move(t));
+        else if (k++ != i)
+            tracks[k - 1] = tracks[i];
     }
-    tracks.swap(kept);
+    tracks.resize(k);
 }
 
 // createNewTracks + Track::Track(Detection&, Tracker*) (tbd.cpp:1043-1055, 67-91);

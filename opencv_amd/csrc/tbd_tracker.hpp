@@ -16,7 +16,6 @@
 #pragma once
 
 #include <cstdint>
-#include <deque>
 #include <vector>
 
 namespace tbdk {
@@ -52,11 +51,34 @@ struct Detection {  // cv::tbd::Detection (tbd.hpp:69-83)
     double confidence = 1.0;
 };
 
+// Fixed-capacity history window: push_back drops the oldest entry when full;
+// [0] is the oldest kept entry.  Trivially movable (no heap), so tracks can be
+// compacted in place every frame.
+template <class T, unsigned N>
+struct Window {
+    T v[N];
+    unsigned head = 0, n = 0;
+    unsigned size() const { return n; }
+    void push_back(const T& x)
+    {
+        if (n < N) {
+            v[(head + n++) % N] = x;
+        } else {
+            v[head] = x;
+            head = (head + 1) % N;
+        }
+    }
+    const T& operator[](unsigned k) const { return v[(head + k) % N]; }
+    const T& back() const { return (*this)[n - 1]; }
+};
+
+constexpr unsigned kMaxTimeWindow = 64;  // bound on TbdArgs::timeWindowSize
+
 struct Track {  // cv::tbd::Track (tbd.hpp:89-114) with bounded history
     unsigned id = 0;
-    std::deque<Rect> bboxes;    // last <= 4 boxes (updateAssignedTracks reads 4)
-    std::deque<int> frames;     // last <= 2 frame ids (motion model reads 2)
-    std::deque<double> scores;  // last <= timeWindowSize scores
+    Window<Rect, 4> bboxes;                // last <= 4 boxes (updateAssignedTracks reads 4)
+    Window<int, 2> frames;                 // last <= 2 frame ids (motion model reads 2)
+    Window<double, kMaxTimeWindow> scores;  // last <= timeWindowSize scores (see push_box)
     unsigned age = 1, totalVisibleCount = 1;
     double maxConfidence = 0, avgConfidence = 0;
     Rect predPosition;
@@ -98,6 +120,13 @@ private:
     std::vector<Track> tracks;
     std::vector<double> cost;  // flat n x n cost matrix
     std::vector<unsigned> assignmentPerRow;
+    // solver scratch, kept across frames
+    std::vector<uint8_t> zero;
+    std::vector<unsigned> rowZeros, colZeros, colRow;
+    std::vector<double> colMin;
+    std::vector<char> rowA, colA, rowM, colM;
+    std::vector<int> predIndex;
+    std::vector<int> detX0, detY0, detX1, detY1, detArea;
 
     void predictNewLocationsOfTracks(int frame_id, const Prediction* preds, int npreds);
     void filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax);

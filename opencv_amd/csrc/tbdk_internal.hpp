@@ -35,7 +35,8 @@ struct tbdk_ctx {
     std::vector<hipEvent_t> free_events;
     // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
     void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
-    int* gftt_max = nullptr;     // int[cap_rois]
+    int* gftt_max = nullptr;     // int[2 x cap_rois]: per-ROI max eig key, candidate count
+    void* gftt_cand = nullptr;   // cap_rois x kGfttCap candidates
     void* gftt_planes = nullptr;  // 3 x cap_px doubles (row sums) + cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
@@ -115,6 +116,8 @@ struct GfttArgs {
     double* rs2;
     float* eig;
     int* roi_max;
+    void* cand;       // nroi x cap candidates (value, address key), global scratch
+    int* cand_count;  // nroi appended-candidate counters
     int cap;        // LDS candidate capacity per ROI (power of two)
     int occ_bytes;  // LDS for the accepted-corner occupancy bitmap
     int max_corners;
@@ -122,6 +125,8 @@ struct GfttArgs {
     float2* corners;  // nroi x max_corners
     int32_t* counts;  // nroi (-1: candidate overflow)
 };
+constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
+constexpr size_t kGfttCandBytes = 8 * (size_t)kGfttCap;
 size_t gftt_select_smem(int cap, int max_corners, int occ_bytes);
 hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s);
 }  // namespace tbdk

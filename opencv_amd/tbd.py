@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -28,13 +29,22 @@ def default_config(width: int, height: int, **overrides) -> _lib.TbdConfig:
     return cfg
 
 
-def detections_from_gt(gt_frame) -> list[tuple]:
+# numpy mirror of tbdk_detection (include/tbdk.h): passed to tbdk_tbd_step without a copy
+DET_DTYPE = np.dtype([("id", "<i4"), ("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", "<i4"),
+                      ("confidence", "<f8")], align=True)
+assert DET_DTYPE.itemsize == C.sizeof(_lib.Detection)
+
+
+def detections_from_gt(gt_frame) -> np.ndarray:
     """GT rows {valid, x, y, w, h} -> detections (id = object index, confidence 1.0),
-    as parseDetections builds them from a ground-truth file (samples/gpu/tbd.cpp:1297-1340)."""
-    out = []
-    for oid, row in enumerate(gt_frame.tolist()):
-        if row[0]:
-            out.append((oid, row[1], row[2], row[3], row[4], 1.0))
+    as parseDetections builds them from a ground-truth file (samples/gpu/tbd.cpp:1297-1340).
+    Returns a DET_DTYPE array (a list of (id, x, y, w, h, conf) tuples is accepted by step too)."""
+    g = np.asarray(gt_frame)
+    idx = np.nonzero(g[:, 0])[0]
+    out = np.zeros(len(idx), DET_DTYPE)
+    out["id"] = idx
+    out["x"], out["y"], out["width"], out["height"] = g[idx, 1], g[idx, 2], g[idx, 3], g[idx, 4]
+    out["confidence"] = 1.0
     return out
 
 
@@ -51,14 +61,20 @@ class TbdLoop:
         if frame.dtype != torch.uint8 or frame.dim() != 2 or not frame.is_cuda or frame.stride(1) != 1:
             raise _lib.TbdkError("frame must be a 2-D uint8 device tensor")
         n = len(dets)
-        if n > len(self._dets):
-            self._dets = (_lib.Detection * (2 * n))()
-        for i, (oid, x, y, w, h, conf) in enumerate(dets):
-            d = self._dets[i]
-            d.id, d.x, d.y, d.width, d.height, d.confidence = oid, x, y, w, h, conf
+        if isinstance(dets, np.ndarray):
+            if dets.dtype != DET_DTYPE or not dets.flags.c_contiguous:
+                raise _lib.TbdkError("detections must be a contiguous DET_DTYPE array")
+            dptr = C.cast(dets.ctypes.data, C.POINTER(_lib.Detection))
+        else:
+            if n > len(self._dets):
+                self._dets = (_lib.Detection * (2 * n))()
+            for i, (oid, x, y, w, h, conf) in enumerate(dets):
+                d = self._dets[i]
+                d.id, d.x, d.y, d.width, d.height, d.confidence = oid, x, y, w, h, conf
+            dptr = self._dets
         m = _lib.FrameMetrics()
         _lib.check(self.ctx.lib.tbdk_tbd_step(self.handle, C.c_void_p(frame.data_ptr()), int(frame.stride(0)),
-                                              int(frame_id), self._dets, n, C.byref(m), _stream_ptr(stream)),
+                                              int(frame_id), dptr, n, C.byref(m), _stream_ptr(stream)),
                    "tbdk_tbd_step")
         return m
 
