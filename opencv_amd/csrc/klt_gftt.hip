@@ -83,11 +83,34 @@ __device__ __forceinline__ Cov sobel_cov(const uint8_t* img, int pitch, const Gf
 
 }  // namespace
 
+// flat pixel grid over all ROIs: ROI r owns blocks [rois[r].blk, rois[r+1].blk)
+__device__ __forceinline__ int roi_of_block(const GfttRoi* rois, int nroi, int b)
+{
+    int lo = 0, hi = nroi - 1;
+    while (lo < hi) {  // block-uniform binary search (scalar loads)
+        const int mid = (lo + hi + 1) >> 1;
+        if (rois[mid].blk <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ int roi_of_cblock(const GfttRoi* rois, int nroi, int b)
+{
+    int lo = 0, hi = nroi - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rois[mid].cblk <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void gftt_rowsum_kernel(GfttArgs a)
 {
-    const int r = blockIdx.y;
+    const int r = roi_of_block(a.rois, a.nroi, blockIdx.x);
     const GfttRoi R = a.rois[r];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = (blockIdx.x - R.blk) * blockDim.x + threadIdx.x;
     if (p >= R.w * R.h) return;
     const int y = p / R.w, x = p - y * R.w;
     const Cov l = sobel_cov(a.img, a.pitch, R, refl(x - 1, R.w), y);
@@ -99,97 +122,104 @@ __global__ __launch_bounds__(256) void gftt_rowsum_kernel(GfttArgs a)
     a.rs2[o] = (double)l.c2 + (double)c.c2 + (double)q.c2;
 }
 
-__global__ __launch_bounds__(256) void gftt_eig_kernel(GfttArgs a)
+__global__ __launch_bounds__(64) void gftt_eig_kernel(GfttArgs a)
 {
     constexpr int CH = 8;  // rows loaded ahead of the add chain
-    const int r = blockIdx.y;
+    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
     const GfttRoi R = a.rois[r];
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.w) return;
-    const double* p0 = a.rs0 + R.off + x;
-    const double* p1 = a.rs1 + R.off + x;
-    const double* p2 = a.rs2 + R.off + x;
-    float* E = a.eig + R.off + x;
-    const size_t W = (size_t)R.w;
-    // ColumnSum: SUM = 0 + row(-1), SUM += row(0); per output y:
-    // s = SUM + row(y+1); out = (float)s; SUM = s - row(y-1)
-    const int rm1 = refl(-1, R.h);
-    double m1_0 = p0[rm1 * W], m1_1 = p1[rm1 * W], m1_2 = p2[rm1 * W];  // row y-1
-    double m0_0 = p0[0], m0_1 = p1[0], m0_2 = p2[0];                    // row y
-    double S0 = 0.0 + m1_0, S1 = 0.0 + m1_1, S2 = 0.0 + m1_2;
-    S0 = S0 + m0_0;
-    S1 = S1 + m0_1;
-    S2 = S2 + m0_2;
+    const int x = (blockIdx.x - R.cblk) * 64 + threadIdx.x;
     int best = INT_MIN;
-    for (int y0 = 0; y0 < R.h; y0 += CH) {
-        double q0[CH], q1[CH], q2[CH];
+    if (x < R.w) {
+        const double* p0 = a.rs0 + R.off + x;
+        const double* p1 = a.rs1 + R.off + x;
+        const double* p2 = a.rs2 + R.off + x;
+        float* E = a.eig + R.off + x;
+        const size_t W = (size_t)R.w;
+        // ColumnSum: SUM = 0 + row(-1), SUM += row(0); per output y:
+        // s = SUM + row(y+1); out = (float)s; SUM = s - row(y-1)
+        const int rm1 = refl(-1, R.h);
+        double m1_0 = p0[rm1 * W], m1_1 = p1[rm1 * W], m1_2 = p2[rm1 * W];  // row y-1
+        double m0_0 = p0[0], m0_1 = p1[0], m0_2 = p2[0];                    // row y
+        double S0 = 0.0 + m1_0, S1 = 0.0 + m1_1, S2 = 0.0 + m1_2;
+        S0 = S0 + m0_0;
+        S1 = S1 + m0_1;
+        S2 = S2 + m0_2;
+        for (int y0 = 0; y0 < R.h; y0 += CH) {
+            double q0[CH], q1[CH], q2[CH];
 #pragma unroll
-        for (int k = 0; k < CH; ++k) {  // independent loads of rows y0+1 .. y0+CH
-            const int yy = y0 + k + 1;
-            const size_t row = (size_t)refl(yy < R.h + 1 ? yy : R.h, R.h) * W;
-            q0[k] = p0[row];
-            q1[k] = p1[row];
-            q2[k] = p2[row];
-        }
+            for (int k = 0; k < CH; ++k) {  // independent loads of rows y0+1 .. y0+CH
+                const int yy = y0 + k + 1;
+                const size_t row = (size_t)refl(yy < R.h + 1 ? yy : R.h, R.h) * W;
+                q0[k] = p0[row];
+                q1[k] = p1[row];
+                q2[k] = p2[row];
+            }
 #pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            const int y = y0 + k;
-            if (y < R.h) {
-                const double t0 = S0 + q0[k], t1 = S1 + q1[k], t2 = S2 + q2[k];
-                S0 = t0 - m1_0;
-                S1 = t1 - m1_1;
-                S2 = t2 - m1_2;
-                m1_0 = m0_0;
-                m1_1 = m0_1;
-                m1_2 = m0_2;
-                m0_0 = q0[k];
-                m0_1 = q1[k];
-                m0_2 = q2[k];
-                const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
-                const float t = aa - cc;
-                const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-                E[(size_t)y * W] = e;
-                const int kk = fkey(e);
-                best = kk > best ? kk : best;
+            for (int k = 0; k < CH; ++k) {
+                const int y = y0 + k;
+                if (y < R.h) {
+                    const double t0 = S0 + q0[k], t1 = S1 + q1[k], t2 = S2 + q2[k];
+                    S0 = t0 - m1_0;
+                    S1 = t1 - m1_1;
+                    S2 = t2 - m1_2;
+                    m1_0 = m0_0;
+                    m1_1 = m0_1;
+                    m1_2 = m0_2;
+                    m0_0 = q0[k];
+                    m0_1 = q1[k];
+                    m0_2 = q2[k];
+                    const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
+                    const float t = aa - cc;
+                    const float e = (aa + cc) - sqrtf(bb * bb + t * t);
+                    E[(size_t)y * W] = e;
+                    const int kk = fkey(e);
+                    best = kk > best ? kk : best;
+                }
             }
         }
     }
-    atomicMax(&a.roi_max[r], best);
+    // per-block max (minMaxLoc is order independent): wave reduction, one plain store
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int v = __shfl_xor(best, o);
+        best = v > best ? v : best;
+    }
+    if (threadIdx.x == 0) a.blk_max[blockIdx.x] = best;
 }
 
-struct Cand {
-    float v;
-    int key;  // (y << 16) | x : same order as the reference's address tie-break
-};
-
-// a before b in the reference order: value desc, then address desc
-__device__ __forceinline__ bool cand_before(const Cand& a, const Cand& b)
+// Candidate sort key: the reference order (value desc, then address desc,
+// featureselect.cpp:56-64) is the descending order of
+//   (orderable bits of the float value) << 32 | (y << 16 | x)
+__device__ __forceinline__ uint64_t cand_key(float v, int y, int x)
 {
-    return a.v > b.v || (a.v == b.v && a.key > b.key);
+    return ((uint64_t)((uint32_t)fkey(v) ^ 0x80000000u) << 32) | (uint32_t)((y << 16) | x);
 }
 
 // threshold-to-zero at max*q + 3x3 dilate-equality on interior pixels, one
-// thread per ROI pixel; candidates appended to the ROI's global list (the
-// append order is irrelevant: the list is sorted by (value, address) next)
+// thread per ROI pixel; candidates go to this block's own kGfttBlock slots
 __global__ __launch_bounds__(256) void gftt_nms_kernel(GfttArgs a)
 {
-    __shared__ int lcount, lbase;
-    const int r = blockIdx.y;
+    __shared__ int lcount;
+    const int r = roi_of_block(a.rois, a.nroi, blockIdx.x);
     const GfttRoi R = a.rois[r];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = (blockIdx.x - R.blk) * blockDim.x + threadIdx.x;
     const int iw = R.w - 2, ih = R.h - 2;
-    if (iw <= 0 || ih <= 0 || (int)(blockIdx.x * blockDim.x) >= iw * ih) return;  // block-uniform
+    if (iw <= 0 || ih <= 0 || (int)((blockIdx.x - R.blk) * blockDim.x) >= iw * ih) {  // block-uniform
+        if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = 0;
+        return;
+    }
     if (threadIdx.x == 0) lcount = 0;
+    int mk = INT_MIN;  // ROI max = max of its column blocks' maxima
+    for (int b = R.cblk, e = R.cblk + (R.w + 63) / 64; b < e; ++b) mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
+    const float thr = (float)((double)fkey_inv(mk) * a.quality);
     __syncthreads();
     bool keep = false;
-    float v = 0.f;
-    int key = 0;
+    uint64_t key = 0;
     if (p < iw * ih) {
         const int y = p / iw + 1, x = p - (y - 1) * iw + 1;
-        const float thr = (float)((double)fkey_inv(a.roi_max[r]) * a.quality);
         const float* E = a.eig + R.off + (size_t)y * R.w + x;
         const float v0 = E[0];
-        v = v0 > thr ? v0 : 0.f;
+        const float v = v0 > thr ? v0 : 0.f;
         if (v != 0.f) {
             float m = v;
 #pragma unroll
@@ -201,178 +231,358 @@ __global__ __launch_bounds__(256) void gftt_nms_kernel(GfttArgs a)
                     m = q > m ? q : m;
                 }
             keep = v == m;
-            key = (y << 16) | x;
+            key = cand_key(v, y, x);
         }
     }
-    // block-aggregated append: one global atomic per block, not per candidate
-    int li = 0;
-    if (keep) li = atomicAdd(&lcount, 1);
+    // no global atomics (same-address atomics from all XCDs serialise far from
+    // the CU): the select kernel gathers the per-block lists
+    if (keep) {
+        const int li = atomicAdd(&lcount, 1);
+        reinterpret_cast<uint64_t*>(a.cand)[(size_t)blockIdx.x * kGfttBlock + li] = key;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) lbase = lcount ? atomicAdd(&a.cand_count[r], lcount) : 0;
-    __syncthreads();
-    const int slot = lbase + li;
-    if (keep && slot < a.cap) reinterpret_cast<Cand*>(a.cand)[(size_t)r * a.cap + slot] = Cand{v, key};
+    if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = lcount;
 }
 
 constexpr int kSelThreads = 512;
 
+// phase hooks for tools/ probes (no-ops in the library build)
+#ifndef GFTT_STAMP
+#define GFTT_STAMP(i)
+#define GFTT_TDECL
+#define GFTT_T(i)
+#define GFTT_TDUMP
+#endif
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int d)
+{
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    const int l2 = __shfl_xor(lo, d), h2 = __shfl_xor(hi, d);
+    return ((uint64_t)(uint32_t)h2 << 32) | (uint32_t)l2;
+}
+
+// Bitonic sort of np2 keys, descending, E keys per thread in registers
+// (element e = tid * E + u): stages with j < E swap registers, E <= j < 64E
+// exchange across lanes of the wave (no barrier), only j >= 64E go through LDS.
+template <int E>
+__device__ void sort_keys(uint64_t* keys, int np2, int tid)
+{
+    uint64_t x[E];
+    const bool active = tid * E < np2;
+#pragma unroll
+    for (int u = 0; u < E; ++u) x[u] = active ? keys[tid * E + u] : 0ull;
+    bool lds_dirty = false;
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+#pragma unroll
+                for (int jj = E / 2; jj >= 1; jj >>= 1) {  // compile-time register indices
+                    if (jj != j) continue;
+#pragma unroll
+                    for (int u = 0; u < E; ++u) {
+                        if (u & jj) continue;
+                        const int e = tid * E + u;
+                        const bool desc = (e & k) == 0;
+                        const uint64_t p = x[u], q = x[u | jj];
+                        const bool sw = desc ? p < q : p > q;
+                        x[u] = sw ? q : p;
+                        x[u | jj] = sw ? p : q;
+                    }
+                }
+            } else if (j < 64 * E) {
+                const int d = j / E;
+                const bool lower = (tid & d) == 0;
+#pragma unroll
+                for (int u = 0; u < E; ++u) {
+                    const uint64_t y = shfl_xor_u64(x[u], d);
+                    const int e = tid * E + u;
+                    const bool desc = (e & k) == 0;
+                    const bool take_max = lower == desc;
+                    x[u] = take_max ? (x[u] > y ? x[u] : y) : (x[u] < y ? x[u] : y);
+                }
+            } else {
+                if (lds_dirty) __syncthreads();  // previous LDS stage's reads are done
+                if (active)
+#pragma unroll
+                    for (int u = 0; u < E; ++u) keys[tid * E + u] = x[u];
+                __syncthreads();
+                if (active)
+#pragma unroll
+                    for (int u = 0; u < E; ++u) {
+                        const int e = tid * E + u;
+                        const uint64_t y = keys[e ^ j];
+                        const bool desc = (e & k) == 0;
+                        const bool take_max = ((e & j) == 0) == desc;
+                        x[u] = take_max ? (x[u] > y ? x[u] : y) : (x[u] < y ? x[u] : y);
+                    }
+                lds_dirty = true;
+            }
+        }
+    }
+    __syncthreads();
+    if (active)
+#pragma unroll
+        for (int u = 0; u < E; ++u) keys[tid * E + u] = x[u];
+    __syncthreads();
+}
+
+// LDS layout of the select kernel (one dynamic region):
+//   scan  : kSelThreads ints (gather prefix sums)
+//   keys  : cap uint64 sort keys
+//   acc   : max_corners float2 accepted positions + 64 float2 (list mode)
+//   img   : img_bytes, one byte per ROI pixel (image mode): 0 empty,
+//           1..64 candidate of the current step (lane + 1), 255 accepted corner
 __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Cand* cand = reinterpret_cast<Cand*>(smem);  // all LDS in the one dynamic region
-    float2* acc = reinterpret_cast<float2*>(smem + sizeof(Cand) * a.cap);
-    float2* bxy = acc + a.max_corners;  // this step's 64 candidate positions
-    uint32_t* occ = reinterpret_cast<uint32_t*>(bxy + 64);
+    int* scan = reinterpret_cast<int*>(smem);
+    uint64_t* keys = reinterpret_cast<uint64_t*>(smem + sizeof(int) * kSelThreads);
+    float2* acc = reinterpret_cast<float2*>(keys + a.cap);
+    float2* bxy = acc + a.max_corners;
+    uint8_t* img = reinterpret_cast<uint8_t*>(acc + ((a.max_corners + 65) & ~1));  // 16-byte aligned
     const int r = blockIdx.x;
     const GfttRoi R = a.rois[r];
     const int tid = threadIdx.x;
-    const int total = a.cand_count[r];
-    if (total > a.cap) {  // candidate buffer overflow: report, never silently truncate
-        if (tid == 0) a.counts[r] = -1;
-        return;
-    }
-    // occupancy bitmap of accepted corners (1 bit per ROI pixel), if it fits
-    const int ow = (R.w + 31) / 32 + 1;  // words per row (+1: two-word window reads)
-    const bool use_occ = (size_t)ow * R.h * 4 <= (size_t)a.occ_bytes;
-    if (use_occ)
-        for (int i = tid; i < ow * R.h; i += kSelThreads) occ[i] = 0u;
-    int np2 = 1;
-    while (np2 < total) np2 <<= 1;
-    const Cand* src = reinterpret_cast<const Cand*>(a.cand) + (size_t)r * a.cap;
-    for (int i = tid; i < np2; i += kSelThreads) cand[i] = i < total ? src[i] : Cand{-FLT_MAX, -1};
-    __syncthreads();
-    // bitonic sort, "before" order first; every thread owns np2/2/threads
-    // compare-exchange pairs per stage (branch-free indexing, loads batched)
-    const int npairs = np2 >> 1;
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int pb = 0; pb < npairs; pb += kSelThreads * 4) {
-                int ii[4];
-                Cand ci[4], cj[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int pidx = pb + u * kSelThreads + tid;
-                    ii[u] = pidx < npairs ? ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)) : -1;
-                    if (ii[u] >= 0) {
-                        ci[u] = cand[ii[u]];
-                        cj[u] = cand[ii[u] + j];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (ii[u] < 0) continue;
-                    const bool up = (ii[u] & k) == 0;
-                    const bool swap = up ? cand_before(cj[u], ci[u]) : cand_before(ci[u], cj[u]);
-                    if (swap) {
-                        cand[ii[u]] = cj[u];
-                        cand[ii[u] + j] = ci[u];
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    if (tid >= 64) return;
-    // ---- greedy walk in sorted order (featureselect.cpp:421-503), 64 candidates per step
-    const int lane = tid;
+    const int area = R.w * R.h;
+    // image mode: the ROI's byte image fits and the distance window is small
     const bool use_dist = a.min_distance >= 1.0;
     const double md2 = a.min_distance * a.min_distance;
     int rad = (int)ceil(a.min_distance) - 1;  // |d| <= rad can be closer than min_distance
     if ((double)(rad + 1) * (rad + 1) < md2) rad++;
-    const bool occ_ok = use_occ && rad <= 31;
+    const bool img_mode = use_dist && area <= a.img_bytes && rad <= 6;
+    if (img_mode)
+        for (int i = tid * 16; i < area; i += kSelThreads * 16) *reinterpret_cast<uint4*>(img + i) = make_uint4(0, 0, 0, 0);
+
+    // ---- gather the candidates of the ROI's NMS blocks, chunk by chunk:
+    // block-wide exclusive scan of the block counts, then one wave per block copies
+    const int nb = (area + kGfttBlock - 1) / kGfttBlock;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(a.cand);
+    int total = 0;
+    for (int b0 = 0; b0 < nb; b0 += kSelThreads) {
+        const int c = b0 + tid < nb ? a.blk_cnt[R.blk + b0 + tid] : 0;
+        scan[tid] = c;
+        __syncthreads();
+        for (int o = 1; o < kSelThreads; o <<= 1) {  // Hillis-Steele inclusive scan
+            const int v = tid >= o ? scan[tid - o] : 0;
+            __syncthreads();
+            scan[tid] += v;
+            __syncthreads();
+        }
+        const int chunk_total = scan[kSelThreads - 1];
+        // one thread per candidate: its block by binary search of the inclusive
+        // scan, so all global loads of the chunk are independent
+        for (int q = tid; q < chunk_total; q += kSelThreads) {
+            int lo = 0, hi = kSelThreads - 1;
+            while (lo < hi) {  // first block whose inclusive sum exceeds q
+                const int mid = (lo + hi) >> 1;
+                if (scan[mid] > q) hi = mid;
+                else lo = mid + 1;
+            }
+            const int within = q - (lo == 0 ? 0 : scan[lo - 1]);
+            if (total + q < a.cap) keys[total + q] = src[(size_t)(R.blk + b0 + lo) * kGfttBlock + within];
+        }
+        total += chunk_total;
+        __syncthreads();
+    }
+    if (total > a.cap) {  // candidate buffer overflow: report, never silently truncate
+        if (tid == 0) a.counts[r] = -1;
+        return;
+    }
+    int np2 = kSelThreads;
+    while (np2 < total) np2 <<= 1;
+    for (int i = total + tid; i < np2; i += kSelThreads) keys[i] = 0ull;  // sorts last
+    __syncthreads();
+    GFTT_STAMP(0);
+    switch (np2 / kSelThreads) {
+    case 1: sort_keys<1>(keys, np2, tid); break;
+    case 2: sort_keys<2>(keys, np2, tid); break;
+    case 4: sort_keys<4>(keys, np2, tid); break;
+    case 8: sort_keys<8>(keys, np2, tid); break;
+    case 16: sort_keys<16>(keys, np2, tid); break;
+    default: sort_keys<32>(keys, np2, tid); break;
+    }
+    GFTT_STAMP(1);
+    GFTT_STAMP(2);
+    if (tid >= 64) return;
+
+    // ---- greedy walk in sorted order (featureselect.cpp:421-503), 64 candidates per step
+    const int lane = tid;
     const int maxc = a.max_corners;
     float2* out = a.corners + (size_t)r * maxc;
     int n = 0;
     bool done = false;
+    GFTT_TDECL;
     for (int i0 = 0; i0 < total && !done; i0 += 64) {
+        GFTT_T(0);
         const int i = i0 + lane;
         const bool valid = i < total;
-        const int key = valid ? cand[i].key : 0;
-        const int ix = key & 0xFFFF, iy = key >> 16;
+        const uint32_t kk = valid ? (uint32_t)keys[i] : 0u;
+        const int ix = (int)(kk & 0xFFFF), iy = (int)(kk >> 16);
         const float fx = (float)ix, fy = (float)iy;
         bool good = valid;
-        unsigned long long cm = 0ull;
-        if (use_dist) {
-            bxy[lane] = make_float2(fx, fy);
-            if (occ_ok) {  // accepted corners within the window, exact distance test
-                for (int dy = -rad; dy <= rad && good; ++dy) {
-                    const int yy = iy + dy;
-                    if (yy < 0 || yy >= R.h) continue;
-                    const int x0 = ix - rad < 0 ? 0 : ix - rad;
-                    const int x1 = ix + rad >= R.w ? R.w - 1 : ix + rad;
-                    for (int wx = x0 >> 5; wx <= (x1 >> 5) && good; ++wx) {
-                        uint32_t bits = occ[yy * ow + wx];
-                        while (bits && good) {
-                            const int b = __builtin_ctz(bits);
-                            bits &= bits - 1u;
-                            const int xx = (wx << 5) + b;
-                            if (xx < x0 || xx > x1) continue;
-                            const float ddx = fx - (float)xx, ddy = fy - (float)yy;
-                            if ((double)(ddx * ddx + ddy * ddy) < md2) good = false;
-                        }
+        unsigned long long inb = 0ull;  // earlier lanes of this step closer than min_distance
+        if (img_mode) {
+            if (valid) img[iy * R.w + ix] = (uint8_t)(lane + 1);
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            GFTT_T(1);
+            if (valid) {
+                // each window row [ix-rad, ix+rad] (<= 13 bytes): three aligned 8-byte
+                // LDS reads, funnel-shifted so byte t is column ix-rad+t; the image
+                // is sparse, so rows are skipped on a zero test and only the
+                // non-zero bytes are visited
+                const int x0 = ix - rad;
+                // window bytes whose column lies inside the ROI (0x80 marker per byte)
+                uint64_t cv_lo = 0, cv_hi = 0;
+                for (int t = 0; t <= 2 * rad; ++t) {
+                    const int xx = x0 + t;
+                    if (xx >= 0 && xx < R.w) {
+                        if (t < 8) cv_lo |= 0x80ull << (8 * t);
+                        else cv_hi |= 0x80ull << (8 * (t - 8));
                     }
                 }
-            } else {
-                for (int q = 0; q < n; ++q) {  // vs corners accepted in earlier steps
-                    const float2 pq = acc[q];
-                    const float dx = fx - pq.x, dy = fy - pq.y;
-                    good = good && !((double)(dx * dx + dy * dy) < md2);
+                for (int dy = -rad; dy <= rad; ++dy) {
+                    const int yy = iy + dy;
+                    if (yy < 0 || yy >= R.h) continue;
+                    const int base = yy * R.w + x0;  // may be < 0 or past the row: masked
+                    const int al = base > 0 ? (base & ~7) : 0;
+                    const uint64_t* wp = reinterpret_cast<const uint64_t*>(img + al);
+                    const uint64_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+                    const int sh = base - al;  // in [-6, 7]
+                    uint64_t lo, hi;
+                    if (sh >= 0) {
+                        const int b8 = 8 * sh;
+                        lo = sh ? (w0 >> b8) | (w1 << (64 - b8)) : w0;
+                        hi = sh ? (w1 >> b8) | (w2 << (64 - b8)) : w1;
+                    } else {  // window starts before the image (first row, x0 < 0)
+                        const int b8 = -8 * sh;
+                        lo = w0 << b8;
+                        hi = (w1 << b8) | (w0 >> (64 - b8));
+                    }
+                    // 0x80 in every non-zero byte, restricted to in-ROI columns
+                    uint64_t nz_lo = (((lo & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | lo) & cv_lo;
+                    uint64_t nz_hi = (((hi & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | hi) & cv_hi;
+                    if (dy == 0) {  // not the candidate itself
+                        if (rad < 8) nz_lo &= ~(0x80ull << (8 * rad));
+                        else nz_hi &= ~(0x80ull << (8 * (rad - 8)));
+                    }
+                    while (nz_lo | nz_hi) {
+                        int t;
+                        uint64_t src;
+                        if (nz_lo) {
+                            t = __builtin_ctzll(nz_lo) >> 3;
+                            nz_lo &= nz_lo - 1ull;
+                            src = lo;
+                        } else {
+                            t = __builtin_ctzll(nz_hi) >> 3;
+                            nz_hi &= nz_hi - 1ull;
+                            src = hi;
+                            t += 8;
+                        }
+                        const int v = (int)((src >> (8 * (t & 7))) & 0xFF);
+                        const int col = x0 + t;
+                        const float ddx = fx - (float)col, ddy = fy - (float)yy;
+                        if (!((double)(ddx * ddx + ddy * ddy) < md2)) continue;
+                        if (v == 255) good = false;                      // accepted earlier
+                        else if (v - 1 < lane) inb |= 1ull << (v - 1);  // earlier in this step
+                    }
                 }
+            }
+        } else if (use_dist) {  // list mode: every accepted corner, then this step's pairs
+            bxy[lane] = make_float2(fx, fy);
+            for (int q = 0; q < n && good; ++q) {
+                const float2 pq = acc[q];
+                const float dx = fx - pq.x, dy = fy - pq.y;
+                if ((double)(dx * dx + dy * dy) < md2) good = false;
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
-#pragma unroll 8
-            for (int j = 0; j < 64; ++j) {  // vs earlier candidates of this step (LDS broadcast reads)
+            for (int j = 0; j < lane; ++j) {
                 const float2 pj = bxy[j];
                 const float dx = fx - pj.x, dy = fy - pj.y;
-                if (j < lane && (double)(dx * dx + dy * dy) < md2) cm |= 1ull << j;
+                if ((double)(dx * dx + dy * dy) < md2) inb |= 1ull << j;
             }
         }
+        // sequential acceptance: lanes without in-step dependencies are final;
+        // the others, in order, are accepted iff no accepted earlier lane conflicts
+        GFTT_T(2);
         const unsigned long long goodm = __ballot(good);
-        unsigned long long accm = 0ull;
-        int cnt = n;
-        for (int k = 0; k < 64; ++k) {  // uniform scalar pass: the sequential acceptance
-            if (!((goodm >> k) & 1ull)) continue;
-            const unsigned long long ck =
-                ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(cm >> 32), k) << 32) |
-                (unsigned)__builtin_amdgcn_readlane((int)(unsigned)cm, k);
-            if (ck & accm) continue;
-            accm |= 1ull << k;
-            if (++cnt == maxc) {
-                done = true;
-                break;
+        const unsigned long long depm = __ballot(good && inb != 0ull);
+        unsigned long long accm = goodm & ~depm;
+        unsigned long long pend = depm;
+        while (pend) {
+            const int k = __builtin_ctzll(pend);
+            pend &= pend - 1ull;
+            const unsigned long long ik =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(inb >> 32), k) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)inb, k);
+            if (!(ik & accm)) accm |= 1ull << k;
+        }
+        GFTT_T(3);
+        // maxCorners: only the first (maxc - n) accepted of this step count
+        const int got = __popcll(accm);
+        if (n + got >= maxc) {
+            int keepn = maxc - n;
+            unsigned long long m = accm, t = 0ull;
+            while (keepn-- > 0) {
+                const unsigned long long low = m & (~m + 1ull);
+                t |= low;
+                m &= m - 1ull;
             }
+            accm = t;
+            done = true;
         }
-        if ((accm >> lane) & 1ull) {
+        GFTT_T(4);
+        const bool mine = (accm >> lane) & 1ull;
+        if (mine) {
             const int pos = n + __popcll(accm & ((1ull << lane) - 1ull));
-            acc[pos] = make_float2(fx, fy);
+            if (!img_mode) acc[pos] = make_float2(fx, fy);
             out[pos] = make_float2(fx + (float)R.x, fy + (float)R.y);
-            if (occ_ok) atomicOr(&occ[iy * ow + (ix >> 5)], 1u << (ix & 31));
         }
-        n = cnt;
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): acc[] / occ[] visible to the next step
+        if (img_mode && valid) img[iy * R.w + ix] = mine ? (uint8_t)255 : (uint8_t)0;
+        n += __popcll(accm);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): img[] / acc[] visible to the next step
         __builtin_amdgcn_wave_barrier();
+        GFTT_T(5);
     }
+    GFTT_TDUMP;
+    GFTT_STAMP(3);
     if (lane == 0) a.counts[r] = n;
 }
 
-size_t gftt_select_smem(int cap, int max_corners, int occ_bytes)
+size_t gftt_select_smem(int cap, int max_corners, int img_bytes)
 {
-    return sizeof(Cand) * (size_t)cap + sizeof(float2) * (size_t)(max_corners + 64) + (size_t)occ_bytes;
+    return sizeof(int) * kSelThreads + sizeof(uint64_t) * (size_t)cap +
+           sizeof(float2) * (size_t)((max_corners + 65) & ~1) + (size_t)img_bytes + 32;  // + window over-read
 }
 
-hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s)
+// LDS plan: the byte image for ROIs up to max_area pixels when that leaves
+// room for >= 4096 sort keys, else list mode with the largest key array
+void gftt_plan(GfttArgs& a, int max_area)
 {
-    hipError_t e = hipMemsetAsync(a.roi_max, 0x80, sizeof(int) * a.nroi, s);  // very negative keys
-    if (e == hipSuccess) e = hipMemsetAsync(a.cand_count, 0, sizeof(int) * a.nroi, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gftt_rowsum_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3((max_w + 63) / 64, a.nroi), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(gftt_nms_kernel, dim3((max_area + 255) / 256, a.nroi), dim3(256), 0, s, a);
-    const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.occ_bytes);
+    const long lds = 160L * 1024;
+    const long fixed = (long)gftt_select_smem(0, a.max_corners, 0);
+    long img = ((long)max_area + 15) & ~15L;
+    long room = lds - fixed - img;
+    if (room < 8L * 4096) {
+        img = 0;
+        room = lds - fixed;
+    }
+    int cap = 512;
+    while (cap < kGfttCap && 8L * cap * 2 <= room) cap <<= 1;
+    a.cap = cap;
+    a.img_bytes = (int)img;
+}
+
+hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(gftt_rowsum_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
+    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
+    const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_select_kernel, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
     return hipGetLastError();

@@ -95,7 +95,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
     if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
-    if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
+    if (ctx->gftt_blk) (void)hipFree(ctx->gftt_blk);
     if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
     if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
     delete ctx;
@@ -320,31 +320,24 @@ extern "C" {
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
 {
     if (!ctx || max_rois < 0 || max_total_pixels < 0) return TBDK_EINVAL;
+    if (max_rois <= ctx->gftt_cap_rois && max_total_pixels <= ctx->gftt_cap_px) return TBDK_OK;
     DeviceGuard g(ctx->device);
-    if (max_rois > ctx->gftt_cap_rois) {
-        if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
-        if (ctx->gftt_max) (void)hipFree(ctx->gftt_max);
-        if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
-        ctx->gftt_rois = nullptr;
-        ctx->gftt_max = nullptr;
-        ctx->gftt_cand = nullptr;
-        ctx->gftt_cap_rois = 0;
-        hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)max_rois);
-        // roi_max and the candidate counters share one allocation
-        if (e == hipSuccess)
-            e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_max), 2 * sizeof(int) * (size_t)max_rois);
-        if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, kGfttCandBytes * (size_t)max_rois);
-        if (e != hipSuccess) return map_err(e);
-        ctx->gftt_cap_rois = max_rois;
+    const int rois = std::max(max_rois, ctx->gftt_cap_rois);
+    const int64_t px = std::max(max_total_pixels, ctx->gftt_cap_px);
+    for (void** p : {&ctx->gftt_rois, reinterpret_cast<void**>(&ctx->gftt_blk), &ctx->gftt_planes, &ctx->gftt_cand}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
     }
-    if (max_total_pixels > ctx->gftt_cap_px) {
-        if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
-        ctx->gftt_planes = nullptr;
-        ctx->gftt_cap_px = 0;
-        hipError_t e = hipMalloc(&ctx->gftt_planes, (sizeof(double) * 3 + sizeof(float)) * (size_t)max_total_pixels);
-        if (e != hipSuccess) return map_err(e);
-        ctx->gftt_cap_px = max_total_pixels;
-    }
+    ctx->gftt_cap_rois = 0;
+    ctx->gftt_cap_px = 0;
+    const int64_t nb = gftt_max_blocks(rois, px), ncb = gftt_max_cblocks(rois, px);
+    hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)std::max(rois, 1));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_blk), sizeof(int) * (size_t)(nb + ncb));
+    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_planes, (sizeof(double) * 3 + sizeof(float)) * (size_t)std::max<int64_t>(px, 1));
+    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, 8 * (size_t)kGfttBlock * (size_t)nb);
+    if (e != hipSuccess) return map_err(e);
+    ctx->gftt_cap_rois = rois;
+    ctx->gftt_cap_px = px;
     return TBDK_OK;
 }
 
@@ -357,16 +350,17 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
         return TBDK_EINVAL;
     std::vector<GfttRoi> tab((size_t)nroi);
-    int64_t total = 0;
-    int max_area = 0, max_w = 0;
+    int64_t total = 0, nblk = 0, ncblk = 0;
+    int max_area = 0;
     for (int i = 0; i < nroi; ++i) {
         const tbdk_roi& r = rois[i];
         if (r.x < 0 || r.y < 0 || r.width <= 0 || r.height <= 0 || r.x + r.width > width || r.y + r.height > height)
             return TBDK_EINVAL;
-        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total};
+        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)nblk, (int)ncblk};
         total += (int64_t)r.width * r.height;
-        max_area = r.width * r.height > max_area ? r.width * r.height : max_area;
-        max_w = r.width > max_w ? r.width : max_w;
+        nblk += ((int64_t)r.width * r.height + kGfttBlock - 1) / kGfttBlock;
+        ncblk += (r.width + 63) / 64;
+        max_area = std::max(max_area, r.width * r.height);
     }
     if (total > INT32_MAX) return TBDK_EINVAL;
     int rc = tbdk_gftt_reserve(ctx, nroi > ctx->gftt_cap_rois ? nroi : ctx->gftt_cap_rois,
@@ -381,25 +375,22 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     a.pitch = pitch;
     a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
     a.nroi = nroi;
+    a.nblk = (int)nblk;
+    a.ncblk = (int)ncblk;
     a.rs0 = static_cast<double*>(ctx->gftt_planes);
     a.rs1 = a.rs0 + ctx->gftt_cap_px;
     a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
     a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
-    a.roi_max = ctx->gftt_max;
-    a.cand_count = ctx->gftt_max + ctx->gftt_cap_rois;
+    a.blk_cnt = ctx->gftt_blk;
+    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
     a.cand = ctx->gftt_cand;
-    a.cap = kGfttCap;
     a.max_corners = p->max_corners;
     a.quality = p->quality_level;
     a.min_distance = p->min_distance;
     a.corners = reinterpret_cast<float2*>(corners);
     a.counts = counts;
-    {
-        const long budget = 160L * 1024 - (long)gftt_select_smem(a.cap, a.max_corners, 0);
-        if (budget < 0) return TBDK_EINVAL;
-        a.occ_bytes = (int)(budget & ~15L);
-    }
-    if (e == hipSuccess) e = launch_gftt(a, max_area, max_w, s);
+    gftt_plan(a, max_area);
+    if (e == hipSuccess) e = launch_gftt(a, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }

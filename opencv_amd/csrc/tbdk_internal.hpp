@@ -35,8 +35,8 @@ struct tbdk_ctx {
     std::vector<hipEvent_t> free_events;
     // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
     void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
-    int* gftt_max = nullptr;     // int[2 x cap_rois]: per-ROI max eig key, candidate count
-    void* gftt_cand = nullptr;   // cap_rois x kGfttCap candidates
+    int* gftt_blk = nullptr;     // per-block ints: column-block maxima, pixel-block counts
+    void* gftt_cand = nullptr;   // kGfttBlock candidate slots per pixel block
     void* gftt_planes = nullptr;  // 3 x cap_px doubles (row sums) + cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
@@ -105,28 +105,36 @@ namespace tbdk {
 struct GfttRoi {
     int x, y, w, h;
     int off;  // first pixel of this ROI in the scratch planes
+    int blk;   // first 256-pixel block of this ROI in the flat per-pixel grids
+    int cblk;  // first 64-column block of this ROI in the flat per-column grid
 };
+constexpr int kGfttBlock = 256;
 struct GfttArgs {
     const uint8_t* img;
     int pitch;
     const GfttRoi* rois;
     int nroi;
+    int nblk;     // total blocks of the flat per-pixel grids
+    int ncblk;    // total blocks of the flat per-column grid
     double* rs0;  // boxFilter horizontal sums of (Dx^2, DxDy, Dy^2), per ROI pixel
     double* rs1;
     double* rs2;
     float* eig;
-    int* roi_max;
-    void* cand;       // nroi x cap candidates (value, address key), global scratch
-    int* cand_count;  // nroi appended-candidate counters
+    int* blk_max;   // per column block: max eigenvalue key
+    int* blk_cnt;   // per pixel block: candidates found by the NMS block
+    void* cand;     // per pixel block: kGfttBlock candidate slots (value, address key)
     int cap;        // LDS candidate capacity per ROI (power of two)
-    int occ_bytes;  // LDS for the accepted-corner occupancy bitmap
+    int img_bytes;  // LDS for the per-ROI byte image of the greedy walk (0: list mode)
     int max_corners;
     double quality, min_distance;
     float2* corners;  // nroi x max_corners
     int32_t* counts;  // nroi (-1: candidate overflow)
 };
 constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
-constexpr size_t kGfttCandBytes = 8 * (size_t)kGfttCap;
-size_t gftt_select_smem(int cap, int max_corners, int occ_bytes);
-hipError_t launch_gftt(const GfttArgs& a, int max_area, int max_w, hipStream_t s);
+// scratch sizes for (rois, pixels): pixel blocks <= px/256 + rois, column blocks <= px/64 + rois
+inline int64_t gftt_max_blocks(int rois, int64_t px) { return px / kGfttBlock + rois; }
+inline int64_t gftt_max_cblocks(int rois, int64_t px) { return px / 64 + rois; }
+size_t gftt_select_smem(int cap, int max_corners, int img_bytes);
+void gftt_plan(GfttArgs& a, int max_area);  // sets cap and img_bytes
+hipError_t launch_gftt(const GfttArgs& a, hipStream_t s);
 }  // namespace tbdk

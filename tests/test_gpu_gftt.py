@@ -25,7 +25,8 @@ def check(frame, rois, c, n, maxc, q, md):
         assert np.array_equal(c[i, :n[i]], r), f"roi {i}: corners differ"
 
 
-@pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (1000, 0.01, 0.0), (64, 0.05, 8.0), (32, 0.3, 1.0)])
+@pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (1000, 0.01, 0.0), (64, 0.05, 8.0), (32, 0.3, 1.0),
+                                       (33, 0.02, 5.0), (300, 0.001, 2.5), (2000, 0.001, 6.5)])
 def test_gftt_rois_match_oracle(gpu, maxc, q, md):
     fr, gt = O.synth(20261015, 640, 480, 32, 0, 1)
     rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]

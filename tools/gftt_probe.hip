@@ -1,0 +1,150 @@
+// gftt_probe.hip — standalone phase timing of the GFTT launches on the bench's
+// frame-0 ground-truth boxes (1080p x 128 synthetic objects).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -I include tools/gftt_probe.hip -o build/gftt_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+__device__ unsigned long long* g_stamps;
+#define GFTT_STAMP(i)                                                                   \
+    do {                                                                                \
+        if (threadIdx.x == 0) g_stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+__device__ unsigned long long* g_tacc;
+#define GFTT_TDECL                      \
+    unsigned long long tacc_[6] = {0}; \
+    unsigned long long tlast_ = 0;      \
+    int tsteps_ = 0
+#define GFTT_T(i)                                                        \
+    do {                                                                 \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+        if ((i) > 0) tacc_[(i)-1] += t_ - tlast_;                         \
+        else tsteps_++;                                                  \
+        tlast_ = t_;                                                     \
+    } while (0)
+#define GFTT_TDUMP                                                                  \
+    do {                                                                            \
+        if (threadIdx.x == 0) {                                                     \
+            for (int q_ = 0; q_ < 5; ++q_) g_tacc[blockIdx.x * 8 + q_] = tacc_[q_]; \
+            g_tacc[blockIdx.x * 8 + 5] = tsteps_;                                   \
+        }                                                                           \
+    } while (0)
+#include "../opencv_amd/csrc/klt_gftt.hip"
+#include "../opencv_amd/csrc/synth_spec.h"
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e_ = (x);                                               \
+        if (e_ != hipSuccess) {                                            \
+            printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                      \
+        }                                                                  \
+    } while (0)
+
+int main()
+{
+    const int W = 1920, H = 1080, N = 128;
+    std::vector<syn_object> objs(N);
+    syn_make_objects(20261015u, W, H, N, objs.data());
+    std::vector<syn_pose> poses(N);
+    for (int o = 0; o < N; ++o) syn_pose_at(&objs[o], W, H, 0, &poses[o]);
+    std::vector<uint8_t> img((size_t)W * H);
+    const uint32_t bg = syn_hash(20261015u ^ 0xB6A5EEDU);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) img[(size_t)y * W + x] = syn_pixel(poses.data(), N, x, y, bg);
+    std::vector<tbdk::GfttRoi> rois;
+    int total = 0, max_area = 0, max_w = 0, nblk = 0, ncblk = 0;
+    for (int o = 0; o < N; ++o) {
+        int32_t b[4];
+        if (!syn_gt_box(&poses[o], W, H, b)) continue;
+        rois.push_back(tbdk::GfttRoi{b[0], b[1], b[2], b[3], total, nblk, ncblk});
+        nblk += (b[2] * b[3] + 255) / 256;
+        ncblk += (b[2] + 63) / 64;
+        total += b[2] * b[3];
+        max_area = std::max(max_area, b[2] * b[3]);
+        max_w = std::max(max_w, b[2]);
+    }
+    const int nroi = (int)rois.size();
+    uint8_t* dimg;
+    tbdk::GfttRoi* drois;
+    double* planes;
+    int *dmax, *dcc, *dcounts;  // per column-block max, per pixel-block count, per-ROI output
+    void* dcand;
+    float2* dcorners;
+    unsigned long long* dst;
+    CK(hipMalloc(&dimg, img.size()));
+    CK(hipMemcpy(dimg, img.data(), img.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&drois, sizeof(tbdk::GfttRoi) * nroi));
+    CK(hipMemcpy(drois, rois.data(), sizeof(tbdk::GfttRoi) * nroi, hipMemcpyHostToDevice));
+    CK(hipMalloc(&planes, (sizeof(double) * 3 + 4) * (size_t)total));
+    CK(hipMalloc(&dmax, 4 * ncblk));
+    CK(hipMalloc(&dcc, 4 * nblk));
+    CK(hipMalloc(&dcounts, 4 * nroi));
+    CK(hipMalloc(&dcand, 8 * 256 * (size_t)nblk));
+    CK(hipMalloc(&dcorners, sizeof(float2) * 256 * nroi));
+    CK(hipMalloc(&dst, 8 * 4 * nroi));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst)));
+    unsigned long long* dtacc;
+    CK(hipMalloc(&dtacc, 8 * 8 * nroi));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_tacc), &dtacc, sizeof(dtacc)));
+    tbdk::GfttArgs a;
+    a.img = dimg;
+    a.pitch = W;
+    a.rois = drois;
+    a.nroi = nroi;
+    a.nblk = nblk;
+    a.ncblk = ncblk;
+    a.rs0 = planes;
+    a.rs1 = planes + total;
+    a.rs2 = planes + 2 * (size_t)total;
+    a.eig = reinterpret_cast<float*>(planes + 3 * (size_t)total);
+    a.blk_max = dmax;
+    a.blk_cnt = dcc;
+    a.cand = dcand;
+    a.max_corners = 256;
+    a.quality = 0.01;
+    a.min_distance = 3.0;
+    a.corners = dcorners;
+    a.counts = dcounts;
+    tbdk::gftt_plan(a, max_area);
+    printf("cap %d img_bytes %d\n", a.cap, a.img_bytes);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int it = 0; it < 5; ++it) CK(tbdk::launch_gftt(a, 0));
+    CK(hipEventRecord(e0, 0));
+    const int reps = 20;
+    for (int it = 0; it < reps; ++it) CK(tbdk::launch_gftt(a, 0));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> st(4 * nroi);
+    std::vector<int> cc(nblk), cnt(nroi);
+    CK(hipMemcpy(st.data(), dst, 8 * 4 * nroi, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(cc.data(), dcc, 4 * nblk, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(cnt.data(), dcounts, 4 * nroi, hipMemcpyDeviceToHost));
+    double ph[3] = {0, 0, 0}, pm[3] = {0, 0, 0};
+    for (int r = 0; r < nroi; ++r)
+        for (int k = 0; k < 3; ++k) {
+            double d = (double)(st[4 * r + k + 1] - st[4 * r + k]);
+            ph[k] += d / nroi;
+            pm[k] = std::max(pm[k], d);
+        }
+    printf("nroi %d total px %d max_area %d: gftt %.1f us/launch\n", nroi, total, max_area, ms * 1000 / reps);
+    printf("select phases (s_memtime ticks) mean/max: load %.0f/%.0f sort %.0f/%.0f walk %.0f/%.0f\n", ph[0], pm[0],
+           ph[1], pm[1], ph[2], pm[2]);
+    long sc = 0, sa = 0;
+    for (int b = 0; b < nblk; ++b) sc += cc[b];
+    for (int r = 0; r < nroi; ++r) sa += cnt[r];
+    std::vector<unsigned long long> ta(8 * nroi);
+    CK(hipMemcpy(ta.data(), dtacc, 8 * 8 * nroi, hipMemcpyDeviceToHost));
+    double tm[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < nroi; ++r)
+        for (int q = 0; q < 6; ++q) tm[q] += (double)ta[8 * r + q] / nroi;
+    printf("walk sub-phases mean ticks: write %.0f window %.0f ballot/resolve %.0f limit %.0f store %.0f; steps %.1f\n",
+           tm[0], tm[1], tm[2], tm[3], tm[4], tm[5]);
+    printf("candidates mean %.1f accepted mean %.1f\n", (double)sc / nroi, (double)sa / nroi);
+    return 0;
+}
