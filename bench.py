@@ -147,7 +147,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     lk_pts = lk_it = klt_pts = ntr = redet = 0
-    h_wait = h_trk = 0.0
+    h_wait = h_trk = h_step = h_launch = 0.0
     for f in range(args.warmup, nframes):
         m = loop.step(frames[f], f, dets[f], stream)
         lk_pts += m.lk_points
@@ -157,6 +157,8 @@ def main():
         redet += m.redetected
         h_wait += m.host_wait_us
         h_trk += m.host_tracker_us
+        h_step += m.host_step_us
+        h_launch += m.host_launch_us
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
@@ -214,7 +216,8 @@ def main():
         "kernels": kstats,
         "per_frame": {"lk_points": lk_pts / args.steps, "tracked_points": klt_pts / args.steps,
                       "tracks": ntr / args.steps, "gftt_rois": redet / args.steps,
-                      "host_wait_us": h_wait / args.steps, "host_tracker_us": h_trk / args.steps},
+                      "host_wait_us": h_wait / args.steps, "host_tracker_us": h_trk / args.steps,
+                      "host_step_us": h_step / args.steps, "host_launch_us": h_launch / args.steps},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nb = min(nframes, 40)

@@ -213,6 +213,8 @@ typedef struct tbdk_frame_metrics {  /* per-frame TP/FN/FP/GT/c/sum d (tbd.hpp:1
     int64_t lk_iters;                /* Newton iterations over all levels (flop accounting) */
     float host_wait_us;              /* host time blocked on the device this step */
     float host_tracker_us;           /* host time in the tracker step (assignment + bookkeeping) */
+    float host_step_us;              /* host time in tbdk_tbd_step, end to end */
+    float host_launch_us;            /* host time issuing the pyramid / LK / fit work (before the sync) */
 } tbdk_frame_metrics;
 
 typedef struct tbdk_track_info {

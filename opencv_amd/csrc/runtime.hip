@@ -315,6 +315,69 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     return map_err(e);
 }
 
+namespace tbdk {
+
+int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tbdk_gftt_params* p, GfttRoi* tab,
+                 GfttPlan* plan)
+{
+    if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
+        return TBDK_EINVAL;
+    int64_t total = 0, nblk = 0, ncblk = 0;
+    int max_area = 0;
+    for (int i = 0; i < nroi; ++i) {
+        const tbdk_roi& r = rois[i];
+        if (r.x < 0 || r.y < 0 || r.width <= 0 || r.height <= 0 || r.x + r.width > width || r.y + r.height > height ||
+            r.width > 65535 || r.height > 65535)
+            return TBDK_EINVAL;
+        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)nblk, (int)ncblk};
+        total += (int64_t)r.width * r.height;
+        nblk += ((int64_t)r.width * r.height + kGfttBlock - 1) / kGfttBlock;
+        ncblk += (r.width + 63) / 64;
+        max_area = std::max(max_area, r.width * r.height);
+    }
+    if (total > INT32_MAX) return TBDK_EINVAL;
+    plan->nroi = nroi;
+    plan->total = total;
+    plan->nblk = (int)nblk;
+    plan->ncblk = (int)ncblk;
+    plan->max_area = max_area;
+    return TBDK_OK;
+}
+
+int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
+                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s)
+{
+    int rc = tbdk_gftt_reserve(ctx, plan.nroi, plan.total);
+    if (rc != TBDK_OK) return rc;
+    DeviceGuard g(ctx->device);
+    int rec = timing_begin(ctx, "gftt", s);
+    GfttArgs a;
+    a.img = img;
+    a.pitch = pitch;
+    a.rois = d_rois;
+    a.nroi = plan.nroi;
+    a.nblk = plan.nblk;
+    a.ncblk = plan.ncblk;
+    a.rs0 = static_cast<double*>(ctx->gftt_planes);
+    a.rs1 = a.rs0 + ctx->gftt_cap_px;
+    a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
+    a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
+    a.blk_cnt = ctx->gftt_blk;
+    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
+    a.cand = ctx->gftt_cand;
+    a.max_corners = p->max_corners;
+    a.quality = p->quality_level;
+    a.min_distance = p->min_distance;
+    a.corners = reinterpret_cast<float2*>(corners);
+    a.counts = counts;
+    gftt_plan(a, plan.max_area);
+    hipError_t e = launch_gftt(a, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+}  // namespace tbdk
+
 extern "C" {
 
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
@@ -347,52 +410,18 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     if (!ctx || !p || nroi < 0) return TBDK_EINVAL;
     if (nroi == 0) return TBDK_OK;
     if (!img || !rois || !corners || !counts || width <= 0 || height <= 0 || pitch < width) return TBDK_EINVAL;
-    if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
-        return TBDK_EINVAL;
+    GfttPlan plan;
     std::vector<GfttRoi> tab((size_t)nroi);
-    int64_t total = 0, nblk = 0, ncblk = 0;
-    int max_area = 0;
-    for (int i = 0; i < nroi; ++i) {
-        const tbdk_roi& r = rois[i];
-        if (r.x < 0 || r.y < 0 || r.width <= 0 || r.height <= 0 || r.x + r.width > width || r.y + r.height > height)
-            return TBDK_EINVAL;
-        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)nblk, (int)ncblk};
-        total += (int64_t)r.width * r.height;
-        nblk += ((int64_t)r.width * r.height + kGfttBlock - 1) / kGfttBlock;
-        ncblk += (r.width + 63) / 64;
-        max_area = std::max(max_area, r.width * r.height);
-    }
-    if (total > INT32_MAX) return TBDK_EINVAL;
-    int rc = tbdk_gftt_reserve(ctx, nroi > ctx->gftt_cap_rois ? nroi : ctx->gftt_cap_rois,
-                               total > ctx->gftt_cap_px ? total : ctx->gftt_cap_px);
+    int rc = gftt_prepare(rois, nroi, width, height, p, tab.data(), &plan);
+    if (rc != TBDK_OK) return rc;
+    rc = tbdk_gftt_reserve(ctx, nroi, plan.total);
     if (rc != TBDK_OK) return rc;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    int rec = timing_begin(ctx, "gftt", s);
+    // pageable source: the copy is staged and complete when the call returns
     hipError_t e = hipMemcpyAsync(ctx->gftt_rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
-    GfttArgs a;
-    a.img = img;
-    a.pitch = pitch;
-    a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
-    a.nroi = nroi;
-    a.nblk = (int)nblk;
-    a.ncblk = (int)ncblk;
-    a.rs0 = static_cast<double*>(ctx->gftt_planes);
-    a.rs1 = a.rs0 + ctx->gftt_cap_px;
-    a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
-    a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
-    a.blk_cnt = ctx->gftt_blk;
-    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
-    a.cand = ctx->gftt_cand;
-    a.max_corners = p->max_corners;
-    a.quality = p->quality_level;
-    a.min_distance = p->min_distance;
-    a.corners = reinterpret_cast<float2*>(corners);
-    a.counts = counts;
-    gftt_plan(a, max_area);
-    if (e == hipSuccess) e = launch_gftt(a, s);
-    timing_end(ctx, rec, s);
-    return map_err(e);
+    if (e != hipSuccess) return map_err(e);
+    return gftt_launch(ctx, img, pitch, static_cast<const GfttRoi*>(ctx->gftt_rois), plan, p, corners, counts, s);
 }
 
 int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int nobj, int t0, int nframes,

@@ -161,14 +161,19 @@ struct tbdk_tbd {
     FitOut* d_fit = nullptr;
     float2* d_corners = nullptr;
     int32_t* d_ccounts = nullptr;
+    int* d_post = nullptr;  // device mirror of h_post
     int* d_roi_slot = nullptr;
     int* d_clear = nullptr;
-    // pinned host (rewritten only after h2d_done has completed)
+    GfttRoi* d_tab = nullptr;
+    // pinned host staging (reuse rules: see tbdk_tbd_step)
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
+    // one pinned block uploaded with a single copy after the tracker step:
+    // [clear slots: S ints][ROI slots: S ints][GFTT ROI table: S GfttRoi]
+    int* h_post = nullptr;
     int* h_roi_slot = nullptr;
     int* h_clear = nullptr;
-    hipEvent_t h2d_done = nullptr;
+    GfttRoi* h_tab = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
     std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
@@ -187,11 +192,10 @@ int release(tbdk_tbd* t)
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_ents,
-                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_roi_slot, t->d_clear};
+                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_post};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    if (t->h2d_done) (void)hipEventDestroy(t->h2d_done);
-    void* host[] = {t->h_ents, t->h_fit, t->h_roi_slot, t->h_clear};
+    void* host[] = {t->h_ents, t->h_fit, t->h_post};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -272,13 +276,19 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     dm(reinterpret_cast<void**>(&t->d_fit), sizeof(FitOut) * S);
     dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
     dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
-    dm(reinterpret_cast<void**>(&t->d_roi_slot), sizeof(int) * S);
-    dm(reinterpret_cast<void**>(&t->d_clear), sizeof(int) * S);
+    const size_t post_bytes = 2 * sizeof(int) * S + sizeof(GfttRoi) * S;
+    dm(reinterpret_cast<void**>(&t->d_post), post_bytes);
     hm(reinterpret_cast<void**>(&t->h_ents), sizeof(FitEntry) * S);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
-    hm(reinterpret_cast<void**>(&t->h_roi_slot), sizeof(int) * S);
-    hm(reinterpret_cast<void**>(&t->h_clear), sizeof(int) * S);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->h2d_done, hipEventDisableTiming);
+    hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
+    if (t->h_post && t->d_post) {
+        t->h_clear = t->h_post;
+        t->h_roi_slot = t->h_post + S;
+        t->h_tab = reinterpret_cast<GfttRoi*>(t->h_post + 2 * S);
+        t->d_clear = t->d_post;
+        t->d_roi_slot = t->d_post + S;
+        t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 2 * S);
+    }
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -315,6 +325,8 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
                   tbdk_frame_metrics* metrics, void* stream)
 {
     if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width) return TBDK_EINVAL;
+    const auto t_step0 = std::chrono::steady_clock::now();
+    double launch_us = 0.0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const tbdk_tbd_config& c = t->cfg;
     tbdk_pyr& P = t->pyr[t->cur];
@@ -323,12 +335,14 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     if (rc != TBDK_OK) return rc;
     (void)hipSetDevice(t->ctx->device);
 
-    // pinned staging buffers are rewritten below: the previous frame's uploads must be done
+    // No host wait here: the pinned staging buffers written before this step's
+    // fit sync (h_ents) were last read by uploads issued before the previous
+    // step's sync, and those written after it (h_clear, h_roi_slot) are only
+    // rewritten after this step's sync, which orders every earlier upload.
+    // So this frame's pyramid / LK / fit queue up behind the previous GFTT.
     using clk = std::chrono::steady_clock;
-    auto tw0 = clk::now();
-    hipError_t ew = hipEventSynchronize(t->h2d_done);
-    double wait_us = std::chrono::duration<double, std::micro>(clk::now() - tw0).count();
-    if (ew != hipSuccess) return map_status(ew);
+    double wait_us = 0.0;
+    bool synced = false;  // has this step waited for the stream (see above)?
 
     // ---- KLT propagation of every live track
     std::vector<tbd::Track>& tracks = t->tracker->getTracks();
@@ -363,9 +377,11 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         timing_end(t->ctx, rec, s);
         e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
         auto ts0 = clk::now();
+        launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);
+        synced = true;
         for (int k = 0; k < nents; ++k) {
             const FitOut& o = t->h_fit[k];
             // map back: entries were filled in track order, skipping slotless tracks
@@ -397,6 +413,10 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     auto tt0 = clk::now();
     t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size());
     const double tracker_us = std::chrono::duration<double, std::micro>(clk::now() - tt0).count();
+    if (!synced) {  // no fit this step: order the previous step's uploads before reusing h_clear / h_roi_slot
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return map_status(e);
+    }
     int nclear = 0;
     for (unsigned id : t->tracker->deletedIds) {
         auto it = t->slot_of.find(id);
@@ -407,13 +427,6 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         }
         t->npts_of.erase(id);
     }
-    if (nclear > 0) {
-        hipError_t e = hipMemcpyAsync(t->d_clear, t->h_clear, sizeof(int) * nclear, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return map_status(e);
-        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, s, t->d_clear, nclear,
-                           t->slot_counts);
-    }
-
     // ---- corners for new tracks and tracks due for re-detection
     t->rois.clear();
     int nroi = 0;
@@ -445,21 +458,31 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
             t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
         }
     }
+    // ---- one upload (clear list, ROI slots, GFTT ROI table), then clear / GFTT / scatter
+    tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
+    GfttPlan plan;
     if (nroi > 0) {
-        tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
-        const tbdk_level& L0 = P.lv[0];
-        rc = tbdk_gftt_rois(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, c.width, c.height, L0.pitch,
-                            t->rois.data(), nroi, &gp, reinterpret_cast<float*>(t->d_corners), t->d_ccounts, stream);
+        rc = gftt_prepare(t->rois.data(), nroi, c.width, c.height, &gp, t->h_tab, &plan);
         if (rc != TBDK_OK) return rc;
-        hipError_t e = hipMemcpyAsync(t->d_roi_slot, t->h_roi_slot, sizeof(int) * nroi, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return map_status(e);
-        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, s, t->d_corners, t->d_ccounts,
-                           t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
-        e = hipGetLastError();
+    }
+    if (nclear > 0 || nroi > 0) {
+        const size_t bytes = nroi > 0 ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) -
+                                            reinterpret_cast<const uint8_t*>(t->h_post)
+                                      : sizeof(int) * nclear;
+        hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return map_status(e);
     }
-    {
-        hipError_t e = hipEventRecord(t->h2d_done, s);
+    if (nclear > 0)
+        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, s, t->d_clear, nclear,
+                           t->slot_counts);
+    if (nroi > 0) {
+        const tbdk_level& L0 = P.lv[0];
+        rc = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
+                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, s);
+        if (rc != TBDK_OK) return rc;
+        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, s, t->d_corners, t->d_ccounts,
+                           t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return map_status(e);
     }
     t->cur ^= 1;
@@ -482,6 +505,8 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         metrics->redetected = nroi;
         metrics->host_wait_us = (float)wait_us;
         metrics->host_tracker_us = (float)tracker_us;
+        metrics->host_launch_us = (float)launch_us;
+        metrics->host_step_us = (float)std::chrono::duration<double, std::micro>(clk::now() - t_step0).count();
     }
     return TBDK_OK;
 }

@@ -12,6 +12,16 @@ namespace tbdk {
 
 __host__ __device__ inline int align_up(int v, int a) { return (v + a - 1) / a * a; }
 
+// XCD-aware block remap (bijective for any grid size): blocks are dealt
+// round-robin over the 8 XCDs, so hardware block b runs on XCD group b % 8;
+// give each group a contiguous range of logical blocks so neighbouring work
+// (points of one track, rows of one image band) shares one XCD's L2.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg)
+{
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // Border width of every padded level: >= win + 1 so the LK window plus its
 // bilinear/Scharr neighbours never leaves the allocation.
 inline int level_pad(int win_w, int win_h)
@@ -136,5 +146,15 @@ inline int64_t gftt_max_blocks(int rois, int64_t px) { return px / kGfttBlock + 
 inline int64_t gftt_max_cblocks(int rois, int64_t px) { return px / 64 + rois; }
 size_t gftt_select_smem(int cap, int max_corners, int img_bytes);
 void gftt_plan(GfttArgs& a, int max_area);  // sets cap and img_bytes
+struct GfttPlan {
+    int nroi = 0, nblk = 0, ncblk = 0, max_area = 0;
+    int64_t total = 0;  // ROI pixels
+};
+// host side of tbdk_gftt_rois: validate and lay out the ROI table (tab: nroi entries)
+int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tbdk_gftt_params* p, GfttRoi* tab,
+                 GfttPlan* plan);
+// launches with a device-resident ROI table (uploaded by the caller on stream s)
+int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
+                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s);
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s);
 }  // namespace tbdk
