@@ -165,6 +165,36 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
                    float* corners, int32_t* counts, void* stream);
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
 
+/* ---- affine warp ------------------------------------------------------------ */
+
+/* interpolation flags / border modes: the reference's values
+ * (imgproc/include/opencv2/imgproc.hpp INTER_*, WARP_INVERSE_MAP;
+ *  core/include/opencv2/core/base.hpp BORDER_*) */
+#define TBDK_INTER_NEAREST 0
+#define TBDK_INTER_LINEAR 1
+#define TBDK_INTER_AREA 3            /* treated as INTER_LINEAR, as cv::warpAffine does */
+#define TBDK_WARP_INVERSE_MAP 16
+#define TBDK_BORDER_CONSTANT 0
+#define TBDK_BORDER_REPLICATE 1
+#define TBDK_BORDER_REFLECT 2
+#define TBDK_BORDER_WRAP 3
+#define TBDK_BORDER_REFLECT_101 4
+#define TBDK_BORDER_TRANSPARENT 5
+
+/* Replaces cv::cuda::warpAffine(src, dst, M, dsize, flags, borderMode, borderValue, stream)
+ * (modules/cudawarping/include/opencv2/cudawarping.hpp:126; impl cudawarping/src/warp.cpp:183-320)
+ * for CV_8UC1, with the numerics of the CPU cv::warpAffine
+ * (imgproc/src/imgwarp.cpp:2572-2682: 10-bit fixed-point map, 5-bit sub-pixel
+ * table, 15-bit bilinear weights) — bit-exact with it.
+ *   src, dst : device u8 images (row pitch in bytes); dst must not alias src
+ *   M        : HOST 2x3 row-major double matrix (dst <- src unless
+ *              TBDK_WARP_INVERSE_MAP, then dst -> src, as in the reference)
+ *   flags    : TBDK_INTER_NEAREST / LINEAR / AREA | TBDK_WARP_INVERSE_MAP
+ *   border   : TBDK_BORDER_*; border_value used by BORDER_CONSTANT */
+int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int src_height, int src_pitch,
+                        uint8_t* dst, int dst_width, int dst_height, int dst_pitch, const double* M,
+                        int flags, int border, int border_value, void* stream);
+
 /* ---- tracking-by-detection loop (one video stream per context) ------------ */
 
 /* Per-stream TBD loop: pyramid -> (GFTT on new / re-detect tracks) -> PyrLK over

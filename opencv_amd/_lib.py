@@ -137,6 +137,8 @@ SIGNATURES = {
     "tbdk_gftt_rois": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Roi), C.c_int,
                                  C.POINTER(GfttParams), C.c_void_p, C.c_void_p, C.c_void_p]),
     "tbdk_gftt_reserve": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
+    "tbdk_warp_affine_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                      C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "tbdk_tbd_default_config": (C.c_int, [C.c_int, C.c_int, C.POINTER(TbdConfig)]),
     "tbdk_tbd_create": (C.c_int, [C.c_void_p, C.POINTER(TbdConfig), C.POINTER(C.c_void_p)]),
     "tbdk_tbd_destroy": (C.c_int, [C.c_void_p]),

@@ -424,6 +424,41 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     return gftt_launch(ctx, img, pitch, static_cast<const GfttRoi*>(ctx->gftt_rois), plan, p, corners, counts, s);
 }
 
+int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int src_height, int src_pitch,
+                        uint8_t* dst, int dst_width, int dst_height, int dst_pitch, const double* M,
+                        int flags, int border, int border_value, void* stream)
+{
+    if (!ctx || !src || !dst || !M) return TBDK_EINVAL;
+    if (src_width <= 0 || src_height <= 0 || dst_width <= 0 || dst_height <= 0 || src_pitch < src_width ||
+        dst_pitch < dst_width || src_width > 32767 || src_height > 32767)  // reference: SHRT_MAX maps
+        return TBDK_EINVAL;
+    int inter = flags & 7;
+    if (inter == TBDK_INTER_AREA) inter = TBDK_INTER_LINEAR;
+    if ((inter != TBDK_INTER_NEAREST && inter != TBDK_INTER_LINEAR) || (flags & ~(7 | TBDK_WARP_INVERSE_MAP)))
+        return TBDK_EINVAL;
+    if (border < TBDK_BORDER_CONSTANT || border > TBDK_BORDER_TRANSPARENT) return TBDK_EINVAL;
+    // dst == src: the reference clones src (imgwarp.cpp:2595-2596); here aliasing is an error
+    const uint8_t* s0 = src;
+    const uint8_t* s1 = src + (size_t)(src_height - 1) * src_pitch + src_width;
+    const uint8_t* d0 = dst;
+    const uint8_t* d1 = dst + (size_t)(dst_height - 1) * dst_pitch + dst_width;
+    if (d0 < s1 && s0 < d1) return TBDK_EINVAL;
+    double minv[6];
+    if (flags & TBDK_WARP_INVERSE_MAP) {
+        for (int i = 0; i < 6; ++i) minv[i] = M[i];
+    } else {
+        invert_affine(M, minv);
+    }
+    const int cval = border_value < 0 ? 0 : (border_value > 255 ? 255 : border_value);  // saturate_cast<uchar>
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "warp_affine", s);
+    hipError_t e = launch_warp_affine(src, src_width, src_height, src_pitch, dst, dst_width, dst_height, dst_pitch,
+                                      minv, inter, border, cval, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
 int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int nobj, int t0, int nframes,
                       uint8_t* out, int pitch, int32_t* gt_boxes, void* stream)
 {

@@ -103,6 +103,11 @@ hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);
 bool lk_strip_supported(int win_w, int win_h);
 hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 
+// ---- affine warp (warp.hip) ----
+void invert_affine(const double* M, double* out);
+hipError_t launch_warp_affine(const uint8_t* src, int sw, int sh, int spitch, uint8_t* dst, int dw, int dh, int dpitch,
+                              const double* minv, int inter, int border, int cval, hipStream_t s);
+
 // ---- synthetic renderer (synth.hip) ----
 struct SynPoseDev;  // == syn_pose
 hipError_t launch_synth(const void* poses_dev, int nobj, uint32_t bgseed, int W, int H, int nframes,

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -140,6 +141,35 @@ def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torc
     _lib.check(ctx.lib.tbdk_pyr_down_u8(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
                                         C.c_void_p(dst.data_ptr()), dst.stride(0), _stream_ptr(stream)),
                "tbdk_pyr_down_u8")
+    return dst
+
+
+# interpolation flags / border modes (reference values, imgproc.hpp / core/base.hpp)
+INTER_NEAREST, INTER_LINEAR, INTER_AREA, WARP_INVERSE_MAP = 0, 1, 3, 16
+BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = range(6)
+
+
+def warp_affine(src: torch.Tensor, M, dsize, flags: int = INTER_LINEAR, borderMode: int = BORDER_CONSTANT,
+                borderValue: int = 0, dst: torch.Tensor | None = None, ctx: Context | None = None,
+                stream=None) -> torch.Tensor:
+    """cv::cuda::warpAffine(src, dst, M, dsize, flags, borderMode, borderValue) for CV_8UC1
+    (cudawarping.hpp:126) with the CPU cv::warpAffine's fixed-point numerics (bit-exact).
+    M: 2x3 (host array-like); dsize = (width, height).  `dst` may be passed to keep its
+    contents where BORDER_TRANSPARENT leaves pixels untouched."""
+    if src.dtype != torch.uint8 or src.dim() != 2 or not src.is_cuda or src.stride(1) != 1:
+        raise _lib.TbdkError("warp_affine expects a 2-D uint8 device tensor")
+    ctx = ctx or Context.get(src.device.index or 0)
+    dw, dh = int(dsize[0]), int(dsize[1])
+    if dst is None:
+        dst = torch.zeros((dh, dw), dtype=torch.uint8, device=src.device)
+    elif dst.shape != (dh, dw) or dst.dtype != torch.uint8 or dst.stride(1) != 1:
+        raise _lib.TbdkError("dst must be a (height, width) uint8 device tensor")
+    m = (C.c_double * 6)(*[float(v) for v in np.asarray(M, dtype=np.float64).reshape(6)])
+    h, w = src.shape
+    _lib.check(ctx.lib.tbdk_warp_affine_u8(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
+                                           C.c_void_p(dst.data_ptr()), dw, dh, dst.stride(0), m, int(flags),
+                                           int(borderMode), int(borderValue), _stream_ptr(stream)),
+               "tbdk_warp_affine_u8")
     return dst
 
 

@@ -105,3 +105,26 @@ void orc_min_eig(const uint8_t* img, int w, int h, int pitch, float* eig);
 #ifdef __cplusplus
 }
 #endif
+
+/* ---- warpAffine (oracle/warp_oracle.c) ---- */
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* border modes / flags: same values as the reference (core/include/opencv2/core/base.hpp,
+ * imgproc/include/opencv2/imgproc.hpp) */
+#define ORC_BORDER_CONSTANT 0
+#define ORC_BORDER_REPLICATE 1
+#define ORC_BORDER_REFLECT 2
+#define ORC_BORDER_WRAP 3
+#define ORC_BORDER_REFLECT_101 4
+#define ORC_BORDER_TRANSPARENT 5
+#define ORC_WARP_INVERSE_MAP 16
+int orc_border_interpolate(int p, int len, int border);
+void orc_invert_affine(const double* M, double* out);
+/* cv::warpAffine of a CV_8UC1 image; flags = INTER_NEAREST(0) / INTER_LINEAR(1) /
+ * INTER_AREA(3, as LINEAR) | WARP_INVERSE_MAP(16); returns -1 for other modes */
+int orc_warp_affine_u8(const uint8_t* src, int sw, int sh, int spitch, uint8_t* dst, int dw, int dh, int dpitch,
+                       const double* M, int flags, int border, int bval);
+#ifdef __cplusplus
+}
+#endif

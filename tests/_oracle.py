@@ -229,3 +229,38 @@ def gftt_rois(frame: np.ndarray, rois, max_corners=256, quality=0.01, min_distan
         c = gftt(frame[y:y + h, x:x + w], max_corners, quality, min_distance)
         res.append(c + np.float32([x, y]))
     return res
+
+
+# border modes / flags (reference values: core/base.hpp, imgproc.hpp)
+BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = range(6)
+INTER_NEAREST, INTER_LINEAR, INTER_AREA = 0, 1, 3
+WARP_INVERSE_MAP = 16
+
+
+def warp_affine(src: np.ndarray, M, dsize, flags=INTER_LINEAR, border=BORDER_CONSTANT, bval=0,
+                dst: np.ndarray | None = None) -> np.ndarray:
+    """cv::warpAffine for CV_8UC1 (oracle/warp_oracle.c). dsize = (width, height).
+    `dst` (optional) supplies the initial contents (BORDER_TRANSPARENT keeps them)."""
+    lib = load()
+    lib.orc_warp_affine_u8.restype = C.c_int
+    lib.orc_warp_affine_u8.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_int, C.c_int, C.c_int]
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dw, dh = dsize
+    out = np.zeros((dh, dw), np.uint8) if dst is None else np.ascontiguousarray(dst, dtype=np.uint8).copy()
+    m = np.ascontiguousarray(np.asarray(M, np.float64).reshape(6))
+    rc = lib.orc_warp_affine_u8(_ptr(src), sw, sh, src.strides[0], _ptr(out), dw, dh, out.strides[0], _ptr(m),
+                                flags, border, bval)
+    if rc != 0:
+        raise ValueError("unsupported warpAffine mode")
+    return out
+
+
+def invert_affine(M) -> np.ndarray:
+    lib = load()
+    lib.orc_invert_affine.argtypes = [C.c_void_p, C.c_void_p]
+    m = np.ascontiguousarray(np.asarray(M, np.float64).reshape(6))
+    out = np.zeros(6, np.float64)
+    lib.orc_invert_affine(_ptr(m), _ptr(out))
+    return out.reshape(2, 3)
