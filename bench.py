@@ -50,6 +50,23 @@ def pyr_bytes(w: int, h: int, nlevels: int) -> int:
     return sum(sizes[i] + sizes[i + 1] for i in range(nlevels - 1))
 
 
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/rNN_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes,
+    see tools/profile_round.sh).  None when no summary covers the kernel."""
+    d = os.path.join(ROOT, "profiles")
+    try:
+        files = sorted(f for f in os.listdir(d) if f.endswith("_pmc.json"))
+    except OSError:
+        return None, None
+    for f in reversed(files):
+        k = json.load(open(os.path.join(d, f)))["kernels"]
+        for name, v in k.items():
+            if kernel_substr in name and v.get("fetch_bytes") is not None and v.get("write_bytes") is not None:
+                return v["fetch_bytes"] + v["write_bytes"], f
+    return None, None
+
+
 def cpu_baseline(frames_host, gt, args, seconds: float):
     """The oracle (CPU restatement of the reference path) running the same
     per-frame KLT work: pyramid, GFTT in every box every `redetect` frames
@@ -180,8 +197,10 @@ def main():
         achieved = flops_per_launch / (lk["avg_us"] * 1e-6) / 1e12
     else:
         flops_per_launch, achieved = 0.0, 0.0
+    traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": None, "kernel": "lk_sparse",
+                "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic, "kernel": "lk_sparse",
+                "traffic_source": traffic_src,
                 "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA use; peak = fp32 vector rate; "
                         "algorithmic flops per SURVEY.md §8(d) with the measured iteration count",
                 "flops_per_launch": flops_per_launch,
@@ -192,6 +211,21 @@ def main():
     pyr_gbs = pb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build"}
+    # north_star's "HBM-read roofline on pyramid+PyrLK": SURVEY §8d bytes B_pyr + B_lk + N*21,
+    # with B_lk at its upper bound (2 full pyramids), over the two stages' summed time
+    w_, h_, lv_bytes = args.width, args.height, 0
+    for _ in range(nlev):
+        lv_bytes += w_ * h_
+        w_, h_ = (w_ + 1) // 2, (h_ + 1) // 2
+    b_lk = 2 * lv_bytes + 21 * (lk_pts / max(1, args.steps))
+    t_pl = ((pyr["avg_us"] or 0.0) + (lk["avg_us"] or 0.0)) * 1e-6
+    hbm_pl = (pb + b_lk) / t_pl / 1e9 if t_pl > 0 else 0.0
+    roof_pl = {"bound": "hbm", "achieved": round(hbm_pl, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+               "frac": round(hbm_pl / PEAK_HBM_GBS, 4), "bytes_per_frame": pb + b_lk,
+               "kernels": "pyr_build + lk_sparse",
+               "note": "B_lk taken at its SURVEY §8d upper bound (2 full pyramids); PyrLK is compute-bound "
+                       "(~360 flop/B vs ridge ~20), so this fraction is structurally small (DESIGN.md §3)"}
+
 
     steps_all = args.steps * world
     out = {
@@ -213,6 +247,7 @@ def main():
                    "tracker_bounds": args.bounds, "parallelism": f"replicas x{world} (one sequence per GPU)"},
         "roofline": roofline,
         "roofline_pyramid": roof_pyr,
+        "roofline_hbm_pyr_lk": roof_pl,
         "kernels": kstats,
         "per_frame": {"lk_points": lk_pts / args.steps, "tracked_points": klt_pts / args.steps,
                       "tracks": ntr / args.steps, "gftt_rois": redet / args.steps,

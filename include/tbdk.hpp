@@ -1,0 +1,276 @@
+// tbdk.hpp — header-only C++ facade over the C ABI (tbdk.h), shaped like the
+// reference's cv::cuda interfaces for this path so a caller of
+//   cv::cuda::SparsePyrLKOpticalFlow   (modules/cudaoptflow/include/opencv2/cudaoptflow.hpp:160-180)
+//   cv::cuda::CornersDetector          (modules/cudaimgproc/include/opencv2/cudaimgproc.hpp:570-604)
+//   cv::cuda::pyrDown / warpAffine     (modules/cudawarping/include/opencv2/cudawarping.hpp:126,201)
+// changes types, not call structure.  Differences from the reference:
+//   - images are non-owning device views (GpuImage) instead of GpuMat; the
+//     caller owns all device memory;
+//   - numerics follow the CPU reference (calcOpticalFlowPyrLK,
+//     goodFeaturesToTrack, warpAffine), not the CUDA module's float variants;
+//   - errors: tbdk::Error (a std::runtime_error carrying the TBDK_E* code)
+//     where the reference throws cv::Exception.
+#ifndef TBDK_HPP
+#define TBDK_HPP
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "tbdk.h"
+
+namespace tbdk {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string& what) : std::runtime_error(what + ": " + name(code)), code_(code) {}
+    int code() const { return code_; }
+    static const char* name(int code)
+    {
+        switch (code) {
+        case TBDK_EINVAL: return "TBDK_EINVAL (bad argument)";
+        case TBDK_EHIP: return "TBDK_EHIP (HIP runtime error)";
+        case TBDK_ENOMEM: return "TBDK_ENOMEM (device allocation failed)";
+        case TBDK_ENODEV: return "TBDK_ENODEV (no such device)";
+        default: return "unknown status";
+        }
+    }
+
+private:
+    int code_;
+};
+
+inline void check(int rc, const char* what)
+{
+    if (rc != TBDK_OK) throw Error(rc, what);
+}
+
+struct Size {
+    int width = 0, height = 0;
+};
+
+// Non-owning device u8 image view (GpuMat of CV_8UC1 analogue).
+struct GpuImage {
+    uint8_t* data = nullptr;
+    int width = 0, height = 0, pitch = 0;  // pitch in bytes
+};
+
+// One context per (host thread, device); owns GFTT scratch and timing records.
+class Context {
+public:
+    explicit Context(int device = 0) { check(tbdk_ctx_create(device, &h_), "tbdk_ctx_create"); }
+    ~Context() { tbdk_ctx_destroy(h_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    tbdk_ctx* get() const { return h_; }
+    int device() const { return tbdk_ctx_device(h_); }
+
+private:
+    tbdk_ctx* h_ = nullptr;
+};
+
+// Padded pyramid with Scharr derivative planes (buildOpticalFlowPyramid with
+// withDerivatives=true, video/src/lkpyramid.cpp:697-793).
+class Pyramid {
+public:
+    Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}) : ctx_(&ctx)
+    {
+        check(tbdk_pyr_create(ctx.get(), width, height, max_level, win.width, win.height, &p_), "tbdk_pyr_create");
+    }
+    ~Pyramid() { tbdk_pyr_destroy(ctx_->get(), &p_); }
+    Pyramid(const Pyramid&) = delete;
+    Pyramid& operator=(const Pyramid&) = delete;
+    void build(const GpuImage& img, void* stream = nullptr)
+    {
+        if (img.width != p_.lv[0].width || img.height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build");
+        check(tbdk_pyr_build(ctx_->get(), img.data, img.pitch, &p_, stream), "tbdk_pyr_build");
+    }
+    const tbdk_pyr& get() const { return p_; }
+    int levels() const { return p_.nlevels; }
+
+private:
+    Context* ctx_;
+    tbdk_pyr p_{};
+};
+
+namespace cuda {
+
+// cv::cuda::SparsePyrLKOpticalFlow (cudaoptflow.hpp:160-180; impl pyrlk.cpp:301-350).
+// Like the reference implementation object it caches the prev/next pyramids
+// (prevPyr_/nextPyr_, pyrlk.cpp:101-102) and rebuilds them per calc() on images.
+class SparsePyrLKOpticalFlow {
+public:
+    static std::unique_ptr<SparsePyrLKOpticalFlow> create(Context& ctx, Size winSize = {21, 21}, int maxLevel = 3,
+                                                          int iters = 30, bool useInitialFlow = false)
+    {
+        return std::unique_ptr<SparsePyrLKOpticalFlow>(
+            new SparsePyrLKOpticalFlow(ctx, winSize, maxLevel, iters, useInitialFlow));
+    }
+
+    Size getWinSize() const { return win_; }
+    void setWinSize(Size s) { win_ = s; pyr_[0].reset(); pyr_[1].reset(); }
+    int getMaxLevel() const { return max_level_; }
+    void setMaxLevel(int v) { max_level_ = v; pyr_[0].reset(); pyr_[1].reset(); }
+    int getNumIters() const { return iters_; }
+    void setNumIters(int v) { iters_ = v; }
+    bool getUseInitialFlow() const { return use_initial_flow_; }
+    void setUseInitialFlow(bool v) { use_initial_flow_ = v; }
+    // CPU-path extras (calcOpticalFlowPyrLK arguments): epsilon, flags, minEigThreshold
+    void setEpsilon(double e) { eps_ = e; }
+    void setMinEigThreshold(float t) { min_eig_ = t; }
+    void setGetMinEigenvals(bool v) { min_eig_flag_ = v; }
+
+    // calc(prevImg, nextImg, prevPts, nextPts, status, err, stream): all point
+    // buffers are device arrays of n entries (float2 points, u8 status, f32 err);
+    // err may be null (noArray()).
+    void calc(const GpuImage& prevImg, const GpuImage& nextImg, const float* prevPts, float* nextPts,
+              uint8_t* status, float* err, int n, void* stream = nullptr)
+    {
+        if (n == 0) return;  // reference: empty prevPts releases the outputs (pyrlk.cpp:221-227)
+        for (int i = 0; i < 2; ++i) {
+            const GpuImage& im = i == 0 ? prevImg : nextImg;
+            if (!pyr_[i] || pyr_[i]->get().lv[0].width != im.width || pyr_[i]->get().lv[0].height != im.height)
+                pyr_[i].reset(new Pyramid(*ctx_, im.width, im.height, max_level_, win_));
+            pyr_[i]->build(im, stream);
+        }
+        calc(*pyr_[0], *pyr_[1], prevPts, nextPts, status, err, n, stream);
+    }
+
+    // Pyramids given explicitly (calcOpticalFlowPyrLK accepts prebuilt pyramids,
+    // video/src/lkpyramid.cpp:1270-1324): the TBD loop reuses prev frame's.
+    void calc(const Pyramid& prev, const Pyramid& next, const float* prevPts, float* nextPts, uint8_t* status,
+              float* err, int n, void* stream = nullptr, int32_t* iters = nullptr)
+    {
+        tbdk_lk_params p;
+        p.win_w = win_.width;
+        p.win_h = win_.height;
+        p.max_level = max_level_;
+        p.max_count = iters_;
+        p.epsilon = eps_;
+        p.flags = (use_initial_flow_ ? TBDK_OPTFLOW_USE_INITIAL_FLOW : 0) |
+                  (min_eig_flag_ ? TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS : 0);
+        p.min_eig_threshold = min_eig_;
+        p.impl = 0;
+        check(tbdk_lk_sparse(ctx_->get(), &prev.get(), &next.get(), prevPts, nextPts, status, err, iters, n, &p,
+                             stream),
+              "tbdk_lk_sparse");
+    }
+
+private:
+    SparsePyrLKOpticalFlow(Context& ctx, Size win, int max_level, int iters, bool uif)
+        : ctx_(&ctx), win_(win), max_level_(max_level), iters_(iters), use_initial_flow_(uif)
+    {
+    }
+    Context* ctx_;
+    Size win_;
+    int max_level_, iters_;
+    bool use_initial_flow_;
+    double eps_ = 0.01;
+    float min_eig_ = 1e-4f;
+    bool min_eig_flag_ = false;
+    std::unique_ptr<Pyramid> pyr_[2];
+};
+
+// cv::cuda::CornersDetector from createGoodFeaturesToTrackDetector(CV_8UC1,
+// maxCorners, qualityLevel, minDistance, blockSize=3, useHarris=false)
+// (cudaimgproc.hpp:582,603-604).  detect() runs on the whole image; detectRois()
+// is the batched per-box form the TBD loop uses (one launch set for all boxes).
+class CornersDetector {
+public:
+    static std::unique_ptr<CornersDetector> create(Context& ctx, int maxCorners = 1000, double qualityLevel = 0.01,
+                                                   double minDistance = 0.0, int blockSize = 3,
+                                                   bool useHarrisDetector = false, double /*harrisK*/ = 0.04)
+    {
+        if (useHarrisDetector || blockSize != 3) throw Error(TBDK_EINVAL, "createGoodFeaturesToTrackDetector");
+        return std::unique_ptr<CornersDetector>(new CornersDetector(ctx, maxCorners, qualityLevel, minDistance));
+    }
+
+    // corners: device, maxCorners float2; count: device int32 (corners found, -1 on
+    // candidate overflow).  The count stays on the device (no host sync).
+    void detect(const GpuImage& image, float* corners, int32_t* count, void* stream = nullptr)
+    {
+        tbdk_roi r{0, 0, image.width, image.height};
+        detectRois(image, &r, 1, corners, count, stream);
+    }
+
+    // rois: host array; corners: device nroi x maxCorners float2; counts: device nroi int32
+    void detectRois(const GpuImage& image, const tbdk_roi* rois, int nroi, float* corners, int32_t* counts,
+                    void* stream = nullptr)
+    {
+        check(tbdk_gftt_rois(ctx_->get(), image.data, image.width, image.height, image.pitch, rois, nroi, &p_,
+                             corners, counts, stream),
+              "tbdk_gftt_rois");
+    }
+
+private:
+    CornersDetector(Context& ctx, int maxc, double q, double md) : ctx_(&ctx)
+    {
+        p_.max_corners = maxc;
+        p_.quality_level = q;
+        p_.min_distance = md;
+        p_.block_size = 3;
+    }
+    Context* ctx_;
+    tbdk_gftt_params p_{};
+};
+
+// cv::cuda::pyrDown (cudawarping.hpp:201): dst must be ((w+1)/2, (h+1)/2)
+inline void pyrDown(Context& ctx, const GpuImage& src, GpuImage& dst, void* stream = nullptr)
+{
+    if (dst.width != (src.width + 1) / 2 || dst.height != (src.height + 1) / 2) throw Error(TBDK_EINVAL, "pyrDown");
+    check(tbdk_pyr_down_u8(ctx.get(), src.data, src.width, src.height, src.pitch, dst.data, dst.pitch, stream),
+          "tbdk_pyr_down_u8");
+}
+
+// cv::cuda::warpAffine(src, dst, M, dsize, flags, borderMode, borderValue, stream)
+// (cudawarping.hpp:126); dsize is dst's size; M is a host 2x3 row-major matrix.
+inline void warpAffine(Context& ctx, const GpuImage& src, GpuImage& dst, const double M[6],
+                       int flags = TBDK_INTER_LINEAR, int borderMode = TBDK_BORDER_CONSTANT, int borderValue = 0,
+                       void* stream = nullptr)
+{
+    check(tbdk_warp_affine_u8(ctx.get(), src.data, src.width, src.height, src.pitch, dst.data, dst.width,
+                              dst.height, dst.pitch, M, flags, borderMode, borderValue, stream),
+          "tbdk_warp_affine_u8");
+}
+
+}  // namespace cuda
+
+// The tracking section of samples/gpu/tbd.cpp:624-706 (cv::tbd::Tracker +
+// KLT box propagation) for one video stream.
+class TbdLoop {
+public:
+    TbdLoop(Context& ctx, const tbdk_tbd_config& cfg) { check(tbdk_tbd_create(ctx.get(), &cfg, &h_), "tbdk_tbd_create"); }
+    ~TbdLoop() { tbdk_tbd_destroy(h_); }
+    TbdLoop(const TbdLoop&) = delete;
+    TbdLoop& operator=(const TbdLoop&) = delete;
+    static tbdk_tbd_config defaultConfig(int width, int height)
+    {
+        tbdk_tbd_config c;
+        check(tbdk_tbd_default_config(width, height, &c), "tbdk_tbd_default_config");
+        return c;
+    }
+    tbdk_frame_metrics step(const GpuImage& frame, int frameId, const std::vector<tbdk_detection>& dets,
+                            void* stream = nullptr)
+    {
+        tbdk_frame_metrics m;
+        check(tbdk_tbd_step(h_, frame.data, frame.pitch, frameId, dets.data(), (int)dets.size(), &m, stream),
+              "tbdk_tbd_step");
+        return m;
+    }
+    std::vector<tbdk_track_info> tracks() const
+    {
+        std::vector<tbdk_track_info> out(4096);
+        int n = 0;
+        check(tbdk_tbd_tracks(h_, out.data(), (int)out.size(), &n), "tbdk_tbd_tracks");
+        out.resize((size_t)(n < (int)out.size() ? n : (int)out.size()));
+        return out;
+    }
+
+private:
+    tbdk_tbd* h_ = nullptr;
+};
+
+}  // namespace tbdk
+
+#endif  // TBDK_HPP

@@ -1,0 +1,60 @@
+// facade_check.cpp — compiles the C++ facade (include/tbdk.hpp) against
+// libtbdk.so and exercises its host-only paths.  Exit code 0 = pass.
+//   no GPU : Context throws tbdk::Error(TBDK_ENODEV) — the product path fails loudly
+//   GPU    : a small pyramid + LK + GFTT + warp round trip through the facade
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "tbdk.hpp"
+
+int main(int argc, char** argv)
+{
+    const bool want_gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+    std::printf("%s\n", tbdk_version());
+    tbdk_tbd_config cfg = tbdk::TbdLoop::defaultConfig(1920, 1080);
+    if (cfg.win != 21 || cfg.max_level != 2 || cfg.bounds_xmax != 1280) return 2;
+    try {
+        tbdk::Context ctx(0);
+        if (!want_gpu) return 3;  // a context without a GPU must not exist
+        const int W = 320, H = 240;
+        std::vector<uint8_t> h((size_t)W * H);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) h[(size_t)y * W + x] = (uint8_t)((x * 7 + y * 13 + ((x / 9) ^ (y / 7)) * 40) & 255);
+        uint8_t *d0, *d1;
+        float *pts, *nxt, *corners;
+        uint8_t* st;
+        int32_t* cnt;
+        if (hipMalloc(&d0, h.size()) || hipMalloc(&d1, h.size()) || hipMalloc(&pts, 8 * 64) ||
+            hipMalloc(&nxt, 8 * 64) || hipMalloc(&st, 64) || hipMalloc(&corners, 8 * 64) || hipMalloc(&cnt, 4))
+            return 4;
+        (void)hipMemcpy(d0, h.data(), h.size(), hipMemcpyHostToDevice);
+        tbdk::GpuImage a{d0, W, H, W}, b{d1, W, H, W};
+        const double M[6] = {1, 0, 1.5, 0, 1, -0.5};  // b = a shifted by (1.5, -0.5)
+        tbdk::cuda::warpAffine(ctx, a, b, M, TBDK_INTER_LINEAR, TBDK_BORDER_REFLECT_101);
+        auto det = tbdk::cuda::CornersDetector::create(ctx, 64, 0.01, 5.0);
+        det->detect(a, corners, cnt);
+        int n = 0;
+        (void)hipMemcpy(&n, cnt, 4, hipMemcpyDeviceToHost);
+        if (n <= 0) return 5;
+        (void)hipMemcpy(pts, corners, 8 * (size_t)n, hipMemcpyDeviceToDevice);
+        auto lk = tbdk::cuda::SparsePyrLKOpticalFlow::create(ctx, {21, 21}, 2);
+        lk->calc(a, b, pts, nxt, st, nullptr, n);
+        std::vector<float> p0(2 * n), p1(2 * n);
+        std::vector<uint8_t> s(n);
+        (void)hipMemcpy(p0.data(), pts, 8 * (size_t)n, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(p1.data(), nxt, 8 * (size_t)n, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(s.data(), st, n, hipMemcpyDeviceToHost);
+        int good = 0;
+        for (int i = 0; i < n; ++i)
+            if (s[i] && std::abs(p1[2 * i] - p0[2 * i] - 1.5f) < 0.1f && std::abs(p1[2 * i + 1] - p0[2 * i + 1] + 0.5f) < 0.1f)
+                ++good;
+        std::printf("corners %d tracked-correctly %d\n", n, good);
+        return good * 10 >= n * 8 ? 0 : 6;
+    } catch (const tbdk::Error& e) {
+        std::printf("tbdk::Error: %s\n", e.what());
+        return (!want_gpu && e.code() == TBDK_ENODEV) ? 0 : 7;
+    }
+}
