@@ -256,6 +256,37 @@ typedef struct tbdk_track_info {
     double max_confidence, bbox_overlap;
 } tbdk_track_info;
 
+/* ---- the tracker alone (host only; no device, no context) ------------------
+ * cv::tbd::Tracker (modules/trackingbydetection/include/opencv2/tbd.hpp:119-184,
+ * src/tbd.cpp:182-1106) as a drop-in: performTrackingStep with an optional
+ * per-track predicted centroid that replaces Track::motionModel (tbd.hpp:111)
+ * for the tracks it names (the KLT box-propagation hook). */
+typedef struct tbdk_tracker tbdk_tracker;
+
+typedef struct tbdk_tracker_args {   /* cv::tbd::TbdArgs (tbd.hpp:25-41) + the bounds filter */
+    double cost_of_non_assignment;
+    int32_t time_window_size, track_age_threshold;   /* time_window_size <= 64 */
+    double track_visibility_threshold, track_confidence_threshold;
+    int32_t bounds_xmin, bounds_xmax, bounds_ymin, bounds_ymax;  /* reference: 0,1280,0,720 */
+} tbdk_tracker_args;
+
+typedef struct tbdk_prediction {
+    uint32_t track_id;
+    int32_t valid;                   /* 0: ignored (motion model used) */
+    double cx, cy;                   /* predicted box centre */
+} tbdk_prediction;
+
+/* defaults of samples/gpu/tbd.cpp:249-254 and the hard-coded filter (tbd.cpp:218) */
+int tbdk_tracker_default_args(tbdk_tracker_args* args);
+int tbdk_tracker_create(const tbdk_tracker_args* args, tbdk_tracker** out);
+int tbdk_tracker_destroy(tbdk_tracker* t);
+/* Tracker::performTrackingStep (tbd.cpp:210-286); metrics: tp, fn, fp, gt,
+ * matches, bbox_overlap and ntracks are filled, the KLT fields are 0. */
+int tbdk_tracker_step(tbdk_tracker* t, const tbdk_detection* dets, int ndets, int frame_id,
+                      const tbdk_prediction* preds, int npreds, tbdk_frame_metrics* metrics);
+/* current tracks in the tracker's order (npoints = 0); *n = number of tracks */
+int tbdk_tracker_tracks(const tbdk_tracker* t, tbdk_track_info* out, int cap, int* n);
+
 int tbdk_tbd_default_config(int width, int height, tbdk_tbd_config* cfg);
 int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out);
 int tbdk_tbd_destroy(tbdk_tbd* tbd);

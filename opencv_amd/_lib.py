@@ -117,6 +117,17 @@ class TrackInfo(C.Structure):
                 ("npoints", C.c_int32), ("max_confidence", C.c_double), ("bbox_overlap", C.c_double)]
 
 
+class TrackerArgs(C.Structure):
+    _fields_ = [("cost_of_non_assignment", C.c_double), ("time_window_size", C.c_int32),
+                ("track_age_threshold", C.c_int32), ("track_visibility_threshold", C.c_double),
+                ("track_confidence_threshold", C.c_double), ("bounds_xmin", C.c_int32), ("bounds_xmax", C.c_int32),
+                ("bounds_ymin", C.c_int32), ("bounds_ymax", C.c_int32)]
+
+
+class Prediction(C.Structure):
+    _fields_ = [("track_id", C.c_uint32), ("valid", C.c_int32), ("cx", C.c_double), ("cy", C.c_double)]
+
+
 # name -> (restype, argtypes); every symbol include/tbdk.h declares
 SIGNATURES = {
     "tbdk_version": (C.c_char_p, []),
@@ -139,6 +150,12 @@ SIGNATURES = {
     "tbdk_gftt_reserve": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
     "tbdk_warp_affine_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
                                       C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "tbdk_tracker_default_args": (C.c_int, [C.POINTER(TrackerArgs)]),
+    "tbdk_tracker_create": (C.c_int, [C.POINTER(TrackerArgs), C.POINTER(C.c_void_p)]),
+    "tbdk_tracker_destroy": (C.c_int, [C.c_void_p]),
+    "tbdk_tracker_step": (C.c_int, [C.c_void_p, C.POINTER(Detection), C.c_int, C.c_int, C.POINTER(Prediction), C.c_int,
+                                    C.POINTER(FrameMetrics)]),
+    "tbdk_tracker_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_tbd_default_config": (C.c_int, [C.c_int, C.c_int, C.POINTER(TbdConfig)]),
     "tbdk_tbd_create": (C.c_int, [C.c_void_p, C.POINTER(TbdConfig), C.POINTER(C.c_void_p)]),
     "tbdk_tbd_destroy": (C.c_int, [C.c_void_p]),

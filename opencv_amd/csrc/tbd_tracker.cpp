@@ -2,6 +2,11 @@
 // function (modules/trackingbydetection/src/tbd.cpp) whose behaviour it restates.
 #include "tbd_tracker.hpp"
 
+#include <cstring>
+#include <new>
+
+#include "../../include/tbdk.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -444,3 +449,115 @@ void Tracker::performTrackingStep(std::vector<Detection>& dets, int frame_id, co
 
 }  // namespace tbd
 }  // namespace tbdk
+
+// ---- host-only C ABI of the tracker (include/tbdk.h) ----
+struct tbdk_tracker {
+    tbdk::tbd::Tracker tracker;
+    std::vector<tbdk::tbd::Detection> dets;
+    std::vector<tbdk::tbd::Prediction> preds;
+    explicit tbdk_tracker(const tbdk::tbd::TbdArgs& a) : tracker(a) {}
+};
+
+extern "C" {
+
+int tbdk_tracker_default_args(tbdk_tracker_args* a)
+{
+    if (!a) return TBDK_EINVAL;
+    const tbdk::tbd::TbdArgs d;
+    a->cost_of_non_assignment = d.costOfNonAssignment;
+    a->time_window_size = (int32_t)d.timeWindowSize;
+    a->track_age_threshold = (int32_t)d.trackAgeThreshold;
+    a->track_visibility_threshold = d.trackVisibilityThreshold;
+    a->track_confidence_threshold = d.trackConfidenceThreshold;
+    a->bounds_xmin = d.boundsXmin;
+    a->bounds_xmax = d.boundsXmax;
+    a->bounds_ymin = d.boundsYmin;
+    a->bounds_ymax = d.boundsYmax;
+    return TBDK_OK;
+}
+
+int tbdk_tracker_create(const tbdk_tracker_args* a, tbdk_tracker** out)
+{
+    if (!a || !out || a->time_window_size <= 0 || a->time_window_size > (int)tbdk::tbd::kMaxTimeWindow ||
+        a->track_age_threshold < 0)
+        return TBDK_EINVAL;
+    tbdk::tbd::TbdArgs t;
+    t.costOfNonAssignment = a->cost_of_non_assignment;
+    t.timeWindowSize = (unsigned)a->time_window_size;
+    t.trackAgeThreshold = (unsigned)a->track_age_threshold;
+    t.trackVisibilityThreshold = a->track_visibility_threshold;
+    t.trackConfidenceThreshold = a->track_confidence_threshold;
+    t.boundsXmin = a->bounds_xmin;
+    t.boundsXmax = a->bounds_xmax;
+    t.boundsYmin = a->bounds_ymin;
+    t.boundsYmax = a->bounds_ymax;
+    *out = new (std::nothrow) tbdk_tracker(t);
+    return *out ? TBDK_OK : TBDK_ENOMEM;
+}
+
+int tbdk_tracker_destroy(tbdk_tracker* t)
+{
+    if (!t) return TBDK_EINVAL;
+    delete t;
+    return TBDK_OK;
+}
+
+int tbdk_tracker_step(tbdk_tracker* t, const tbdk_detection* dets, int ndets, int frame_id,
+                      const tbdk_prediction* preds, int npreds, tbdk_frame_metrics* m)
+{
+    if (!t || ndets < 0 || (ndets > 0 && !dets) || npreds < 0 || (npreds > 0 && !preds)) return TBDK_EINVAL;
+    t->dets.resize((size_t)ndets);
+    for (int i = 0; i < ndets; ++i) {
+        tbdk::tbd::Detection& d = t->dets[(size_t)i];
+        d.id = dets[i].id;
+        d.frame_id = frame_id;
+        d.bbox = tbdk::tbd::Rect(dets[i].x, dets[i].y, dets[i].width, dets[i].height);
+        d.confidence = dets[i].confidence;
+    }
+    t->preds.resize((size_t)npreds);
+    for (int i = 0; i < npreds; ++i)
+        t->preds[(size_t)i] = tbdk::tbd::Prediction{preds[i].track_id, preds[i].valid, preds[i].cx, preds[i].cy};
+    t->tracker.performTrackingStep(t->dets, frame_id, t->preds.data(), npreds);
+    if (m) {
+        std::memset(m, 0, sizeof(*m));
+        const tbdk::tbd::Tracker& k = t->tracker;
+        m->tp = k.truePositives.back();
+        m->fn = k.falseNegatives.back();
+        m->fp = k.falsePositives.back();
+        m->gt = k.groundTruths.back();
+        m->matches = k.numMatches.back();
+        m->bbox_overlap = k.bboxOverlap.back();
+        m->ntracks = (int32_t)t->tracker.getTracks().size();
+    }
+    return TBDK_OK;
+}
+
+int tbdk_tracker_tracks(const tbdk_tracker* t, tbdk_track_info* out, int cap, int* n)
+{
+    if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
+    const auto& tracks = const_cast<tbdk_tracker*>(t)->tracker.getTracks();
+    int k = 0;
+    for (const auto& tr : tracks) {
+        if (k >= cap) break;
+        tbdk_track_info& o = out[k++];
+        const tbdk::tbd::Rect& b = tr.bboxes.back();
+        o.id = tr.id;
+        o.x = b.x;
+        o.y = b.y;
+        o.width = b.width;
+        o.height = b.height;
+        o.pred_x = tr.predPosition.x;
+        o.pred_y = tr.predPosition.y;
+        o.pred_w = tr.predPosition.width;
+        o.pred_h = tr.predPosition.height;
+        o.age = (int32_t)tr.age;
+        o.total_visible = (int32_t)tr.totalVisibleCount;
+        o.npoints = 0;
+        o.max_confidence = tr.maxConfidence;
+        o.bbox_overlap = tr.bboxOverlap;
+    }
+    *n = (int)tracks.size();
+    return TBDK_OK;
+}
+
+}  // extern "C"
