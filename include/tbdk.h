@@ -165,6 +165,29 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
                    float* corners, int32_t* counts, void* stream);
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
 
+/* ---- KLT box propagation ----------------------------------------------------- */
+
+/* Result of fitting one box's tracked corners (prev -> next). */
+typedef struct tbdk_box_fit {
+    double m[6];                     /* 2x3 row-major [p -q tx; q p ty] */
+    double cx, cy;                   /* the box's integer centre (x + w/2, y + h/2) mapped by m */
+    int32_t npoints;                 /* correspondences used (status != 0) */
+    int32_t valid;                   /* npoints >= min_points, non-singular, scale in (0.5, 2) */
+} tbdk_box_fit;
+
+/* Batched similarity fit per box: the non-full-affine getRTMatrix of
+ * cv::estimateRigidTransform (video/src/lkpyramid.cpp:1398-1470) on each box's
+ * corner pairs, then the box centre mapped through it — the Track::motionModel
+ * (tbd.hpp:111) the TBD loop uses instead of constant velocity.
+ *   prev_pts, next_pts : device float2 arrays (all boxes' points, concatenated)
+ *   status             : device u8 per point (NULL = all used)
+ *   offsets            : device int32, nboxes + 1: box i owns points [offsets[i], offsets[i+1])
+ *   boxes              : device tbdk_roi per box
+ *   out                : device tbdk_box_fit per box */
+int tbdk_box_propagate(tbdk_ctx* ctx, const float* prev_pts, const float* next_pts, const uint8_t* status,
+                       const int32_t* offsets, const tbdk_roi* boxes, int nboxes, int min_points,
+                       tbdk_box_fit* out, void* stream);
+
 /* ---- affine warp ------------------------------------------------------------ */
 
 /* interpolation flags / border modes: the reference's values

@@ -117,6 +117,11 @@ class TrackInfo(C.Structure):
                 ("npoints", C.c_int32), ("max_confidence", C.c_double), ("bbox_overlap", C.c_double)]
 
 
+class BoxFit(C.Structure):
+    _fields_ = [("m", C.c_double * 6), ("cx", C.c_double), ("cy", C.c_double), ("npoints", C.c_int32),
+                ("valid", C.c_int32)]
+
+
 class TrackerArgs(C.Structure):
     _fields_ = [("cost_of_non_assignment", C.c_double), ("time_window_size", C.c_int32),
                 ("track_age_threshold", C.c_int32), ("track_visibility_threshold", C.c_double),
@@ -148,6 +153,8 @@ SIGNATURES = {
     "tbdk_gftt_rois": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(Roi), C.c_int,
                                  C.POINTER(GfttParams), C.c_void_p, C.c_void_p, C.c_void_p]),
     "tbdk_gftt_reserve": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
+    "tbdk_box_propagate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                     C.c_int, C.c_void_p, C.c_void_p]),
     "tbdk_warp_affine_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
                                       C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "tbdk_tracker_default_args": (C.c_int, [C.POINTER(TrackerArgs)]),

@@ -424,6 +424,21 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     return gftt_launch(ctx, img, pitch, static_cast<const GfttRoi*>(ctx->gftt_rois), plan, p, corners, counts, s);
 }
 
+int tbdk_box_propagate(tbdk_ctx* ctx, const float* prev_pts, const float* next_pts, const uint8_t* status,
+                       const int32_t* offsets, const tbdk_roi* boxes, int nboxes, int min_points,
+                       tbdk_box_fit* out, void* stream)
+{
+    if (!ctx || nboxes < 0) return TBDK_EINVAL;
+    if (nboxes == 0) return TBDK_OK;
+    if (!prev_pts || !next_pts || !offsets || !boxes || !out || min_points < 0) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "box_propagate", s);
+    hipError_t e = launch_box_propagate(prev_pts, next_pts, status, offsets, boxes, nboxes, min_points, out, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
 int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int src_height, int src_pitch,
                         uint8_t* dst, int dst_width, int dst_height, int dst_pitch, const double* M,
                         int flags, int border, int border_value, void* stream)

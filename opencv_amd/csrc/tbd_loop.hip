@@ -24,6 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "box_fit.hpp"
 #include "tbd_tracker.hpp"
 #include "tbdk_internal.hpp"
 
@@ -82,17 +83,6 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
     for (int off = 32; off >= 1; off >>= 1) it += __shfl_xor(it, off, 64);
     if (lane == 0) {
         slot_counts[E.slot] = m;
-        double s00 = 0, s02 = 0, s03 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-        for (int i = 0; i < m; ++i) {
-            const float ax = sa[i].x, ay = sa[i].y, bx = sb[i].x, by = sb[i].y;
-            s00 += ax * ax + ay * ay;
-            s02 += ax;
-            s03 += ay;
-            b0 += ax * bx + ay * by;
-            b1 += ax * by - ay * bx;
-            b2 += bx;
-            b3 += by;
-        }
         FitOut o;
         o.n = m;
         o.npts = cnt;
@@ -101,17 +91,12 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
         o.cx = o.cy = 0.0;
         o.scale = 0.0;
         if (m >= min_fit && m > 0) {
-            const double n = (double)m;
-            const double den = s00 - (s02 * s02 + s03 * s03) / n;
-            if (den > 1e-9) {
-                const double p = (b0 - (s02 * b2 + s03 * b3) / n) / den;
-                const double q = (b1 + (s03 * b2 - s02 * b3) / n) / den;
-                const double tx = (b2 - s02 * p + s03 * q) / n;
-                const double ty = (b3 - s03 * p - s02 * q) / n;
+            const SimilarityFit f = fit_similarity(sa, sb, m);
+            if (f.ok) {
                 const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
-                o.cx = p * cx0 - q * cy0 + tx;
-                o.cy = q * cx0 + p * cy0 + ty;
-                o.scale = sqrt(p * p + q * q);
+                o.cx = f.p * cx0 - f.q * cy0 + f.tx;
+                o.cy = f.q * cx0 + f.p * cy0 + f.ty;
+                o.scale = sqrt(f.p * f.p + f.q * f.q);
                 o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
             }
         }

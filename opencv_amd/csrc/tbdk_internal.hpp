@@ -103,6 +103,10 @@ hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);
 bool lk_strip_supported(int win_w, int win_h);
 hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 
+// ---- box propagation (box_fit.hip) ----
+hipError_t launch_box_propagate(const float* prev, const float* next, const uint8_t* status, const int32_t* offsets,
+                                const tbdk_roi* boxes, int nboxes, int min_points, tbdk_box_fit* out, hipStream_t s);
+
 // ---- affine warp (warp.hip) ----
 void invert_affine(const double* M, double* out);
 hipError_t launch_warp_affine(const uint8_t* src, int sw, int sh, int spitch, uint8_t* dst, int dw, int dh, int dpitch,
