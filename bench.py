@@ -50,6 +50,26 @@ def pyr_bytes(w: int, h: int, nlevels: int) -> int:
     return sum(sizes[i] + sizes[i + 1] for i in range(nlevels - 1))
 
 
+def max_over_ranks(value: float, world: int, device=None) -> float:
+    """Max of a per-rank wall time over all ranks (the contract's job time).
+    Collective only when world > 1; the tensor lives on `device` (cuda for
+    RCCL, cpu for gloo)."""
+    if world <= 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def replica_throughput(steps: int, world: int, max_elapsed: float) -> float:
+    """Whole-job frames/s: every rank runs its own sequence of `steps` frames
+    (replicas, weak scaling), all finished within the max-over-ranks time."""
+    return steps * world / max_elapsed
+
+
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/rNN_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes,
@@ -180,9 +200,7 @@ def main():
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(el, world, device="cuda")
 
     kstats = {}
     for name in ("pyr_build", "lk_sparse", "gftt", "tbd_fit"):
@@ -227,10 +245,9 @@ def main():
                        "(~360 flop/B vs ridge ~20), so this fraction is structurally small (DESIGN.md §3)"}
 
 
-    steps_all = args.steps * world
     out = {
         "metric": METRIC,
-        "value": round(steps_all / el, 2),
+        "value": round(replica_throughput(args.steps, world, el), 2),
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
