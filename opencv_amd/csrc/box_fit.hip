@@ -1,8 +1,8 @@
 // box_fit.hip — tbdk_box_propagate: per-box similarity fit from tracked
 // corner pairs + box-centre propagation (the KLT motion model of the TBD loop
 // as a standalone batched call).  One wave per box: tracked pairs are
-// compacted in point order into LDS 256 at a time (ballot + mbcnt), lane 0
-// accumulates the getRTMatrix sums (box_fit.hpp) and solves.
+// compacted in point order into LDS 256 at a time (ballot + mbcnt), the
+// getRTMatrix sums (box_fit.hpp) are accumulated wave-parallel and solved.
 #include "box_fit.hpp"
 #include "tbdk_internal.hpp"
 
@@ -22,7 +22,9 @@ __global__ __launch_bounds__(64) void box_propagate_kernel(const float2* __restr
     if (e >= nboxes) return;
     const int lane = threadIdx.x;
     const int beg = offsets[e], end = offsets[e + 1];
-    SimilaritySums sums;
+    // tracked pairs of the box, compacted in point order, summed wave-parallel
+    SimilaritySums part;
+    int used = 0;
     for (int c0 = beg; c0 < end; c0 += CH) {
         int m = 0;
         for (int j0 = c0; j0 < c0 + CH && j0 < end; j0 += 64) {
@@ -38,9 +40,19 @@ __global__ __launch_bounds__(64) void box_propagate_kernel(const float2* __restr
             m += __popcll(bal);
         }
         __syncthreads();
-        if (lane == 0) sums.add(sa, sb, m);
+        for (int i = lane; i < m; i += 64) part.add(sa + i, sb + i, 1);
+        used += m;
         __syncthreads();
     }
+    SimilaritySums sums;
+    sums.s00 = wave_sum_f64(part.s00);
+    sums.s02 = wave_sum_f64(part.s02);
+    sums.s03 = wave_sum_f64(part.s03);
+    sums.b0 = wave_sum_f64(part.b0);
+    sums.b1 = wave_sum_f64(part.b1);
+    sums.b2 = wave_sum_f64(part.b2);
+    sums.b3 = wave_sum_f64(part.b3);
+    sums.m = used;
     if (lane == 0) {
         tbdk_box_fit o;
         const SimilarityFit f = sums.solve();

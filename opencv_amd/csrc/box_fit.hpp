@@ -53,6 +53,34 @@ struct SimilaritySums {
     }
 };
 
+#if defined(__HIPCC__)
+__device__ __forceinline__ double wave_sum_f64(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Wave-parallel form: lane l sums pairs l, l+64, ... in order, then a fixed
+// xor-butterfly combines the 64 partial sums (deterministic; differs from the
+// sequential order only by double rounding, like the reference's own solve).
+__device__ inline SimilarityFit wave_fit_similarity(const float2* a, const float2* b, int m, int lane)
+{
+    SimilaritySums p;
+    for (int i = lane; i < m; i += 64) p.add(a + i, b + i, 1);
+    SimilaritySums s;
+    s.s00 = wave_sum_f64(p.s00);
+    s.s02 = wave_sum_f64(p.s02);
+    s.s03 = wave_sum_f64(p.s03);
+    s.b0 = wave_sum_f64(p.b0);
+    s.b1 = wave_sum_f64(p.b1);
+    s.b2 = wave_sum_f64(p.b2);
+    s.b3 = wave_sum_f64(p.b3);
+    s.m = m;
+    return s.solve();
+}
+#endif
+
 template <class P>
 __host__ __device__ inline SimilarityFit fit_similarity(P a, P b, int m)
 {

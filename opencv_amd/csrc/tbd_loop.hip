@@ -47,8 +47,8 @@ struct FitOut {
 };
 
 // One wave per live track.  Fit terms follow getRTMatrix's non-full-affine
-// branch: float products summed in double, in point order (one lane, so the
-// double rounding sequence is fixed and matches the oracle).
+// branch (float products summed in double), accumulated wave-parallel in a
+// fixed order (box_fit.hpp: wave_fit_similarity).
 __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict__ ents, int nents,
                                                      float2* __restrict__ slot_pts,
                                                      const float2* __restrict__ slot_next,
@@ -81,6 +81,7 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
     __syncthreads();
     for (int j = lane; j < m; j += 64) slot_pts[base + j] = sb[j];
     for (int off = 32; off >= 1; off >>= 1) it += __shfl_xor(it, off, 64);
+    const SimilarityFit f = wave_fit_similarity(sa, sb, m, lane);
     if (lane == 0) {
         slot_counts[E.slot] = m;
         FitOut o;
@@ -90,15 +91,12 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
         o.valid = 0;
         o.cx = o.cy = 0.0;
         o.scale = 0.0;
-        if (m >= min_fit && m > 0) {
-            const SimilarityFit f = fit_similarity(sa, sb, m);
-            if (f.ok) {
-                const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
-                o.cx = f.p * cx0 - f.q * cy0 + f.tx;
-                o.cy = f.q * cx0 + f.p * cy0 + f.ty;
-                o.scale = sqrt(f.p * f.p + f.q * f.q);
-                o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
-            }
+        if (m >= min_fit && m > 0 && f.ok) {
+            const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
+            o.cx = f.p * cx0 - f.q * cy0 + f.tx;
+            o.cy = f.q * cx0 + f.p * cy0 + f.ty;
+            o.scale = sqrt(f.p * f.p + f.q * f.q);
+            o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
         }
         out[e] = o;
     }
@@ -150,6 +148,11 @@ struct tbdk_tbd {
     int* d_roi_slot = nullptr;
     int* d_clear = nullptr;
     GfttRoi* d_tab = nullptr;
+    // post-tracker work (clear / GFTT / scatter) runs on `side`, so the next
+    // frame's pyramid, enqueued on the caller's stream, overlaps it; the
+    // caller's stream waits for `post_done` before its LK launch
+    hipStream_t side = nullptr;
+    hipEvent_t post_done = nullptr;
     // pinned host staging (reuse rules: see tbdk_tbd_step)
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
@@ -174,6 +177,9 @@ namespace {
 int release(tbdk_tbd* t)
 {
     if (!t) return TBDK_OK;
+    if (t->side) (void)hipStreamSynchronize(t->side);
+    if (t->post_done) (void)hipEventDestroy(t->post_done);
+    if (t->side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_ents,
@@ -274,6 +280,8 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         t->d_roi_slot = t->d_post + S;
         t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 2 * S);
     }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->post_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -319,6 +327,10 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     int rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, stream);
     if (rc != TBDK_OK) return rc;
     (void)hipSetDevice(t->ctx->device);
+    {  // the previous frame's clear / GFTT / scatter (on `side`) before this frame's LK
+        hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents) were last read by uploads issued before the previous
@@ -454,20 +466,24 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         const size_t bytes = nroi > 0 ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) -
                                             reinterpret_cast<const uint8_t*>(t->h_post)
                                       : sizeof(int) * nclear;
-        hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, s);
+        hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
         if (e != hipSuccess) return map_status(e);
     }
     if (nclear > 0)
-        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, s, t->d_clear, nclear,
+        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, t->side, t->d_clear, nclear,
                            t->slot_counts);
     if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
         rc = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
-                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, s);
+                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side);
         if (rc != TBDK_OK) return rc;
-        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, s, t->d_corners, t->d_ccounts,
+        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, t->side, t->d_corners, t->d_ccounts,
                            t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
         hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return map_status(e);
+    }
+    if (nclear > 0 || nroi > 0) {
+        hipError_t e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
     }
     t->cur ^= 1;
@@ -501,7 +517,9 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
     if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
     const auto& tracks = t->tracker->getTracks();
     std::vector<int32_t> counts((size_t)t->cfg.max_tracks);
-    hipError_t e = hipMemcpy(counts.data(), t->slot_counts, sizeof(int32_t) * counts.size(), hipMemcpyDeviceToHost);
+    (void)hipSetDevice(t->ctx->device);
+    hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work runs on the side stream
+    if (e == hipSuccess) e = hipMemcpy(counts.data(), t->slot_counts, sizeof(int32_t) * counts.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return map_status(e);
     int k = 0;
     for (const auto& tr : tracks) {
