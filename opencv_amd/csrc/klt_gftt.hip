@@ -8,23 +8,20 @@
 // -ffp-contract=off so every expression rounds exactly as written.
 //
 // Three launches, all ROIs of a frame batched in each:
-//   1. gftt_rowsum: one thread per ROI pixel: Sobel 3x3 (reflect-101 inside
-//                   the ROI) at x-1, x, x+1 -> cov = (Dx^2, DxDy, Dy^2) ->
-//                   the boxFilter's horizontal sums in double (RowSum ksize 3,
-//                   box_filter.simd.hpp:84-89), three double planes
-//   2. gftt_eig   : one thread per ROI column: the reference's running column
-//                   sum (ColumnSum, box_filter.simd.hpp:176-273) walked top to
-//                   bottom — loads of 8 rows are issued ahead of the dependent
-//                   add chain — then the min eigenvalue and a per-ROI max
-//   3. gftt_select: one 256-thread workgroup per ROI: threshold-to-zero at
-//                   max*q, 3x3 non-max test, candidates compacted into LDS,
-//                   bitonic sort by (value desc, address desc) — the
-//                   reference's deterministic tie-break (featureselect.cpp:56-64)
-//                   — then the greedy min-distance walk (:421-503) by one wave,
-//                   64 candidates per step: each lane tests its candidate
-//                   against the accepted list, in-batch conflicts become a
-//                   64-bit mask, and a scalar pass over the lanes in order
-//                   accepts exactly what the sequential walk would.
+//   1. gftt_eig   : one wave per 60-column strip of a ROI: Sobel 3x3
+//                   (reflect-101 inside the ROI) -> cov = (Dx^2, DxDy, Dy^2) ->
+//                   the boxFilter's row sums in double (neighbour columns by
+//                   DPP wave shifts) -> the reference's running ColumnSum walked
+//                   top to bottom -> min eigenvalue; per-strip max
+//   2. gftt_nms   : one thread per ROI pixel: threshold-to-zero at max*q,
+//                   3x3 dilate-equality, candidates to per-block slots
+//   3. gftt_select: one 512-thread workgroup per ROI: gather, sort by
+//                   (value desc, address desc) — the reference's deterministic
+//                   tie-break (featureselect.cpp:56-64) — then the greedy
+//                   min-distance walk (:421-503) by one wave, 64 candidates per
+//                   step over a byte image of the ROI; in-step conflicts are
+//                   resolved in lane order so exactly the sequential walk's
+//                   corners are accepted.
 #include <cfloat>
 
 #include "tbdk_internal.hpp"
@@ -52,35 +49,6 @@ __device__ __forceinline__ int fkey(float f)
 }
 __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
-struct Cov {
-    float c0, c1, c2;
-};
-
-// Sobel (deriv.cpp:414-465 -> sepFilter2D) of ROI column x, row y, then cov
-__device__ __forceinline__ Cov sobel_cov(const uint8_t* img, int pitch, const GfttRoi& R, int x, int y)
-{
-    const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
-    const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
-    const int xl = refl(x - 1, R.w), xr = refl(x + 1, R.w);
-    float rx[3], ry[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const uint8_t* s = img + (size_t)(R.y + refl(y + j - 1, R.h)) * pitch + R.x;
-        const float s0 = s[xl], s1 = s[x], s2 = s[xr];
-        float t = -1.f * s0;
-        t = t + 0.f * s1;
-        t = t + 1.f * s2;
-        rx[j] = t;
-        float u = k * s0;
-        u = u + k2 * s1;
-        u = u + k * s2;
-        ry[j] = u;
-    }
-    const float dx = (rx[0] + rx[2]) * k + (rx[1] * k2 + 0.f);
-    const float dy = (ry[2] - ry[0]) + 0.f;
-    return Cov{dx * dx, dx * dy, dy * dy};
-}
-
 }  // namespace
 
 // flat pixel grid over all ROIs: ROI r owns blocks [rois[r].blk, rois[r+1].blk)
@@ -106,85 +74,177 @@ __device__ __forceinline__ int roi_of_cblock(const GfttRoi* rois, int nroi, int 
     return lo;
 }
 
-__global__ __launch_bounds__(256) void gftt_rowsum_kernel(GfttArgs a)
+// DPP wave shifts (GFX9): lane i receives lane i-1 (shr) / lane i+1 (shl)
+__device__ __forceinline__ float from_left(float v)
 {
-    const int r = roi_of_block(a.rois, a.nroi, blockIdx.x);
-    const GfttRoi R = a.rois[r];
-    const int p = (blockIdx.x - R.blk) * blockDim.x + threadIdx.x;
-    if (p >= R.w * R.h) return;
-    const int y = p / R.w, x = p - y * R.w;
-    const Cov l = sobel_cov(a.img, a.pitch, R, refl(x - 1, R.w), y);
-    const Cov c = sobel_cov(a.img, a.pitch, R, x, y);
-    const Cov q = sobel_cov(a.img, a.pitch, R, refl(x + 1, R.w), y);
-    const size_t o = (size_t)R.off + p;
-    a.rs0[o] = (double)l.c0 + (double)c.c0 + (double)q.c0;
-    a.rs1[o] = (double)l.c1 + (double)c.c1 + (double)q.c1;
-    a.rs2[o] = (double)l.c2 + (double)c.c2 + (double)q.c2;
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_right(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
 }
 
+// Sobel rows of one image row at columns (x-1, x, x+1) in the reference's
+// filter-engine order (see oracle/gftt_oracle.c): rx = [-1 0 1], ry = [k 2k k]
+struct SobelRow {
+    float rx, ry;
+};
+__device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, float k, float k2)
+{
+    float t = -1.f * s0;
+    t = t + 0.f * s1;
+    t = t + 1.f * s2;
+    float u = k * s0;
+    u = u + k2 * s1;
+    u = u + k * s2;
+    return SobelRow{t, u};
+}
+
+struct RowSums {
+    double s0, s1, s2;
+};
+
+// Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 60-column strip of
+// a ROI per wave.  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
+// output, two halo lanes per side); each lane loads only its own pixel of a
+// row and gets its neighbours by DPP wave shifts, reflect-101 at the ROI edges
+// turning the missing neighbour into the other one.  Rows are walked top to
+// bottom so the column sums follow the reference's running ColumnSum exactly
+// (box_filter.simd.hpp:176-273): SUM = 0 + rs(-1); SUM += rs(0); per row y:
+// s = SUM + rs(y+1); out = (float)s; SUM = s - rs(y-1), rows reflect-101.
+// Image rows are loaded in batches of 8, one batch ahead of the walk.
 __global__ __launch_bounds__(64) void gftt_eig_kernel(GfttArgs a)
 {
-    constexpr int CH = 8;  // rows loaded ahead of the add chain
+    constexpr int B = 8;
     const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
     const GfttRoi R = a.rois[r];
-    const int x = (blockIdx.x - R.cblk) * 64 + threadIdx.x;
-    int best = INT_MIN;
-    if (x < R.w) {
-        const double* p0 = a.rs0 + R.off + x;
-        const double* p1 = a.rs1 + R.off + x;
-        const double* p2 = a.rs2 + R.off + x;
-        float* E = a.eig + R.off + x;
-        const size_t W = (size_t)R.w;
-        // ColumnSum: SUM = 0 + row(-1), SUM += row(0); per output y:
-        // s = SUM + row(y+1); out = (float)s; SUM = s - row(y-1)
-        const int rm1 = refl(-1, R.h);
-        double m1_0 = p0[rm1 * W], m1_1 = p1[rm1 * W], m1_2 = p2[rm1 * W];  // row y-1
-        double m0_0 = p0[0], m0_1 = p1[0], m0_2 = p2[0];                    // row y
-        double S0 = 0.0 + m1_0, S1 = 0.0 + m1_1, S2 = 0.0 + m1_2;
-        S0 = S0 + m0_0;
-        S1 = S1 + m0_1;
-        S2 = S2 + m0_2;
-        for (int y0 = 0; y0 < R.h; y0 += CH) {
-            double q0[CH], q1[CH], q2[CH];
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {  // independent loads of rows y0+1 .. y0+CH
-                const int yy = y0 + k + 1;
-                const size_t row = (size_t)refl(yy < R.h + 1 ? yy : R.h, R.h) * W;
-                q0[k] = p0[row];
-                q1[k] = p1[row];
-                q2[k] = p2[row];
-            }
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                const int y = y0 + k;
-                if (y < R.h) {
-                    const double t0 = S0 + q0[k], t1 = S1 + q1[k], t2 = S2 + q2[k];
-                    S0 = t0 - m1_0;
-                    S1 = t1 - m1_1;
-                    S2 = t2 - m1_2;
-                    m1_0 = m0_0;
-                    m1_1 = m0_1;
-                    m1_2 = m0_2;
-                    m0_0 = q0[k];
-                    m0_1 = q1[k];
-                    m0_2 = q2[k];
-                    const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
-                    const float t = aa - cc;
-                    const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-                    E[(size_t)y * W] = e;
-                    const int kk = fkey(e);
-                    best = kk > best ? kk : best;
-                }
-            }
+    const int lane = threadIdx.x;
+    const int xc = (blockIdx.x - R.cblk) * kGfttStrip - 2 + lane;  // this lane's ROI column
+    const bool out_lane = lane >= 2 && lane < 2 + kGfttStrip && xc < R.w;
+    const int x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
+    const bool at_left = x == 0, at_right = x == R.w - 1;
+    const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
+    const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
+    const uint8_t* col = a.img + (size_t)R.y * a.pitch + R.x + x;
+    const int H = R.h;
+    auto pix = [&](int yy) { return (float)col[(size_t)refl(yy, H) * a.pitch]; };
+    const int hm2 = H >= 2 ? H - 2 : 0;
+    auto pix_fwd = [&](int yy) {  // yy in [0, H]: branch-free reflect-101 of the one row past the end
+        return (float)col[(size_t)(yy < H ? yy : hm2) * a.pitch];
+    };
+    auto srow = [&](float v) {  // Sobel row terms of the pixel row whose own value is v
+        float l = from_left(v), rr = from_right(v);
+        const float l2 = at_left ? rr : l, r2 = at_right ? l : rr;
+        return sobel_row(at_left && at_right ? v : l2, v, at_left && at_right ? v : r2, k, k2);
+    };
+    auto sums = [&](const SobelRow& p, const SobelRow& c, const SobelRow& n) {
+        const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
+        const float dy = (n.ry - p.ry) + 0.f;
+        const float c0 = dx * dx, c1 = dx * dy, c2 = dy * dy;
+        float l0 = from_left(c0), l1 = from_left(c1), l2 = from_left(c2);
+        float r0 = from_right(c0), r1 = from_right(c1), r2 = from_right(c2);
+        if (at_left) {
+            l0 = at_right ? c0 : r0;
+            l1 = at_right ? c1 : r1;
+            l2 = at_right ? c2 : r2;
         }
+        if (at_right) {
+            r0 = at_left ? c0 : l0;
+            r1 = at_left ? c1 : l1;
+            r2 = at_left ? c2 : l2;
+        }
+        return RowSums{(double)l0 + (double)c0 + (double)r0, (double)l1 + (double)c1 + (double)r1,
+                       (double)l2 + (double)c2 + (double)r2};
+    };
+    // entering rows -1 (= cov row refl(-1), the box filter reflects cov rows) and 0
+    const int rm1 = refl(-1, H);
+    const RowSums em1 = sums(srow(pix(rm1 - 1)), srow(pix(rm1)), srow(pix(rm1 + 1)));
+    SobelRow wa = srow(pix(0)), wb = srow(pix(1));  // image rows y, y+1 for cov(y+1)
+    const RowSums e0 = sums(srow(pix(-1)), wa, wb);
+    double S0 = 0.0 + em1.s0, S1 = 0.0 + em1.s1, S2 = 0.0 + em1.s2;
+    S0 = S0 + e0.s0;
+    S1 = S1 + e0.s1;
+    S2 = S2 + e0.s2;
+    RowSums q0 = em1, q1 = e0;  // rs(y-1), rs(y)
+    float* E = a.eig + R.off + x;
+    int best = INT_MIN;
+    auto emit = [&](int y, double t0, double t1, double t2) {
+        const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
+        const float t = aa - cc;
+        const float e = (aa + cc) - sqrtf(bb * bb + t * t);
+        if (out_lane) {
+            E[(size_t)y * R.w] = e;
+            const int kk = fkey(e);
+            best = kk > best ? kk : best;
+        }
+    };
+    // full batches (every row y of the batch has y + 1 < H): straight-line code,
+    // so the independent Sobel / cov / row-sum / eigenvalue work of B rows
+    // interleaves around the short running-sum chain
+    float nxt[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) nxt[j] = pix_fwd(min(2 + j, H));
+    int y0 = 0;
+    for (; y0 + B < H; y0 += B) {
+        float cur[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+#pragma unroll
+        for (int j = 0; j < B; ++j) nxt[j] = pix_fwd(min(y0 + B + 2 + j, H));  // next batch in flight
+        SobelRow sr[B + 2];
+        sr[0] = wa;
+        sr[1] = wb;
+#pragma unroll
+        for (int j = 0; j < B; ++j) sr[j + 2] = srow(cur[j]);
+        RowSums en[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) en[j] = sums(sr[j], sr[j + 1], sr[j + 2]);
+        double t0[B], t1[B], t2[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {  // the sequential ColumnSum chain
+            t0[j] = S0 + en[j].s0;
+            t1[j] = S1 + en[j].s1;
+            t2[j] = S2 + en[j].s2;
+            S0 = t0[j] - q0.s0;
+            S1 = t1[j] - q0.s1;
+            S2 = t2[j] - q0.s2;
+            q0 = q1;
+            q1 = en[j];
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) emit(y0 + j, t0[j], t1[j], t2[j]);
+        wa = sr[B];
+        wb = sr[B + 1];
     }
-    // per-block max (minMaxLoc is order independent): wave reduction, one plain store
+    // tail: the last (<= B) rows, the final one entering rs(refl(h)) == rs(h - 2)
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+        const int y = y0 + j;
+        if (y >= H) break;
+        RowSums en;
+        if (y + 1 < H) {
+            const SobelRow wc = srow(nxt[j]);
+            en = sums(wa, wb, wc);
+            wa = wb;
+            wb = wc;
+        } else {
+            en = q0;
+        }
+        const double t0 = S0 + en.s0, t1 = S1 + en.s1, t2 = S2 + en.s2;
+        S0 = t0 - q0.s0;
+        S1 = t1 - q0.s1;
+        S2 = t2 - q0.s2;
+        q0 = q1;
+        q1 = en;
+        emit(y, t0, t1, t2);
+    }
+    // per-strip max (minMaxLoc is order independent): wave reduction, one plain store
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const int v = __shfl_xor(best, o);
         best = v > best ? v : best;
     }
-    if (threadIdx.x == 0) a.blk_max[blockIdx.x] = best;
+    if (lane == 0) a.blk_max[blockIdx.x] = best;
 }
 
 // Candidate sort key: the reference order (value desc, then address desc,
@@ -210,7 +270,8 @@ __global__ __launch_bounds__(256) void gftt_nms_kernel(GfttArgs a)
     }
     if (threadIdx.x == 0) lcount = 0;
     int mk = INT_MIN;  // ROI max = max of its column blocks' maxima
-    for (int b = R.cblk, e = R.cblk + (R.w + 63) / 64; b < e; ++b) mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
+    for (int b = R.cblk, e = R.cblk + (R.w + kGfttStrip - 1) / kGfttStrip; b < e; ++b)
+        mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
     const float thr = (float)((double)fkey_inv(mk) * a.quality);
     __syncthreads();
     bool keep = false;
@@ -576,7 +637,6 @@ void gftt_plan(GfttArgs& a, int max_area)
 
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(gftt_rowsum_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
     hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64), 0, s, a);
     hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);

@@ -332,7 +332,7 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
         tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)nblk, (int)ncblk};
         total += (int64_t)r.width * r.height;
         nblk += ((int64_t)r.width * r.height + kGfttBlock - 1) / kGfttBlock;
-        ncblk += (r.width + 63) / 64;
+        ncblk += (r.width + kGfttStrip - 1) / kGfttStrip;
         max_area = std::max(max_area, r.width * r.height);
     }
     if (total > INT32_MAX) return TBDK_EINVAL;
@@ -358,10 +358,7 @@ int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_r
     a.nroi = plan.nroi;
     a.nblk = plan.nblk;
     a.ncblk = plan.ncblk;
-    a.rs0 = static_cast<double*>(ctx->gftt_planes);
-    a.rs1 = a.rs0 + ctx->gftt_cap_px;
-    a.rs2 = a.rs0 + 2 * ctx->gftt_cap_px;
-    a.eig = reinterpret_cast<float*>(a.rs0 + 3 * ctx->gftt_cap_px);
+    a.eig = static_cast<float*>(ctx->gftt_planes);
     a.blk_cnt = ctx->gftt_blk;
     a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
     a.cand = ctx->gftt_cand;
@@ -396,7 +393,7 @@ int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
     const int64_t nb = gftt_max_blocks(rois, px), ncb = gftt_max_cblocks(rois, px);
     hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)std::max(rois, 1));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_blk), sizeof(int) * (size_t)(nb + ncb));
-    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_planes, (sizeof(double) * 3 + sizeof(float)) * (size_t)std::max<int64_t>(px, 1));
+    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_planes, sizeof(float) * (size_t)std::max<int64_t>(px, 1));
     if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, 8 * (size_t)kGfttBlock * (size_t)nb);
     if (e != hipSuccess) return map_err(e);
     ctx->gftt_cap_rois = rois;

@@ -47,7 +47,7 @@ struct tbdk_ctx {
     void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
     int* gftt_blk = nullptr;     // per-block ints: column-block maxima, pixel-block counts
     void* gftt_cand = nullptr;   // kGfttBlock candidate slots per pixel block
-    void* gftt_planes = nullptr;  // 3 x cap_px doubles (row sums) + cap_px floats (eig)
+    void* gftt_planes = nullptr;  // cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
 };
@@ -125,9 +125,10 @@ struct GfttRoi {
     int x, y, w, h;
     int off;  // first pixel of this ROI in the scratch planes
     int blk;   // first 256-pixel block of this ROI in the flat per-pixel grids
-    int cblk;  // first 64-column block of this ROI in the flat per-column grid
+    int cblk;  // first kGfttStrip-column strip of this ROI in the flat per-strip grid
 };
 constexpr int kGfttBlock = 256;
+constexpr int kGfttStrip = 60;  // output columns per wave of the eigenvalue walk (+2 halo lanes per side)
 struct GfttArgs {
     const uint8_t* img;
     int pitch;
@@ -135,10 +136,7 @@ struct GfttArgs {
     int nroi;
     int nblk;     // total blocks of the flat per-pixel grids
     int ncblk;    // total blocks of the flat per-column grid
-    double* rs0;  // boxFilter horizontal sums of (Dx^2, DxDy, Dy^2), per ROI pixel
-    double* rs1;
-    double* rs2;
-    float* eig;
+    float* eig;   // min eigenvalue per ROI pixel
     int* blk_max;   // per column block: max eigenvalue key
     int* blk_cnt;   // per pixel block: candidates found by the NMS block
     void* cand;     // per pixel block: kGfttBlock candidate slots (value, address key)
@@ -152,7 +150,7 @@ struct GfttArgs {
 constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
 // scratch sizes for (rois, pixels): pixel blocks <= px/256 + rois, column blocks <= px/64 + rois
 inline int64_t gftt_max_blocks(int rois, int64_t px) { return px / kGfttBlock + rois; }
-inline int64_t gftt_max_cblocks(int rois, int64_t px) { return px / 64 + rois; }
+inline int64_t gftt_max_cblocks(int rois, int64_t px) { return px / kGfttStrip + rois; }
 size_t gftt_select_smem(int cap, int max_corners, int img_bytes);
 void gftt_plan(GfttArgs& a, int max_area);  // sets cap and img_bytes
 struct GfttPlan {

@@ -60,7 +60,7 @@ int main()
         if (!syn_gt_box(&poses[o], W, H, b)) continue;
         rois.push_back(tbdk::GfttRoi{b[0], b[1], b[2], b[3], total, nblk, ncblk});
         nblk += (b[2] * b[3] + 255) / 256;
-        ncblk += (b[2] + 63) / 64;
+        ncblk += (b[2] + tbdk::kGfttStrip - 1) / tbdk::kGfttStrip;
         total += b[2] * b[3];
         max_area = std::max(max_area, b[2] * b[3]);
         max_w = std::max(max_w, b[2]);
@@ -95,10 +95,7 @@ int main()
     a.nroi = nroi;
     a.nblk = nblk;
     a.ncblk = ncblk;
-    a.rs0 = planes;
-    a.rs1 = planes + total;
-    a.rs2 = planes + 2 * (size_t)total;
-    a.eig = reinterpret_cast<float*>(planes + 3 * (size_t)total);
+    a.eig = reinterpret_cast<float*>(planes);
     a.blk_max = dmax;
     a.blk_cnt = dcc;
     a.cand = dcand;
