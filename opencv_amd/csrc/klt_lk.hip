@@ -45,9 +45,8 @@ size_t lk_smem_bytes(int win_w, int win_h)
 __global__ __launch_bounds__(64) void lk_sparse_kernel(LkArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int i = xcd_swizzle(blockIdx.x, gridDim.x);
-    if (i >= a.n) return;
-    if (a.seg_counts && i % a.seg_stride >= a.seg_counts[i / a.seg_stride]) return;
+    const int i = seg_point(a, xcd_swizzle(blockIdx.x, gridDim.x));
+    if (i < 0) return;
     const int lane = threadIdx.x;
     const int winW = a.win_w, winH = a.win_h, area = winW * winH;
     const int SW = winW + 3, SH = winH + 3, DW = winW + 1;

@@ -107,9 +107,8 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
     constexpr int R = (WH + G - 1) / G;  // patch rows per lane
     constexpr int GRP = R <= 4 ? 16 : (R <= 8 ? 8 : 4);  // exact-reduction group (see wave_sum_exact)
     const int lane = threadIdx.x & 63;
-    const int i = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    if (i >= a.n) return;  // wave-uniform
-    if (a.seg_counts && i % a.seg_stride >= a.seg_counts[i / a.seg_stride]) return;
+    const int i = seg_point(a, xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (i < 0) return;  // wave-uniform
 
     const int grp = lane / WW;
     const int x = lane - grp * WW;

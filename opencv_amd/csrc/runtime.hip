@@ -264,7 +264,7 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
 
 int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts,
                       float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
-                      const int32_t* seg_counts, int seg_stride, void* stream)
+                      const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list)
 {
     if (!ctx || !prev || !next || !p || n < 0) return TBDK_EINVAL;
     if (n == 0) return TBDK_OK;
@@ -300,8 +300,9 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     a.iters = iters;
     a.n = n;
     a.seg_counts = seg_counts;
+    a.seg_list = seg_list;
     a.seg_stride = seg_stride > 0 ? seg_stride : 1;
-    if (seg_counts && seg_stride <= 0) return TBDK_EINVAL;
+    if ((seg_counts && seg_stride <= 0) || (seg_list && !seg_counts)) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     bool have_d = true;

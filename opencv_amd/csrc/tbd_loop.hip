@@ -154,6 +154,12 @@ struct tbdk_tbd {
     hipStream_t side = nullptr;
     hipEvent_t post_done = nullptr;
     // pinned host staging (reuse rules: see tbdk_tbd_step)
+    // [fit entries: S FitEntry][LK slot lists: S int32 (unchanged sets, then refreshed ones)]
+    void* h_pre = nullptr;
+    void* d_pre = nullptr;
+    int32_t* h_lists = nullptr;
+    int32_t* d_lists = nullptr;
+    std::vector<char> refreshed;  // slot got new corners in the last post phase
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
     // one pinned block uploaded with a single copy after the tracker step:
@@ -182,11 +188,11 @@ int release(tbdk_tbd* t)
     if (t->side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
-    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_ents,
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre,
                    t->d_fit,    t->d_corners, t->d_ccounts,   t->d_post};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {t->h_ents, t->h_fit, t->h_post};
+    void* host[] = {t->h_pre, t->h_fit, t->h_post};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -263,13 +269,21 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     dm(reinterpret_cast<void**>(&t->slot_status), S * kSlotPts);
     dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * S * kSlotPts);
     dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * S);
-    dm(reinterpret_cast<void**>(&t->d_ents), sizeof(FitEntry) * S);
+    const size_t pre_bytes = (sizeof(FitEntry) + sizeof(int32_t)) * S;
+    dm(&t->d_pre, pre_bytes);
     dm(reinterpret_cast<void**>(&t->d_fit), sizeof(FitOut) * S);
     dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
     dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
     const size_t post_bytes = 2 * sizeof(int) * S + sizeof(GfttRoi) * S;
     dm(reinterpret_cast<void**>(&t->d_post), post_bytes);
-    hm(reinterpret_cast<void**>(&t->h_ents), sizeof(FitEntry) * S);
+    hm(&t->h_pre, pre_bytes);
+    if (t->h_pre && t->d_pre) {
+        t->h_ents = static_cast<FitEntry*>(t->h_pre);
+        t->h_lists = reinterpret_cast<int32_t*>(t->h_ents + S);
+        t->d_ents = static_cast<FitEntry*>(t->d_pre);
+        t->d_lists = reinterpret_cast<int32_t*>(t->d_ents + S);
+    }
+    t->refreshed.assign((size_t)S, 0);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
     hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
     if (t->h_post && t->d_post) {
@@ -327,10 +341,6 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     int rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, stream);
     if (rc != TBDK_OK) return rc;
     (void)hipSetDevice(t->ctx->device);
-    {  // the previous frame's clear / GFTT / scatter (on `side`) before this frame's LK
-        hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
-        if (e != hipSuccess) return map_status(e);
-    }
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents) were last read by uploads issued before the previous
@@ -341,33 +351,56 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     double wait_us = 0.0;
     bool synced = false;  // has this step waited for the stream (see above)?
 
-    // ---- KLT propagation of every live track
+    // ---- KLT propagation of every live track.  Slots whose point set the previous
+    // frame's post-tracker work (on `side`) leaves untouched are tracked first,
+    // overlapping that work; the refreshed ones after it completes.
     std::vector<tbd::Track>& tracks = t->tracker->getTracks();
-    int nents = 0, klt_points = 0, klt_pred = 0, hi_slot = 0, lk_points = 0;
+    int nents = 0, klt_points = 0, klt_pred = 0, lk_points = 0, nA = 0, nB = 0;
     int64_t lk_iters = 0;
-    for (const auto& kv : t->slot_of) hi_slot = std::max(hi_slot, kv.second + 1);
     t->preds.clear();
-    if (c.use_klt && t->have_prev && !tracks.empty()) {
+    const bool run_klt = c.use_klt && t->have_prev && !tracks.empty();
+    tbdk_lk_params lp;
+    lp.win_w = lp.win_h = c.win;
+    lp.max_level = c.max_level;
+    lp.max_count = c.lk_iters;
+    lp.epsilon = c.lk_epsilon;
+    lp.flags = 0;
+    lp.min_eig_threshold = c.min_eig_threshold;
+    lp.impl = 0;
+    if (run_klt) {
+        const int S = c.max_tracks;
         for (const auto& tr : tracks) {
             auto it = t->slot_of.find(tr.id);
             if (it == t->slot_of.end()) continue;
             const tbd::Rect& b = tr.bboxes.back();
             t->h_ents[nents++] = FitEntry{it->second, b.x, b.y, b.width, b.height};
+            if (t->refreshed[(size_t)it->second]) t->h_lists[S - 1 - nB++] = it->second;  // from the end
+            else t->h_lists[nA++] = it->second;
         }
-        tbdk_lk_params lp;
-        lp.win_w = lp.win_h = c.win;
-        lp.max_level = c.max_level;
-        lp.max_count = c.lk_iters;
-        lp.epsilon = c.lk_epsilon;
-        lp.flags = 0;
-        lp.min_eig_threshold = c.min_eig_threshold;
-        lp.impl = 0;
-        rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
-                         reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                         hi_slot * kSlotPts, &lp, t->slot_counts, kSlotPts, stream);
-        if (rc != TBDK_OK) return rc;
-        hipError_t e = hipMemcpyAsync(t->d_ents, t->h_ents, sizeof(FitEntry) * nents, hipMemcpyHostToDevice, s);
+        for (int k = 0; k < nB; ++k) t->h_lists[nA + k] = t->h_lists[S - 1 - k];
+        const size_t bytes = sizeof(FitEntry) * S + sizeof(int32_t) * (size_t)(nA + nB);
+        hipError_t e = hipMemcpyAsync(t->d_pre, t->h_pre, bytes, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return map_status(e);
+        if (nA > 0) {
+            rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
+                             reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                             nA * kSlotPts, &lp, t->slot_counts, kSlotPts, stream, t->d_lists);
+            if (rc != TBDK_OK) return rc;
+        }
+    }
+    std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
+    {  // the previous frame's clear / GFTT / scatter (on `side`) before the refreshed sets
+        hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
+    if (run_klt) {
+        if (nB > 0) {
+            rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
+                             reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                             nB * kSlotPts, &lp, t->slot_counts, kSlotPts, stream, t->d_lists + nA);
+            if (rc != TBDK_OK) return rc;
+        }
+        hipError_t e;
         int rec = timing_begin(t->ctx, "tbd_fit", s);
         hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
@@ -452,6 +485,7 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
                 t->rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
             t->h_roi_slot[nroi++] = slot;
+            t->refreshed[(size_t)slot] = 1;
             t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
         }
     }

@@ -77,8 +77,10 @@ struct LkLevel {
 struct LkArgs {
     LkLevel lv[TBDK_MAX_LEVELS];
     // optional segmented layout: point i = seg * seg_stride + j is valid iff
-    // j < seg_counts[seg]; invalid points are skipped (outputs untouched)
+    // j < seg_counts[seg]; invalid points are skipped (outputs untouched).
+    // With seg_list, launch index k runs segment seg_list[k / seg_stride].
     const int32_t* seg_counts;
+    const int32_t* seg_list;
     int seg_stride;
     int max_level, win_w, win_h, max_count, flags, n;
     double eps2;
@@ -90,10 +92,20 @@ struct LkArgs {
     int32_t* iters;
 };
 
+// launch index -> point index under the segmented layout, -1 if none
+__device__ __forceinline__ int seg_point(const LkArgs& a, int k)
+{
+    if (k >= a.n) return -1;
+    if (!a.seg_counts) return k;
+    const int seg = k / a.seg_stride, j = k - seg * a.seg_stride;
+    const int s = a.seg_list ? a.seg_list[seg] : seg;
+    return j < a.seg_counts[s] ? s * a.seg_stride + j : -1;
+}
+
 // argument checking + kernel choice shared by tbdk_lk_sparse and the TBD loop
 int lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts, float* next_pts,
                 uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
-                const int32_t* seg_counts, int seg_stride, void* stream);
+                const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list = nullptr);
 int map_status(hipError_t e);
 
 size_t lk_smem_bytes(int win_w, int win_h);
