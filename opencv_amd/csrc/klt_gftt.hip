@@ -105,87 +105,76 @@ struct RowSums {
 };
 
 // Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 60-column strip of
-// a ROI per wave.  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
+// a ROI per workgroup of three waves, wave c carrying cov channel c
+// (Dx^2, DxDy, Dy^2).  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
 // output, two halo lanes per side); each lane loads only its own pixel of a
 // row and gets its neighbours by DPP wave shifts, reflect-101 at the ROI edges
 // turning the missing neighbour into the other one.  Rows are walked top to
-// bottom so the column sums follow the reference's running ColumnSum exactly
-// (box_filter.simd.hpp:176-273): SUM = 0 + rs(-1); SUM += rs(0); per row y:
-// s = SUM + rs(y+1); out = (float)s; SUM = s - rs(y-1), rows reflect-101.
-// Image rows are loaded in batches of 8, one batch ahead of the walk.
-__global__ __launch_bounds__(64) void gftt_eig_kernel(GfttArgs a)
+// bottom so each channel's column sum follows the reference's running
+// ColumnSum exactly (box_filter.simd.hpp:176-273): SUM = 0 + rs(-1);
+// SUM += rs(0); per row y: s = SUM + rs(y+1); out = (float)s; SUM = s - rs(y-1),
+// rows reflect-101.  Per batch of 8 rows the three (float) box sums meet in LDS
+// and the waves share the eigenvalue work (rows j = c mod 3 of the batch).
+constexpr int kEigBatch = 16;  // rows per batch of the eigenvalue walk
+
+template <int CH>
+__device__ __forceinline__ void eig_walk(const GfttArgs& a, const GfttRoi& R, float (*box)[3][kEigBatch][64],
+                                         int* smax)
 {
-    constexpr int B = 8;
-    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
-    const GfttRoi R = a.rois[r];
-    const int lane = threadIdx.x;
+    constexpr int B = kEigBatch;
+    const int lane = threadIdx.x & 63;
     const int xc = (blockIdx.x - R.cblk) * kGfttStrip - 2 + lane;  // this lane's ROI column
     const bool out_lane = lane >= 2 && lane < 2 + kGfttStrip && xc < R.w;
     const int x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
     const bool at_left = x == 0, at_right = x == R.w - 1;
     const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
     const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
-    const uint8_t* col = a.img + (size_t)R.y * a.pitch + R.x + x;
     const int H = R.h;
-    auto pix = [&](int yy) { return (float)col[(size_t)refl(yy, H) * a.pitch]; };
     const int hm2 = H >= 2 ? H - 2 : 0;
-    auto pix_fwd = [&](int yy) {  // yy in [0, H]: branch-free reflect-101 of the one row past the end
-        return (float)col[(size_t)(yy < H ? yy : hm2) * a.pitch];
-    };
+    // pixel rows through buffer loads: lane offset x in a VGPR, row offset in an SGPR
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.img + (size_t)R.y * a.pitch + R.x), (short)0, a.pitch * H, 0x00020000);
+    auto ld = [&](int row) { return (float)__builtin_amdgcn_raw_buffer_load_b8(rs, x, row * a.pitch, 0); };
+    auto pix = [&](int yy) { return ld(refl(yy, H)); };
+    auto pix_fwd = [&](int yy) { return ld(yy < H ? yy : hm2); };  // yy in [0, H]
     auto srow = [&](float v) {  // Sobel row terms of the pixel row whose own value is v
-        float l = from_left(v), rr = from_right(v);
+        const float l = from_left(v), rr = from_right(v);
         const float l2 = at_left ? rr : l, r2 = at_right ? l : rr;
         return sobel_row(at_left && at_right ? v : l2, v, at_left && at_right ? v : r2, k, k2);
     };
-    auto sums = [&](const SobelRow& p, const SobelRow& c, const SobelRow& n) {
-        const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
-        const float dy = (n.ry - p.ry) + 0.f;
-        const float c0 = dx * dx, c1 = dx * dy, c2 = dy * dy;
-        float l0 = from_left(c0), l1 = from_left(c1), l2 = from_left(c2);
-        float r0 = from_right(c0), r1 = from_right(c1), r2 = from_right(c2);
-        if (at_left) {
-            l0 = at_right ? c0 : r0;
-            l1 = at_right ? c1 : r1;
-            l2 = at_right ? c2 : r2;
+    // channel CH of cov, then its boxFilter row sum ((l + c) + r in double)
+    auto rsum = [&](const SobelRow& p, const SobelRow& c, const SobelRow& n) {
+        float cv;
+        if constexpr (CH == 0) {
+            const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
+            cv = dx * dx;
+        } else if constexpr (CH == 1) {
+            const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
+            const float dy = (n.ry - p.ry) + 0.f;
+            cv = dx * dy;
+        } else {
+            const float dy = (n.ry - p.ry) + 0.f;
+            cv = dy * dy;
         }
-        if (at_right) {
-            r0 = at_left ? c0 : l0;
-            r1 = at_left ? c1 : l1;
-            r2 = at_left ? c2 : l2;
-        }
-        return RowSums{(double)l0 + (double)c0 + (double)r0, (double)l1 + (double)c1 + (double)r1,
-                       (double)l2 + (double)c2 + (double)r2};
+        float l = from_left(cv), rr = from_right(cv);
+        if (at_left) l = at_right ? cv : rr;
+        if (at_right) rr = at_left ? cv : l;
+        return (double)l + (double)cv + (double)rr;
     };
-    // entering rows -1 (= cov row refl(-1), the box filter reflects cov rows) and 0
+    // entering rows -1 (= cov row refl(-1): the box filter reflects cov rows) and 0
     const int rm1 = refl(-1, H);
-    const RowSums em1 = sums(srow(pix(rm1 - 1)), srow(pix(rm1)), srow(pix(rm1 + 1)));
+    const double em1 = rsum(srow(pix(rm1 - 1)), srow(pix(rm1)), srow(pix(rm1 + 1)));
     SobelRow wa = srow(pix(0)), wb = srow(pix(1));  // image rows y, y+1 for cov(y+1)
-    const RowSums e0 = sums(srow(pix(-1)), wa, wb);
-    double S0 = 0.0 + em1.s0, S1 = 0.0 + em1.s1, S2 = 0.0 + em1.s2;
-    S0 = S0 + e0.s0;
-    S1 = S1 + e0.s1;
-    S2 = S2 + e0.s2;
-    RowSums q0 = em1, q1 = e0;  // rs(y-1), rs(y)
+    const double e0 = rsum(srow(pix(-1)), wa, wb);
+    double S = 0.0 + em1;
+    S = S + e0;
+    double q0 = em1, q1 = e0;  // rs(y-1), rs(y)
     float* E = a.eig + R.off + x;
     int best = INT_MIN;
-    auto emit = [&](int y, double t0, double t1, double t2) {
-        const float aa = (float)t0 * 0.5f, bb = (float)t1, cc = (float)t2 * 0.5f;
-        const float t = aa - cc;
-        const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-        if (out_lane) {
-            E[(size_t)y * R.w] = e;
-            const int kk = fkey(e);
-            best = kk > best ? kk : best;
-        }
-    };
-    // full batches (every row y of the batch has y + 1 < H): straight-line code,
-    // so the independent Sobel / cov / row-sum / eigenvalue work of B rows
-    // interleaves around the short running-sum chain
     float nxt[B];
 #pragma unroll
     for (int j = 0; j < B; ++j) nxt[j] = pix_fwd(min(2 + j, H));
-    int y0 = 0;
-    for (; y0 + B < H; y0 += B) {
+    for (int y0 = 0, par = 0; y0 < H; y0 += B, par ^= 1) {
         float cur[B];
 #pragma unroll
         for (int j = 0; j < B; ++j) cur[j] = nxt[j];
@@ -196,55 +185,66 @@ __global__ __launch_bounds__(64) void gftt_eig_kernel(GfttArgs a)
         sr[1] = wb;
 #pragma unroll
         for (int j = 0; j < B; ++j) sr[j + 2] = srow(cur[j]);
-        RowSums en[B];
+        double en[B];
 #pragma unroll
-        for (int j = 0; j < B; ++j) en[j] = sums(sr[j], sr[j + 1], sr[j + 2]);
-        double t0[B], t1[B], t2[B];
+        for (int j = 0; j < B; ++j) en[j] = rsum(sr[j], sr[j + 1], sr[j + 2]);
+        const int nb = H - y0 < B ? H - y0 : B;  // rows of this batch (uniform)
 #pragma unroll
-        for (int j = 0; j < B; ++j) {  // the sequential ColumnSum chain
-            t0[j] = S0 + en[j].s0;
-            t1[j] = S1 + en[j].s1;
-            t2[j] = S2 + en[j].s2;
-            S0 = t0[j] - q0.s0;
-            S1 = t1[j] - q0.s1;
-            S2 = t2[j] - q0.s2;
-            q0 = q1;
-            q1 = en[j];
+        for (int j = 0; j < B; ++j) {  // the sequential ColumnSum chain of this channel
+            if (j < nb) {
+                const double in = y0 + j + 1 < H ? en[j] : q0;  // rs(refl(h)) == rs(h - 2) == rs(y - 1)
+                const double t = S + in;
+                S = t - q0;
+                q0 = q1;
+                q1 = in;
+                box[par][CH][j][lane] = (float)t;
+            }
         }
-#pragma unroll
-        for (int j = 0; j < B; ++j) emit(y0 + j, t0[j], t1[j], t2[j]);
         wa = sr[B];
         wb = sr[B + 1];
-    }
-    // tail: the last (<= B) rows, the final one entering rs(refl(h)) == rs(h - 2)
+        // LDS-only barrier: __syncthreads() would also wait for the next batch's
+        // image loads (vmcnt) and expose their latency every batch
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int j = 0; j < B; ++j) {
-        const int y = y0 + j;
-        if (y >= H) break;
-        RowSums en;
-        if (y + 1 < H) {
-            const SobelRow wc = srow(nxt[j]);
-            en = sums(wa, wb, wc);
-            wa = wb;
-            wb = wc;
-        } else {
-            en = q0;
+        for (int j = CH; j < B; j += 3) {  // eigenvalues of this wave's share of the batch
+            if (j < nb) {
+                const float aa = box[par][0][j][lane] * 0.5f, bb = box[par][1][j][lane],
+                            cc = box[par][2][j][lane] * 0.5f;
+                const float t = aa - cc;
+                const float e = (aa + cc) - sqrtf(bb * bb + t * t);
+                if (out_lane) {
+                    E[(size_t)(y0 + j) * R.w] = e;
+                    const int kk = fkey(e);
+                    best = kk > best ? kk : best;
+                }
+            }
         }
-        const double t0 = S0 + en.s0, t1 = S1 + en.s1, t2 = S2 + en.s2;
-        S0 = t0 - q0.s0;
-        S1 = t1 - q0.s1;
-        S2 = t2 - q0.s2;
-        q0 = q1;
-        q1 = en;
-        emit(y, t0, t1, t2);
     }
-    // per-strip max (minMaxLoc is order independent): wave reduction, one plain store
+    // per-strip max (minMaxLoc is order independent)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const int v = __shfl_xor(best, o);
         best = v > best ? v : best;
     }
-    if (lane == 0) a.blk_max[blockIdx.x] = best;
+    if (lane == 0) smax[CH] = best;
+}
+
+__global__ __launch_bounds__(192) void gftt_eig_kernel(GfttArgs a)
+{
+    __shared__ float box[2][3][kEigBatch][64];  // [batch parity][channel][row][lane]
+    __shared__ int smax[3];
+    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
+    const GfttRoi R = a.rois[r];
+    const int ch = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform channel
+    if (ch == 0) eig_walk<0>(a, R, box, smax);
+    else if (ch == 1) eig_walk<1>(a, R, box, smax);
+    else eig_walk<2>(a, R, box, smax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int m01 = smax[0] > smax[1] ? smax[0] : smax[1];
+        a.blk_max[blockIdx.x] = m01 > smax[2] ? m01 : smax[2];
+    }
 }
 
 // Candidate sort key: the reference order (value desc, then address desc,
@@ -637,7 +637,7 @@ void gftt_plan(GfttArgs& a, int max_area)
 
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(192), 0, s, a);
     hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
