@@ -326,7 +326,7 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int d)
 // (element e = tid * E + u): stages with j < E swap registers, E <= j < 64E
 // exchange across lanes of the wave (no barrier), only j >= 64E go through LDS.
 template <int E>
-__device__ void sort_keys(uint64_t* keys, int np2, int tid)
+__device__ __forceinline__ void sort_keys(uint64_t* keys, int np2, int tid)
 {
     uint64_t x[E];
     const bool active = tid * E < np2;
@@ -387,6 +387,79 @@ __device__ void sort_keys(uint64_t* keys, int np2, int tid)
     __syncthreads();
 }
 
+// Greedy-walk distance test of one candidate against the byte image (image
+// mode): for every window pixel closer than min_distance, 255 = an accepted
+// corner (the candidate is rejected), 1..64 = a candidate of this step in lane
+// v-1 (recorded in inb when it precedes this lane).  RAD is the window radius;
+// all window rows are read before any is examined (one LDS round trip).
+template <int RAD>
+__device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, int ix, int iy, float fx, float fy,
+                                            int lane, double md2, bool& good, unsigned long long& inb)
+{
+    constexpr int NR = 2 * RAD + 1;
+    constexpr bool THREE = NR + 7 > 16;  // the shifted window can need a third word
+    const int x0 = ix - RAD;
+    uint64_t cv_lo = 0, cv_hi = 0;  // window bytes whose column lies inside the ROI
+#pragma unroll
+    for (int t = 0; t < NR; ++t) {
+        const int xx = x0 + t;
+        const uint64_t bit = (xx >= 0 && xx < rw) ? 0x80ull : 0ull;
+        if (t < 8) cv_lo |= bit << (8 * t);
+        else cv_hi |= bit << (8 * (t - 8));
+    }
+    uint64_t w0[NR], w1[NR], w2[NR];
+    int sh[NR];
+#pragma unroll
+    for (int d = 0; d < NR; ++d) {
+        const int yy = iy - RAD + d;
+        const int yc = yy < 0 ? 0 : (yy >= rh ? rh - 1 : yy);  // out-of-ROI rows: read any row, masked below
+        const int base = yc * rw + x0;                       // may be < 0 or past the row: masked
+        const int al = base > 0 ? (base & ~7) : 0;
+        const uint64_t* wp = reinterpret_cast<const uint64_t*>(img + al);
+        w0[d] = wp[0];
+        w1[d] = wp[1];
+        w2[d] = THREE ? wp[2] : 0ull;
+        sh[d] = base - al;  // in [-RAD, 7]
+    }
+#pragma unroll
+    for (int d = 0; d < NR; ++d) {
+        const int yy = iy - RAD + d;
+        if (yy < 0 || yy >= rh) continue;
+        uint64_t lo, hi;
+        if (sh[d] >= 0) {
+            const int b8 = 8 * sh[d];
+            lo = sh[d] ? (w0[d] >> b8) | (w1[d] << (64 - b8)) : w0[d];
+            hi = sh[d] ? (w1[d] >> b8) | (w2[d] << (64 - b8)) : w1[d];
+        } else {  // window starts before the image (first row, x0 < 0)
+            const int b8 = -8 * sh[d];
+            lo = w0[d] << b8;
+            hi = (w1[d] << b8) | (w0[d] >> (64 - b8));
+        }
+        uint64_t nz_lo = (((lo & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | lo) & cv_lo;
+        uint64_t nz_hi = (((hi & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | hi) & cv_hi;
+        if (d == RAD) nz_lo &= ~(0x80ull << (8 * RAD));  // not the candidate itself
+        while (nz_lo | nz_hi) {
+            int t;
+            uint64_t src;
+            if (nz_lo) {
+                t = __builtin_ctzll(nz_lo) >> 3;
+                nz_lo &= nz_lo - 1ull;
+                src = lo;
+            } else {
+                t = __builtin_ctzll(nz_hi) >> 3;
+                nz_hi &= nz_hi - 1ull;
+                src = hi;
+                t += 8;
+            }
+            const int v = (int)((src >> (8 * (t & 7))) & 0xFF);
+            const float ddx = fx - (float)(x0 + t), ddy = fy - (float)yy;
+            if (!((double)(ddx * ddx + ddy * ddy) < md2)) continue;
+            if (v == 255) good = false;                      // accepted earlier
+            else if (v - 1 < lane) inb |= 1ull << (v - 1);  // earlier in this step
+        }
+    }
+}
+
 // LDS layout of the select kernel (one dynamic region):
 //   scan  : kSelThreads ints (gather prefix sums)
 //   keys  : cap uint64 sort keys
@@ -404,6 +477,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     const int r = blockIdx.x;
     const GfttRoi R = a.rois[r];
     const int tid = threadIdx.x;
+    GFTT_STAMP(0);
     const int area = R.w * R.h;
     // image mode: the ROI's byte image fits and the distance window is small
     const bool use_dist = a.min_distance >= 1.0;
@@ -421,14 +495,21 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     int total = 0;
     for (int b0 = 0; b0 < nb; b0 += kSelThreads) {
         const int c = b0 + tid < nb ? a.blk_cnt[R.blk + b0 + tid] : 0;
-        scan[tid] = c;
-        __syncthreads();
-        for (int o = 1; o < kSelThreads; o <<= 1) {  // Hillis-Steele inclusive scan
-            const int v = tid >= o ? scan[tid - o] : 0;
-            __syncthreads();
-            scan[tid] += v;
-            __syncthreads();
+        // inclusive scan: wave prefix sums by DPP-free shuffles, then the wave totals
+        int v = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o);
+            v += (tid & 63) >= o ? u : 0;
         }
+        __shared__ int wtot[kSelThreads / 64];
+        if ((tid & 63) == 63) wtot[tid >> 6] = v;
+        __syncthreads();
+        int off = 0;
+#pragma unroll
+        for (int w = 0; w < kSelThreads / 64; ++w) off += w < (tid >> 6) ? wtot[w] : 0;
+        scan[tid] = v + off;
+        __syncthreads();
         const int chunk_total = scan[kSelThreads - 1];
         // one thread per candidate: its block by binary search of the inclusive
         // scan, so all global loads of the chunk are independent
@@ -453,7 +534,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     while (np2 < total) np2 <<= 1;
     for (int i = total + tid; i < np2; i += kSelThreads) keys[i] = 0ull;  // sorts last
     __syncthreads();
-    GFTT_STAMP(0);
+    GFTT_STAMP(1);
     switch (np2 / kSelThreads) {
     case 1: sort_keys<1>(keys, np2, tid); break;
     case 2: sort_keys<2>(keys, np2, tid); break;
@@ -462,7 +543,6 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     case 16: sort_keys<16>(keys, np2, tid); break;
     default: sort_keys<32>(keys, np2, tid); break;
     }
-    GFTT_STAMP(1);
     GFTT_STAMP(2);
     if (tid >= 64) return;
 
@@ -488,65 +568,14 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
             __builtin_amdgcn_wave_barrier();
             GFTT_T(1);
             if (valid) {
-                // each window row [ix-rad, ix+rad] (<= 13 bytes): three aligned 8-byte
-                // LDS reads, funnel-shifted so byte t is column ix-rad+t; the image
-                // is sparse, so rows are skipped on a zero test and only the
-                // non-zero bytes are visited
-                const int x0 = ix - rad;
-                // window bytes whose column lies inside the ROI (0x80 marker per byte)
-                uint64_t cv_lo = 0, cv_hi = 0;
-                for (int t = 0; t <= 2 * rad; ++t) {
-                    const int xx = x0 + t;
-                    if (xx >= 0 && xx < R.w) {
-                        if (t < 8) cv_lo |= 0x80ull << (8 * t);
-                        else cv_hi |= 0x80ull << (8 * (t - 8));
-                    }
-                }
-                for (int dy = -rad; dy <= rad; ++dy) {
-                    const int yy = iy + dy;
-                    if (yy < 0 || yy >= R.h) continue;
-                    const int base = yy * R.w + x0;  // may be < 0 or past the row: masked
-                    const int al = base > 0 ? (base & ~7) : 0;
-                    const uint64_t* wp = reinterpret_cast<const uint64_t*>(img + al);
-                    const uint64_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
-                    const int sh = base - al;  // in [-6, 7]
-                    uint64_t lo, hi;
-                    if (sh >= 0) {
-                        const int b8 = 8 * sh;
-                        lo = sh ? (w0 >> b8) | (w1 << (64 - b8)) : w0;
-                        hi = sh ? (w1 >> b8) | (w2 << (64 - b8)) : w1;
-                    } else {  // window starts before the image (first row, x0 < 0)
-                        const int b8 = -8 * sh;
-                        lo = w0 << b8;
-                        hi = (w1 << b8) | (w0 >> (64 - b8));
-                    }
-                    // 0x80 in every non-zero byte, restricted to in-ROI columns
-                    uint64_t nz_lo = (((lo & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | lo) & cv_lo;
-                    uint64_t nz_hi = (((hi & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | hi) & cv_hi;
-                    if (dy == 0) {  // not the candidate itself
-                        if (rad < 8) nz_lo &= ~(0x80ull << (8 * rad));
-                        else nz_hi &= ~(0x80ull << (8 * (rad - 8)));
-                    }
-                    while (nz_lo | nz_hi) {
-                        int t;
-                        uint64_t src;
-                        if (nz_lo) {
-                            t = __builtin_ctzll(nz_lo) >> 3;
-                            nz_lo &= nz_lo - 1ull;
-                            src = lo;
-                        } else {
-                            t = __builtin_ctzll(nz_hi) >> 3;
-                            nz_hi &= nz_hi - 1ull;
-                            src = hi;
-                            t += 8;
-                        }
-                        const int v = (int)((src >> (8 * (t & 7))) & 0xFF);
-                        const int col = x0 + t;
-                        const float ddx = fx - (float)col, ddy = fy - (float)yy;
-                        if (!((double)(ddx * ddx + ddy * ddy) < md2)) continue;
-                        if (v == 255) good = false;                      // accepted earlier
-                        else if (v - 1 < lane) inb |= 1ull << (v - 1);  // earlier in this step
-                    }
+                switch (rad) {  // uniform
+                case 0: window_test<0>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                case 1: window_test<1>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                case 2: window_test<2>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                case 3: window_test<3>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                case 4: window_test<4>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                case 5: window_test<5>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                default: window_test<6>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
                 }
             }
         } else if (use_dist) {  // list mode: every accepted corner, then this step's pairs
