@@ -9,6 +9,9 @@
 
 #include <algorithm>
 #include <cmath>
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 #include <cstdint>
 
 namespace tbdk {
@@ -113,6 +116,28 @@ void Tracker::filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax)
     tracks.resize(k);
 }
 
+// min over a row with the reference's `(v < m) ? v : m` step.  The value does
+// not depend on the scan order (a NaN is never selected by `<`), so it is
+// taken two lanes at a time: MINPD(v, m) is exactly (v < m) ? v : m per lane.
+static double row_min(const double* row, unsigned n, double init)
+{
+    unsigned c = 0;
+    double m = init;
+#if defined(__SSE2__)
+    __m128d a = _mm_set1_pd(init), b = _mm_set1_pd(init);
+    for (; c + 4 <= n; c += 4) {
+        a = _mm_min_pd(_mm_loadu_pd(row + c), a);
+        b = _mm_min_pd(_mm_loadu_pd(row + c + 2), b);
+    }
+    a = _mm_min_pd(b, a);
+    double t[2];
+    _mm_storeu_pd(t, a);
+    m = (t[1] < t[0]) ? t[1] : t[0];
+#endif
+    for (; c < n; ++c) m = (row[c] < m) ? row[c] : m;
+    return m;
+}
+
 // calculateCostMatrix + solveAssignmentProblem + classifyAssignments
 // (tbd.cpp:333-891) on a flat n x n matrix.  The reference's operation order
 // on every matrix entry is kept (row minima, column minima, the step-4
@@ -129,13 +154,22 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
     const double huge = 10000000.0;
     const double pad = args.costOfNonAssignment * 2;
     cost.resize((size_t)n * n);
-    // detections as SoA for a branch-free, vectorisable IoU row
     detX0.resize(nD); detY0.resize(nD); detX1.resize(nD); detY1.resize(nD); detArea.resize(nD);
+    detOrder.resize(nD);
+    int maxW = 0;
     for (unsigned j = 0; j < nD; ++j) {
         const Rect& b = dets[j].bbox;
         detX0[j] = b.x; detY0[j] = b.y; detX1[j] = b.x + b.width; detY1[j] = b.y + b.height;
         detArea[j] = b.area();
+        detOrder[j] = j;
+        maxW = std::max(maxW, b.width);
     }
+    // detections by left edge: a track row only visits the detections whose x-range
+    // can touch its box; all others are strictly separated, where the reference's
+    // computeBoundingBoxOverlap returns exactly 0.0 (cost exactly 1.0)
+    std::sort(detOrder.begin(), detOrder.end(), [&](unsigned a, unsigned b) { return detX0[a] < detX0[b]; });
+    sortedX0.resize(nD);
+    for (unsigned k = 0; k < nD; ++k) sortedX0[k] = detX0[detOrder[k]];
     assignmentPerRow.assign(n, n);
     if (n == 0) return;
     // calculateCostMatrix (:333-351) fused with step 1, the row minima (:494-516)
@@ -145,66 +179,61 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
         if (r < nT) {
             const Rect& p = tracks[r].predPosition;
             const int px0 = p.x, py0 = p.y, px1 = p.x + p.width, py1 = p.y + p.height, pa = p.area();
-            for (unsigned j = 0; j < nD; ++j) {  // computeBoundingBoxOverlap, branch-free
+            for (unsigned j = 0; j < nD; ++j) row[j] = 1.0;
+            const unsigned lb = (unsigned)(std::lower_bound(sortedX0.begin(), sortedX0.end(), px0 - maxW) -
+                                           sortedX0.begin());
+            const unsigned ub = (unsigned)(std::upper_bound(sortedX0.begin(), sortedX0.end(), px1) - sortedX0.begin());
+            for (unsigned k = lb; k < ub; ++k) {
+                const unsigned j = detOrder[k];
+                if (detX0[j] > px1 || detX1[j] < px0 || detY0[j] > py1 || detY1[j] < py0) continue;
                 const int xl = std::max(px0, detX0[j]), xr = std::min(px1, detX1[j]);
                 const int yt = std::max(py0, detY0[j]), yb = std::min(py1, detY1[j]);
+                if (xr < xl || yb < yt) continue;  // (:1094-1097) -> 0.0
                 const double inter = (double)(xr - xl) * (double)(yb - yt);
                 const double uni = (double)(pa + detArea[j]) - inter;
-                const double iou = (xr < xl || yb < yt) ? 0.0 : inter / uni;
-                row[j] = 1.0 - iou;
+                row[j] = 1.0 - inter / uni;
             }
             c0 = nD;
         }
         for (unsigned c = c0; c < n; ++c) row[c] = pad;
-        // the reference's sequential min; the value is order independent (no NaN
-        // can be selected by `<`), so four interleaved partial minima are used
-        double m0 = huge, m1 = huge, m2 = huge, m3 = huge;
-        unsigned c = 0;
-        for (; c + 4 <= n; c += 4) {
-            m0 = (row[c] < m0) ? row[c] : m0;
-            m1 = (row[c + 1] < m1) ? row[c + 1] : m1;
-            m2 = (row[c + 2] < m2) ? row[c + 2] : m2;
-            m3 = (row[c + 3] < m3) ? row[c + 3] : m3;
-        }
-        for (; c < n; ++c) m0 = (row[c] < m0) ? row[c] : m0;
-        m0 = (m1 < m0) ? m1 : m0;
-        m2 = (m3 < m2) ? m3 : m2;
-        const double m = (m2 < m0) ? m2 : m0;
+        const double m = row_min(row, n, huge);
         for (unsigned k = 0; k < n; ++k) row[k] -= m;
     }
     {
-        // step 2: column minima (:539-561), scanned in the same r order per column
+        // step 2: column minima (:539-561), scanned in the same r order per column;
+        // their subtraction is fused into the first round's zero pass
         colMin.assign(n, huge);
         for (unsigned r = 0; r < n; ++r) {
             const double* row = &cost[(size_t)r * n];
             for (unsigned c = 0; c < n; ++c) colMin[c] = (row[c] < colMin[c]) ? row[c] : colMin[c];
         }
-        for (unsigned r = 0; r < n; ++r) {
-            double* row = &cost[(size_t)r * n];
-            for (unsigned c = 0; c < n; ++c) row[c] -= colMin[c];
-        }
         zero.resize((size_t)n * n);
         rowZeros.resize(n);
         colZeros.resize(n);
+        colLast.resize(n);
         colRow.resize(n);
         rowA.resize(n);
         colA.resize(n);
         rowM.resize(n);
         colM.resize(n);
+        bool first = true;
         while (true) {  // (:585-887)
             std::fill(colZeros.begin(), colZeros.end(), 0u);
             for (unsigned r = 0; r < n; ++r) {
-                const double* row = &cost[(size_t)r * n];
+                double* row = &cost[(size_t)r * n];
                 uint8_t* z = &zero[(size_t)r * n];
                 unsigned cnt = 0;
-                for (unsigned c = 0; c < n; ++c) {
-                    const uint8_t b = std::fabs(row[c]) < 0.00000001 ? 1 : 0;  // == equalsZero
-                    z[c] = b;
-                    cnt += b;
-                    colZeros[c] += b;
+                if (first)
+                    for (unsigned c = 0; c < n; ++c) row[c] -= colMin[c];
+                for (unsigned c = 0; c < n; ++c) z[c] = std::fabs(row[c]) < 0.00000001 ? 1 : 0;  // == equalsZero
+                for (unsigned c = 0; c < n; ++c) cnt += z[c];
+                if (cnt) {
+                    for (unsigned c = 0; c < n; ++c) colZeros[c] += z[c];
+                    for (unsigned c = 0; c < n; ++c) colLast[c] = z[c] ? r : colLast[c];  // row of a column's single zero
                 }
                 rowZeros[r] = cnt;
             }
+            first = false;
             std::fill(rowA.begin(), rowA.end(), 0);
             std::fill(colA.begin(), colA.end(), 0);
             std::fill(colRow.begin(), colRow.end(), n);
@@ -233,8 +262,7 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
                 // columns with exactly one zero (:639-668)
                 for (unsigned c = 0; c < n; ++c) {
                     if (colA[c] || colZeros[c] != 1) continue;
-                    unsigned r = 0;
-                    while (!zero[(size_t)r * n + c]) ++r;
+                    const unsigned r = colLast[c];
                     if (!rowA[r]) {
                         assign(r, c);
                         made = true;

@@ -122,11 +122,11 @@ private:
     std::vector<unsigned> assignmentPerRow;
     // solver scratch, kept across frames
     std::vector<uint8_t> zero;
-    std::vector<unsigned> rowZeros, colZeros, colRow;
+    std::vector<unsigned> rowZeros, colZeros, colRow, colLast, detOrder;
     std::vector<double> colMin;
     std::vector<char> rowA, colA, rowM, colM;
     std::vector<int> predIndex;
-    std::vector<int> detX0, detY0, detX1, detY1, detArea;
+    std::vector<int> detX0, detY0, detX1, detY1, detArea, sortedX0;
 
     void predictNewLocationsOfTracks(int frame_id, const Prediction* preds, int npreds);
     void filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax);
