@@ -318,6 +318,9 @@ int tbdk_tbd_destroy(tbdk_tbd* tbd);
 int tbdk_tbd_step(tbdk_tbd* tbd, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
                   int ndets, tbdk_frame_metrics* metrics, void* stream);
 int tbdk_tbd_tracks(tbdk_tbd* tbd, tbdk_track_info* out, int cap, int* n);
+/* The KLT predictions the last tbdk_tbd_step handed to the tracker (one per
+ * track with a valid box fit, in track order); *n = their number. */
+int tbdk_tbd_predictions(const tbdk_tbd* tbd, tbdk_prediction* out, int cap, int* n);
 
 /* ---- synthetic sequences (bench / test input) ----------------------------- */
 

@@ -546,6 +546,18 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     return TBDK_OK;
 }
 
+int tbdk_tbd_predictions(const tbdk_tbd* t, tbdk_prediction* out, int cap, int* n)
+{
+    if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
+    int k = 0;
+    for (const auto& p : t->preds) {
+        if (k >= cap) break;
+        out[k++] = tbdk_prediction{p.id, p.valid, p.cx, p.cy};
+    }
+    *n = (int)t->preds.size();
+    return TBDK_OK;
+}
+
 int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
 {
     if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;

@@ -78,6 +78,13 @@ class TbdLoop:
                    "tbdk_tbd_step")
         return m
 
+    def predictions(self) -> dict:
+        """{track id: (cx, cy)} of the KLT predictions the last step gave the tracker."""
+        arr = (_lib.Prediction * 4096)()
+        n = C.c_int()
+        _lib.check(self.ctx.lib.tbdk_tbd_predictions(self.handle, arr, 4096, C.byref(n)), "tbdk_tbd_predictions")
+        return {arr[i].track_id: (arr[i].cx, arr[i].cy) for i in range(min(n.value, 4096)) if arr[i].valid}
+
     def tracks(self):
         cap = 4096
         arr = (_lib.TrackInfo * cap)()

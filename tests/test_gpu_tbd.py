@@ -48,3 +48,44 @@ def test_tbd_loop_reference_bounds_quirk(gpu):
         m = loop.step(frames[f], f, tbd.detections_from_gt(gt[f].numpy()))
     tr = loop.tracks()
     assert len(tr) > 0
+
+
+def test_tbd_loop_tracker_matches_reference_restatement(gpu):
+    """End to end: every frame, the loop's tracker state equals the pure-Python
+    cv::tbd::Tracker restatement (oracle/tbd_oracle.py) fed the same detections
+    and the KLT predictions the loop computed on the GPU (ids, boxes, predicted
+    boxes, ages, visibility, confidence, overlap, TP/FN/FP/GT)."""
+    import math
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import tbd_oracle as T
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 1280, 720, 24, 40
+    frames, gt = klt.synth_render(11, W, H, N, 0, F, ctx=gpu)
+    loop = tbd.TbdLoop(tbd.default_config(W, H), ctx=gpu)
+    ora = T.Tracker(bounds=(0, 1280, 0, 720))
+    rng = np.random.default_rng(5)
+    used_preds = 0
+    for f in range(F):
+        d = tbd.detections_from_gt(gt[f].numpy())
+        d = d[rng.random(len(d)) > 0.1]  # detector dropouts
+        m = loop.step(frames[f], f, d)
+        preds = loop.predictions()
+        used_preds += len(preds)
+        ora.step([T.Detection(int(r["id"]), f, T.Rect(int(r["x"]), int(r["y"]), int(r["width"]), int(r["height"])),
+                              float(r["confidence"])) for r in d], f, preds)
+        assert (m.tp, m.fn, m.fp, m.gt) == (ora.true_positives[-1], ora.false_negatives[-1],
+                                            ora.false_positives[-1], ora.ground_truths[-1]), f
+        tr = loop.tracks()
+        assert len(tr) == len(ora.tracks), f
+        for g, t in zip(tr, ora.tracks):
+            b, p = t.bboxes[-1], t.predPosition
+            assert (g["id"], g["x"], g["y"], g["width"], g["height"]) == (t.id, b.x, b.y, b.width, b.height), f
+            assert (g["pred_x"], g["pred_y"], g["pred_w"], g["pred_h"]) == (p.x, p.y, p.width, p.height), f
+            assert (g["age"], g["total_visible"]) == (t.age, t.totalVisibleCount), f
+            assert g["max_confidence"] == t.maxConfidence
+            assert g["bbox_overlap"] == t.bboxOverlap or (math.isnan(g["bbox_overlap"]) and math.isnan(t.bboxOverlap))
+    assert used_preds > 0  # the KLT motion model was exercised
