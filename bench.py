@@ -4,7 +4,9 @@
 Workload (BASELINE.json configs[2]): one synthetic 1920x1080 sequence of
 `warmup + steps` frames with 128 moving textured objects per GPU, rendered
 into HBM before timing (tbdk_synth_render).  A "step" is one frame through the
-full loop of libtbdk (tbdk_tbd_step): 3-level pyramid + Scharr planes, GFTT in
+full loop of libtbdk (tbdk_tbd_run over the timed frames: per frame the same
+work as tbdk_tbd_step, with the next frame's pyramid and tracker-independent
+PyrLK enqueued before the host tracker step): 3-level pyramid + Scharr planes, GFTT in
 the boxes of new / re-detect tracks, sparse PyrLK (win 21) over every track's
 corners, per-track similarity fit (KLT box propagation), and the native
 cv::tbd::Tracker step on the frame's ground-truth detections.
@@ -141,6 +143,14 @@ def main():
                     help="reference: the tracker's hard-coded 1280x720 filter (tbd.cpp:218); frame: W x H")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--api", choices=["run", "ahead", "step"], default="run",
+                    help="run: tbdk_tbd_run (native frame loop with look-ahead); ahead: per-frame "
+                         "tbdk_tbd_step_ahead; step: per-frame tbdk_tbd_step (no look-ahead)")
+    ap.add_argument("--kstats", default="lk_sparse",
+                    help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
+                         "each timed launch adds two event records to the frame's host work.  The other "
+                         "kernels are timed in a separate pass over the same frames (not `value`)")
+    ap.add_argument("--no-step-api", action="store_true", help="skip the secondary per-frame tbdk_tbd_step pass")
     args = ap.parse_args()
 
     import numpy as np
@@ -177,16 +187,32 @@ def main():
 
     for f in range(args.warmup):
         loop.step(frames[f], f, dets[f], stream)
+    frame_list = [frames[f] for f in range(args.warmup, nframes)]
+    packed = tbd.TbdLoop.pack_detections(dets[args.warmup:])  # host detections staged like the frames
 
-    ctx.timing_enable(True)
+    timed = ["pyr_build", "lk_sparse", "gftt", "tbd_fit"] if args.kstats == "all" else \
+        [] if args.kstats == "none" else [k for k in args.kstats.split(",") if k]
+    ctx.timing_select(timed or None)
+    ctx.timing_enable(bool(timed))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if args.api == "run":
+        ms = loop.run(frame_list, args.warmup, None, stream, packed=packed)
+    else:
+        ms = []
+        for f in range(args.warmup, nframes):
+            nxt = frames[f + 1] if args.api == "ahead" and f + 1 < nframes else None
+            ms.append(loop.step(frames[f], f, dets[f], stream, next_frame=nxt))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    el = max_over_ranks(el, world, device="cuda")
     lk_pts = lk_it = klt_pts = ntr = redet = 0
     h_wait = h_trk = h_step = h_launch = 0.0
-    for f in range(args.warmup, nframes):
-        m = loop.step(frames[f], f, dets[f], stream)
+    for m in ms:
         lk_pts += m.lk_points
         lk_it += m.lk_iters
         klt_pts += m.klt_points
@@ -196,19 +222,54 @@ def main():
         h_trk += m.host_tracker_us
         h_step += m.host_step_us
         h_launch += m.host_launch_us
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    el = max_over_ranks(el, world, device="cuda")
 
     kstats = {}
-    for name in ("pyr_build", "lk_sparse", "gftt", "tbd_fit"):
+    for name in timed:
         c, ms = ctx.timing_query(name)
         kstats[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "total_ms": ms}
     ctx.timing_enable(False)
+    ctx.timing_select(None)
+    nolaunch = {"launches": 0, "avg_us": None, "total_ms": 0.0}
 
-    lk = kstats["lk_sparse"]
+    # secondary: the same frames through the per-frame tbdk_tbd_step API (no
+    # look-ahead), a fresh loop, no timing events; reported, never `value`
+    step_api = None
+    if args.api != "step" and not args.no_step_api:
+        loop2 = tbd.TbdLoop(cfg, ctx=ctx)
+        for f in range(args.warmup):
+            loop2.step(frames[f], f, dets[f], stream)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for f in range(args.warmup, nframes):
+            loop2.step(frames[f], f, dets[f], stream)
+        torch.cuda.synchronize()
+        el2 = max_over_ranks(time.perf_counter() - t1, world, device="cuda")
+        step_api = {"value": round(replica_throughput(args.steps, world, el2), 2), "unit": "frames/s",
+                    "api": "tbdk_tbd_step per frame from Python"}
+        del loop2
+
+    # the kernels not timed in the timed region: a separate pass over the same
+    # frames with events on them (a fresh loop; its wall time is not reported)
+    rest = [k for k in ("pyr_build", "lk_sparse", "gftt", "tbd_fit") if k not in timed]
+    kstats_aside = {}
+    if rest:
+        loop3 = tbd.TbdLoop(cfg, ctx=ctx)
+        for f in range(args.warmup):
+            loop3.step(frames[f], f, dets[f], stream)
+        ctx.timing_select(rest)
+        ctx.timing_enable(True)
+        loop3.run(frame_list, args.warmup, None, stream, packed=packed)
+        torch.cuda.synchronize()
+        for name in rest:
+            c, ms = ctx.timing_query(name)
+            kstats_aside[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "total_ms": ms}
+        ctx.timing_enable(False)
+        ctx.timing_select(None)
+        del loop3
+
+    lk = kstats.get("lk_sparse", nolaunch)
     nlev = args.max_level + 1
     if lk["launches"]:
         flops_per_launch = lk_flops(lk_pts * nlev, lk_it, args.win) / lk["launches"]
@@ -225,7 +286,7 @@ def main():
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}
     pb = pyr_bytes(args.width, args.height, nlev)
-    pyr = kstats["pyr_build"]
+    pyr = kstats.get("pyr_build", kstats_aside.get("pyr_build", nolaunch))
     pyr_gbs = pb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build"}
@@ -261,11 +322,15 @@ def main():
         "config": {"workload": f"TBD loop {args.width}x{args.height} x {args.objects} objects "
                                f"(BASELINE configs[2]), {nframes}-frame sequence per GPU",
                    "levels": nlev, "win": args.win, "gftt": f"256/box, q 0.01, minDist 3, every {args.redetect}",
-                   "tracker_bounds": args.bounds, "parallelism": f"replicas x{world} (one sequence per GPU)"},
+                   "tracker_bounds": args.bounds, "parallelism": f"replicas x{world} (one sequence per GPU)",
+                   "api": {"run": "tbdk_tbd_run (native frame loop, look-ahead)",
+                           "ahead": "tbdk_tbd_step_ahead per frame", "step": "tbdk_tbd_step per frame"}[args.api]},
+        "step_api": step_api,
         "roofline": roofline,
         "roofline_pyramid": roof_pyr,
         "roofline_hbm_pyr_lk": roof_pl,
         "kernels": kstats,
+        "kernels_aside": kstats_aside,
         "per_frame": {"lk_points": lk_pts / args.steps, "tracked_points": klt_pts / args.steps,
                       "tracks": ntr / args.steps, "gftt_rois": redet / args.steps,
                       "host_wait_us": h_wait / args.steps, "host_tracker_us": h_trk / args.steps,

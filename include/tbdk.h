@@ -85,6 +85,9 @@ int tbdk_timing_enable(tbdk_ctx* ctx, int enable);
  * ("pyr_build", "lk_sparse", ...), the number of launches and the summed
  * device milliseconds. */
 int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
+/* Restrict recording to the comma-separated kernel names in `names` (NULL or
+ * "" = all).  Each timed launch costs two event records on the host. */
+int tbdk_timing_select(tbdk_ctx* ctx, const char* names);
 
 /* ---- pyramids ------------------------------------------------------------ */
 
@@ -317,6 +320,25 @@ int tbdk_tbd_destroy(tbdk_tbd* tbd);
  * dets: HOST array.  Synchronises the stream once (predictions -> host tracker). */
 int tbdk_tbd_step(tbdk_tbd* tbd, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
                   int ndets, tbdk_frame_metrics* metrics, void* stream);
+/* tbdk_tbd_step when the next frame is already on the device (a decode
+ * pipeline, or a clip): the next frame's pyramid is enqueued behind this
+ * frame's fit (the device builds it while the host tracks), and the next
+ * frame's PyrLK of every point set this step leaves unchanged behind the
+ * post-tracker GFTT, without returning to the caller in between.
+ * next_frame must keep its pixels until the next step, which must pass the
+ * same pointer, pitch and stream to use that work (otherwise it is redone).
+ * Per-frame results are identical to tbdk_tbd_step's. */
+int tbdk_tbd_step_ahead(tbdk_tbd* tbd, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
+                        int ndets, const uint8_t* next_frame, int next_pitch, tbdk_frame_metrics* metrics,
+                        void* stream);
+/* The loop of samples/gpu/tbd.cpp:624-706 over nframes resident frames:
+ * frames = host array of device pointers (same pitch), frame ids
+ * first_frame_id + i, frame i's detections dets[det_offsets[i] ..
+ * det_offsets[i+1]) (host), metrics = nframes entries or NULL.  Equivalent to
+ * tbdk_tbd_step_ahead over the sequence. */
+int tbdk_tbd_run(tbdk_tbd* tbd, const uint8_t* const* frames, int pitch, int first_frame_id,
+                 const tbdk_detection* dets, const int32_t* det_offsets, int nframes, tbdk_frame_metrics* metrics,
+                 void* stream);
 int tbdk_tbd_tracks(tbdk_tbd* tbd, tbdk_track_info* out, int cap, int* n);
 /* The KLT predictions the last tbdk_tbd_step handed to the tracker (one per
  * track with a valid box fit, in track order); *n = their number. */

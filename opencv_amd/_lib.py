@@ -140,6 +140,7 @@ SIGNATURES = {
     "tbdk_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tbdk_ctx_device": (C.c_int, [C.c_void_p]),
     "tbdk_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "tbdk_timing_select": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
@@ -168,6 +169,10 @@ SIGNATURES = {
     "tbdk_tbd_destroy": (C.c_int, [C.c_void_p]),
     "tbdk_tbd_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(Detection), C.c_int,
                                 C.POINTER(FrameMetrics), C.c_void_p]),
+    "tbdk_tbd_step_ahead": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(Detection), C.c_int,
+                                      C.c_void_p, C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
+    "tbdk_tbd_run": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(Detection),
+                               C.POINTER(C.c_int32), C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
     "tbdk_tbd_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_tbd_predictions": (C.c_int, [C.c_void_p, C.POINTER(Prediction), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -22,6 +22,7 @@
 //                   step over a byte image of the ROI; in-step conflicts are
 //                   resolved in lane order so exactly the sequential walk's
 //                   corners are accepted.
+#include <atomic>
 #include <cfloat>
 
 #include "tbdk_internal.hpp"
@@ -650,7 +651,7 @@ size_t gftt_select_smem(int cap, int max_corners, int img_bytes)
 // room for >= 4096 sort keys, else list mode with the largest key array
 void gftt_plan(GfttArgs& a, int max_area)
 {
-    const long lds = 160L * 1024;
+    const long lds = 160L * 1024 - 256;  // static LDS (scan totals) stays out of the dynamic budget
     const long fixed = (long)gftt_select_smem(0, a.max_corners, 0);
     long img = ((long)max_area + 15) & ~15L;
     long room = lds - fixed - img;
@@ -669,10 +670,23 @@ hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
     hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(192), 0, s, a);
     hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
-    // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950);
+    // done once per device, for the whole LDS, off the per-frame path
+    static std::atomic<unsigned long long> opted{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(opted.load(std::memory_order_acquire) & bit)) {
+        hipFuncAttributes fa;
+        e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&gftt_select_kernel));
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(160L * 1024 - (long)fa.sharedSizeBytes));
+        if (e != hipSuccess) return e;
+        opted.fetch_or(bit, std::memory_order_acq_rel);
+    }
     hipLaunchKernelGGL(gftt_select_kernel, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
     return hipGetLastError();
 }

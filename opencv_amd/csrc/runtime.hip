@@ -25,6 +25,9 @@ static hipEvent_t take_event(tbdk_ctx* ctx)
 int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
 {
     if (!ctx->timing) return -1;
+    if (!ctx->timing_only.empty() &&
+        ctx->timing_only.find("," + std::string(name) + ",") == std::string::npos)
+        return -1;
     TimingRec r{name, take_event(ctx), take_event(ctx)};
     if (!r.begin || !r.end) return -1;
     (void)hipEventRecord(r.begin, s);
@@ -114,6 +117,19 @@ int tbdk_timing_enable(tbdk_ctx* ctx, int enable)
     }
     ctx->recs.clear();
     ctx->timing = enable != 0;
+    return TBDK_OK;
+}
+
+int tbdk_timing_select(tbdk_ctx* ctx, const char* names)
+{
+    if (!ctx) return TBDK_EINVAL;
+    ctx->timing_only.clear();
+    if (names && *names) {
+        ctx->timing_only = ",";
+        for (const char* c = names; *c; ++c)
+            if (*c != ' ') ctx->timing_only += *c;
+        ctx->timing_only += ",";
+    }
     return TBDK_OK;
 }
 

@@ -153,6 +153,21 @@ struct tbdk_tbd {
     // caller's stream waits for `post_done` before its LK launch
     hipStream_t side = nullptr;
     hipEvent_t post_done = nullptr;
+    // look-ahead (tbdk_tbd_step_ahead): the next frame's pyramid, enqueued
+    // behind this frame's fit (built while the host tracks), and the next
+    // frame's PyrLK of the point sets this step leaves unchanged, enqueued
+    // behind the post-tracker GFTT
+    hipEvent_t fit_done = nullptr;   // this frame's predictions are on the host
+    hipEvent_t la_done = nullptr;    // look-ahead pyramid (+ PyrLK) complete
+    int32_t* h_la = nullptr;         // look-ahead slot list (pinned) / device copy
+    int32_t* d_la = nullptr;
+    int la_n = 0;
+    std::vector<char> la_member;     // slot tracked by the look-ahead PyrLK
+    const uint8_t* la_frame = nullptr;
+    int la_pitch = 0;
+    hipStream_t la_stream = nullptr;
+    bool la_pyr = false;             // pyr[cur] already holds la_frame's pyramid
+    bool la_lk = false;              // ... and the la_member slots are tracked into it
     // pinned host staging (reuse rules: see tbdk_tbd_step)
     // [fit entries: S FitEntry][LK slot lists: S int32 (unchanged sets, then refreshed ones)]
     void* h_pre = nullptr;
@@ -160,6 +175,7 @@ struct tbdk_tbd {
     int32_t* h_lists = nullptr;
     int32_t* d_lists = nullptr;
     std::vector<char> refreshed;  // slot got new corners in the last post phase
+    std::vector<int32_t> b_list;  // scratch: refreshed slots in track order
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
     // one pinned block uploaded with a single copy after the tracker step:
@@ -185,14 +201,16 @@ int release(tbdk_tbd* t)
     if (!t) return TBDK_OK;
     if (t->side) (void)hipStreamSynchronize(t->side);
     if (t->post_done) (void)hipEventDestroy(t->post_done);
+    if (t->fit_done) (void)hipEventDestroy(t->fit_done);
+    if (t->la_done) (void)hipEventDestroy(t->la_done);
     if (t->side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre,
-                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_post};
+                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_post,    t->d_la};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {t->h_pre, t->h_fit, t->h_post};
+    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -284,6 +302,10 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         t->d_lists = reinterpret_cast<int32_t*>(t->d_ents + S);
     }
     t->refreshed.assign((size_t)S, 0);
+    t->la_member.assign((size_t)S, 0);
+    t->b_list.assign((size_t)S, 0);
+    dm(reinterpret_cast<void**>(&t->d_la), sizeof(int32_t) * S);
+    hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
     hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
     if (t->h_post && t->d_post) {
@@ -294,8 +316,15 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         t->d_roi_slot = t->d_post + S;
         t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 2 * S);
     }
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking);
+    // the post-tracker GFTT heads the next frame's critical path (the refreshed
+    // sets' PyrLK waits for it): it gets the highest priority, ahead of the
+    // look-ahead PyrLK it shares the device with
+    int prio_least = 0, prio_greatest = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_greatest);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->post_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -328,32 +357,56 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
 
 int tbdk_tbd_destroy(tbdk_tbd* t) { return release(t); }
 
-int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets, int ndets,
-                  tbdk_frame_metrics* metrics, void* stream)
+}  // extern "C"
+
+namespace {
+
+// One frame.  With next != nullptr the step also enqueues look-ahead work for
+// the next frame: its pyramid behind this frame's fit (the device has it to run
+// while the host tracker runs), and its PyrLK of the unchanged point sets
+// behind the post-tracker GFTT; the next step skips what was done.
+int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets, int ndets,
+              const uint8_t* next, int next_pitch, tbdk_frame_metrics* metrics, hipStream_t s)
 {
-    if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width) return TBDK_EINVAL;
-    const auto t_step0 = std::chrono::steady_clock::now();
+    if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width ||
+        (next && next_pitch < t->cfg.width))
+        return TBDK_EINVAL;
+    using clk = std::chrono::steady_clock;
+    const auto t_step0 = clk::now();
     double launch_us = 0.0;
-    hipStream_t s = static_cast<hipStream_t>(stream);
     const tbdk_tbd_config& c = t->cfg;
     tbdk_pyr& P = t->pyr[t->cur];
     tbdk_pyr& Pprev = t->pyr[t->cur ^ 1];
-    int rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, stream);
-    if (rc != TBDK_OK) return rc;
     (void)hipSetDevice(t->ctx->device);
+    int rc = TBDK_OK;
+
+    // ---- the previous step's look-ahead, if it was for this frame
+    const bool la_valid = t->la_pyr && t->la_frame == frame && t->la_pitch == pitch;
+    const bool had_la_lk = t->la_lk;
+    const bool la_lk = la_valid && had_la_lk;
+    if (t->la_pyr && t->la_stream != s) {  // look-ahead work was enqueued on another stream
+        hipError_t e = hipStreamWaitEvent(s, t->la_done, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
+    t->la_pyr = t->la_lk = false;
+    if (!la_valid) {
+        rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, s);
+        if (rc != TBDK_OK) return rc;
+    }
 
     // No host wait here: the pinned staging buffers written before this step's
-    // fit sync (h_ents) were last read by uploads issued before the previous
-    // step's sync, and those written after it (h_clear, h_roi_slot) are only
-    // rewritten after this step's sync, which orders every earlier upload.
-    // So this frame's pyramid / LK / fit queue up behind the previous GFTT.
-    using clk = std::chrono::steady_clock;
+    // fit sync (h_ents, h_lists) were last read by uploads issued before the
+    // previous step's sync, and those written after it (h_clear, h_roi_slot,
+    // h_la) are only rewritten after this step's sync, which orders every
+    // earlier upload.  So this frame's pyramid / LK / fit queue up behind the
+    // previous GFTT.
     double wait_us = 0.0;
     bool synced = false;  // has this step waited for the stream (see above)?
 
     // ---- KLT propagation of every live track.  Slots whose point set the previous
     // frame's post-tracker work (on `side`) leaves untouched are tracked first,
-    // overlapping that work; the refreshed ones after it completes.
+    // overlapping that work (or were tracked by the look-ahead); the refreshed
+    // ones after it completes.
     std::vector<tbd::Track>& tracks = t->tracker->getTracks();
     int nents = 0, klt_points = 0, klt_pred = 0, lk_points = 0, nA = 0, nB = 0;
     int64_t lk_iters = 0;
@@ -367,37 +420,50 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
     lp.flags = 0;
     lp.min_eig_threshold = c.min_eig_threshold;
     lp.impl = 0;
+    const int S = c.max_tracks;
     if (run_klt) {
-        const int S = c.max_tracks;
         for (const auto& tr : tracks) {
             auto it = t->slot_of.find(tr.id);
             if (it == t->slot_of.end()) continue;
+            const int slot = it->second;
             const tbd::Rect& b = tr.bboxes.back();
-            t->h_ents[nents++] = FitEntry{it->second, b.x, b.y, b.width, b.height};
-            if (t->refreshed[(size_t)it->second]) t->h_lists[S - 1 - nB++] = it->second;  // from the end
-            else t->h_lists[nA++] = it->second;
+            t->h_ents[nents++] = FitEntry{slot, b.x, b.y, b.width, b.height};
+            if (t->refreshed[(size_t)slot]) t->b_list[nB++] = slot;
+            else if (!(la_lk && t->la_member[(size_t)slot])) t->h_lists[nA++] = slot;
         }
-        for (int k = 0; k < nB; ++k) t->h_lists[nA + k] = t->h_lists[S - 1 - k];
+        // refreshed sets after the unchanged ones (a separate scratch list: with
+        // every slot live, nA + nB == S and the two ranges tile h_lists exactly)
+        std::copy(t->b_list.begin(), t->b_list.begin() + nB, t->h_lists + nA);
         const size_t bytes = sizeof(FitEntry) * S + sizeof(int32_t) * (size_t)(nA + nB);
         hipError_t e = hipMemcpyAsync(t->d_pre, t->h_pre, bytes, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return map_status(e);
         if (nA > 0) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             nA * kSlotPts, &lp, t->slot_counts, kSlotPts, stream, t->d_lists);
+                             nA * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists);
             if (rc != TBDK_OK) return rc;
         }
     }
+    if (had_la_lk)
+        for (int k = 0; k < t->la_n; ++k) t->la_member[(size_t)t->h_la[k]] = 0;
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
     {  // the previous frame's clear / GFTT / scatter (on `side`) before the refreshed sets
         hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
         if (e != hipSuccess) return map_status(e);
     }
+    tbdk_pyr& Pnext = Pprev;  // the look-ahead pyramid replaces the previous frame's
+    auto enqueue_next_pyr = [&]() -> int {
+        t->la_frame = next;
+        t->la_pitch = next_pitch;
+        t->la_stream = s;
+        t->la_pyr = true;
+        return tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, s);
+    };
     if (run_klt) {
         if (nB > 0) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             nB * kSlotPts, &lp, t->slot_counts, kSlotPts, stream, t->d_lists + nA);
+                             nB * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + nA);
             if (rc != TBDK_OK) return rc;
         }
         hipError_t e;
@@ -406,9 +472,15 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
         timing_end(t->ctx, rec, s);
         e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(t->fit_done, s);
+        if (e != hipSuccess) return map_status(e);
+        if (next) {  // runs on the device while this step waits for the fit and tracks
+            rc = enqueue_next_pyr();
+            if (rc != TBDK_OK) return rc;
+        }
         auto ts0 = clk::now();
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        e = hipEventSynchronize(t->fit_done);
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);
         synced = true;
@@ -429,6 +501,9 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
                 klt_pred++;
             }
         }
+    } else if (next) {
+        rc = enqueue_next_pyr();
+        if (rc != TBDK_OK) return rc;
     }
 
     // ---- host tracker step (cv::tbd::Tracker::performTrackingStep)
@@ -489,7 +564,11 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
             t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
         }
     }
-    // ---- one upload (clear list, ROI slots, GFTT ROI table), then clear / GFTT / scatter
+    // ---- one upload (clear list, ROI slots, GFTT ROI table), then GFTT / clear / scatter.
+    // With a next frame, the PyrLK of the point sets this leaves unchanged is
+    // enqueued after it (the look-ahead PyrLK): GFTT heads the next frame's
+    // critical path, so it is queued first and the PyrLK fills the device
+    // around it.
     tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
     GfttPlan plan;
     if (nroi > 0) {
@@ -503,21 +582,46 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
         if (e != hipSuccess) return map_status(e);
     }
-    if (nclear > 0)
-        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, t->side, t->d_clear, nclear,
-                           t->slot_counts);
     if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
         rc = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
                          reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side);
         if (rc != TBDK_OK) return rc;
+    }
+    if (nclear > 0)
+        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, t->side, t->d_clear, nclear,
+                           t->slot_counts);
+    if (nroi > 0)
         hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, t->side, t->d_corners, t->d_ccounts,
                            t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
+    if (nclear > 0 || nroi > 0) {
         hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
     }
-    if (nclear > 0 || nroi > 0) {
-        hipError_t e = hipEventRecord(t->post_done, t->side);
+    // ---- look-ahead: PyrLK of the next frame for every live track whose point
+    // set was not refreshed just now (exactly the next step's unchanged sets)
+    if (next) {
+        if (c.use_klt && !t->tracker->getTracks().empty()) {
+            int n = 0;
+            for (const auto& tr : t->tracker->getTracks()) {
+                auto it = t->slot_of.find(tr.id);
+                if (it == t->slot_of.end() || t->refreshed[(size_t)it->second]) continue;
+                t->h_la[n++] = it->second;
+                t->la_member[(size_t)it->second] = 1;
+            }
+            t->la_n = n;
+            if (n > 0) {
+                hipError_t e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, s);
+                if (e != hipSuccess) return map_status(e);
+                rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
+                                 reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_la);
+                if (rc != TBDK_OK) return rc;
+                t->la_lk = true;
+            }
+        }
+        hipError_t e = hipEventRecord(t->la_done, s);
         if (e != hipSuccess) return map_status(e);
     }
     t->cur ^= 1;
@@ -542,6 +646,42 @@ int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, co
         metrics->host_tracker_us = (float)tracker_us;
         metrics->host_launch_us = (float)launch_us;
         metrics->host_step_us = (float)std::chrono::duration<double, std::micro>(clk::now() - t_step0).count();
+    }
+    return TBDK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
+                  int ndets, tbdk_frame_metrics* metrics, void* stream)
+{
+    return step_impl(t, frame, pitch, frame_id, dets, ndets, nullptr, 0, metrics, static_cast<hipStream_t>(stream));
+}
+
+int tbdk_tbd_step_ahead(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
+                        int ndets, const uint8_t* next_frame, int next_pitch, tbdk_frame_metrics* metrics,
+                        void* stream)
+{
+    return step_impl(t, frame, pitch, frame_id, dets, ndets, next_frame, next_pitch, metrics,
+                     static_cast<hipStream_t>(stream));
+}
+
+int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,
+                 const tbdk_detection* dets, const int32_t* det_offsets, int nframes, tbdk_frame_metrics* metrics,
+                 void* stream)
+{
+    if (!t || nframes < 0 || (nframes > 0 && (!frames || !det_offsets))) return TBDK_EINVAL;
+    for (int i = 0; i < nframes; ++i)
+        if (!frames[i] || det_offsets[i + 1] < det_offsets[i] || det_offsets[i] < 0) return TBDK_EINVAL;
+    if (nframes > 0 && det_offsets[nframes] > det_offsets[0] && !dets) return TBDK_EINVAL;
+    for (int i = 0; i < nframes; ++i) {
+        const uint8_t* next = i + 1 < nframes ? frames[i + 1] : nullptr;
+        int rc = step_impl(t, frames[i], pitch, first_frame_id + i, dets ? dets + det_offsets[i] : nullptr,
+                           det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr,
+                           static_cast<hipStream_t>(stream));
+        if (rc != TBDK_OK) return rc;
     }
     return TBDK_OK;
 }

@@ -41,6 +41,7 @@ struct TimingRec {
 struct tbdk_ctx {
     int device = 0;
     bool timing = false;
+    std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
     // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)

@@ -64,6 +64,11 @@ class Context:
     def timing_enable(self, on: bool = True) -> None:
         _lib.check(self.lib.tbdk_timing_enable(self.handle, int(bool(on))), "tbdk_timing_enable")
 
+    def timing_select(self, names=None) -> None:
+        """Record only these kernels (iterable of names; None = all)."""
+        arg = ",".join(names).encode() if names else None
+        _lib.check(self.lib.tbdk_timing_select(self.handle, arg), "tbdk_timing_select")
+
     def timing_query(self, name: str) -> tuple[int, float]:
         n = C.c_int64()
         ms = C.c_double()

@@ -57,9 +57,18 @@ class TbdLoop:
         self.handle = h
         self._dets = (_lib.Detection * 4096)()
 
-    def step(self, frame: torch.Tensor, frame_id: int, dets, stream=None) -> _lib.FrameMetrics:
+    @staticmethod
+    def _check_frame(frame):
         if frame.dtype != torch.uint8 or frame.dim() != 2 or not frame.is_cuda or frame.stride(1) != 1:
             raise _lib.TbdkError("frame must be a 2-D uint8 device tensor")
+
+    def step(self, frame: torch.Tensor, frame_id: int, dets, stream=None,
+             next_frame: torch.Tensor = None) -> _lib.FrameMetrics:
+        """One frame (tbdk_tbd_step).  With next_frame (which the next call must
+        pass as its frame, unmodified) the next frame's pyramid and the PyrLK the
+        tracker step cannot affect run while this step tracks
+        (tbdk_tbd_step_ahead); results are the same."""
+        self._check_frame(frame)
         n = len(dets)
         if isinstance(dets, np.ndarray):
             if dets.dtype != DET_DTYPE or not dets.flags.c_contiguous:
@@ -73,10 +82,48 @@ class TbdLoop:
                 d.id, d.x, d.y, d.width, d.height, d.confidence = oid, x, y, w, h, conf
             dptr = self._dets
         m = _lib.FrameMetrics()
-        _lib.check(self.ctx.lib.tbdk_tbd_step(self.handle, C.c_void_p(frame.data_ptr()), int(frame.stride(0)),
-                                              int(frame_id), dptr, n, C.byref(m), _stream_ptr(stream)),
-                   "tbdk_tbd_step")
+        if next_frame is None:
+            _lib.check(self.ctx.lib.tbdk_tbd_step(self.handle, C.c_void_p(frame.data_ptr()), int(frame.stride(0)),
+                                                  int(frame_id), dptr, n, C.byref(m), _stream_ptr(stream)),
+                       "tbdk_tbd_step")
+        else:
+            self._check_frame(next_frame)
+            _lib.check(self.ctx.lib.tbdk_tbd_step_ahead(
+                self.handle, C.c_void_p(frame.data_ptr()), int(frame.stride(0)), int(frame_id), dptr, n,
+                C.c_void_p(next_frame.data_ptr()), int(next_frame.stride(0)), C.byref(m), _stream_ptr(stream)),
+                "tbdk_tbd_step_ahead")
         return m
+
+    @staticmethod
+    def pack_detections(dets_per_frame):
+        """(concatenated DET_DTYPE array, int32 offsets) for run()."""
+        arrs = [d if isinstance(d, np.ndarray) else np.array([tuple(x) for x in d], dtype=DET_DTYPE)
+                for d in dets_per_frame]
+        offs = np.zeros(len(arrs) + 1, dtype=np.int32)
+        offs[1:] = np.cumsum([len(a) for a in arrs])
+        cat = np.concatenate(arrs).astype(DET_DTYPE, copy=False) if arrs else np.zeros(0, DET_DTYPE)
+        return np.ascontiguousarray(cat), offs
+
+    def run(self, frames, first_frame_id: int, dets, stream=None, packed=None):
+        """tbdk_tbd_run: the whole frame loop in native code (tbd.cpp:624-706).
+        frames: list of equal-pitch 2-D uint8 device tensors; dets: per-frame
+        detections (or packed=pack_detections(...) prepared ahead).  Returns the
+        per-frame FrameMetrics array."""
+        nf = len(frames)
+        for f in frames:
+            self._check_frame(f)
+        if nf and any(f.stride(0) != frames[0].stride(0) for f in frames):
+            raise _lib.TbdkError("frames must share one pitch")
+        cat, offs = packed if packed is not None else self.pack_detections(dets)
+        if len(offs) != nf + 1:
+            raise _lib.TbdkError("one detection list per frame")
+        ptrs = (C.c_void_p * max(1, nf))(*[f.data_ptr() for f in frames])
+        ms = (_lib.FrameMetrics * max(1, nf))()
+        _lib.check(self.ctx.lib.tbdk_tbd_run(
+            self.handle, ptrs, int(frames[0].stride(0)) if nf else 0, int(first_frame_id),
+            C.cast(cat.ctypes.data, C.POINTER(_lib.Detection)),
+            C.cast(offs.ctypes.data, C.POINTER(C.c_int32)), nf, ms, _stream_ptr(stream)), "tbdk_tbd_run")
+        return ms[:nf]
 
     def predictions(self) -> dict:
         """{track id: (cx, cy)} of the KLT predictions the last step gave the tracker."""

@@ -89,3 +89,72 @@ def test_tbd_loop_tracker_matches_reference_restatement(gpu):
             assert g["max_confidence"] == t.maxConfidence
             assert g["bbox_overlap"] == t.bboxOverlap or (math.isnan(g["bbox_overlap"]) and math.isnan(t.bboxOverlap))
     assert used_preds > 0  # the KLT motion model was exercised
+
+
+def _mkey(m):
+    return (m.tp, m.fn, m.fp, m.gt, m.matches, m.bbox_overlap, m.ntracks, m.lk_points, m.klt_points,
+            m.klt_predicted, m.redetected, m.lk_iters)
+
+
+@pytest.mark.parametrize("W,H,N,F,cfg", [
+    (1280, 720, 24, 30, {}),
+    (640, 480, 20, 24, {"redetect_every": 3, "min_points": 120}),  # frequent refreshes
+    (640, 480, 40, 24, {"max_tracks": 24, "track_age_threshold": 2}),  # slot pool exhausted, slots reused
+])
+def test_tbd_lookahead_and_run_match_step(gpu, W, H, N, F, cfg):
+    """tbdk_tbd_step_ahead and tbdk_tbd_run (the next frame's pyramid and the
+    tracker-independent PyrLK enqueued before the tracker step) give the same
+    per-frame metrics, predictions and final tracks as tbdk_tbd_step."""
+    from opencv_amd import klt, tbd
+
+    frames, gt = klt.synth_render(21, W, H, N, 0, F, ctx=gpu)
+    rng = np.random.default_rng(9)
+    dets = []
+    for f in range(F):
+        d = tbd.detections_from_gt(gt[f].numpy())
+        dets.append(np.ascontiguousarray(d[rng.random(len(d)) > 0.15]))
+    c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, **cfg)
+
+    plain = tbd.TbdLoop(c, ctx=gpu)
+    ahead = tbd.TbdLoop(c, ctx=gpu)
+    ma, mb = [], []
+    for f in range(F):
+        ma.append(_mkey(plain.step(frames[f], f, dets[f])))
+        pa = plain.predictions()
+        mb.append(_mkey(ahead.step(frames[f], f, dets[f], next_frame=frames[f + 1] if f + 1 < F else None)))
+        assert ahead.predictions() == pa, f"frame {f}"
+    assert ma == mb
+    assert plain.tracks() == ahead.tracks()
+
+    batch = tbd.TbdLoop(c, ctx=gpu)
+    ms = batch.run(frames, 0, dets)
+    assert [_mkey(m) for m in ms] == ma
+    assert batch.tracks() == plain.tracks()
+    assert sum(m[9] for m in ma) > 0 and sum(m[10] for m in ma) > 0
+
+
+def test_tbd_lookahead_discarded_on_other_frame(gpu):
+    """A step whose frame is not the one announced as next_frame (or runs on
+    another stream) recomputes everything: same results as plain steps."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 640, 480, 16, 12
+    frames, gt = klt.synth_render(4, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H)
+    plain = tbd.TbdLoop(c, ctx=gpu)
+    odd = tbd.TbdLoop(c, ctx=gpu)
+    other = torch.cuda.Stream()
+    wrong = frames[0].clone()
+    for f in range(F):
+        a = _mkey(plain.step(frames[f], f, dets[f]))
+        if f % 3 == 0:    # announce a different buffer than the one passed next
+            b = _mkey(odd.step(frames[f], f, dets[f], next_frame=wrong))
+        elif f % 3 == 1:  # announce the right frame, then step on another stream
+            b = _mkey(odd.step(frames[f], f, dets[f], next_frame=frames[f + 1]))
+        else:
+            b = _mkey(odd.step(frames[f], f, dets[f], stream=other))
+        assert a == b, f"frame {f}"
+        assert plain.predictions() == odd.predictions()
+    torch.cuda.synchronize()
+    assert plain.tracks() == odd.tracks()
