@@ -75,6 +75,12 @@ typedef struct tbdk_lk_params {
 /* Creates a context bound to HIP device `device` (one per thread x device). */
 int tbdk_ctx_create(int device, tbdk_ctx** out);
 int tbdk_ctx_destroy(tbdk_ctx* ctx);
+/* Context options (test and tuning knobs; TBDK_EINVAL for unknown names):
+ *   "gftt_eig_redo" (0/1): walk every row segment of the GFTT eigenvalue
+ *       strips in sequence, the path taken when a segment's fresh start
+ *       differs from the reference's running box-filter sum (results equal). */
+int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
+
 /* device ordinal of the context */
 int tbdk_ctx_device(const tbdk_ctx* ctx);
 
@@ -166,6 +172,15 @@ typedef struct tbdk_gftt_params {
 int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch,
                    const tbdk_roi* rois, int nroi, const tbdk_gftt_params* params,
                    float* corners, int32_t* counts, void* stream);
+
+/* cv::cuda::createMinEigenValCorner(CV_8UC1, blockSize 3, ksize 3,
+ * BORDER_REFLECT_101)->compute(src, dst) (cudaimgproc/src/corners.cpp:150-189,
+ * cudaimgproc.hpp:564): the minimum-eigenvalue map GFTT selects from, with
+ * the CPU cornerMinEigenVal numerics (float Sobel, double box sums).
+ * dst: device float plane, dst_pitch in bytes.  Uses the context's GFTT
+ * scratch (one launch + one device copy on `stream`). */
+int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
+                            int dst_pitch, void* stream);
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
 
 /* ---- KLT box propagation ----------------------------------------------------- */

@@ -140,6 +140,9 @@ SIGNATURES = {
     "tbdk_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tbdk_ctx_device": (C.c_int, [C.c_void_p]),
     "tbdk_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "tbdk_corner_min_eig_val": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                          C.c_void_p]),
+    "tbdk_ctx_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     "tbdk_timing_select": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),

@@ -101,126 +101,191 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
     return SobelRow{t, u};
 }
 
-struct RowSums {
-    double s0, s1, s2;
-};
-
 // Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 60-column strip of
-// a ROI per workgroup of three waves, wave c carrying cov channel c
-// (Dx^2, DxDy, Dy^2).  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
+// a ROI per workgroup.  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
 // output, two halo lanes per side); each lane loads only its own pixel of a
 // row and gets its neighbours by DPP wave shifts, reflect-101 at the ROI edges
-// turning the missing neighbour into the other one.  Rows are walked top to
-// bottom so each channel's column sum follows the reference's running
-// ColumnSum exactly (box_filter.simd.hpp:176-273): SUM = 0 + rs(-1);
-// SUM += rs(0); per row y: s = SUM + rs(y+1); out = (float)s; SUM = s - rs(y-1),
-// rows reflect-101.  Per batch of 8 rows the three (float) box sums meet in LDS
-// and the waves share the eigenvalue work (rows j = c mod 3 of the batch).
-constexpr int kEigBatch = 16;  // rows per batch of the eigenvalue walk
+// turning the missing neighbour into the other one.
+//
+// The box filter is the reference's running ColumnSum (box_filter.simd.hpp:
+// 176-273), per channel: SUM = (0 + rs(-1)) + rs(0); per row y:
+// s = SUM + rs(y+1); out = (float)s; SUM = s - rs(y-1), rows reflect-101.
+// The strip's rows are split into kEigWaves segments, one wave each, all three
+// channels per wave, walked concurrently.  A segment starting at y0 > 0 starts
+// its SUM fresh as (0 + rs(y0-1)) + rs(y0), which is the reference's running
+// value exactly when every earlier chain operation was exact; this is checked
+// where it matters: segment k is right iff segment k-1 was right and the SUM
+// k-1 ends with equals k's fresh start (segment 0 starts as the reference
+// does).  From the first mismatch on (not observed on natural images, forced
+// by the "gftt_eig_redo" option in the tests) the segments are walked again one
+// after another, each from its predecessor's final SUM: the reference's
+// sequential order.
+constexpr int kEigWaves = 8;  // row segments (waves) per strip
+constexpr int kEigPref = 8;   // pixel rows in flight per wave
 
-template <int CH>
-__device__ __forceinline__ void eig_walk(const GfttArgs& a, const GfttRoi& R, float (*box)[3][kEigBatch][64],
-                                         int* smax)
+struct EigLane {
+    __amdgpu_buffer_rsrc_t rs;
+    int x, H, hm2, pitch;
+    bool at_left, at_right, out_lane;
+    float k, k2;
+};
+
+__device__ __forceinline__ float eig_ld(const EigLane& g, int row)
 {
-    constexpr int B = kEigBatch;
-    const int lane = threadIdx.x & 63;
-    const int xc = (blockIdx.x - R.cblk) * kGfttStrip - 2 + lane;  // this lane's ROI column
-    const bool out_lane = lane >= 2 && lane < 2 + kGfttStrip && xc < R.w;
-    const int x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
-    const bool at_left = x == 0, at_right = x == R.w - 1;
-    const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
-    const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
-    const int H = R.h;
-    const int hm2 = H >= 2 ? H - 2 : 0;
-    // pixel rows through buffer loads: lane offset x in a VGPR, row offset in an SGPR
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.img + (size_t)R.y * a.pitch + R.x), (short)0, a.pitch * H, 0x00020000);
-    auto ld = [&](int row) { return (float)__builtin_amdgcn_raw_buffer_load_b8(rs, x, row * a.pitch, 0); };
-    auto pix = [&](int yy) { return ld(refl(yy, H)); };
-    auto pix_fwd = [&](int yy) { return ld(yy < H ? yy : hm2); };  // yy in [0, H]
-    auto srow = [&](float v) {  // Sobel row terms of the pixel row whose own value is v
-        const float l = from_left(v), rr = from_right(v);
-        const float l2 = at_left ? rr : l, r2 = at_right ? l : rr;
-        return sobel_row(at_left && at_right ? v : l2, v, at_left && at_right ? v : r2, k, k2);
-    };
-    // channel CH of cov, then its boxFilter row sum ((l + c) + r in double)
-    auto rsum = [&](const SobelRow& p, const SobelRow& c, const SobelRow& n) {
-        float cv;
-        if constexpr (CH == 0) {
-            const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
-            cv = dx * dx;
-        } else if constexpr (CH == 1) {
-            const float dx = (p.rx + n.rx) * k + (c.rx * k2 + 0.f);
-            const float dy = (n.ry - p.ry) + 0.f;
-            cv = dx * dy;
-        } else {
-            const float dy = (n.ry - p.ry) + 0.f;
-            cv = dy * dy;
-        }
-        float l = from_left(cv), rr = from_right(cv);
-        if (at_left) l = at_right ? cv : rr;
-        if (at_right) rr = at_left ? cv : l;
-        return (double)l + (double)cv + (double)rr;
-    };
-    // entering rows -1 (= cov row refl(-1): the box filter reflects cov rows) and 0
-    const int rm1 = refl(-1, H);
-    const double em1 = rsum(srow(pix(rm1 - 1)), srow(pix(rm1)), srow(pix(rm1 + 1)));
-    SobelRow wa = srow(pix(0)), wb = srow(pix(1));  // image rows y, y+1 for cov(y+1)
-    const double e0 = rsum(srow(pix(-1)), wa, wb);
-    double S = 0.0 + em1;
-    S = S + e0;
-    double q0 = em1, q1 = e0;  // rs(y-1), rs(y)
-    float* E = a.eig + R.off + x;
-    int best = INT_MIN;
-    float nxt[B];
+    return (float)__builtin_amdgcn_raw_buffer_load_b8(g.rs, g.x, row * g.pitch, 0);
+}
+
+// Sobel row terms of the pixel row whose own value is v (neighbours by DPP)
+__device__ __forceinline__ SobelRow eig_srow(const EigLane& g, float v)
+{
+    const float l = from_left(v), rr = from_right(v);
+    const float l2 = g.at_left ? rr : l, r2 = g.at_right ? l : rr;
+    const bool one = g.at_left && g.at_right;
+    return sobel_row(one ? v : l2, v, one ? v : r2, g.k, g.k2);
+}
+
+// the three cov channels of one row and their boxFilter row sums ((l + c) + r in double)
+__device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p, const SobelRow& c,
+                                            const SobelRow& n, double (&out)[3])
+{
+    const float dx = (p.rx + n.rx) * g.k + (c.rx * g.k2 + 0.f);
+    const float dy = (n.ry - p.ry) + 0.f;
+    const float cv[3] = {dx * dx, dx * dy, dy * dy};
 #pragma unroll
-    for (int j = 0; j < B; ++j) nxt[j] = pix_fwd(min(2 + j, H));
-    for (int y0 = 0, par = 0; y0 < H; y0 += B, par ^= 1) {
-        float cur[B];
+    for (int ch = 0; ch < 3; ++ch) {
+        float l = from_left(cv[ch]), rr = from_right(cv[ch]);
+        if (g.at_left) l = g.at_right ? cv[ch] : rr;
+        if (g.at_right) rr = g.at_left ? cv[ch] : l;
+        out[ch] = (double)l + (double)cv[ch] + (double)rr;
+    }
+}
+
+// Rows [y0, y1) of the strip: box sums from SUM (fresh: the start above),
+// eigenvalues to E, max key into best.  S0 = the SUM the walk started from;
+// S = the SUM after row y1 - 1 (the state row y1 starts from).
+__device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, int w, int y0, int y1, bool fresh,
+                                         double (&S)[3], double (&S0)[3], int& best)
+{
+    const int H = g.H;
+    auto pix = [&](int yy) { return eig_ld(g, refl(yy, H)); };
+    auto pix_fwd = [&](int yy) { return eig_ld(g, yy < H ? yy : g.hm2); };  // yy in [0, H]
+    double qa[3], qb[3];  // rs(y - 1), rs(y)
+    {
+        const int rm = refl(y0 - 1, H);  // the box filter reflects cov rows
+        eig_rowsums(g, eig_srow(g, pix(rm - 1)), eig_srow(g, pix(rm)), eig_srow(g, pix(rm + 1)), qa);
+    }
+    SobelRow wa = eig_srow(g, pix(y0)), wb = eig_srow(g, pix(y0 + 1));
+    eig_rowsums(g, eig_srow(g, pix(y0 - 1)), wa, wb, qb);
+    if (fresh) {
 #pragma unroll
-        for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+        for (int ch = 0; ch < 3; ++ch) S[ch] = (0.0 + qa[ch]) + qb[ch];
+    }
 #pragma unroll
-        for (int j = 0; j < B; ++j) nxt[j] = pix_fwd(min(y0 + B + 2 + j, H));  // next batch in flight
-        SobelRow sr[B + 2];
-        sr[0] = wa;
-        sr[1] = wb;
+    for (int ch = 0; ch < 3; ++ch) S0[ch] = S[ch];
+    float nxt[kEigPref];
 #pragma unroll
-        for (int j = 0; j < B; ++j) sr[j + 2] = srow(cur[j]);
-        double en[B];
+    for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(y0 + 2 + j, H));
+    for (int yb = y0; yb < y1; yb += kEigPref) {
+        float cur[kEigPref];
 #pragma unroll
-        for (int j = 0; j < B; ++j) en[j] = rsum(sr[j], sr[j + 1], sr[j + 2]);
-        const int nb = H - y0 < B ? H - y0 : B;  // rows of this batch (uniform)
+        for (int j = 0; j < kEigPref; ++j) cur[j] = nxt[j];
 #pragma unroll
-        for (int j = 0; j < B; ++j) {  // the sequential ColumnSum chain of this channel
+        for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(yb + kEigPref + 2 + j, H));  // in flight
+        const int nb = y1 - yb < kEigPref ? y1 - yb : kEigPref;  // uniform
+#pragma unroll
+        for (int j = 0; j < kEigPref; ++j) {
             if (j < nb) {
-                const double in = y0 + j + 1 < H ? en[j] : q0;  // rs(refl(h)) == rs(h - 2) == rs(y - 1)
-                const double t = S + in;
-                S = t - q0;
-                q0 = q1;
-                q1 = in;
-                box[par][CH][j][lane] = (float)t;
-            }
-        }
-        wa = sr[B];
-        wb = sr[B + 1];
-        // LDS-only barrier: __syncthreads() would also wait for the next batch's
-        // image loads (vmcnt) and expose their latency every batch
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
+                const int y = yb + j;
+                double in[3];
+                SobelRow wc = wb;
+                if (y + 1 < H) {  // entering cov row y + 1 (image rows y, y+1, y+2)
+                    wc = eig_srow(g, cur[j]);
+                    eig_rowsums(g, wa, wb, wc, in);
+                } else {  // rs(refl(H)) == rs(H - 2) == rs(y - 1)
 #pragma unroll
-        for (int j = CH; j < B; j += 3) {  // eigenvalues of this wave's share of the batch
-            if (j < nb) {
-                const float aa = box[par][0][j][lane] * 0.5f, bb = box[par][1][j][lane],
-                            cc = box[par][2][j][lane] * 0.5f;
+                    for (int ch = 0; ch < 3; ++ch) in[ch] = qa[ch];
+                }
+                float box[3];
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const double t = S[ch] + in[ch];
+                    box[ch] = (float)t;
+                    S[ch] = t - qa[ch];
+                    qa[ch] = qb[ch];
+                    qb[ch] = in[ch];
+                }
+                wa = wb;
+                wb = wc;
+                const float aa = box[0] * 0.5f, bb = box[1], cc = box[2] * 0.5f;
                 const float t = aa - cc;
                 const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-                if (out_lane) {
-                    E[(size_t)(y0 + j) * R.w] = e;
+                if (g.out_lane) {
+                    E[(size_t)y * w] = e;
                     const int kk = fkey(e);
                     best = kk > best ? kk : best;
                 }
             }
         }
+    }
+}
+
+__global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
+{
+    __shared__ double s_end[kEigWaves][3][64];
+    __shared__ int s_best[kEigWaves];
+    __shared__ int s_bad;
+    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
+    const GfttRoi R = a.rois[r];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int H = R.h;
+
+    EigLane g;
+    const int xc = (blockIdx.x - R.cblk) * kGfttStrip - 2 + lane;  // this lane's ROI column
+    g.out_lane = lane >= 2 && lane < 2 + kGfttStrip && xc < R.w;
+    g.x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
+    g.at_left = g.x == 0;
+    g.at_right = g.x == R.w - 1;
+    const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
+    g.k = (float)(1.0 * scale);
+    g.k2 = (float)(2.0 * scale);
+    g.H = H;
+    g.hm2 = H >= 2 ? H - 2 : 0;
+    g.pitch = a.pitch;
+    g.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.img + (size_t)R.y * a.pitch + R.x), (short)0,
+                                             a.pitch * H, 0x00020000);
+    float* E = a.eig + R.off + g.x;
+
+    const int L = (H + kEigWaves - 1) / kEigWaves;  // rows per segment
+    const int y0 = wv * L, y1 = min(H, y0 + L);
+    const bool live = y0 < y1;
+    int best = INT_MIN;
+    double S[3], S0[3];
+    if (threadIdx.x == 0) s_bad = kEigWaves;
+    if (live) {
+        eig_segment(g, E, R.w, y0, y1, true, S, S0, best);
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) s_end[wv][ch][lane] = S[ch];
+    }
+    __syncthreads();
+    if (live && wv > 0) {
+        bool diff = a.eig_redo != 0;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) diff |= S0[ch] != s_end[wv - 1][ch][lane];
+        if (__any(diff) && lane == 0) atomicMin(&s_bad, wv);
+    }
+    __syncthreads();
+    const int bad = s_bad;  // first segment whose start differs from the reference's SUM
+    for (int k = bad; k < kEigWaves; ++k) {  // cold: the reference's sequential order
+        if (wv == k && live) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) S[ch] = s_end[k - 1][ch][lane];
+            best = INT_MIN;
+            eig_segment(g, E, R.w, y0, y1, false, S, S0, best);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) s_end[k][ch][lane] = S[ch];
+        }
+        __syncthreads();
     }
     // per-strip max (minMaxLoc is order independent)
 #pragma unroll
@@ -228,23 +293,13 @@ __device__ __forceinline__ void eig_walk(const GfttArgs& a, const GfttRoi& R, fl
         const int v = __shfl_xor(best, o);
         best = v > best ? v : best;
     }
-    if (lane == 0) smax[CH] = best;
-}
-
-__global__ __launch_bounds__(192) void gftt_eig_kernel(GfttArgs a)
-{
-    __shared__ float box[2][3][kEigBatch][64];  // [batch parity][channel][row][lane]
-    __shared__ int smax[3];
-    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
-    const GfttRoi R = a.rois[r];
-    const int ch = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform channel
-    if (ch == 0) eig_walk<0>(a, R, box, smax);
-    else if (ch == 1) eig_walk<1>(a, R, box, smax);
-    else eig_walk<2>(a, R, box, smax);
+    if (lane == 0) s_best[wv] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int m01 = smax[0] > smax[1] ? smax[0] : smax[1];
-        a.blk_max[blockIdx.x] = m01 > smax[2] ? m01 : smax[2];
+        int m = s_best[0];
+#pragma unroll
+        for (int k = 1; k < kEigWaves; ++k) m = s_best[k] > m ? s_best[k] : m;
+        a.blk_max[blockIdx.x] = m;
     }
 }
 
@@ -665,9 +720,15 @@ void gftt_plan(GfttArgs& a, int max_area)
     a.img_bytes = (int)img;
 }
 
+hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(192), 0, s, a);
+    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
     hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950);

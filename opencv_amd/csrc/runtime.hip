@@ -120,6 +120,16 @@ int tbdk_timing_enable(tbdk_ctx* ctx, int enable)
     return TBDK_OK;
 }
 
+int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
+{
+    if (!ctx || !name) return TBDK_EINVAL;
+    if (std::strcmp(name, "gftt_eig_redo") == 0) {
+        ctx->opt_gftt_eig_redo = value != 0;
+        return TBDK_OK;
+    }
+    return TBDK_EINVAL;
+}
+
 int tbdk_timing_select(tbdk_ctx* ctx, const char* names)
 {
     if (!ctx) return TBDK_EINVAL;
@@ -384,6 +394,7 @@ int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_r
     a.min_distance = p->min_distance;
     a.corners = reinterpret_cast<float2*>(corners);
     a.counts = counts;
+    a.eig_redo = ctx->opt_gftt_eig_redo;
     gftt_plan(a, plan.max_area);
     hipError_t e = launch_gftt(a, s);
     timing_end(ctx, rec, s);
@@ -436,6 +447,44 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     hipError_t e = hipMemcpyAsync(ctx->gftt_rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
     return gftt_launch(ctx, img, pitch, static_cast<const GfttRoi*>(ctx->gftt_rois), plan, p, corners, counts, s);
+}
+
+int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
+                            int dst_pitch, void* stream)
+{
+    if (!ctx || !img || !dst || width <= 0 || height <= 0 || pitch < width || dst_pitch < width * 4 ||
+        dst_pitch % 4 != 0)
+        return TBDK_EINVAL;
+    tbdk_roi roi{0, 0, width, height};
+    tbdk_gftt_params p{1, 0.01, 0.0, 3};
+    GfttPlan plan;
+    GfttRoi tab;
+    int rc = gftt_prepare(&roi, 1, width, height, &p, &tab, &plan);
+    if (rc != TBDK_OK) return rc;
+    rc = tbdk_gftt_reserve(ctx, 1, plan.total);
+    if (rc != TBDK_OK) return rc;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemcpyAsync(ctx->gftt_rois, &tab, sizeof(GfttRoi), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return map_err(e);
+    int rec = timing_begin(ctx, "corner_min_eig", s);
+    GfttArgs a{};
+    a.img = img;
+    a.pitch = pitch;
+    a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
+    a.nroi = 1;
+    a.nblk = plan.nblk;
+    a.ncblk = plan.ncblk;
+    a.eig = static_cast<float*>(ctx->gftt_planes);
+    a.blk_cnt = ctx->gftt_blk;
+    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
+    a.eig_redo = ctx->opt_gftt_eig_redo;
+    e = launch_gftt_eig(a, s);
+    timing_end(ctx, rec, s);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt_planes, (size_t)width * 4, (size_t)width * 4, height,
+                             hipMemcpyDeviceToDevice, s);
+    return map_err(e);
 }
 
 int tbdk_box_propagate(tbdk_ctx* ctx, const float* prev_pts, const float* next_pts, const uint8_t* status,

@@ -41,6 +41,7 @@ struct TimingRec {
 struct tbdk_ctx {
     int device = 0;
     bool timing = false;
+    int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
@@ -159,6 +160,7 @@ struct GfttArgs {
     double quality, min_distance;
     float2* corners;  // nroi x max_corners
     int32_t* counts;  // nroi (-1: candidate overflow)
+    int eig_redo;     // test option: walk every eig strip segment in sequence
 };
 constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
 // scratch sizes for (rois, pixels): pixel blocks <= px/256 + rois, column blocks <= px/64 + rois
@@ -177,4 +179,5 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
 int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
                 const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s);
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s);
+hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s);  // eigenvalue planes only
 }  // namespace tbdk

@@ -64,6 +64,10 @@ class Context:
     def timing_enable(self, on: bool = True) -> None:
         _lib.check(self.lib.tbdk_timing_enable(self.handle, int(bool(on))), "tbdk_timing_enable")
 
+    def set_option(self, name: str, value: int) -> None:
+        """tbdk_ctx_set_option (see include/tbdk.h)."""
+        _lib.check(self.lib.tbdk_ctx_set_option(self.handle, name.encode(), int(value)), "tbdk_ctx_set_option")
+
     def timing_select(self, names=None) -> None:
         """Record only these kernels (iterable of names; None = all)."""
         arg = ",".join(names).encode() if names else None
@@ -146,6 +150,20 @@ def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torc
     _lib.check(ctx.lib.tbdk_pyr_down_u8(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
                                         C.c_void_p(dst.data_ptr()), dst.stride(0), _stream_ptr(stream)),
                "tbdk_pyr_down_u8")
+    return dst
+
+
+def corner_min_eigen_val(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torch.Tensor:
+    """cv::cuda::createMinEigenValCorner(CV_8UC1, 3, 3)->compute: float32 (h, w)
+    minimum-eigenvalue map, bit-exact with the CPU cornerMinEigenVal."""
+    if src.dtype != torch.uint8 or src.dim() != 2 or not src.is_cuda or src.stride(1) != 1:
+        raise _lib.TbdkError("corner_min_eigen_val expects a 2-D uint8 device tensor")
+    ctx = ctx or Context.get(src.device.index or 0)
+    h, w = src.shape
+    dst = torch.empty((h, w), dtype=torch.float32, device=src.device)
+    _lib.check(ctx.lib.tbdk_corner_min_eig_val(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
+                                               C.c_void_p(dst.data_ptr()), dst.stride(0) * 4, _stream_ptr(stream)),
+               "tbdk_corner_min_eig_val")
     return dst
 
 

@@ -57,3 +57,45 @@ def test_gftt_1080p_128_boxes(gpu):
     c, n = detect(gpu, fr[0], rois, 256, 0.01, 3.0)
     check(fr[0], rois, c, n, 256, 0.01, 3.0)
     assert (n > 0).all()
+
+
+@pytest.mark.parametrize("redo", [0, 1])
+@pytest.mark.parametrize("shape", [(480, 640), (37, 61), (3, 3), (1, 7), (9, 1), (1080, 1920), (130, 121)])
+def test_corner_min_eig_matches_oracle(gpu, shape, redo):
+    """cornerMinEigenVal map (the GFTT eigenvalue kernel over one full-image
+    ROI) bit-exact with the oracle, on the concurrent segment walk and on the
+    sequential re-walk (option gftt_eig_redo)."""
+    from opencv_amd import klt
+
+    h, w = shape
+    if h >= 200:
+        fr, _ = O.synth(77, w, h, 12, 0, 1)
+        img = np.ascontiguousarray(fr[0])
+    else:
+        img = np.random.default_rng(h * 1000 + w).integers(0, 256, (h, w), dtype=np.uint8)
+    gpu.set_option("gftt_eig_redo", redo)
+    try:
+        got = klt.corner_min_eigen_val(torch.from_numpy(img).cuda(), ctx=gpu).cpu().numpy()
+    finally:
+        gpu.set_option("gftt_eig_redo", 0)
+    ref = O.min_eig(img)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (300, 0.001, 2.5)])
+def test_gftt_rois_sequential_eig_path(gpu, maxc, q, md):
+    """GFTT results with every eigenvalue strip re-walked in sequence (the
+    path a fresh-start mismatch takes) equal the oracle's."""
+    fr, gt = O.synth(31, 1280, 720, 40, 0, 1)
+    rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]
+    clipped = []
+    for x, y, w, h in rois:
+        x0, y0, x1, y1 = max(x, 0), max(y, 0), min(x + w, 1280), min(y + h, 720)
+        if x1 - x0 >= 3 and y1 - y0 >= 3:
+            clipped.append((x0, y0, x1 - x0, y1 - y0))
+    gpu.set_option("gftt_eig_redo", 1)
+    try:
+        c, n = detect(gpu, fr[0], clipped, maxc, q, md)
+    finally:
+        gpu.set_option("gftt_eig_redo", 0)
+    check(fr[0], clipped, c, n, maxc, q, md)
