@@ -99,3 +99,17 @@ def test_gftt_rois_sequential_eig_path(gpu, maxc, q, md):
     finally:
         gpu.set_option("gftt_eig_redo", 0)
     check(fr[0], clipped, c, n, maxc, q, md)
+
+
+@pytest.mark.parametrize("maxc,md", [(5000, 1.5), (700, 4.0), (3000, 0.0)])
+def test_gftt_large_candidate_sets(gpu, maxc, md):
+    """ROIs with thousands of candidates (noise texture, a flat band of ties):
+    multi-thousand-key sorts and long greedy walks give the oracle's corner
+    lists exactly."""
+    rng = np.random.default_rng(123)
+    img = rng.integers(0, 256, (300, 400), dtype=np.uint8)
+    img[100:140, 50:300] = 77  # flat band: ties and empty regions
+    rois = [(0, 0, 200, 150), (10, 20, 150, 120), (200, 100, 180, 190)]
+    c, n = detect(gpu, img, rois, maxc, 0.001, md)
+    assert (n > 0).all()
+    check(img, rois, c, n, maxc, 0.001, md)
