@@ -52,18 +52,6 @@ __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(k >= 0 
 
 }  // namespace
 
-// flat pixel grid over all ROIs: ROI r owns blocks [rois[r].blk, rois[r+1].blk)
-__device__ __forceinline__ int roi_of_block(const GfttRoi* rois, int nroi, int b)
-{
-    int lo = 0, hi = nroi - 1;
-    while (lo < hi) {  // block-uniform binary search (scalar loads)
-        const int mid = (lo + hi + 1) >> 1;
-        if (rois[mid].blk <= b) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
 __device__ __forceinline__ int roi_of_cblock(const GfttRoi* rois, int nroi, int b)
 {
     int lo = 0, hi = nroi - 1;
@@ -101,9 +89,9 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
     return SobelRow{t, u};
 }
 
-// Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 60-column strip of
-// a ROI per workgroup.  Lane L holds ROI column x0 - 2 + L (lanes 2..61 produce
-// output, two halo lanes per side); each lane loads only its own pixel of a
+// Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 58-column strip of
+// a ROI per workgroup.  Lane L holds ROI column x0 - 3 + L (lanes 3..60 produce
+// output, three halo lanes per side); each lane loads only its own pixel of a
 // row and gets its neighbours by DPP wave shifts, reflect-101 at the ROI edges
 // turning the missing neighbour into the other one.
 //
@@ -160,42 +148,54 @@ __device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p,
     }
 }
 
-// Rows [y0, y1) of the strip: box sums from SUM (fresh: the start above),
-// eigenvalues to E, max key into best.  S0 = the SUM the walk started from;
-// S = the SUM after row y1 - 1 (the state row y1 starts from).
-__device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, int w, int y0, int y1, bool fresh,
-                                         double (&S)[3], double (&S0)[3], int& best)
+// Walk rows [ys, ye) of the strip (own rows [y0, y1) plus one halo row on
+// each side inside the ROI): box sums from SUM (fresh: the start above, at
+// ys), eigenvalues of the own rows to E, their max key into best, and for own
+// interior rows the ballot of lanes whose value is >= all 8 neighbours (the
+// threshold-independent half of the reference's threshold + 3x3 dilate test)
+// into lm.  S0 = the SUM the walk started from; Scap = the SUM before row
+// ycap (the next segment's fresh-start row); S = the SUM after the last row.
+__device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, uint64_t* __restrict__ lm,
+                                            int w, int y0, int y1, int ys, int ye, int ycap, bool fresh,
+                                            double (&S)[3], double (&S0)[3], double (&Scap)[3], int& best)
 {
     const int H = g.H;
     auto pix = [&](int yy) { return eig_ld(g, refl(yy, H)); };
     auto pix_fwd = [&](int yy) { return eig_ld(g, yy < H ? yy : g.hm2); };  // yy in [0, H]
+    const int lane = threadIdx.x & 63;
+    const bool x_in = g.out_lane && g.x >= 1 && g.x <= w - 2;
     double qa[3], qb[3];  // rs(y - 1), rs(y)
     {
-        const int rm = refl(y0 - 1, H);  // the box filter reflects cov rows
+        const int rm = refl(ys - 1, H);  // the box filter reflects cov rows
         eig_rowsums(g, eig_srow(g, pix(rm - 1)), eig_srow(g, pix(rm)), eig_srow(g, pix(rm + 1)), qa);
     }
-    SobelRow wa = eig_srow(g, pix(y0)), wb = eig_srow(g, pix(y0 + 1));
-    eig_rowsums(g, eig_srow(g, pix(y0 - 1)), wa, wb, qb);
+    SobelRow wa = eig_srow(g, pix(ys)), wb = eig_srow(g, pix(ys + 1));
+    eig_rowsums(g, eig_srow(g, pix(ys - 1)), wa, wb, qb);
     if (fresh) {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) S[ch] = (0.0 + qa[ch]) + qb[ch];
     }
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) S0[ch] = S[ch];
+    float e1 = 0.f, e2 = 0.f;  // eigenvalues of rows y - 1, y - 2
     float nxt[kEigPref];
 #pragma unroll
-    for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(y0 + 2 + j, H));
-    for (int yb = y0; yb < y1; yb += kEigPref) {
+    for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(ys + 2 + j, H));
+    for (int yb = ys; yb < ye; yb += kEigPref) {
         float cur[kEigPref];
 #pragma unroll
         for (int j = 0; j < kEigPref; ++j) cur[j] = nxt[j];
 #pragma unroll
         for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(yb + kEigPref + 2 + j, H));  // in flight
-        const int nb = y1 - yb < kEigPref ? y1 - yb : kEigPref;  // uniform
+        const int nb = ye - yb < kEigPref ? ye - yb : kEigPref;  // uniform
 #pragma unroll
         for (int j = 0; j < kEigPref; ++j) {
             if (j < nb) {
                 const int y = yb + j;
+                if (y == ycap) {
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) Scap[ch] = S[ch];
+                }
                 double in[3];
                 SobelRow wc = wb;
                 if (y + 1 < H) {  // entering cov row y + 1 (image rows y, y+1, y+2)
@@ -219,11 +219,22 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
                 const float aa = box[0] * 0.5f, bb = box[1], cc = box[2] * 0.5f;
                 const float t = aa - cc;
                 const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-                if (g.out_lane) {
+                if (y >= y0 && y < y1 && g.out_lane) {
                     E[(size_t)y * w] = e;
                     const int kk = fkey(e);
                     best = kk > best ? kk : best;
                 }
+                const int yc = y - 1;  // row whose 3x3 neighbourhood is now complete
+                if (yc >= y0 && yc < y1 && yc >= 1 && yc <= H - 2) {  // uniform
+                    float m = fmaxf(e2, e);
+                    m = fmaxf(m, fmaxf(from_left(e2), from_right(e2)));
+                    m = fmaxf(m, fmaxf(from_left(e1), from_right(e1)));
+                    m = fmaxf(m, fmaxf(from_left(e), from_right(e)));
+                    const unsigned long long bal = __ballot(x_in && e1 >= m);
+                    if (lane == 0 && lm) lm[yc] = bal;
+                }
+                e2 = e1;
+                e1 = e;
             }
         }
     }
@@ -231,7 +242,7 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
 
 __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
 {
-    __shared__ double s_end[kEigWaves][3][64];
+    __shared__ double s_cap[kEigWaves][3][64];
     __shared__ int s_best[kEigWaves];
     __shared__ int s_bad;
     const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
@@ -241,8 +252,9 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     const int H = R.h;
 
     EigLane g;
-    const int xc = (blockIdx.x - R.cblk) * kGfttStrip - 2 + lane;  // this lane's ROI column
-    g.out_lane = lane >= 2 && lane < 2 + kGfttStrip && xc < R.w;
+    const int strip = blockIdx.x - R.cblk;
+    const int xc = strip * kGfttStrip - kGfttHalo + lane;  // this lane's ROI column
+    g.out_lane = lane >= kGfttHalo && lane < kGfttHalo + kGfttStrip && xc < R.w;
     g.x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
     g.at_left = g.x == 0;
     g.at_right = g.x == R.w - 1;
@@ -255,23 +267,30 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     g.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.img + (size_t)R.y * a.pitch + R.x), (short)0,
                                              a.pitch * H, 0x00020000);
     float* E = a.eig + R.off + g.x;
+    // local-maximum words of this strip (ROIs of at least 3x3; never written otherwise)
+    uint64_t* lm = a.lmax + R.moff + (size_t)strip * H;
+    const bool has_lm = R.w >= 3 && H >= 3;
 
-    const int L = (H + kEigWaves - 1) / kEigWaves;  // rows per segment
+    const int L = (H + kEigWaves - 1) / kEigWaves;  // own rows per segment
     const int y0 = wv * L, y1 = min(H, y0 + L);
     const bool live = y0 < y1;
+    const int ys = y0 > 0 ? y0 - 1 : 0, ye = min(H, y1 + 1);
+    const int ycap = y1 < H ? y1 - 1 : -1;  // the next segment starts fresh at y1 - 1
     int best = INT_MIN;
-    double S[3], S0[3];
+    double S[3], S0[3], Scap[3];
     if (threadIdx.x == 0) s_bad = kEigWaves;
     if (live) {
-        eig_segment(g, E, R.w, y0, y1, true, S, S0, best);
+        eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
+        if (ycap >= 0) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) s_end[wv][ch][lane] = S[ch];
+            for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
+        }
     }
     __syncthreads();
     if (live && wv > 0) {
         bool diff = a.eig_redo != 0;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) diff |= S0[ch] != s_end[wv - 1][ch][lane];
+        for (int ch = 0; ch < 3; ++ch) diff |= S0[ch] != s_cap[wv - 1][ch][lane];
         if (__any(diff) && lane == 0) atomicMin(&s_bad, wv);
     }
     __syncthreads();
@@ -279,11 +298,13 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     for (int k = bad; k < kEigWaves; ++k) {  // cold: the reference's sequential order
         if (wv == k && live) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) S[ch] = s_end[k - 1][ch][lane];
+            for (int ch = 0; ch < 3; ++ch) S[ch] = s_cap[k - 1][ch][lane];
             best = INT_MIN;
-            eig_segment(g, E, R.w, y0, y1, false, S, S0, best);
+            eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, false, S, S0, Scap, best);
+            if (ycap >= 0) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) s_end[k][ch][lane] = S[ch];
+                for (int ch = 0; ch < 3; ++ch) s_cap[k][ch][lane] = Scap[ch];
+            }
         }
         __syncthreads();
     }
@@ -309,56 +330,6 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
 __device__ __forceinline__ uint64_t cand_key(float v, int y, int x)
 {
     return ((uint64_t)((uint32_t)fkey(v) ^ 0x80000000u) << 32) | (uint32_t)((y << 16) | x);
-}
-
-// threshold-to-zero at max*q + 3x3 dilate-equality on interior pixels, one
-// thread per ROI pixel; candidates go to this block's own kGfttBlock slots
-__global__ __launch_bounds__(256) void gftt_nms_kernel(GfttArgs a)
-{
-    __shared__ int lcount;
-    const int r = roi_of_block(a.rois, a.nroi, blockIdx.x);
-    const GfttRoi R = a.rois[r];
-    const int p = (blockIdx.x - R.blk) * blockDim.x + threadIdx.x;
-    const int iw = R.w - 2, ih = R.h - 2;
-    if (iw <= 0 || ih <= 0 || (int)((blockIdx.x - R.blk) * blockDim.x) >= iw * ih) {  // block-uniform
-        if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = 0;
-        return;
-    }
-    if (threadIdx.x == 0) lcount = 0;
-    int mk = INT_MIN;  // ROI max = max of its column blocks' maxima
-    for (int b = R.cblk, e = R.cblk + (R.w + kGfttStrip - 1) / kGfttStrip; b < e; ++b)
-        mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
-    const float thr = (float)((double)fkey_inv(mk) * a.quality);
-    __syncthreads();
-    bool keep = false;
-    uint64_t key = 0;
-    if (p < iw * ih) {
-        const int y = p / iw + 1, x = p - (y - 1) * iw + 1;
-        const float* E = a.eig + R.off + (size_t)y * R.w + x;
-        const float v0 = E[0];
-        const float v = v0 > thr ? v0 : 0.f;
-        if (v != 0.f) {
-            float m = v;
-#pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    const float q0 = E[dy * R.w + dx];
-                    const float q = q0 > thr ? q0 : 0.f;
-                    m = q > m ? q : m;
-                }
-            keep = v == m;
-            key = cand_key(v, y, x);
-        }
-    }
-    // no global atomics (same-address atomics from all XCDs serialise far from
-    // the CU): the select kernel gathers the per-block lists
-    if (keep) {
-        const int li = atomicAdd(&lcount, 1);
-        reinterpret_cast<uint64_t*>(a.cand)[(size_t)blockIdx.x * kGfttBlock + li] = key;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = lcount;
 }
 
 constexpr int kSelThreads = 512;
@@ -517,7 +488,6 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
 }
 
 // LDS layout of the select kernel (one dynamic region):
-//   scan  : kSelThreads ints (gather prefix sums)
 //   keys  : cap uint64 sort keys
 //   acc   : max_corners float2 accepted positions + 64 float2 (list mode)
 //   img   : img_bytes, one byte per ROI pixel (image mode): 0 empty,
@@ -525,14 +495,14 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
 __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int* scan = reinterpret_cast<int*>(smem);
-    uint64_t* keys = reinterpret_cast<uint64_t*>(smem + sizeof(int) * kSelThreads);
+    uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
     float2* acc = reinterpret_cast<float2*>(keys + a.cap);
     float2* bxy = acc + a.max_corners;
     uint8_t* img = reinterpret_cast<uint8_t*>(acc + ((a.max_corners + 65) & ~1));  // 16-byte aligned
     const int r = blockIdx.x;
     const GfttRoi R = a.rois[r];
     const int tid = threadIdx.x;
+    __shared__ int s_total;
     GFTT_STAMP(0);
     const int area = R.w * R.h;
     // image mode: the ROI's byte image fits and the distance window is small
@@ -544,44 +514,63 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     if (img_mode)
         for (int i = tid * 16; i < area; i += kSelThreads * 16) *reinterpret_cast<uint4*>(img + i) = make_uint4(0, 0, 0, 0);
 
-    // ---- gather the candidates of the ROI's NMS blocks, chunk by chunk:
-    // block-wide exclusive scan of the block counts, then one wave per block copies
-    const int nb = (area + kGfttBlock - 1) / kGfttBlock;
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(a.cand);
-    int total = 0;
-    for (int b0 = 0; b0 < nb; b0 += kSelThreads) {
-        const int c = b0 + tid < nb ? a.blk_cnt[R.blk + b0 + tid] : 0;
-        // inclusive scan: wave prefix sums by DPP-free shuffles, then the wave totals
-        int v = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(v, o);
-            v += (tid & 63) >= o ? u : 0;
-        }
-        __shared__ int wtot[kSelThreads / 64];
-        if ((tid & 63) == 63) wtot[tid >> 6] = v;
-        __syncthreads();
-        int off = 0;
-#pragma unroll
-        for (int w = 0; w < kSelThreads / 64; ++w) off += w < (tid >> 6) ? wtot[w] : 0;
-        scan[tid] = v + off;
-        __syncthreads();
-        const int chunk_total = scan[kSelThreads - 1];
-        // one thread per candidate: its block by binary search of the inclusive
-        // scan, so all global loads of the chunk are independent
-        for (int q = tid; q < chunk_total; q += kSelThreads) {
-            int lo = 0, hi = kSelThreads - 1;
-            while (lo < hi) {  // first block whose inclusive sum exceeds q
-                const int mid = (lo + hi) >> 1;
-                if (scan[mid] > q) hi = mid;
-                else lo = mid + 1;
+    // ---- candidates (featureselect.cpp: threshold-to-zero at max*q, 3x3
+    // dilate, interior pixels equal to the dilation): ROI max = max of its
+    // strips' maxima; with max > 0 (so thr > 0) a pixel is a candidate iff its
+    // value > thr and it is >= all 8 neighbours (any larger neighbour exceeds
+    // thr too), i.e. its local-maximum bit from the eigenvalue walk is set.
+    // thr <= 0 (no positive eigenvalue in the ROI): the literal test.
+    int mk = INT_MIN;
+    for (int b = R.cblk, e = R.cblk + (R.w + kGfttStrip - 1) / kGfttStrip; b < e; ++b)
+        mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
+    const float thr = (float)((double)fkey_inv(mk) * a.quality);
+    if (tid == 0) s_total = 0;
+    __syncthreads();
+    const float* Ep = a.eig + R.off;
+    if (R.w >= 3 && R.h >= 3) {
+        if (thr > 0.f) {
+            const int nstrip = (R.w + kGfttStrip - 1) / kGfttStrip;
+            const int nw = nstrip * R.h;
+            for (int wi = tid; wi < nw; wi += kSelThreads) {
+                const int st = wi / R.h, y = wi - st * R.h;
+                if (y < 1 || y > R.h - 2) continue;
+                uint64_t word = a.lmax[R.moff + wi];
+                while (word) {
+                    const int l = __builtin_ctzll(word);
+                    word &= word - 1ull;
+                    const int x = st * kGfttStrip + l - kGfttHalo;
+                    const float v = Ep[(size_t)y * R.w + x];
+                    if (v > thr) {
+                        const int q = atomicAdd(&s_total, 1);
+                        if (q < a.cap) keys[q] = cand_key(v, y, x);
+                    }
+                }
             }
-            const int within = q - (lo == 0 ? 0 : scan[lo - 1]);
-            if (total + q < a.cap) keys[total + q] = src[(size_t)(R.blk + b0 + lo) * kGfttBlock + within];
+        } else {
+            const int iw = R.w - 2, n = iw * (R.h - 2);
+            for (int p = tid; p < n; p += kSelThreads) {
+                const int y = p / iw + 1, x = p - (y - 1) * iw + 1;
+                const float* Ec = Ep + (size_t)y * R.w + x;
+                const float v = Ec[0] > thr ? Ec[0] : 0.f;
+                if (v == 0.f) continue;
+                float m = v;
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const float q0 = Ec[dy * R.w + dx];
+                        const float q = q0 > thr ? q0 : 0.f;
+                        m = q > m ? q : m;
+                    }
+                if (v == m) {
+                    const int q = atomicAdd(&s_total, 1);
+                    if (q < a.cap) keys[q] = cand_key(v, y, x);
+                }
+            }
         }
-        total += chunk_total;
-        __syncthreads();
     }
+    __syncthreads();
+    const int total = s_total;
     if (total > a.cap) {  // candidate buffer overflow: report, never silently truncate
         if (tid == 0) a.counts[r] = -1;
         return;
@@ -698,7 +687,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
 
 size_t gftt_select_smem(int cap, int max_corners, int img_bytes)
 {
-    return sizeof(int) * kSelThreads + sizeof(uint64_t) * (size_t)cap +
+    return sizeof(uint64_t) * (size_t)cap +
            sizeof(float2) * (size_t)((max_corners + 65) & ~1) + (size_t)img_bytes + 32;  // + window over-read
 }
 
@@ -706,7 +695,7 @@ size_t gftt_select_smem(int cap, int max_corners, int img_bytes)
 // room for >= 4096 sort keys, else list mode with the largest key array
 void gftt_plan(GfttArgs& a, int max_area)
 {
-    const long lds = 160L * 1024 - 256;  // static LDS (scan totals) stays out of the dynamic budget
+    const long lds = 160L * 1024 - 256;  // static LDS (counters) stays out of the dynamic budget
     const long fixed = (long)gftt_select_smem(0, a.max_corners, 0);
     long img = ((long)max_area + 15) & ~15L;
     long room = lds - fixed - img;
@@ -726,10 +715,13 @@ hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_gftt(const GfttArgs& a, hipStream_t s)
+hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig)
 {
     hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
-    hipLaunchKernelGGL(gftt_nms_kernel, dim3(a.nblk), dim3(kGfttBlock), 0, s, a);
+    if (after_eig) {
+        const hipError_t e = hipEventRecord(after_eig, s);
+        if (e != hipSuccess) return e;
+    }
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950);
     // done once per device, for the whole LDS, off the per-frame path

@@ -349,30 +349,31 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
 {
     if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
         return TBDK_EINVAL;
-    int64_t total = 0, nblk = 0, ncblk = 0;
+    int64_t total = 0, ncblk = 0, words = 0;
     int max_area = 0;
     for (int i = 0; i < nroi; ++i) {
         const tbdk_roi& r = rois[i];
         if (r.x < 0 || r.y < 0 || r.width <= 0 || r.height <= 0 || r.x + r.width > width || r.y + r.height > height ||
             r.width > 65535 || r.height > 65535)
             return TBDK_EINVAL;
-        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)nblk, (int)ncblk};
+        tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)words, (int)ncblk};
+        const int64_t strips = (r.width + kGfttStrip - 1) / kGfttStrip;
         total += (int64_t)r.width * r.height;
-        nblk += ((int64_t)r.width * r.height + kGfttBlock - 1) / kGfttBlock;
-        ncblk += (r.width + kGfttStrip - 1) / kGfttStrip;
+        ncblk += strips;
+        if (r.width >= 3 && r.height >= 3) words += strips * r.height;  // smaller ROIs have no interior
         max_area = std::max(max_area, r.width * r.height);
     }
-    if (total > INT32_MAX) return TBDK_EINVAL;
+    if (total > INT32_MAX || words > INT32_MAX) return TBDK_EINVAL;
     plan->nroi = nroi;
     plan->total = total;
-    plan->nblk = (int)nblk;
     plan->ncblk = (int)ncblk;
+    plan->words = words;
     plan->max_area = max_area;
     return TBDK_OK;
 }
 
 int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
-                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s)
+                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s, hipEvent_t after_eig)
 {
     int rc = tbdk_gftt_reserve(ctx, plan.nroi, plan.total);
     if (rc != TBDK_OK) return rc;
@@ -383,12 +384,10 @@ int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_r
     a.pitch = pitch;
     a.rois = d_rois;
     a.nroi = plan.nroi;
-    a.nblk = plan.nblk;
     a.ncblk = plan.ncblk;
     a.eig = static_cast<float*>(ctx->gftt_planes);
-    a.blk_cnt = ctx->gftt_blk;
-    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
-    a.cand = ctx->gftt_cand;
+    a.blk_max = ctx->gftt_blk;
+    a.lmax = static_cast<uint64_t*>(ctx->gftt_cand);
     a.max_corners = p->max_corners;
     a.quality = p->quality_level;
     a.min_distance = p->min_distance;
@@ -396,7 +395,7 @@ int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_r
     a.counts = counts;
     a.eig_redo = ctx->opt_gftt_eig_redo;
     gftt_plan(a, plan.max_area);
-    hipError_t e = launch_gftt(a, s);
+    hipError_t e = launch_gftt(a, s, after_eig);
     timing_end(ctx, rec, s);
     return map_err(e);
 }
@@ -418,11 +417,11 @@ int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
     }
     ctx->gftt_cap_rois = 0;
     ctx->gftt_cap_px = 0;
-    const int64_t nb = gftt_max_blocks(rois, px), ncb = gftt_max_cblocks(rois, px);
+    const int64_t ncb = gftt_max_cblocks(rois, px), nw = gftt_max_words(px);
     hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)std::max(rois, 1));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_blk), sizeof(int) * (size_t)(nb + ncb));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_blk), sizeof(int) * (size_t)ncb);
     if (e == hipSuccess) e = hipMalloc(&ctx->gftt_planes, sizeof(float) * (size_t)std::max<int64_t>(px, 1));
-    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, 8 * (size_t)kGfttBlock * (size_t)nb);
+    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, sizeof(uint64_t) * (size_t)nw);
     if (e != hipSuccess) return map_err(e);
     ctx->gftt_cap_rois = rois;
     ctx->gftt_cap_px = px;
@@ -473,11 +472,10 @@ int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int he
     a.pitch = pitch;
     a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
     a.nroi = 1;
-    a.nblk = plan.nblk;
     a.ncblk = plan.ncblk;
     a.eig = static_cast<float*>(ctx->gftt_planes);
-    a.blk_cnt = ctx->gftt_blk;
-    a.blk_max = ctx->gftt_blk + gftt_max_blocks(ctx->gftt_cap_rois, ctx->gftt_cap_px);
+    a.blk_max = ctx->gftt_blk;
+    a.lmax = static_cast<uint64_t*>(ctx->gftt_cand);
     a.eig_redo = ctx->opt_gftt_eig_redo;
     e = launch_gftt_eig(a, s);
     timing_end(ctx, rec, s);

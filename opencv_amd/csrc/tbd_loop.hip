@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <new>
@@ -158,7 +159,13 @@ struct tbdk_tbd {
     // frame's PyrLK of the point sets this step leaves unchanged, enqueued
     // behind the post-tracker GFTT
     hipEvent_t fit_done = nullptr;   // this frame's predictions are on the host
-    hipEvent_t la_done = nullptr;    // look-ahead pyramid (+ PyrLK) complete
+    hipEvent_t la_ready = nullptr;   // look-ahead pyramid complete (recorded on the step's stream)
+    hipEvent_t la_done = nullptr;    // look-ahead PyrLK complete (recorded on la_s)
+    // the look-ahead PyrLK runs on its own stream behind the GFTT eigenvalue
+    // kernel, so the refreshed sets' PyrLK of the next step (caller's stream)
+    // does not queue behind it; only the fit waits for it
+    hipStream_t la_s = nullptr;
+    hipEvent_t eig_done = nullptr;   // this step's GFTT eigenvalue kernel complete (on `side`)
     int32_t* h_la = nullptr;         // look-ahead slot list (pinned) / device copy
     int32_t* d_la = nullptr;
     int la_n = 0;
@@ -202,7 +209,11 @@ int release(tbdk_tbd* t)
     if (t->side) (void)hipStreamSynchronize(t->side);
     if (t->post_done) (void)hipEventDestroy(t->post_done);
     if (t->fit_done) (void)hipEventDestroy(t->fit_done);
+    if (t->la_s) (void)hipStreamSynchronize(t->la_s);
     if (t->la_done) (void)hipEventDestroy(t->la_done);
+    if (t->la_ready) (void)hipEventDestroy(t->la_ready);
+    if (t->la_s) (void)hipStreamDestroy(t->la_s);
+    if (t->eig_done) (void)hipEventDestroy(t->eig_done);
     if (t->side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
@@ -325,6 +336,9 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->post_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->la_s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -384,7 +398,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const bool la_valid = t->la_pyr && t->la_frame == frame && t->la_pitch == pitch;
     const bool had_la_lk = t->la_lk;
     const bool la_lk = la_valid && had_la_lk;
-    if (t->la_pyr && t->la_stream != s) {  // look-ahead work was enqueued on another stream
+    if (t->la_pyr && t->la_stream != s) {  // the look-ahead pyramid was built on another stream
+        hipError_t e = hipStreamWaitEvent(s, t->la_ready, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
+    if (had_la_lk && !la_valid) {  // discarded: it may still read the pyramid about to be rebuilt
         hipError_t e = hipStreamWaitEvent(s, t->la_done, 0);
         if (e != hipSuccess) return map_status(e);
     }
@@ -467,6 +485,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (rc != TBDK_OK) return rc;
         }
         hipError_t e;
+        if (la_lk) {  // the fit reads the look-ahead PyrLK's results
+            e = hipStreamWaitEvent(s, t->la_done, 0);
+            if (e != hipSuccess) return map_status(e);
+        }
         int rec = timing_begin(t->ctx, "tbd_fit", s);
         hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
@@ -585,7 +607,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
         rc = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
-                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side);
+                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side, next ? t->eig_done : nullptr);
         if (rc != TBDK_OK) return rc;
     }
     if (nclear > 0)
@@ -602,6 +624,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
     // set was not refreshed just now (exactly the next step's unchanged sets)
     if (next) {
+        hipError_t e = hipEventRecord(t->la_ready, s);
+        if (e != hipSuccess) return map_status(e);
         if (c.use_klt && !t->tracker->getTracks().empty()) {
             int n = 0;
             for (const auto& tr : t->tracker->getTracks()) {
@@ -612,17 +636,24 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             }
             t->la_n = n;
             if (n > 0) {
-                hipError_t e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, s);
+                // on la_s, after the fit and the pyramid (la_ready) and behind the
+                // GFTT eigenvalue kernel: its many large workgroups would otherwise
+                // wait for the long-lived PyrLK waves to drain
+                hipStream_t ls = t->la_s;
+                e = hipStreamWaitEvent(ls, t->la_ready, 0);
+                if (e == hipSuccess && nroi > 0) e = hipStreamWaitEvent(ls, t->eig_done, 0);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
                 if (e != hipSuccess) return map_status(e);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_la);
+                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la);
                 if (rc != TBDK_OK) return rc;
+                e = hipEventRecord(t->la_done, ls);
+                if (e != hipSuccess) return map_status(e);
                 t->la_lk = true;
             }
         }
-        hipError_t e = hipEventRecord(t->la_done, s);
-        if (e != hipSuccess) return map_status(e);
     }
     t->cur ^= 1;
     t->have_prev = true;

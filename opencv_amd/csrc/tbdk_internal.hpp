@@ -47,8 +47,8 @@ struct tbdk_ctx {
     std::vector<hipEvent_t> free_events;
     // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
     void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
-    int* gftt_blk = nullptr;     // per-block ints: column-block maxima, pixel-block counts
-    void* gftt_cand = nullptr;   // kGfttBlock candidate slots per pixel block
+    int* gftt_blk = nullptr;     // per-strip eigenvalue maxima
+    void* gftt_cand = nullptr;   // local-maximum words (uint64 per strip row)
     void* gftt_planes = nullptr;  // cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
@@ -137,25 +137,25 @@ namespace tbdk {
 // ---- GFTT over ROIs (klt_gftt.hip) ----
 struct GfttRoi {
     int x, y, w, h;
-    int off;  // first pixel of this ROI in the scratch planes
-    int blk;   // first 256-pixel block of this ROI in the flat per-pixel grids
+    int off;   // first pixel of this ROI in the eigenvalue plane
+    int moff;  // first local-maximum word of this ROI (one uint64 per strip row)
     int cblk;  // first kGfttStrip-column strip of this ROI in the flat per-strip grid
 };
-constexpr int kGfttBlock = 256;
-constexpr int kGfttStrip = 60;  // output columns per wave of the eigenvalue walk (+2 halo lanes per side)
+// output columns per wave of the eigenvalue walk: lanes 3..60 (3 halo lanes per
+// side: eigenvalues are exact in lanes 2..61, the 3x3 local-maximum test in 3..60)
+constexpr int kGfttStrip = 58;
+constexpr int kGfttHalo = 3;
 struct GfttArgs {
     const uint8_t* img;
     int pitch;
     const GfttRoi* rois;
     int nroi;
-    int nblk;     // total blocks of the flat per-pixel grids
-    int ncblk;    // total blocks of the flat per-column grid
-    float* eig;   // min eigenvalue per ROI pixel
-    int* blk_max;   // per column block: max eigenvalue key
-    int* blk_cnt;   // per pixel block: candidates found by the NMS block
-    void* cand;     // per pixel block: kGfttBlock candidate slots (value, address key)
-    int cap;        // LDS candidate capacity per ROI (power of two)
-    int img_bytes;  // LDS for the per-ROI byte image of the greedy walk (0: list mode)
+    int ncblk;       // strips over all ROIs (eigenvalue workgroups)
+    float* eig;      // min eigenvalue per ROI pixel
+    int* blk_max;    // per strip: max eigenvalue key
+    uint64_t* lmax;  // per strip row: ballot of the lanes holding an interior 3x3 local maximum
+    int cap;         // LDS candidate capacity per ROI (power of two)
+    int img_bytes;   // LDS for the per-ROI byte image of the greedy walk (0: list mode)
     int max_corners;
     double quality, min_distance;
     float2* corners;  // nroi x max_corners
@@ -163,21 +163,25 @@ struct GfttArgs {
     int eig_redo;     // test option: walk every eig strip segment in sequence
 };
 constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
-// scratch sizes for (rois, pixels): pixel blocks <= px/256 + rois, column blocks <= px/64 + rois
-inline int64_t gftt_max_blocks(int rois, int64_t px) { return px / kGfttBlock + rois; }
+// scratch sizes for (rois, pixels): strips <= px/60 + rois; local-maximum words
+// (ROIs of at least 3x3 only) <= px/60 + px/3
 inline int64_t gftt_max_cblocks(int rois, int64_t px) { return px / kGfttStrip + rois; }
+inline int64_t gftt_max_words(int64_t px) { return px / kGfttStrip + px / 3 + 1; }
 size_t gftt_select_smem(int cap, int max_corners, int img_bytes);
 void gftt_plan(GfttArgs& a, int max_area);  // sets cap and img_bytes
 struct GfttPlan {
-    int nroi = 0, nblk = 0, ncblk = 0, max_area = 0;
+    int nroi = 0, ncblk = 0, max_area = 0;
     int64_t total = 0;  // ROI pixels
+    int64_t words = 0;  // local-maximum words
 };
 // host side of tbdk_gftt_rois: validate and lay out the ROI table (tab: nroi entries)
 int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tbdk_gftt_params* p, GfttRoi* tab,
                  GfttPlan* plan);
 // launches with a device-resident ROI table (uploaded by the caller on stream s)
+// after_eig (optional): recorded between the eigenvalue and select launches
 int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
-                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s);
-hipError_t launch_gftt(const GfttArgs& a, hipStream_t s);
+                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
+                hipEvent_t after_eig = nullptr);
+hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig = nullptr);
 hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s);  // eigenvalue planes only
 }  // namespace tbdk
