@@ -535,14 +535,25 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                 const int st = wi / R.h, y = wi - st * R.h;
                 if (y < 1 || y > R.h - 2) continue;
                 uint64_t word = a.lmax[R.moff + wi];
-                while (word) {
-                    const int l = __builtin_ctzll(word);
-                    word &= word - 1ull;
-                    const int x = st * kGfttStrip + l - kGfttHalo;
-                    const float v = Ep[(size_t)y * R.w + x];
-                    if (v > thr) {
-                        const int q = atomicAdd(&s_total, 1);
-                        if (q < a.cap) keys[q] = cand_key(v, y, x);
+                const float* Er = Ep + (size_t)y * R.w + st * kGfttStrip - kGfttHalo;
+                while (word) {  // up to 8 value loads in flight per round
+                    int xs[8];
+                    float vs[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        xs[u] = -1;
+                        if (word) {
+                            xs[u] = __builtin_ctzll(word);
+                            word &= word - 1ull;
+                            vs[u] = Er[xs[u]];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (xs[u] >= 0 && vs[u] > thr) {
+                            const int q = atomicAdd(&s_total, 1);
+                            if (q < a.cap) keys[q] = cand_key(vs[u], y, st * kGfttStrip + xs[u] - kGfttHalo);
+                        }
                     }
                 }
             }
