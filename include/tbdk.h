@@ -76,9 +76,10 @@ typedef struct tbdk_lk_params {
 int tbdk_ctx_create(int device, tbdk_ctx** out);
 int tbdk_ctx_destroy(tbdk_ctx* ctx);
 /* Context options (test and tuning knobs; TBDK_EINVAL for unknown names):
- *   "gftt_eig_redo" (0/1): walk every row segment of the GFTT eigenvalue
- *       strips in sequence, the path taken when a segment's fresh start
- *       differs from the reference's running box-filter sum (results equal). */
+ *   "gftt_eig_redo" (0/1): treat every row-segment boundary of the GFTT
+ *       eigenvalue strips as a fresh-start mismatch, forcing the re-walk
+ *       rounds taken when a segment's fresh start differs from the
+ *       reference's running box-filter sum (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 
 /* device ordinal of the context */

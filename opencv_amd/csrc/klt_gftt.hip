@@ -243,6 +243,7 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
 __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
 {
     __shared__ double s_cap[kEigWaves][3][64];
+    __shared__ double s_drift[3][64];
     __shared__ int s_best[kEigWaves];
     __shared__ int s_bad;
     const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
@@ -278,7 +279,23 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     const int ycap = y1 < H ? y1 - 1 : -1;  // the next segment starts fresh at y1 - 1
     int best = INT_MIN;
     double S[3], S0[3], Scap[3];
-    if (threadIdx.x == 0) s_bad = kEigWaves;
+    // lanes whose box sums reach an output: the eigenvalues of lanes 2..61 (the
+    // local-maximum test of lanes 3..60 reads their neighbours) inside the ROI;
+    // the outer halo lanes and clamped columns carry sums nothing reads
+    const bool need = lane >= kGfttHalo - 1 && lane <= kGfttHalo + kGfttStrip && xc >= 0 && xc < R.w;
+    // segment `from` on: the first whose start may differ from the reference's SUM
+    auto first_mismatch = [&](int from) {
+        if (threadIdx.x == 0) s_bad = kEigWaves;
+        __syncthreads();
+        if (live && wv > from) {
+            bool diff = a.eig_redo != 0 && wv == from + 1;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) diff |= need && S0[ch] != s_cap[wv - 1][ch][lane];
+            if (__any(diff) && lane == 0) atomicMin(&s_bad, wv);
+        }
+        __syncthreads();
+        return s_bad;
+    };
     if (live) {
         eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
         if (ycap >= 0) {
@@ -286,27 +303,34 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
             for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
         }
     }
-    __syncthreads();
-    if (live && wv > 0) {
-        bool diff = a.eig_redo != 0;
+    int bad = first_mismatch(0);
+    // Cold: segment `bad` is walked again from its predecessor's final SUM (the
+    // reference's value: the predecessor's own start was verified), and the
+    // segments after it concurrently from their fresh starts plus the drift
+    // d = true - fresh found at `bad` (a rounding in the chain shifts every later
+    // SUM by the same amount unless another rounding intervenes); the
+    // boundaries are checked again.  Each round fixes at least segment `bad`.
+    while (bad < kEigWaves) {
+        if (wv == bad && live) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) diff |= S0[ch] != s_cap[wv - 1][ch][lane];
-        if (__any(diff) && lane == 0) atomicMin(&s_bad, wv);
-    }
-    __syncthreads();
-    const int bad = s_bad;  // first segment whose start differs from the reference's SUM
-    for (int k = bad; k < kEigWaves; ++k) {  // cold: the reference's sequential order
-        if (wv == k && live) {
+            for (int ch = 0; ch < 3; ++ch) s_drift[ch][lane] = s_cap[bad - 1][ch][lane] - S0[ch];
+        }
+        __syncthreads();
+        if (wv >= bad && live) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) S[ch] = s_cap[k - 1][ch][lane];
+            for (int ch = 0; ch < 3; ++ch)
+                S[ch] = wv == bad ? s_cap[bad - 1][ch][lane] : S0[ch] + s_drift[ch][lane];
+        }
+        __syncthreads();  // s_cap is rewritten below
+        if (wv >= bad && live) {
             best = INT_MIN;
             eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, false, S, S0, Scap, best);
             if (ycap >= 0) {
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) s_cap[k][ch][lane] = Scap[ch];
+                for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
             }
         }
-        __syncthreads();
+        bad = first_mismatch(bad);
     }
     // per-strip max (minMaxLoc is order independent)
 #pragma unroll

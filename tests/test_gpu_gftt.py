@@ -59,12 +59,14 @@ def test_gftt_1080p_128_boxes(gpu):
     assert (n > 0).all()
 
 
+@pytest.mark.parametrize("shape", [(480, 640), (37, 61), (3, 3), (1, 7), (9, 1), (1080, 1920), (130, 121),
+                                   (17, 200), (33, 58), (34, 59), (2, 2)])
 @pytest.mark.parametrize("redo", [0, 1])
-@pytest.mark.parametrize("shape", [(480, 640), (37, 61), (3, 3), (1, 7), (9, 1), (1080, 1920), (130, 121)])
 def test_corner_min_eig_matches_oracle(gpu, shape, redo):
     """cornerMinEigenVal map (the GFTT eigenvalue kernel over one full-image
-    ROI) bit-exact with the oracle, on the concurrent segment walk and on the
-    sequential re-walk (option gftt_eig_redo)."""
+    ROI, strips of 58 columns) bit-exact with the oracle, on the concurrent
+    segment walk and with a fresh-start mismatch forced at every segment
+    boundary (option gftt_eig_redo: the drift-corrected re-walk rounds)."""
     from opencv_amd import klt
 
     h, w = shape
@@ -82,23 +84,40 @@ def test_corner_min_eig_matches_oracle(gpu, shape, redo):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
+def test_gftt_bench_frames_many_rois(gpu):
+    """GFTT over the bench's 1080p frames and boxes (several frames: the
+    box-filter double rounding that makes the running sum history-dependent
+    occurs in a fraction of strips) equals the oracle."""
+    fr, gt = O.synth(20261015, 1920, 1080, 128, 0, 12)
+    for t in range(0, 12, 3):
+        rois = []
+        for g in gt[t]:
+            if not g[0]:
+                continue
+            x, y, w, h = (int(v) for v in g[1:])
+            x0, y0, x1, y1 = max(x, 0), max(y, 0), min(x + w, 1920), min(y + h, 1080)
+            if x1 - x0 >= 3 and y1 - y0 >= 3:
+                rois.append((x0, y0, x1 - x0, y1 - y0))
+        c, n = detect(gpu, fr[t], rois, 256, 0.01, 3.0)
+        check(fr[t], rois, c, n, 256, 0.01, 3.0)
+
+
 @pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (300, 0.001, 2.5)])
-def test_gftt_rois_sequential_eig_path(gpu, maxc, q, md):
-    """GFTT results with every eigenvalue strip re-walked in sequence (the
-    path a fresh-start mismatch takes) equal the oracle's."""
+def test_gftt_rois_forced_rewalk(gpu, maxc, q, md):
+    """GFTT results with a fresh-start mismatch forced at every eigenvalue
+    segment boundary (the cold re-walk rounds) equal the oracle's."""
     fr, gt = O.synth(31, 1280, 720, 40, 0, 1)
-    rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]
-    clipped = []
-    for x, y, w, h in rois:
+    rois = []
+    for x, y, w, h in (tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]):
         x0, y0, x1, y1 = max(x, 0), max(y, 0), min(x + w, 1280), min(y + h, 720)
         if x1 - x0 >= 3 and y1 - y0 >= 3:
-            clipped.append((x0, y0, x1 - x0, y1 - y0))
+            rois.append((x0, y0, x1 - x0, y1 - y0))
     gpu.set_option("gftt_eig_redo", 1)
     try:
-        c, n = detect(gpu, fr[0], clipped, maxc, q, md)
+        c, n = detect(gpu, fr[0], rois, maxc, q, md)
     finally:
         gpu.set_option("gftt_eig_redo", 0)
-    check(fr[0], clipped, c, n, maxc, q, md)
+    check(fr[0], rois, c, n, maxc, q, md)
 
 
 @pytest.mark.parametrize("maxc,md", [(5000, 1.5), (700, 4.0), (3000, 0.0)])
