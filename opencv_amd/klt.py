@@ -167,6 +167,33 @@ def corner_min_eigen_val(src: torch.Tensor, ctx: Context | None = None, stream=N
     return dst
 
 
+# numpy mirror of tbdk_box_fit (include/tbdk.h)
+BOX_FIT_DTYPE = np.dtype([("m", "<f8", 6), ("cx", "<f8"), ("cy", "<f8"), ("npoints", "<i4"), ("valid", "<i4")])
+
+
+def box_propagate(prev_pts: torch.Tensor, next_pts: torch.Tensor, status, offsets: torch.Tensor,
+                  boxes: torch.Tensor, min_points: int = 4, ctx: Context | None = None, stream=None) -> np.ndarray:
+    """tbdk_box_propagate: per box b, the 4-DOF similarity (getRTMatrix, non
+    full-affine) fitted to points offsets[b]..offsets[b+1] (status != 0 only)
+    and the box centre it carries.  Device tensors: prev/next float32 (N, 2),
+    status uint8 (N) or None, offsets int32 (nboxes + 1), boxes int32
+    (nboxes, 4).  Returns a BOX_FIT_DTYPE array (synchronises the stream)."""
+    for t in (prev_pts, next_pts, offsets, boxes) + ((status,) if status is not None else ()):
+        if not t.is_cuda or not t.is_contiguous():
+            raise _lib.TbdkError("box_propagate expects contiguous device tensors")
+    nb = boxes.shape[0]
+    if offsets.dtype != torch.int32 or boxes.dtype != torch.int32 or offsets.numel() != nb + 1:
+        raise _lib.TbdkError("offsets: int32 (nboxes + 1), boxes: int32 (nboxes, 4)")
+    ctx = ctx or Context.get(prev_pts.device.index or 0)
+    out = torch.zeros(max(1, nb) * BOX_FIT_DTYPE.itemsize, dtype=torch.uint8, device=prev_pts.device)
+    ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    _lib.check(ctx.lib.tbdk_box_propagate(ctx.handle, ptr(prev_pts), ptr(next_pts), ptr(status), ptr(offsets),
+                                          ptr(boxes), nb, int(min_points), ptr(out), _stream_ptr(stream)),
+               "tbdk_box_propagate")
+    res = out.cpu().numpy()
+    return np.frombuffer(res.tobytes(), BOX_FIT_DTYPE)[:nb].copy()
+
+
 # interpolation flags / border modes (reference values, imgproc.hpp / core/base.hpp)
 INTER_NEAREST, INTER_LINEAR, INTER_AREA, WARP_INVERSE_MAP = 0, 1, 3, 16
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = range(6)

@@ -148,3 +148,58 @@ class TbdLoop:
             except Exception:
                 pass
             self.handle = None
+
+
+class Tracker:
+    """cv::tbd::Tracker (modules/trackingbydetection/include/opencv2/tbd.hpp:
+    121-177) on the host through tbdk_tracker_*: performTrackingStep(detections,
+    frame_id) updates the tracks exactly as the reference does; `predictions`
+    ({track id: (cx, cy)}) replace a track's constant-velocity motion model for
+    that step (the KLT hook of Track::motionModel, tbd.hpp:111)."""
+
+    def __init__(self, bounds=(0, 1280, 0, 720), cost_of_non_assignment: float = 10.0,
+                 time_window_size: int = 16, track_age_threshold: int = 4,
+                 track_visibility_threshold: float = 0.3, track_confidence_threshold: float = 0.2):
+        self.lib = _lib.load()
+        a = _lib.TrackerArgs()
+        _lib.check(self.lib.tbdk_tracker_default_args(C.byref(a)), "tbdk_tracker_default_args")
+        a.cost_of_non_assignment = cost_of_non_assignment
+        a.time_window_size = time_window_size
+        a.track_age_threshold = track_age_threshold
+        a.track_visibility_threshold = track_visibility_threshold
+        a.track_confidence_threshold = track_confidence_threshold
+        a.bounds_xmin, a.bounds_xmax, a.bounds_ymin, a.bounds_ymax = bounds
+        self.handle = C.c_void_p()
+        _lib.check(self.lib.tbdk_tracker_create(C.byref(a), C.byref(self.handle)), "tbdk_tracker_create")
+
+    def performTrackingStep(self, detections, frame_id: int, predictions=None) -> _lib.FrameMetrics:
+        """detections: DET_DTYPE array or (id, x, y, w, h, confidence) tuples."""
+        d = detections if isinstance(detections, np.ndarray) else \
+            np.array([tuple(x) for x in detections], dtype=DET_DTYPE)
+        d = np.ascontiguousarray(d, dtype=DET_DTYPE)
+        preds = predictions or {}
+        pa = (_lib.Prediction * max(1, len(preds)))()
+        for i, (tid, (cx, cy)) in enumerate(preds.items()):
+            pa[i].track_id, pa[i].valid, pa[i].cx, pa[i].cy = tid, 1, cx, cy
+        m = _lib.FrameMetrics()
+        _lib.check(self.lib.tbdk_tracker_step(self.handle, C.cast(d.ctypes.data, C.POINTER(_lib.Detection)), len(d),
+                                              int(frame_id), pa, len(preds), C.byref(m)), "tbdk_tracker_step")
+        return m
+
+    def getTracks(self):
+        """TrackInfo records in the tracker's order (Tracker::getTracks, tbd.hpp:163)."""
+        cap = 4096
+        out = (_lib.TrackInfo * cap)()
+        n = C.c_int()
+        _lib.check(self.lib.tbdk_tracker_tracks(self.handle, out, cap, C.byref(n)), "tbdk_tracker_tracks")
+        return [out[i] for i in range(min(n.value, cap))]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.tbdk_tracker_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+

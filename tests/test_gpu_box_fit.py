@@ -5,7 +5,6 @@ kernel in closed form, so the two agree to double rounding scaled by the
 system's condition number: |dM| <= 64 * eps * cond(A) * max(1, |M|), the
 propagated centre within 1e-4 px (far below the 0.5 px that could move the
 track's rounded box), identical point counts and validity."""
-import ctypes as C
 import os
 import sys
 
@@ -18,22 +17,13 @@ import box_fit_oracle as BF  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-BOX_FIT = np.dtype([("m", "<f8", 6), ("cx", "<f8"), ("cy", "<f8"), ("npoints", "<i4"), ("valid", "<i4")])
-
-
 def run(gpu, prev, nxt, status, offsets, boxes, min_points):
-    from opencv_amd import _lib
+    from opencv_amd import klt
 
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-    P, N, O = d(prev), d(nxt), d(offsets.astype(np.int32))
-    S = None if status is None else d(status.astype(np.uint8))
-    Bx = d(np.asarray(boxes, np.int32).reshape(-1, 4))
-    out = torch.zeros(len(boxes) * BOX_FIT.itemsize, dtype=torch.uint8, device="cuda")
-    ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-    _lib.check(gpu.lib.tbdk_box_propagate(gpu.handle, ptr(P), ptr(N), ptr(S), ptr(O), ptr(Bx), len(boxes),
-                                          min_points, ptr(out), None), "tbdk_box_propagate")
-    torch.cuda.synchronize()
-    return np.frombuffer(out.cpu().numpy().tobytes(), BOX_FIT)
+    return klt.box_propagate(d(prev), d(nxt), None if status is None else d(status.astype(np.uint8)),
+                             d(offsets.astype(np.int32)), d(np.asarray(boxes, np.int32).reshape(-1, 4)),
+                             min_points, ctx=gpu)
 
 
 def make_case(rng, nboxes, max_pts):
