@@ -329,6 +329,108 @@ int tbdk_tracker_step(tbdk_tracker* t, const tbdk_detection* dets, int ndets, in
 /* current tracks in the tracker's order (npoints = 0); *n = number of tracks */
 int tbdk_tracker_tracks(const tbdk_tracker* t, tbdk_track_info* out, int cap, int* n);
 
+/* ---- the sample's tracking driver (host only) -------------------------------
+ * samples/gpu/tbd.cpp feeds the tracker ground-truth or external detections
+ * from bbox files and writes MOT metrics.  Restated natively (tbd_app.cpp). */
+
+/* Tracker::reset (tbd.cpp:197-208) */
+int tbdk_tracker_reset(tbdk_tracker* t);
+/* tbdk_tracker_step that also records the tracking result of every detection
+ * carrying a ground-truth id into `traj` (performTrackingStep's trajectoryMap
+ * argument, tbd.cpp:236-265); traj may be NULL. */
+typedef struct tbdk_trajectories tbdk_trajectories;
+int tbdk_tracker_step_traj(tbdk_tracker* t, const tbdk_detection* dets, int ndets, int frame_id,
+                           const tbdk_prediction* preds, int npreds, tbdk_trajectories* traj,
+                           tbdk_frame_metrics* metrics);
+
+/* glibc rand() restated with private state (srand(seed); the sample's rand()
+ * is never seeded = seed 1).  Attached to a tracker, each new track draws its
+ * display colour from it (3 calls, tbd.cpp:71-73), as the reference does from
+ * the global rand(); the sample's history draw shares the sequence. */
+typedef struct tbdk_rand tbdk_rand;
+int tbdk_rand_create(uint32_t seed, tbdk_rand** out);
+int tbdk_rand_destroy(tbdk_rand* r);
+int tbdk_rand_next(tbdk_rand* r, int32_t* out);
+int tbdk_tracker_set_rand(tbdk_tracker* t, tbdk_rand* r);   /* r NULL: colours not drawn */
+/* Args::parseHistoryDistribution (samples/gpu/tbd.cpp:258-291): "7,3" -> normalised floats */
+int tbdk_parse_history_distribution(const char* s, float* out, int cap, int* n);
+/* one history-age draw (samples/gpu/tbd.cpp:656-671): 1 + index of the first
+ * cumulative float weight above rand()/RAND_MAX, else n */
+int tbdk_history_age(tbdk_rand* r, const float* dist, int n, uint32_t* age);
+
+/* Parsed bbox files (parseBboxFile, samples/gpu/tbd.cpp:1163-1295): per class
+ * (0 pedestrians, 1 vehicles) the per-frame rows of one file; camera poses
+ * (object id -1 rows) and a "history|a,b,..." line shared, as in the sample.
+ * Lines "frame|id|x1|x2|y1|y2[|wx|wy[|wz]]" are ground truth (more than four
+ * separators, frames offset by the first frame number), "frame|x1|x2|y1|y2"
+ * external detections (id -2, frames from 0). */
+typedef struct tbdk_sequence tbdk_sequence;
+int tbdk_sequence_create(tbdk_sequence** out);
+int tbdk_sequence_destroy(tbdk_sequence* s);
+/* TBDK_EINVAL where the sample's stoi/stoul/stod throw (message: tbdk_sequence_error) */
+int tbdk_sequence_parse_bbox_file(tbdk_sequence* s, int cls, const char* path, uint32_t num_frames);
+const char* tbdk_sequence_error(const tbdk_sequence* s);
+int tbdk_sequence_info(const tbdk_sequence* s, int cls, int32_t* nframes, int32_t* nposes, int32_t* nhistory);
+int tbdk_sequence_history(const tbdk_sequence* s, uint32_t* out, int cap, int* n);
+int tbdk_sequence_camera_pose(const tbdk_sequence* s, int index, double* out, int cap, int* n);
+/* parseDetections (samples/gpu/tbd.cpp:1297-1340): frame `frame`'s detections
+ * (confidence 1.0); ground-truth rows also add their position to traj (may be NULL) */
+int tbdk_sequence_detections(const tbdk_sequence* s, int cls, int frame, tbdk_trajectories* traj,
+                             tbdk_detection* out, int cap, int* n);
+
+/* std::map<int, Trajectory> (tbd.hpp:46-80) */
+int tbdk_trajectories_create(tbdk_trajectories** out);
+int tbdk_trajectories_destroy(tbdk_trajectories* t);
+int tbdk_trajectories_add_position(tbdk_trajectories* t, int id, int frame, int x, int y, int w, int h);
+int tbdk_trajectories_count(const tbdk_trajectories* t, int* n);
+
+/* the sample's per-history-age output buffers of tracks (samples/gpu/tbd.cpp:524-531, 679-704):
+ * store = buffer[slot] = getTracks(); load = setTracks(buffer[slot]) (slot < 0: empty) */
+typedef struct tbdk_track_buffer tbdk_track_buffer;
+int tbdk_track_buffer_create(int nslots, tbdk_track_buffer** out);
+int tbdk_track_buffer_destroy(tbdk_track_buffer* b);
+int tbdk_tracker_store_tracks(tbdk_tracker* t, tbdk_track_buffer* b, int slot);
+int tbdk_tracker_load_tracks(tbdk_tracker* t, const tbdk_track_buffer* b, int slot);
+
+typedef struct tbdk_scenario_metrics {  /* the "scenario|" line + totals */
+    int32_t mt, pt, ml;              /* mostly tracked / partially / mostly lost trajectories */
+    int32_t idsw, fm;                /* ID switches, fragmentations (sums) */
+    int32_t frames;                  /* "frame|" lines */
+    double mota, amota, motp;
+} tbdk_scenario_metrics;
+
+/* App::writeTrackingOutputToFile (samples/gpu/tbd.cpp:946-1120): appends the
+ * history / object / frame / scenario lines to `path` (NULL or "": metrics
+ * only).  frame_count = frames processed; log_switches prints the sample's
+ * "[frame f] target ... switched" lines to stdout. */
+int tbdk_tracking_write(const tbdk_tracker* t, const uint32_t* history_ages, int nages, int frame_count,
+                        tbdk_trajectories* traj, const char* path, int log_switches, tbdk_scenario_metrics* out);
+
+typedef struct tbdk_app_args {       /* the sample's tracking flags (samples/gpu/tbd.cpp:221-257, 293-331) */
+    const char* pedestrian_bbox_filename;
+    const char* vehicle_bbox_filename;
+    const char* pedestrian_tracking_filepath;
+    const char* vehicle_tracking_filepath;
+    const char* history_distribution;   /* "--history_distribution", NULL = "1" */
+    int32_t write_tracking;
+    int32_t num_tracking_iters;         /* 1 */
+    int32_t num_tracking_frames;        /* 100 */
+    uint32_t rand_seed;                 /* 1 = the sample's unseeded rand() */
+    int32_t verbose;                    /* print ID-switch lines / errors to stdout */
+    tbdk_tracker_args tracker;          /* TbdArgs defaults (samples/gpu/tbd.cpp:249-254) */
+} tbdk_app_args;
+
+typedef struct tbdk_app_result {
+    int64_t frames, detections;         /* over all iterations */
+    tbdk_scenario_metrics scenario[2];  /* last iteration, pedestrians / vehicles */
+} tbdk_app_result;
+
+int tbdk_app_default_args(tbdk_app_args* args);
+/* App::run's tracking loop (samples/gpu/tbd.cpp:479-706, 823-841) over the
+ * bbox files: history-age draw, setTracks from the output buffer,
+ * performTrackingStep per class, tracking output per iteration. */
+int tbdk_app_run(const tbdk_app_args* args, tbdk_app_result* result);
+
 int tbdk_tbd_default_config(int width, int height, tbdk_tbd_config* cfg);
 int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out);
 int tbdk_tbd_destroy(tbdk_tbd* tbd);
@@ -356,6 +458,13 @@ int tbdk_tbd_run(tbdk_tbd* tbd, const uint8_t* const* frames, int pitch, int fir
                  const tbdk_detection* dets, const int32_t* det_offsets, int nframes, tbdk_frame_metrics* metrics,
                  void* stream);
 int tbdk_tbd_tracks(tbdk_tbd* tbd, tbdk_track_info* out, int cap, int* n);
+/* Attach a trajectory map (NULL detaches): every later step records, for each
+ * detection with a ground-truth id (id >= 0), its position (parseDetections,
+ * samples/gpu/tbd.cpp:1327-1338) and its tracking result (tbd.cpp:236-265). */
+int tbdk_tbd_set_trajectories(tbdk_tbd* tbd, tbdk_trajectories* traj);
+/* tbdk_tracking_write for the loop's tracker and attached trajectories */
+int tbdk_tbd_tracking_write(tbdk_tbd* tbd, const uint32_t* history_ages, int nages, int frame_count,
+                            const char* path, int log_switches, tbdk_scenario_metrics* out);
 /* The KLT predictions the last tbdk_tbd_step handed to the tracker (one per
  * track with a valid box fit, in track order); *n = their number. */
 int tbdk_tbd_predictions(const tbdk_tbd* tbd, tbdk_prediction* out, int cap, int* n);

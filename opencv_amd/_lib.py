@@ -133,6 +133,26 @@ class Prediction(C.Structure):
     _fields_ = [("track_id", C.c_uint32), ("valid", C.c_int32), ("cx", C.c_double), ("cy", C.c_double)]
 
 
+class ScenarioMetrics(C.Structure):
+    _fields_ = [("mt", C.c_int32), ("pt", C.c_int32), ("ml", C.c_int32), ("idsw", C.c_int32), ("fm", C.c_int32),
+                ("frames", C.c_int32), ("mota", C.c_double), ("amota", C.c_double), ("motp", C.c_double)]
+
+
+class AppArgs(C.Structure):
+    _fields_ = [("pedestrian_bbox_filename", C.c_char_p), ("vehicle_bbox_filename", C.c_char_p),
+                ("pedestrian_tracking_filepath", C.c_char_p), ("vehicle_tracking_filepath", C.c_char_p),
+                ("history_distribution", C.c_char_p), ("write_tracking", C.c_int32),
+                ("num_tracking_iters", C.c_int32), ("num_tracking_frames", C.c_int32), ("rand_seed", C.c_uint32),
+                ("verbose", C.c_int32), ("tracker", TrackerArgs)]
+
+
+class AppResult(C.Structure):
+    _fields_ = [("frames", C.c_int64), ("detections", C.c_int64), ("scenario", ScenarioMetrics * 2)]
+
+
+_P = C.c_void_p
+_PI = C.POINTER(C.c_int)
+
 # name -> (restype, argtypes); every symbol include/tbdk.h declares
 SIGNATURES = {
     "tbdk_version": (C.c_char_p, []),
@@ -167,6 +187,36 @@ SIGNATURES = {
     "tbdk_tracker_step": (C.c_int, [C.c_void_p, C.POINTER(Detection), C.c_int, C.c_int, C.POINTER(Prediction), C.c_int,
                                     C.POINTER(FrameMetrics)]),
     "tbdk_tracker_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
+    "tbdk_tracker_reset": (C.c_int, [_P]),
+    "tbdk_tracker_step_traj": (C.c_int, [_P, C.POINTER(Detection), C.c_int, C.c_int, C.POINTER(Prediction), C.c_int,
+                                         _P, C.POINTER(FrameMetrics)]),
+    "tbdk_rand_create": (C.c_int, [C.c_uint32, C.POINTER(_P)]),
+    "tbdk_rand_destroy": (C.c_int, [_P]),
+    "tbdk_rand_next": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "tbdk_tracker_set_rand": (C.c_int, [_P, _P]),
+    "tbdk_parse_history_distribution": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, _PI]),
+    "tbdk_history_age": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_uint32)]),
+    "tbdk_sequence_create": (C.c_int, [C.POINTER(_P)]),
+    "tbdk_sequence_destroy": (C.c_int, [_P]),
+    "tbdk_sequence_parse_bbox_file": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_uint32]),
+    "tbdk_sequence_error": (C.c_char_p, [_P]),
+    "tbdk_sequence_info": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int32)]),
+    "tbdk_sequence_history": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int, _PI]),
+    "tbdk_sequence_camera_pose": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.c_int, _PI]),
+    "tbdk_sequence_detections": (C.c_int, [_P, C.c_int, C.c_int, _P, C.POINTER(Detection), C.c_int, _PI]),
+    "tbdk_trajectories_create": (C.c_int, [C.POINTER(_P)]),
+    "tbdk_trajectories_destroy": (C.c_int, [_P]),
+    "tbdk_trajectories_add_position": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "tbdk_trajectories_count": (C.c_int, [_P, _PI]),
+    "tbdk_track_buffer_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "tbdk_track_buffer_destroy": (C.c_int, [_P]),
+    "tbdk_tracker_store_tracks": (C.c_int, [_P, _P, C.c_int]),
+    "tbdk_tracker_load_tracks": (C.c_int, [_P, _P, C.c_int]),
+    "tbdk_tracking_write": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int, C.c_int, _P, C.c_char_p, C.c_int,
+                                      C.POINTER(ScenarioMetrics)]),
+    "tbdk_app_default_args": (C.c_int, [C.POINTER(AppArgs)]),
+    "tbdk_app_run": (C.c_int, [C.POINTER(AppArgs), C.POINTER(AppResult)]),
     "tbdk_tbd_default_config": (C.c_int, [C.c_int, C.c_int, C.POINTER(TbdConfig)]),
     "tbdk_tbd_create": (C.c_int, [C.c_void_p, C.POINTER(TbdConfig), C.POINTER(C.c_void_p)]),
     "tbdk_tbd_destroy": (C.c_int, [C.c_void_p]),
@@ -176,6 +226,9 @@ SIGNATURES = {
                                       C.c_void_p, C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
     "tbdk_tbd_run": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(Detection),
                                C.POINTER(C.c_int32), C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
+    "tbdk_tbd_set_trajectories": (C.c_int, [_P, _P]),
+    "tbdk_tbd_tracking_write": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_char_p, C.c_int,
+                                          C.POINTER(ScenarioMetrics)]),
     "tbdk_tbd_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_tbd_predictions": (C.c_int, [C.c_void_p, C.POINTER(Prediction), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -135,6 +135,7 @@ struct tbdk_tbd {
     int cur = 0;
     bool have_prev = false;
     tbd::Tracker* tracker = nullptr;
+    tbdk_trajectories* traj = nullptr;  // caller-owned; records per-object tracking results
     // device
     float2* slot_pts = nullptr;
     float2* slot_next = nullptr;
@@ -371,6 +372,24 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
 
 int tbdk_tbd_destroy(tbdk_tbd* t) { return release(t); }
 
+int tbdk_tbd_set_trajectories(tbdk_tbd* t, tbdk_trajectories* traj)
+{
+    if (!t) return TBDK_EINVAL;
+    t->traj = traj;
+    return TBDK_OK;
+}
+
+int tbdk_tbd_tracking_write(tbdk_tbd* t, const uint32_t* history_ages, int nages, int frame_count, const char* path,
+                            int log_switches, tbdk_scenario_metrics* out)
+{
+    if (!t || !t->traj || nages < 0 || (nages > 0 && !history_ages) || frame_count < 0) return TBDK_EINVAL;
+    std::vector<unsigned> ages(history_ages, history_ages + nages);
+    return app::write_tracking_output(*t->tracker, ages, t->traj->map, (unsigned)frame_count, path,
+                                      log_switches ? stdout : nullptr, out)
+               ? TBDK_OK
+               : TBDK_EINVAL;
+}
+
 }  // extern "C"
 
 namespace {
@@ -538,7 +557,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         d.confidence = dets[i].confidence;
     }
     auto tt0 = clk::now();
-    t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size());
+    if (t->traj) app::add_positions(t->traj->map, t->dets, frame_id);
+    t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size(),
+                                    t->traj ? &t->traj->map : nullptr);
     const double tracker_us = std::chrono::duration<double, std::micro>(clk::now() - tt0).count();
     if (!synced) {  // no fit this step: order the previous step's uploads before reusing h_clear / h_roi_slot
         hipError_t e = hipStreamSynchronize(s);

@@ -41,6 +41,58 @@ static inline bool equalsZero(double v)  // tbd.hpp:178-181
     return (v < 0.0) ? (v > -0.00000001) : (v < 0.00000001);
 }
 
+// srandom_r / random_r, TYPE_3 (glibc stdlib/random_r.c)
+void CRand::srand(uint32_t seed)
+{
+    if (seed == 0) seed = 1;
+    int32_t word = (int32_t)seed;
+    ring[0] = word;
+    for (int i = 1; i < 31; ++i) {
+        // 16807 * word % 2147483647 without overflow (Schrage)
+        const long hi = word / 127773, lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        ring[i] = word;
+    }
+    f = 3;
+    b = 0;
+    for (int i = 0; i < 310; ++i) rand();
+}
+
+int CRand::rand()
+{
+    const uint32_t val = (uint32_t)ring[f] + (uint32_t)ring[b];
+    ring[f] = (int32_t)val;
+    if (++f >= 31) {
+        f = 0;
+        ++b;
+    } else if (++b >= 31) {
+        b = 0;
+    }
+    return (int)(val >> 1);
+}
+
+void Trajectory::addPosition(int frame, const Rect& bbox)
+{
+    presentFrames.push_back(frame);
+    positionPerFrame[frame] = bbox;
+}
+
+void Trajectory::addTrackingInfo(int frame, const Track* track)
+{
+    if (track) {
+        isTrackedPerFrame[frame] = true;
+        trackIdPerFrame[frame] = (int)track->id;
+        const Rect& bbox = track->bboxes.back();
+        const Rect& gt = positionPerFrame[frame];  // default-inserted if absent, as map::operator[]
+        trackPosPerFrame[frame] = bbox;
+        predPosPerFrame[frame] = track->predPosition;
+        bboxOverlapPerFrame[frame] = computeBoundingBoxOverlap(bbox, gt);
+    } else {
+        isTrackedPerFrame[frame] = false;
+    }
+}
+
 Tracker::Tracker(const TbdArgs& a) : args(a) {}
 
 void Tracker::reset()  // tbd.cpp:197-208
@@ -423,7 +475,7 @@ void Tracker::deleteLostTracks()
 }
 
 // createNewTracks + Track::Track(Detection&, Tracker*) (tbd.cpp:1043-1055, 67-91);
-// the display colour drawn from rand() (:71-74) is not reproduced
+// the display colour is drawn from the attached CRand (rand() % 256 x 3, :71-74)
 void Tracker::createNewTracks(std::vector<Detection>& dets, const std::vector<unsigned>& un)
 {
     for (unsigned j : un) {
@@ -440,13 +492,16 @@ void Tracker::createNewTracks(std::vector<Detection>& dets, const std::vector<un
         t.predPosition = d.bbox;
         t.bboxOverlap = 1.0;
         t.historyLength = 1;
+        if (rng)
+            for (int c = 0; c < 3; ++c) t.color[c] = rng->rand() % 256;
         createdIds.push_back(t.id);
         tracks.push_back(std::move(t));
     }
 }
 
 // performTrackingStep (tbd.cpp:210-286)
-void Tracker::performTrackingStep(std::vector<Detection>& dets, int frame_id, const Prediction* preds, int npreds)
+void Tracker::performTrackingStep(std::vector<Detection>& dets, int frame_id, const Prediction* preds, int npreds,
+                                  TrajectoryMap* traj)
 {
     createdIds.clear();
     deletedIds.clear();
@@ -458,8 +513,16 @@ void Tracker::performTrackingStep(std::vector<Detection>& dets, int frame_id, co
     updateAssignedTracks(dets, assignments);
     updateUnassignedTracks(unassignedTracks, frame_id);
     unsigned numAssigned = 0;
-    for (size_t i = 0; i < tracks.size(); ++i)
-        if (assignments[i] >= 0) numAssigned++;
+    for (size_t i = 0; i < tracks.size(); ++i) {
+        if (assignments[i] < 0) continue;
+        numAssigned++;
+        const Detection& d = dets[(size_t)assignments[i]];
+        if (traj && d.id >= 0) (*traj)[d.id].addTrackingInfo(frame_id, &tracks[i]);
+    }
+    // unassigned detections: the tracks created for them below are not recorded (tbd.cpp:255-265)
+    if (traj)
+        for (unsigned j : unassignedDetections)
+            if (dets[j].id >= 0) (*traj)[dets[j].id].addTrackingInfo(frame_id, nullptr);
     lastAssignments = assignments;
     deleteLostTracks();
     createNewTracks(dets, unassignedDetections);
@@ -479,12 +542,6 @@ void Tracker::performTrackingStep(std::vector<Detection>& dets, int frame_id, co
 }  // namespace tbdk
 
 // ---- host-only C ABI of the tracker (include/tbdk.h) ----
-struct tbdk_tracker {
-    tbdk::tbd::Tracker tracker;
-    std::vector<tbdk::tbd::Detection> dets;
-    std::vector<tbdk::tbd::Prediction> preds;
-    explicit tbdk_tracker(const tbdk::tbd::TbdArgs& a) : tracker(a) {}
-};
 
 extern "C" {
 

@@ -16,7 +16,11 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
+#include <map>
 #include <vector>
+
+#include "../../include/tbdk.h"
 
 namespace tbdk {
 namespace tbd {
@@ -84,8 +88,46 @@ struct Track {  // cv::tbd::Track (tbd.hpp:89-114) with bounded history
     Rect predPosition;
     double bboxOverlap = 1.0;
     int64_t historyLength = 1;  // number of boxes the reference vector would hold
+    int color[3] = {0, 0, 0};   // display colour (tbd.cpp:71-74), drawn when the tracker has a CRand
     int slot = -1;              // GPU point-set slot (product bookkeeping, not in the reference)
 };
+
+// glibc rand()/srand() (TYPE_3 additive feedback generator, degree 31,
+// separation 3; glibc stdlib/random_r.c) restated with private state.  The
+// sample draws from the process-global rand(): 3 calls per new track for its
+// colour (tbd.cpp:71-73) and one per frame for the history age
+// (samples/gpu/tbd.cpp:660), never seeded (= srand(1)).  Keeping that
+// sequence is what makes the history choices of a replay identical.
+class CRand {
+public:
+    explicit CRand(uint32_t seed = 1) { srand(seed); }
+    void srand(uint32_t seed);
+    int rand();
+    static constexpr int kRandMax = 2147483647;
+
+private:
+    int32_t ring[31];
+    unsigned f = 3, b = 0;  // front / rear taps into the ring
+};
+
+// cv::tbd::Trajectory (tbd.hpp:46-80, tbd.cpp:119-171): the ground-truth
+// history of one object and the tracking result per frame.  std::map keeps the
+// reference's operator[] semantics (absent keys default-insert).
+struct Trajectory {
+    int id = -1;
+    std::vector<int> presentFrames;
+    std::map<int, Rect> positionPerFrame;
+    std::map<int, bool> isTrackedPerFrame;
+    std::map<int, int> trackIdPerFrame;
+    std::map<int, Rect> predPosPerFrame;
+    std::map<int, Rect> trackPosPerFrame;
+    std::map<int, double> bboxOverlapPerFrame;
+    Trajectory() = default;
+    explicit Trajectory(int id_) : id(id_) {}
+    void addPosition(int frame, const Rect& bbox);  // tbd.cpp:141-146 (world position: display only)
+    void addTrackingInfo(int frame, const struct Track* track);  // tbd.cpp:148-171
+};
+using TrajectoryMap = std::map<int, Trajectory>;
 
 // predicted centroid supplied by the KLT box propagation (per track id)
 struct Prediction {
@@ -100,11 +142,16 @@ public:
     void reset();
     unsigned getNextTrackId() { return nextTrackId++; }
     std::vector<Track>& getTracks() { return tracks; }
+    void setTracks(const std::vector<Track>& t) { tracks = t; }  // tbd.cpp:187-190
+    // the rand() the new tracks' colours are drawn from (null: not drawn)
+    void setRand(CRand* r) { rng = r; }
 
     // Tracker::performTrackingStep (tbd.cpp:210-286).  preds (may be null)
     // override the motion model for the tracks they name.
+    // traj (may be null) receives addTrackingInfo for the detections that
+    // carry a ground-truth id (tbd.cpp:236-265).
     void performTrackingStep(std::vector<Detection>& dets, int frame_id, const Prediction* preds = nullptr,
-                             int npreds = 0);
+                             int npreds = 0, TrajectoryMap* traj = nullptr);
 
     // per-frame metrics (tbd.hpp:145-151)
     std::vector<int> truePositives, falseNegatives, falsePositives, groundTruths, numMatches;
@@ -116,6 +163,7 @@ public:
 
 private:
     TbdArgs args;
+    CRand* rng = nullptr;
     unsigned nextTrackId = 0;
     std::vector<Track> tracks;
     std::vector<double> cost;  // flat n x n cost matrix
@@ -142,4 +190,30 @@ private:
 double computeBoundingBoxOverlap(const Rect& a, const Rect& b);  // tbd.cpp:1085-1106
 
 }  // namespace tbd
+
+namespace app {  // tbd_app.cpp
+// App::writeTrackingOutputToFile (samples/gpu/tbd.cpp:946-1120); path NULL/"" = metrics only
+bool write_tracking_output(const tbd::Tracker& tk, const std::vector<unsigned>& historyAges,
+                           tbd::TrajectoryMap& trajectoryMap, unsigned frame_count, const char* path, FILE* log,
+                           tbdk_scenario_metrics* out);
+// parseDetections' addPosition for every detection with a ground-truth id
+void add_positions(tbd::TrajectoryMap& traj, const std::vector<tbd::Detection>& dets, int frame);
+}  // namespace app
+
+namespace tbd {
+
+}  // namespace tbd
 }  // namespace tbdk
+
+// the host tracker behind the tbdk_tracker_* C ABI (tbd_tracker.cpp, tbd_app.cpp)
+struct tbdk_tracker {
+    tbdk::tbd::Tracker tracker;
+    std::vector<tbdk::tbd::Detection> dets;
+    std::vector<tbdk::tbd::Prediction> preds;
+    explicit tbdk_tracker(const tbdk::tbd::TbdArgs& a) : tracker(a) {}
+};
+
+// std::map<int, Trajectory> behind the tbdk_trajectories C ABI (tbd_app.cpp, tbd_loop.hip)
+struct tbdk_trajectories {
+    tbdk::tbd::TrajectoryMap map;
+};

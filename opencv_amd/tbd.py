@@ -125,6 +125,24 @@ class TbdLoop:
             C.cast(offs.ctypes.data, C.POINTER(C.c_int32)), nf, ms, _stream_ptr(stream)), "tbdk_tbd_run")
         return ms[:nf]
 
+    def set_trajectories(self, traj: "Trajectories | None"):
+        """Record per-object tracking results of detections with ground-truth ids
+        (tbdk_tbd_set_trajectories); keep `traj` alive while attached."""
+        self._traj = traj
+        _lib.check(self.ctx.lib.tbdk_tbd_set_trajectories(self.handle, traj.handle if traj else None),
+                   "tbdk_tbd_set_trajectories")
+
+    def write_tracking_output(self, frame_count: int, path: str | None = None, history_ages=None,
+                              log_switches: bool = False) -> dict:
+        """The sample's tracking output / MOT metrics for this loop (history age 1 per frame)."""
+        ages = list(history_ages) if history_ages is not None else [1] * int(frame_count)
+        arr = (C.c_uint32 * max(1, len(ages)))(*ages)
+        m = _lib.ScenarioMetrics()
+        _lib.check(self.ctx.lib.tbdk_tbd_tracking_write(self.handle, arr, len(ages), int(frame_count),
+                                                        str(path).encode() if path else None, int(log_switches),
+                                                        C.byref(m)), "tbdk_tbd_tracking_write")
+        return {k: getattr(m, k) for k, _ in _lib.ScenarioMetrics._fields_}
+
     def predictions(self) -> dict:
         """{track id: (cx, cy)} of the KLT predictions the last step gave the tracker."""
         arr = (_lib.Prediction * 4096)()
@@ -172,8 +190,11 @@ class Tracker:
         self.handle = C.c_void_p()
         _lib.check(self.lib.tbdk_tracker_create(C.byref(a), C.byref(self.handle)), "tbdk_tracker_create")
 
-    def performTrackingStep(self, detections, frame_id: int, predictions=None) -> _lib.FrameMetrics:
-        """detections: DET_DTYPE array or (id, x, y, w, h, confidence) tuples."""
+    def performTrackingStep(self, detections, frame_id: int, predictions=None,
+                            trajectories: "Trajectories | None" = None) -> _lib.FrameMetrics:
+        """detections: DET_DTYPE array or (id, x, y, w, h, confidence) tuples;
+        trajectories: the trajectoryMap argument of the reference (ground-truth
+        detections record their tracking result there)."""
         d = detections if isinstance(detections, np.ndarray) else \
             np.array([tuple(x) for x in detections], dtype=DET_DTYPE)
         d = np.ascontiguousarray(d, dtype=DET_DTYPE)
@@ -182,9 +203,27 @@ class Tracker:
         for i, (tid, (cx, cy)) in enumerate(preds.items()):
             pa[i].track_id, pa[i].valid, pa[i].cx, pa[i].cy = tid, 1, cx, cy
         m = _lib.FrameMetrics()
-        _lib.check(self.lib.tbdk_tracker_step(self.handle, C.cast(d.ctypes.data, C.POINTER(_lib.Detection)), len(d),
-                                              int(frame_id), pa, len(preds), C.byref(m)), "tbdk_tracker_step")
+        _lib.check(self.lib.tbdk_tracker_step_traj(
+            self.handle, C.cast(d.ctypes.data, C.POINTER(_lib.Detection)), len(d), int(frame_id), pa, len(preds),
+            trajectories.handle if trajectories is not None else None, C.byref(m)), "tbdk_tracker_step_traj")
         return m
+
+    def reset(self):
+        _lib.check(self.lib.tbdk_tracker_reset(self.handle), "tbdk_tracker_reset")
+
+    def setRand(self, rng: "CRand | None"):
+        """Draw new tracks' colours from rng (the reference's global rand())."""
+        self._rng = rng
+        _lib.check(self.lib.tbdk_tracker_set_rand(self.handle, rng.handle if rng else None), "tbdk_tracker_set_rand")
+
+    def storeTracks(self, buf: "TrackBuffer", slot: int):
+        """buf[slot] = getTracks() (the sample's track output buffer)."""
+        _lib.check(self.lib.tbdk_tracker_store_tracks(self.handle, buf.handle, int(slot)), "tbdk_tracker_store_tracks")
+
+    def setTracks(self, buf: "TrackBuffer | None", slot: int = -1):
+        """setTracks(buf[slot]); no buffer or slot < 0 sets no tracks (tbd.cpp:187-190)."""
+        _lib.check(self.lib.tbdk_tracker_load_tracks(self.handle, buf.handle if buf else None, int(slot)),
+                   "tbdk_tracker_load_tracks")
 
     def getTracks(self):
         """TrackInfo records in the tracker's order (Tracker::getTracks, tbd.hpp:163)."""
@@ -203,3 +242,168 @@ class Tracker:
                 pass
             self.handle = None
 
+
+
+class _Handle:
+    _destroy = ""
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                getattr(self.lib, self._destroy)(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class CRand(_Handle):
+    """glibc rand() with private state (srand(seed)); the sample's rand() is unseeded (seed 1)."""
+    _destroy = "tbdk_rand_destroy"
+
+    def __init__(self, seed: int = 1):
+        self.lib = _lib.load()
+        self.handle = C.c_void_p()
+        _lib.check(self.lib.tbdk_rand_create(int(seed), C.byref(self.handle)), "tbdk_rand_create")
+
+    def rand(self) -> int:
+        v = C.c_int32()
+        _lib.check(self.lib.tbdk_rand_next(self.handle, C.byref(v)), "tbdk_rand_next")
+        return v.value
+
+    def history_age(self, dist) -> int:
+        """The sample's history-age draw over a normalised distribution."""
+        a = (C.c_float * len(dist))(*dist)
+        age = C.c_uint32()
+        _lib.check(self.lib.tbdk_history_age(self.handle, a, len(dist), C.byref(age)), "tbdk_history_age")
+        return age.value
+
+
+def parse_history_distribution(s: str) -> list:
+    """Args::parseHistoryDistribution (samples/gpu/tbd.cpp:258-291)."""
+    lib = _lib.load()
+    out = (C.c_float * 256)()
+    n = C.c_int()
+    _lib.check(lib.tbdk_parse_history_distribution(s.encode(), out, 256, C.byref(n)),
+               "tbdk_parse_history_distribution")
+    return [out[i] for i in range(min(n.value, 256))]
+
+
+class Trajectories(_Handle):
+    """std::map<int, cv::tbd::Trajectory> (tbd.hpp:46-80)."""
+    _destroy = "tbdk_trajectories_destroy"
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.handle = C.c_void_p()
+        _lib.check(self.lib.tbdk_trajectories_create(C.byref(self.handle)), "tbdk_trajectories_create")
+
+    def addPosition(self, obj_id: int, frame: int, x: int, y: int, w: int, h: int):
+        _lib.check(self.lib.tbdk_trajectories_add_position(self.handle, obj_id, frame, x, y, w, h),
+                   "tbdk_trajectories_add_position")
+
+    def __len__(self):
+        n = C.c_int()
+        _lib.check(self.lib.tbdk_trajectories_count(self.handle, C.byref(n)), "tbdk_trajectories_count")
+        return n.value
+
+
+class TrackBuffer(_Handle):
+    """The sample's per-history-age track output buffers (samples/gpu/tbd.cpp:524-531)."""
+    _destroy = "tbdk_track_buffer_destroy"
+
+    def __init__(self, nslots: int):
+        self.lib = _lib.load()
+        self.handle = C.c_void_p()
+        _lib.check(self.lib.tbdk_track_buffer_create(int(nslots), C.byref(self.handle)), "tbdk_track_buffer_create")
+
+
+PEDESTRIANS, VEHICLES = 0, 1
+
+
+class Sequence(_Handle):
+    """Parsed bbox files (parseBboxFile, samples/gpu/tbd.cpp:1163-1295): per class
+    the per-frame rows; camera poses and history choices shared between files."""
+    _destroy = "tbdk_sequence_destroy"
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.handle = C.c_void_p()
+        _lib.check(self.lib.tbdk_sequence_create(C.byref(self.handle)), "tbdk_sequence_create")
+
+    def parseBboxFile(self, path: str, num_frames: int, cls: int = PEDESTRIANS):
+        rc = self.lib.tbdk_sequence_parse_bbox_file(self.handle, int(cls), str(path).encode(), int(num_frames))
+        if rc != _lib.TBDK_OK:
+            raise _lib.TbdkError(f"parseBboxFile: {self.lib.tbdk_sequence_error(self.handle).decode()}")
+
+    def info(self, cls: int = PEDESTRIANS):
+        nf, npose, nh = C.c_int32(), C.c_int32(), C.c_int32()
+        _lib.check(self.lib.tbdk_sequence_info(self.handle, int(cls), C.byref(nf), C.byref(npose), C.byref(nh)),
+                   "tbdk_sequence_info")
+        return nf.value, npose.value, nh.value
+
+    def history(self) -> list:
+        n = C.c_int()
+        _lib.check(self.lib.tbdk_sequence_history(self.handle, None, 0, C.byref(n)), "tbdk_sequence_history")
+        out = (C.c_uint32 * max(1, n.value))()
+        _lib.check(self.lib.tbdk_sequence_history(self.handle, out, n.value, C.byref(n)), "tbdk_sequence_history")
+        return list(out[:n.value])
+
+    def cameraPose(self, index: int) -> list:
+        out = (C.c_double * 16)()
+        n = C.c_int()
+        _lib.check(self.lib.tbdk_sequence_camera_pose(self.handle, int(index), out, 16, C.byref(n)),
+                   "tbdk_sequence_camera_pose")
+        return list(out[:min(n.value, 16)])
+
+    def detections(self, frame: int, cls: int = PEDESTRIANS, trajectories: Trajectories | None = None) -> np.ndarray:
+        """parseDetections (samples/gpu/tbd.cpp:1297-1340) -> DET_DTYPE array."""
+        n = C.c_int()
+        tr = trajectories.handle if trajectories is not None else None
+        _lib.check(self.lib.tbdk_sequence_detections(self.handle, int(cls), int(frame), None, None, 0, C.byref(n)),
+                   "tbdk_sequence_detections")
+        out = np.zeros(n.value, DET_DTYPE)
+        _lib.check(self.lib.tbdk_sequence_detections(self.handle, int(cls), int(frame), tr,
+                                                      C.cast(out.ctypes.data, C.POINTER(_lib.Detection)), n.value,
+                                                      C.byref(n)), "tbdk_sequence_detections")
+        return out
+
+
+def write_tracking_output(tracker: Tracker, history_ages, trajectories: Trajectories, frame_count: int,
+                          path: str | None = None, log_switches: bool = False) -> dict:
+    """App::writeTrackingOutputToFile (samples/gpu/tbd.cpp:946-1120): appends the
+    sample's output to path (if given); returns the scenario metrics."""
+    lib = _lib.load()
+    ages = (C.c_uint32 * max(1, len(history_ages)))(*history_ages)
+    m = _lib.ScenarioMetrics()
+    _lib.check(lib.tbdk_tracking_write(tracker.handle, ages, len(history_ages), int(frame_count), trajectories.handle,
+                                       str(path).encode() if path else None, int(log_switches), C.byref(m)),
+               "tbdk_tracking_write")
+    return {k: getattr(m, k) for k, _ in _lib.ScenarioMetrics._fields_}
+
+
+def run_app(pedestrian_bbox_filename=None, vehicle_bbox_filename=None, pedestrian_tracking_filepath=None,
+            vehicle_tracking_filepath=None, history_distribution=None, write_tracking=True, num_tracking_iters=1,
+            num_tracking_frames=100, seed=1, verbose=False, **tracker_args):
+    """The sample's tracking loop over bbox files (tbdk_app_run; CLI: opencv_amd/bin/tbdk_tbd_app).
+    Returns {"frames", "detections", "scenario": [pedestrians, vehicles]}."""
+    lib = _lib.load()
+    a = _lib.AppArgs()
+    _lib.check(lib.tbdk_app_default_args(C.byref(a)), "tbdk_app_default_args")
+    enc = lambda v: str(v).encode() if v else None  # noqa: E731
+    a.pedestrian_bbox_filename = enc(pedestrian_bbox_filename)
+    a.vehicle_bbox_filename = enc(vehicle_bbox_filename)
+    a.pedestrian_tracking_filepath = enc(pedestrian_tracking_filepath)
+    a.vehicle_tracking_filepath = enc(vehicle_tracking_filepath)
+    a.history_distribution = enc(history_distribution)
+    a.write_tracking = int(bool(write_tracking))
+    a.num_tracking_iters = int(num_tracking_iters)
+    a.num_tracking_frames = int(num_tracking_frames)
+    a.rand_seed = int(seed)
+    a.verbose = int(bool(verbose))
+    for k, v in tracker_args.items():
+        setattr(a.tracker, k, v)
+    r = _lib.AppResult()
+    _lib.check(lib.tbdk_app_run(C.byref(a), C.byref(r)), "tbdk_app_run")
+    sc = [{k: getattr(r.scenario[c], k) for k, _ in _lib.ScenarioMetrics._fields_} for c in range(2)]
+    return {"frames": r.frames, "detections": r.detections, "scenario": sc}

@@ -31,6 +31,7 @@ double division by zero gives inf/nan as IEEE does.
 """
 from __future__ import annotations
 
+import copy
 import math
 from dataclasses import dataclass, field
 
@@ -89,6 +90,15 @@ class Track:
     avgConfidence: float = 0.0
     predPosition: Rect | None = None
     bboxOverlap: float = 1.0
+    color: tuple = (0, 0, 0)
+
+
+def traj_get(traj: dict, key: int):
+    """std::map<int, Trajectory>::operator[]: default-constructs (id -1) when absent."""
+    if key not in traj:
+        from tbd_app_oracle import Trajectory  # noqa: PLC0415 (sibling module, avoids a cycle)
+        traj[key] = Trajectory(-1)
+    return traj[key]
 
 
 def equals_zero(v: float) -> bool:
@@ -131,6 +141,7 @@ class Tracker:
         self.track_visibility_threshold = track_visibility_threshold
         self.track_confidence_threshold = track_confidence_threshold
         self.bounds = bounds
+        self.rng = None            # CRand drawn for track colours (tbd_app_oracle), or None
         self.next_track_id = 0
         self.tracks: list[Track] = []
         self.true_positives, self.false_negatives, self.false_positives = [], [], []
@@ -140,6 +151,8 @@ class Tracker:
     def _new_track(self, d: Detection) -> Track:
         t = Track(id=self.next_track_id)
         self.next_track_id += 1
+        if self.rng is not None:  # Scalar(rand() % 256, rand() % 256, rand() % 256), tbd.cpp:71-74
+            t.color = (self.rng.rand() % 256, self.rng.rand() % 256, self.rng.rand() % 256)
         t.bboxes.append(d.bbox)
         t.scores.append(d.confidence)
         t.frames.append(d.frame_id)
@@ -151,14 +164,36 @@ class Tracker:
         t.bboxOverlap = 1.0
         return t
 
-    # tbd.cpp:210-286
-    def step(self, dets: list[Detection], frame_id: int, preds: dict | None = None):
+    # tbd.cpp:197-208
+    def reset(self):
+        self.next_track_id = 0
+        self.tracks = []
+        self.true_positives, self.false_negatives, self.false_positives = [], [], []
+        self.ground_truths, self.num_matches, self.bbox_overlap = [], [], []
+
+    # tbd.cpp:187-190 (Track copy constructor per element, tbd.cpp:93-117)
+    def set_tracks(self, tracks):
+        self.tracks = [copy.deepcopy(t) for t in tracks]
+
+    # tbd.cpp:210-286; traj: {gt id: Trajectory} (tbd_app_oracle), or None
+    def step(self, dets: list[Detection], frame_id: int, preds: dict | None = None, traj: dict | None = None):
         self._predict(frame_id, preds or {})
         self._filter_out_of_bounds(*self.bounds)
         assignments, un_tracks, un_dets = self._assign(dets)
         self._update_assigned(dets, assignments)
         self._update_unassigned(un_tracks, frame_id)
-        num_assigned = sum(1 for a in assignments if a >= 0)
+        num_assigned = 0
+        for i, t in enumerate(self.tracks):
+            if assignments[i] < 0:
+                continue
+            num_assigned += 1
+            d = dets[assignments[i]]
+            if traj is not None and d.id >= 0:
+                traj_get(traj, d.id).add_tracking_info(frame_id, t)
+        if traj is not None:
+            for j in un_dets:
+                if dets[j].id >= 0:
+                    traj_get(traj, dets[j].id).add_tracking_info(frame_id, None)
         self._delete_lost()
         for j in un_dets:
             self.tracks.append(self._new_track(dets[j]))

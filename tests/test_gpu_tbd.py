@@ -50,7 +50,7 @@ def test_tbd_loop_reference_bounds_quirk(gpu):
     assert len(tr) > 0
 
 
-def test_tbd_loop_tracker_matches_reference_restatement(gpu):
+def test_tbd_loop_tracker_matches_reference_restatement(gpu, tmp_path):
     """End to end: every frame, the loop's tracker state equals the pure-Python
     cv::tbd::Tracker restatement (oracle/tbd_oracle.py) fed the same detections
     and the KLT predictions the loop computed on the GPU (ids, boxes, predicted
@@ -60,12 +60,15 @@ def test_tbd_loop_tracker_matches_reference_restatement(gpu):
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import tbd_app_oracle as A
     import tbd_oracle as T
     from opencv_amd import klt, tbd
 
     W, H, N, F = 1280, 720, 24, 40
     frames, gt = klt.synth_render(11, W, H, N, 0, F, ctx=gpu)
     loop = tbd.TbdLoop(tbd.default_config(W, H), ctx=gpu)
+    traj, otraj = tbd.Trajectories(), {}
+    loop.set_trajectories(traj)
     ora = T.Tracker(bounds=(0, 1280, 0, 720))
     rng = np.random.default_rng(5)
     used_preds = 0
@@ -75,8 +78,11 @@ def test_tbd_loop_tracker_matches_reference_restatement(gpu):
         m = loop.step(frames[f], f, d)
         preds = loop.predictions()
         used_preds += len(preds)
-        ora.step([T.Detection(int(r["id"]), f, T.Rect(int(r["x"]), int(r["y"]), int(r["width"]), int(r["height"])),
-                              float(r["confidence"])) for r in d], f, preds)
+        od = [T.Detection(int(r["id"]), f, T.Rect(int(r["x"]), int(r["y"]), int(r["width"]), int(r["height"])),
+                          float(r["confidence"])) for r in d]
+        for x in od:  # parseDetections' trajectory positions
+            otraj.setdefault(x.id, A.Trajectory(x.id)).add_position(f, x.bbox)
+        ora.step(od, f, preds, traj=otraj)
         assert (m.tp, m.fn, m.fp, m.gt) == (ora.true_positives[-1], ora.false_negatives[-1],
                                             ora.false_positives[-1], ora.ground_truths[-1]), f
         tr = loop.tracks()
@@ -89,6 +95,12 @@ def test_tbd_loop_tracker_matches_reference_restatement(gpu):
             assert g["max_confidence"] == t.maxConfidence
             assert g["bbox_overlap"] == t.bboxOverlap or (math.isnan(g["bbox_overlap"]) and math.isnan(t.bboxOverlap))
     assert used_preds > 0  # the KLT motion model was exercised
+    # the sample's tracking output (history|object|frame|scenario lines) of the GPU loop
+    out = os.path.join(str(tmp_path), "track.txt")
+    m = loop.write_tracking_output(F, out)
+    txt, om = A.write_tracking_output(ora, [1] * F, otraj, F)
+    assert open(out).read() == txt
+    assert m["mt"] == om["mt"] and m["mota"] == om["mota"]
 
 
 def _mkey(m):
