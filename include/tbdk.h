@@ -237,6 +237,54 @@ int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int sr
                         uint8_t* dst, int dst_width, int dst_height, int dst_pitch, const double* M,
                         int flags, int border, int border_value, void* stream);
 
+/* ---- dense Farneback optical flow ------------------------------------------ */
+
+/* flag value of the reference (video/include/opencv2/video/tracking.hpp:58) */
+#define TBDK_OPTFLOW_FARNEBACK_GAUSSIAN 256
+
+/* cv::cuda::FarnebackOpticalFlow::create(numLevels, pyrScale, fastPyramids,
+ * winSize, numIters, polyN, polySigma, flags)
+ * (modules/cudaoptflow/include/opencv2/cudaoptflow.hpp:210-252) */
+typedef struct tbdk_farneback_params {
+    int32_t num_levels;              /* 5 */
+    double pyr_scale;                /* 0.5; < 1 (CV_Assert, optflowgf.cpp:1113-1114) */
+    int32_t fast_pyramids;           /* 0; the CUDA-only pyrDown pyramids are not provided (TBDK_EINVAL) */
+    int32_t win_size;                /* 13; 1..21 */
+    int32_t num_iters;               /* 10 */
+    int32_t poly_n;                  /* 5; 1..15 */
+    double poly_sigma;               /* 1.1 */
+    int32_t flags;                   /* 0 | TBDK_OPTFLOW_FARNEBACK_GAUSSIAN (USE_INITIAL_FLOW: TBDK_EINVAL) */
+} tbdk_farneback_params;
+
+int tbdk_farneback_default_params(tbdk_farneback_params* p);
+/* level count and sizes calc uses for a width x height frame
+ * (optflowgf.cpp:1125-1144): *nlevels = levels + 1, sizes[2*k] = width of level k,
+ * sizes[2*k+1] = height (sizes may be NULL; else room for 2 * (num_levels + 1)) */
+int tbdk_farneback_levels(int width, int height, const tbdk_farneback_params* p, int* nlevels, int32_t* sizes);
+
+/* Replaces cv::cuda::FarnebackOpticalFlow::calc(I0, I1, flow, stream)
+ * (cudaoptflow/src/farneback.cpp:164-196) with the numerics of the CPU
+ * cv::calcOpticalFlowFarneback (video/src/optflowgf.cpp:1096-1190).
+ *   prev, next : device u8 frames (width x height, row pitch in bytes)
+ *   flow       : device CV_32FC2 output, interleaved (dx, dy) per pixel,
+ *                flow_pitch in bytes (multiple of 8)
+ * Scratch (15 float planes of the frame size + the blur buffer) is owned by
+ * the context and grown on demand; the call is asynchronous on `stream`. */
+int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int width, int height, int pitch,
+                   float* flow, int flow_pitch, const tbdk_farneback_params* params, void* stream);
+
+/* Stage entry points of tbdk_farneback (parity tests):
+ * level image = resize(GaussianBlur(float(img), (smooth_size, smooth_size), sigma),
+ * (dst_width, dst_height), INTER_LINEAR) (optflowgf.cpp:1170-1172); dst device
+ * float plane, dst_pitch in bytes. */
+int tbdk_fb_level_image(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int dst_width,
+                        int dst_height, int smooth_size, double sigma, float* dst, int dst_pitch, void* stream);
+/* FarnebackPolyExp (optflowgf.cpp:116-202): src device float plane; dst = 5
+ * device float planes (plane c at byte offset c * height * dst_pitch) holding
+ * the reference's CV_32FC5 channels c = 0..4. */
+int tbdk_fb_poly_exp(tbdk_ctx* ctx, const float* src, int width, int height, int src_pitch, int poly_n,
+                     double poly_sigma, float* dst, int dst_pitch, void* stream);
+
 /* ---- tracking-by-detection loop (one video stream per context) ------------ */
 
 /* Per-stream TBD loop: pyramid -> (GFTT on new / re-detect tracks) -> PyrLK over

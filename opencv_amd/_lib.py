@@ -150,6 +150,14 @@ class AppResult(C.Structure):
     _fields_ = [("frames", C.c_int64), ("detections", C.c_int64), ("scenario", ScenarioMetrics * 2)]
 
 
+class FarnebackParams(C.Structure):
+    _fields_ = [("num_levels", C.c_int32), ("pyr_scale", C.c_double), ("fast_pyramids", C.c_int32),
+                ("win_size", C.c_int32), ("num_iters", C.c_int32), ("poly_n", C.c_int32),
+                ("poly_sigma", C.c_double), ("flags", C.c_int32)]
+
+
+OPTFLOW_FARNEBACK_GAUSSIAN = 256
+
 _P = C.c_void_p
 _PI = C.POINTER(C.c_int)
 
@@ -233,6 +241,12 @@ SIGNATURES = {
     "tbdk_tbd_predictions": (C.c_int, [C.c_void_p, C.POINTER(Prediction), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "tbdk_farneback_default_params": (C.c_int, [C.POINTER(FarnebackParams)]),
+    "tbdk_farneback_levels": (C.c_int, [C.c_int, C.c_int, C.POINTER(FarnebackParams), _PI, C.POINTER(C.c_int32)]),
+    "tbdk_farneback": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.POINTER(FarnebackParams), _P]),
+    "tbdk_fb_level_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, _P,
+                                      C.c_int, _P]),
+    "tbdk_fb_poly_exp": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, _P, C.c_int, _P]),
 }
 
 _lib = None

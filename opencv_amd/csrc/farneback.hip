@@ -1,0 +1,1039 @@
+// farneback.hip — dense Farneback optical flow on gfx950, the numerics of the
+// CPU cv::calcOpticalFlowFarneback (video/src/optflowgf.cpp:57-578, 1096-1190)
+// behind the cv::cuda::FarnebackOpticalFlow interface
+// (cudaoptflow/include/opencv2/cudaoptflow.hpp:210-252, impl
+// cudaoptflow/src/farneback.cpp:164-474).
+//
+// Per pyramid level k (coarsest first), for each of the two frames:
+//   fb_rowpass / fb_colpass  GaussianBlur(float(img), smooth_sz, sigma) then
+//                            resize(INTER_LINEAR) to the level size, evaluated
+//                            only at the source rows/columns the resize samples
+//                            (the blur's separable row filter, its column
+//                            filter, then the resize's weights, each in the
+//                            reference's float operation order).
+//   fb_polyexp               FarnebackPolyExp (optflowgf.cpp:116-202): float
+//                            vertical pass, double horizontal pass -> R (5 planes).
+// then flow init (zeros, or the previous level's flow resized INTER_LINEAR and
+// scaled by 1/pyrScale) and numIters launches of
+//   fb_iter                  one Jacobi step: M = FarnebackUpdateMatrices(R0, R1,
+//                            flow) (optflowgf.cpp:217-312) recomputed on the fly
+//                            for a 128-column strip walking down a row segment
+//                            (ring of the last 2m+1 rows of M in registers), the
+//                            vertical window sum (box: exact-order double sum;
+//                            FARNEBACK_GAUSSIAN: the reference's float weighted
+//                            sum), the horizontal window from LDS, the 2x2 solve
+//                            in double -> next flow (optflowgf.cpp:341-403, 446-569).
+// The reference interleaves UpdateMatrices with the blur in row stripes; the
+// rows it updates are never read again by that pass (y1 = y - block_size), so it
+// is exactly flow_{i+1} = solve(blur(M(flow_i))): M is never stored here, each
+// iteration reads flow + R0 + R1 (48 B/px) and writes flow (8 B/px).
+//
+// Numerics: every float/double expression is written as the reference's (this
+// file is compiled with -ffp-contract=off), so the level images, R, M, the
+// Gaussian-variant blur and the solve round exactly as the reference's scalar/SSE2
+// code.  The box variant's vertical/horizontal sums are exact-order double
+// window sums instead of the reference's running sums (whose float-rounded
+// row differences accumulate over the whole image): that variant is compared to
+// the oracle within a stated tolerance, the Gaussian variant bit for bit.
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <type_traits>
+#include <utility>
+
+#include "tbdk_internal.hpp"
+
+namespace tbdk {
+
+struct FbScratch {
+    float* R0 = nullptr;  // 5 planes
+    float* R1 = nullptr;  // 5 planes
+    float* F[2] = {nullptr, nullptr};  // flow ping-pong, 2 planes each
+    float* T = nullptr;   // row-pass buffer
+    float* I = nullptr;   // level image
+    int64_t cap_px = 0;   // floats per plane
+    int64_t cap_T = 0;
+};
+
+namespace {
+
+constexpr int kFbMaxKs = 255;   // GaussianBlur ksize of the level images
+constexpr int kFbMaxPolyN = 15;
+constexpr int kFbMaxHalf = 10;  // winsize <= 21
+constexpr int kFbStrip = 128;   // fb_iter strip width (lanes, incl. the 2m halo)
+constexpr int kFbRB = 4;        // rows per horizontal batch of fb_iter
+
+enum { kModeNone = 0, kModeArea2 = 1, kModeLinear = 2 };
+
+__host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+// cvFloor(float): x86 cvttss2si yields INT_MIN for NaN / out of range
+__device__ __forceinline__ int cv_floorf(float v)
+{
+    if (!(v >= -2147483648.f && v < 2147483648.f)) return INT_MIN;
+    const int i = (int)v;
+    return i - (i > v);
+}
+
+// resize INTER_LINEAR source column / weight of destination column dx
+// (imgproc/src/resize.cpp:3600-3640, ksize2 = 1)
+struct LinX {
+    int sx;
+    float fx;
+    bool inner;  // dx < xmax: two taps
+};
+__device__ __forceinline__ LinX lin_x(int dx, double scale_x, int sw)
+{
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floorf(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    LinX r;
+    r.inner = !(sx + 1 >= sw);
+    if (sx + 1 >= sw && sx >= sw - 1) fx = 0, sx = sw - 1;
+    r.sx = sx;
+    r.fx = fx;
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// level image: GaussianBlur (sepFilter2D, REFLECT_101) + resize INTER_LINEAR
+
+struct FbRowArgs {
+    const uint8_t* img;
+    int W, H, pitch;
+    float* T;
+    int tpitch, nc;
+    int mode;        // kMode*
+    double scale_x;  // LINEAR: W / dw
+    int ks;
+    float k[kFbMaxKs];
+};
+
+// row filter of row y at source column c (filter.simd.hpp SymmRowSmallFilter /
+// RowFilter scalar and SSE orders, see oracle/farneback_oracle.c)
+__global__ __launch_bounds__(256) void fb_rowpass_kernel(FbRowArgs a)
+{
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (j >= a.nc) return;
+    int c = j;
+    if (a.mode == kModeLinear) {
+        const LinX lx = lin_x(j >> 1, a.scale_x, a.W);
+        c = (j & 1) && lx.inner ? lx.sx + 1 : lx.sx;
+    }
+    const uint8_t* S = a.img + (size_t)y * a.pitch;
+    const int r = a.ks >> 1;
+#define SX(o) ((float)S[reflect101(c + (o), a.W)])
+    float s;
+    if (a.ks == 3) {
+        s = SX(0) * a.k[1] + (SX(-1) + SX(1)) * a.k[0];
+    } else if (a.ks == 5) {
+        s = SX(0) * a.k[2] + (SX(-1) + SX(1)) * a.k[1] + (SX(-2) + SX(2)) * a.k[0];
+    } else {
+        s = a.k[0] * SX(-r);
+        for (int t = 1; t < a.ks; ++t) s += a.k[t] * SX(t - r);
+    }
+#undef SX
+    a.T[(size_t)y * a.tpitch + j] = s;
+}
+
+struct FbColArgs {
+    const float* T;
+    int tpitch, H;  // source rows
+    int W;          // source columns (LINEAR bounds)
+    float* I;
+    int w, h, ipitch;
+    int mode;
+    double scale_x, scale_y;
+    int ks;
+    float k[kFbMaxKs];
+};
+
+// column filter at source row y over T column j (SymmColumnSmallFilter /
+// SymmColumnFilter, delta 0)
+__device__ __forceinline__ float fb_colf(const FbColArgs& a, int y, int j)
+{
+    const float* T = a.T + j;
+    const int r = a.ks >> 1;
+#define SY(o) T[(size_t)reflect101(y + (o), a.H) * a.tpitch]
+    float s;
+    if (a.ks == 3) {
+        s = (SY(-1) + SY(1)) * a.k[0] + SY(0) * a.k[1] + 0.0f;
+    } else {
+        s = a.k[r] * SY(0) + 0.0f;
+        for (int t = 1; t <= r; ++t) s += a.k[r + t] * (SY(t) + SY(-t));
+    }
+#undef SY
+    return s;
+}
+
+__global__ __launch_bounds__(256) void fb_colpass_kernel(FbColArgs a)
+{
+    const int dx = blockIdx.x * 256 + threadIdx.x;
+    const int dy = blockIdx.y;
+    if (dx >= a.w) return;
+    float v;
+    if (a.mode == kModeNone) {
+        v = fb_colf(a, dy, dx);
+    } else if (a.mode == kModeArea2) {
+        // resizeAreaFast 2x (resize.cpp:2471-2497 SIMD part, 2626-2640 scalar tail)
+        const float p0 = fb_colf(a, 2 * dy, 2 * dx), p1 = fb_colf(a, 2 * dy, 2 * dx + 1);
+        const float q0 = fb_colf(a, 2 * dy + 1, 2 * dx), q1 = fb_colf(a, 2 * dy + 1, 2 * dx + 1);
+        if (dx < (a.w & ~3)) {
+            v = ((p0 + p1) + (q0 + q1)) * 0.25f;
+        } else {
+            float sum = 0;
+            sum += p0 + p1 + q0 + q1;
+            v = sum * 0.25f;
+        }
+    } else {
+        const LinX lx = lin_x(dx, a.scale_x, a.W);
+        float fy = (float)((dy + 0.5) * a.scale_y - 0.5);
+        const int sy = cv_floorf(fy);
+        fy -= sy;
+        const float b0 = 1.f - fy, b1 = fy;
+        const float a0 = 1.f - lx.fx, a1 = lx.fx;
+        float hrow[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int yy = clampi(sy + t, 0, a.H - 1);
+            const float s0 = fb_colf(a, yy, 2 * dx);
+            hrow[t] = lx.inner ? s0 * a0 + fb_colf(a, yy, 2 * dx + 1) * a1 : s0;
+        }
+        v = hrow[0] * b0 + hrow[1] * b1;
+    }
+    a.I[(size_t)dy * a.ipitch + dx] = v;
+}
+
+// ---------------------------------------------------------------------------
+// FarnebackPolyExp (optflowgf.cpp:116-202); R planes: R[c][y][x]
+
+struct FbPolyArgs {
+    const float* I;
+    int w, h, ipitch;
+    float* R;
+    int rpitch;
+    int64_t rplane;
+    int n;
+    float g[kFbMaxPolyN + 1], xg[kFbMaxPolyN + 1], xxg[kFbMaxPolyN + 1];  // index 0..n
+    double ig11, ig03, ig33, ig55;
+};
+
+__global__ __launch_bounds__(256) void fb_polyexp_kernel(FbPolyArgs a)
+{
+    __shared__ float tr[3][256 + 2 * kFbMaxPolyN];
+    const int x0 = blockIdx.x * 256;
+    const int y = blockIdx.y;
+    const int n = a.n;
+    // vertical part of the convolution, replicated borders (row[-1-x] = row[2-x])
+    for (int i = threadIdx.x; i < 256 + 2 * n; i += 256) {
+        const int c = clampi(x0 - n + i, 0, a.w - 1);
+        const float* col = a.I + c;
+        float t0 = col[(size_t)y * a.ipitch] * a.g[0], t1 = 0.f, t2 = 0.f;
+        for (int k = 1; k <= n; ++k) {
+            const float s0 = col[(size_t)(y - k < 0 ? 0 : y - k) * a.ipitch];
+            const float s1 = col[(size_t)(y + k > a.h - 1 ? a.h - 1 : y + k) * a.ipitch];
+            const float p = s0 + s1;
+            t0 = t0 + a.g[k] * p;
+            t1 = t1 + a.xg[k] * (s1 - s0);
+            t2 = t2 + a.xxg[k] * p;
+        }
+        tr[0][i] = t0;
+        tr[1][i] = t1;
+        tr[2][i] = t2;
+    }
+    __syncthreads();
+    const int x = x0 + threadIdx.x;
+    if (x >= a.w) return;
+    const int o = threadIdx.x + n;
+    float g0 = a.g[0];
+    double b1 = tr[0][o] * g0, b2 = 0, b3 = tr[1][o] * g0, b4 = 0, b5 = tr[2][o] * g0, b6 = 0;
+    for (int k = 1; k <= n; ++k) {
+        const double tg = tr[0][o + k] + tr[0][o - k];
+        g0 = a.g[k];
+        b1 += tg * g0;
+        b4 += tg * a.xxg[k];
+        b2 += (tr[0][o + k] - tr[0][o - k]) * a.xg[k];
+        b3 += (tr[1][o + k] + tr[1][o - k]) * g0;
+        b6 += (tr[1][o + k] - tr[1][o - k]) * a.xg[k];
+        b5 += (tr[2][o + k] + tr[2][o - k]) * g0;
+    }
+    float* R = a.R + (size_t)y * a.rpitch + x;
+    R[a.rplane] = (float)(b2 * a.ig11);
+    R[0] = (float)(b3 * a.ig11);
+    R[3 * a.rplane] = (float)(b1 * a.ig03 + b4 * a.ig33);
+    R[2 * a.rplane] = (float)(b1 * a.ig03 + b5 * a.ig33);
+    R[4 * a.rplane] = (float)(b6 * a.ig55);
+}
+
+// ---------------------------------------------------------------------------
+// flow between levels: resize(prevFlow, INTER_LINEAR) then *= 1/pyrScale
+
+struct FbFlowUpArgs {
+    const float* src;
+    int sw, sh, spitch;
+    int64_t splane;
+    float* dst;
+    int w, h, dpitch;
+    int64_t dplane;
+    double scale_x, scale_y;
+    float alpha;
+};
+
+__global__ __launch_bounds__(256) void fb_flow_up_kernel(FbFlowUpArgs a)
+{
+    const int dx = blockIdx.x * 256 + threadIdx.x;
+    const int dy = blockIdx.y;
+    if (dx >= a.w) return;
+    const LinX lx = lin_x(dx, a.scale_x, a.sw);
+    float fy = (float)((dy + 0.5) * a.scale_y - 0.5);
+    const int sy = cv_floorf(fy);
+    fy -= sy;
+    const float b0 = 1.f - fy, b1 = fy, a0 = 1.f - lx.fx, a1 = lx.fx;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        float hrow[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const float* S = a.src + c * a.splane + (size_t)clampi(sy + t, 0, a.sh - 1) * a.spitch;
+            hrow[t] = lx.inner ? S[lx.sx] * a0 + S[lx.sx + 1] * a1 : S[lx.sx];
+        }
+        const float v = hrow[0] * b0 + hrow[1] * b1;
+        a.dst[c * a.dplane + (size_t)dy * a.dpitch + dx] = v * a.alpha + 0.0f;  // convertTo(alpha, 0)
+    }
+}
+
+// planar -> interleaved CV_32FC2 (numIters == 0 at level 0)
+__global__ __launch_bounds__(256) void fb_interleave_kernel(const float* src, int w, int h, int spitch, int64_t splane,
+                                                           float* dst, int dpitch)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= w) return;
+    const size_t o = (size_t)y * spitch + x;
+    float2 v = make_float2(src[o], src[o + splane]);
+    *reinterpret_cast<float2*>(dst + (size_t)y * dpitch + 2 * x) = v;
+}
+
+// ---------------------------------------------------------------------------
+// one iteration: flow_out = solve(blur(M(flow_in, R0, R1)))
+
+struct FbIterArgs {
+    const float* fin;  // planes x, y
+    float* fout;       // planes x, y (or interleaved when out_il)
+    const float* R0;
+    const float* R1;
+    int w, h, pitch;   // plane pitch (floats)
+    int64_t fplane, rplane;
+    int seg;           // output rows per workgroup
+    int out_il, out_pitch;
+    double scale;      // box: 1 / (winsize^2)
+    float gk[kFbMaxHalf + 1];  // Gaussian variant: kernel[0..m]
+};
+
+__device__ __forceinline__ float fb_border(int i) { return i < 2 ? 0.14f : 0.4472f; }
+
+// FarnebackUpdateMatrices at pixel (x, y) (optflowgf.cpp:235-309)
+__device__ __forceinline__ void fb_matrices(const FbIterArgs& a, int x, int y, float M[5])
+{
+    const size_t o = (size_t)y * a.pitch + x;
+    const float dx = a.fin[o], dy = a.fin[o + a.fplane];
+    const float* R0 = a.R0 + o;
+    const float R00 = R0[0], R01 = R0[a.rplane], R02 = R0[2 * a.rplane], R03 = R0[3 * a.rplane],
+                R04 = R0[4 * a.rplane];
+    float fx = (float)x + dx, fy = (float)y + dy;
+    const int x1 = cv_floorf(fx), y1 = cv_floorf(fy);
+    float r2, r3, r4, r5, r6;
+    fx -= x1;
+    fy -= y1;
+    if ((unsigned)x1 < (unsigned)(a.w - 1) && (unsigned)y1 < (unsigned)(a.h - 1)) {
+        const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+        const float* p = a.R1 + (size_t)y1 * a.pitch + x1;
+        float r[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            const float* q = p + c * a.rplane;
+            r[c] = a00 * q[0] + a01 * q[1] + a10 * q[a.pitch] + a11 * q[a.pitch + 1];
+        }
+        r2 = r[0];
+        r3 = r[1];
+        r4 = (R02 + r[2]) * 0.5f;
+        r5 = (R03 + r[3]) * 0.5f;
+        r6 = (R04 + r[4]) * 0.25f;
+    } else {
+        r2 = r3 = 0.f;
+        r4 = R02;
+        r5 = R03;
+        r6 = R04 * 0.5f;
+    }
+    r2 = (R00 - r2) * 0.5f;
+    r3 = (R01 - r3) * 0.5f;
+    r2 += r4 * dy + r6 * dx;
+    r3 += r6 * dy + r5 * dx;
+    if ((unsigned)(x - 5) >= (unsigned)(a.w - 10) || (unsigned)(y - 5) >= (unsigned)(a.h - 10)) {
+        const float scale = (x < 5 ? fb_border(x) : 1.f) * (x >= a.w - 5 ? fb_border(a.w - x - 1) : 1.f) *
+                            (y < 5 ? fb_border(y) : 1.f) * (y >= a.h - 5 ? fb_border(a.h - y - 1) : 1.f);
+        r2 *= scale;
+        r3 *= scale;
+        r4 *= scale;
+        r5 *= scale;
+        r6 *= scale;
+    }
+    M[0] = r4 * r4 + r6 * r6;
+    M[1] = (r4 + r5) * r6;
+    M[2] = r5 * r5 + r6 * r6;
+    M[3] = r4 * r2 + r6 * r3;
+    M[4] = r6 * r2 + r5 * r3;
+}
+
+// LDS slot of strip lane l: one pad double every 4, so the horizontal runs
+// (thread q reads lanes 4q..4q+3+2m) hit distinct banks
+__device__ __forceinline__ int fb_slot(int l) { return l + (l >> 2); }
+constexpr int kFbSlots = kFbStrip + kFbStrip / 4;
+
+// horizontal window + 2x2 solve of one batch row: thread task -> (row r, 4
+// consecutive output columns starting at strip offset o0)
+template <int M, bool GAUSS>
+__device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
+                                              int y, int ox0)
+{
+    constexpr int NW = 4 + 2 * M;
+    constexpr int OW = kFbStrip - 2 * M;
+    using ST = typename std::conditional<GAUSS, float, double>::type;
+    ST out[5][4];
+#pragma unroll
+    for (int ch = 0; ch < 5; ++ch) {
+        const float* row = vb[r][ch];
+        if (GAUSS) {
+            // optflowgf.cpp:548-553: sum = v[x]*k0; sum += k[i]*(v[x-i] + v[x+i])
+            float win[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float s = win[k + M] * a.gk[0];
+#pragma unroll
+                for (int i = 1; i <= M; ++i) s += a.gk[i] * (win[k + M - i] + win[k + M + i]);
+                out[ch][k] = s;
+            }
+        } else {
+            // window sums in double, left to right, streamed: out[k] = v[k] + ... + v[k+2m]
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const double v = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (i == k) out[ch][k] = v;
+                    else if (i > k && i <= k + 2 * M) out[ch][k] += v;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int o = o0 + k, x = ox0 + o;
+        if (o >= OW || x >= a.w) break;
+        double g11, g12, g22, h1, h2;
+        if (GAUSS) {
+            g11 = out[0][k];
+            g12 = out[1][k];
+            g22 = out[2][k];
+            h1 = out[3][k];
+            h2 = out[4][k];
+        } else {
+            g11 = out[0][k] * a.scale;
+            g12 = out[1][k] * a.scale;
+            g22 = out[2][k] * a.scale;
+            h1 = out[3][k] * a.scale;
+            h2 = out[4][k] * a.scale;
+        }
+        const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+        const float fx = (float)((g11 * h2 - g12 * h1) * idet);
+        const float fy = (float)((g22 * h1 - g12 * h2) * idet);
+        if (a.out_il) {
+            *reinterpret_cast<float2*>(a.fout + (size_t)y * a.out_pitch + 2 * x) = make_float2(fx, fy);
+        } else {
+            const size_t off = (size_t)y * a.pitch + x;
+            a.fout[off] = fx;
+            a.fout[off + a.fplane] = fy;
+        }
+    }
+}
+
+// step J of a block (static ring slot J): M of row y0 + m + s into ring[J];
+// for s >= 0 the vertical window of centre row y0 + s into LDS row J
+template <int M, bool GAUSS, int J>
+__device__ __forceinline__ void fb_step(const FbIterArgs& a, float (&ring)[2 * M + 1][5], float (*vb)[5][kFbSlots],
+                                        int x, int y0, int s, int nrows, int sl)
+{
+    constexpr int K = 2 * M + 1;
+    if (s >= nrows) return;
+    fb_matrices(a, x, clampi(y0 + M + s, 0, a.h - 1), ring[J]);
+    if (s < 0) return;
+    constexpr int CS = (J + M + 1) % K;  // ring slot of the centre row; row c+d is slot (CS + d) mod K
+#pragma unroll
+    for (int ch = 0; ch < 5; ++ch) {
+        float v;
+        if (GAUSS) {
+            // optflowgf.cpp:509-515: s0 = M(c)*k0; s0 += (M(c+i) + M(c-i))*k[i]
+            v = ring[CS][ch] * a.gk[0];
+#pragma unroll
+            for (int i = 1; i <= M; ++i) v += (ring[(CS + i) % K][ch] + ring[(CS + K - i) % K][ch]) * a.gk[i];
+        } else {
+            // exact-order window: rows c-m .. c+m summed in double from the top
+            double sum = 0;
+#pragma unroll
+            for (int i = -M; i <= M; ++i) sum += ring[(CS + K + i) % K][ch];
+            v = (float)sum;
+        }
+        vb[J][ch][sl] = v;
+    }
+}
+
+template <int M, bool GAUSS, int... J>
+__device__ __forceinline__ void fb_block(std::integer_sequence<int, J...>, const FbIterArgs& a,
+                                         float (&ring)[2 * M + 1][5], float (*vb)[5][kFbSlots], int x, int y0, int s0,
+                                         int nrows, int sl)
+{
+    (fb_step<M, GAUSS, J>(a, ring, vb, x, y0, s0 + J, nrows, sl), ...);
+}
+
+// One workgroup = one 128-column strip (lane = column, m halo lanes per side)
+// walking the output rows [y0, y0 + seg).  Steps s = -2m .. seg-1 each compute
+// M of row y0 + m + s (clamped = BORDER_REPLICATE) into a register ring of
+// 2m+1 rows; a block of 2m+1 steps is expanded at compile time, so every ring
+// slot is static.  Steps s >= 0 store the vertical window of centre row
+// y0 + s (box: exact-order double sum rounded to float; Gaussian: the
+// reference's float weighted sum) in LDS row J of the block; after each block
+// the workgroup sums the horizontal windows and solves.  Every value is a
+// fixed-order function of the pixel's neighbourhood, independent of the
+// strip/segment split.
+template <int M, bool GAUSS>
+__global__ __launch_bounds__(kFbStrip) void fb_iter_kernel(FbIterArgs a)
+{
+    constexpr int K = 2 * M + 1;
+    constexpr int OW = kFbStrip - 2 * M;
+    constexpr int NQ = (OW + 3) / 4;  // 4-column tasks per row
+    __shared__ float vb[K][5][kFbSlots];
+
+    const int lane = threadIdx.x;
+    const int ox0 = blockIdx.x * OW;
+    const int x = clampi(ox0 - M + lane, 0, a.w - 1);
+    const int y0 = blockIdx.y * a.seg;
+    const int nrows = min(a.h, y0 + a.seg) - y0;
+    const int sl = fb_slot(lane);
+
+    float ring[K][5];
+    for (int s0 = -2 * M; s0 < nrows; s0 += K) {
+        fb_block<M, GAUSS>(std::make_integer_sequence<int, K>{}, a, ring, vb, x, y0, s0, nrows, sl);
+        const int jbeg = s0 < 0 ? -s0 : 0;
+        const int jend = min(K, nrows - s0);
+        __syncthreads();
+        for (int task = threadIdx.x; task < (jend - jbeg) * NQ; task += kFbStrip) {
+            const int r = jbeg + task / NQ, q = task - (task / NQ) * NQ;
+            if (ox0 + 4 * q < a.w) fb_horizontal<M, GAUSS>(a, vb, r, 4 * q, y0 + s0 + r, ox0);
+        }
+        __syncthreads();
+    }
+}
+
+template <int M>
+hipError_t launch_fb_iter_m(const FbIterArgs& a, bool gauss, dim3 grid, hipStream_t s)
+{
+    if (gauss) hipLaunchKernelGGL((fb_iter_kernel<M, true>), grid, dim3(kFbStrip), 0, s, a);
+    else hipLaunchKernelGGL((fb_iter_kernel<M, false>), grid, dim3(kFbStrip), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fb_iter(const FbIterArgs& a, int m, bool gauss, hipStream_t s)
+{
+    const int ow = kFbStrip - 2 * m;
+    const int nstrips = (a.w + ow - 1) / ow;
+    const int nseg = (a.h + a.seg - 1) / a.seg;
+    const dim3 grid(nstrips, nseg);
+    switch (m) {
+    case 0: return launch_fb_iter_m<0>(a, gauss, grid, s);
+    case 1: return launch_fb_iter_m<1>(a, gauss, grid, s);
+    case 2: return launch_fb_iter_m<2>(a, gauss, grid, s);
+    case 3: return launch_fb_iter_m<3>(a, gauss, grid, s);
+    case 4: return launch_fb_iter_m<4>(a, gauss, grid, s);
+    case 5: return launch_fb_iter_m<5>(a, gauss, grid, s);
+    case 6: return launch_fb_iter_m<6>(a, gauss, grid, s);
+    case 7: return launch_fb_iter_m<7>(a, gauss, grid, s);
+    case 8: return launch_fb_iter_m<8>(a, gauss, grid, s);
+    case 9: return launch_fb_iter_m<9>(a, gauss, grid, s);
+    case 10: return launch_fb_iter_m<10>(a, gauss, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host helpers: the reference's kernels (computed on the host, as it does)
+
+int cv_round(double v) { return (int)lrint(v); }
+
+// getGaussianKernel(n, sigma, CV_32F) (imgproc/src/smooth.dispatch.cpp:70-122)
+void gaussian_kernel(int n, double sigma, float* cf)
+{
+    static const float tab[4][7] = {{1.f},
+                                    {0.25f, 0.5f, 0.25f},
+                                    {0.0625f, 0.25f, 0.375f, 0.25f, 0.0625f},
+                                    {0.03125f, 0.109375f, 0.21875f, 0.28125f, 0.21875f, 0.109375f, 0.03125f}};
+    const float* fixed = (n % 2 == 1 && n <= 7 && sigma <= 0) ? tab[n >> 1] : nullptr;
+    const double sigmaX = sigma > 0 ? sigma : ((n - 1) * 0.5 - 1) * 0.3 + 0.8;
+    const double scale2X = -0.5 / (sigmaX * sigmaX);
+    double sum = 0;
+    for (int i = 0; i < n; i++) {
+        const double x = i - (n - 1) * 0.5;
+        const double t = fixed ? (double)fixed[i] : std::exp(scale2X * x * x);
+        cf[i] = (float)t;
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; i++) cf[i] = (float)(cf[i] * sum);
+}
+
+// FarnebackPrepareGaussian (optflowgf.cpp:60-114) incl. invert(G, DECOMP_CHOLESKY)
+// (hal::Cholesky64f, core/src/matrix_decomp.cpp:95-170)
+void prepare_gaussian(int n, double sigma, float* g, float* xg, float* xxg, double* ig)
+{
+    if (sigma < FLT_EPSILON) sigma = n * 0.3;
+    float gb[2 * kFbMaxPolyN + 1], xgb[2 * kFbMaxPolyN + 1], xxgb[2 * kFbMaxPolyN + 1];
+    float* G_ = gb + n;
+    float* XG = xgb + n;
+    float* XXG = xxgb + n;
+    double s = 0.;
+    for (int x = -n; x <= n; x++) {
+        G_[x] = (float)std::exp(-x * x / (2 * sigma * sigma));
+        s += G_[x];
+    }
+    s = 1. / s;
+    for (int x = -n; x <= n; x++) {
+        G_[x] = (float)(G_[x] * s);
+        XG[x] = (float)(x * G_[x]);
+        XXG[x] = (float)(x * x * G_[x]);
+    }
+    double G[36] = {0};
+    for (int y = -n; y <= n; y++)
+        for (int x = -n; x <= n; x++) {
+            G[0] += G_[y] * G_[x];
+            G[7] += G_[y] * G_[x] * x * x;
+            G[21] += G_[y] * G_[x] * x * x * x * x;
+            G[35] += G_[y] * G_[x] * x * x * y * y;
+        }
+    G[14] = G[3] = G[4] = G[18] = G[24] = G[7];
+    G[28] = G[21];
+    G[22] = G[27] = G[35];
+    double* A = G;
+    double b[36] = {0};
+    for (int i = 0; i < 6; i++) b[i * 6 + i] = 1;
+    int i, j, k;
+    for (i = 0; i < 6; i++) {
+        for (j = 0; j < i; j++) {
+            s = A[i * 6 + j];
+            for (k = 0; k < j; k++) s -= A[i * 6 + k] * A[j * 6 + k];
+            A[i * 6 + j] = s * A[j * 6 + j];
+        }
+        s = A[i * 6 + i];
+        for (k = 0; k < j; k++) {
+            const double t = A[i * 6 + k];
+            s -= t * t;
+        }
+        A[i * 6 + i] = 1. / std::sqrt(s);
+    }
+    for (i = 0; i < 6; i++)
+        for (j = 0; j < 6; j++) {
+            s = b[i * 6 + j];
+            for (k = 0; k < i; k++) s -= A[i * 6 + k] * b[k * 6 + j];
+            b[i * 6 + j] = s * A[i * 6 + i];
+        }
+    for (i = 5; i >= 0; i--)
+        for (j = 0; j < 6; j++) {
+            s = b[i * 6 + j];
+            for (k = 5; k > i; k--) s -= A[k * 6 + i] * b[k * 6 + j];
+            b[i * 6 + j] = s * A[i * 6 + i];
+        }
+    ig[0] = b[1 * 6 + 1];
+    ig[1] = b[0 * 6 + 3];
+    ig[2] = b[3 * 6 + 3];
+    ig[3] = b[5 * 6 + 5];
+    for (int x = 0; x <= n; x++) {
+        g[x] = G_[x];
+        xg[x] = XG[x];
+        xxg[x] = XXG[x];
+    }
+}
+
+struct LevelImagePlan {
+    int mode, nc, ks;
+    double scale_x, scale_y;
+    float k[kFbMaxKs];
+};
+
+// resize()'s path choice for (W,H) -> (w,h) (resize.cpp:3483-3550)
+int plan_level_image(int W, int H, int w, int h, int ks, double sigma, LevelImagePlan* p)
+{
+    if (ks < 1 || ks > kFbMaxKs || !(ks & 1)) return TBDK_EINVAL;
+    p->ks = ks;
+    gaussian_kernel(ks, sigma, p->k);
+    p->scale_x = 1. / ((double)w / W);
+    p->scale_y = 1. / ((double)h / H);
+    if (w == W && h == H) {
+        p->mode = kModeNone;
+        p->nc = W;
+        return TBDK_OK;
+    }
+    const int isx = cv_round(p->scale_x), isy = cv_round(p->scale_y);
+    const bool fast = std::fabs(p->scale_x - isx) < DBL_EPSILON && std::fabs(p->scale_y - isy) < DBL_EPSILON;
+    if (fast && isx == 2 && isy == 2) {
+        p->mode = kModeArea2;
+        p->nc = W;
+    } else {
+        p->mode = kModeLinear;
+        p->nc = 2 * w;
+    }
+    return TBDK_OK;
+}
+
+hipError_t launch_level_image(const LevelImagePlan& p, const uint8_t* img, int W, int H, int pitch, float* T,
+                              int tpitch, float* I, int w, int h, int ipitch, hipStream_t s)
+{
+    FbRowArgs ra;
+    ra.img = img;
+    ra.W = W;
+    ra.H = H;
+    ra.pitch = pitch;
+    ra.T = T;
+    ra.tpitch = tpitch;
+    ra.nc = p.nc;
+    ra.mode = p.mode;
+    ra.scale_x = p.scale_x;
+    ra.ks = p.ks;
+    std::memcpy(ra.k, p.k, sizeof(float) * p.ks);
+    hipLaunchKernelGGL(fb_rowpass_kernel, dim3((p.nc + 255) / 256, H), dim3(256), 0, s, ra);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    FbColArgs ca;
+    ca.T = T;
+    ca.tpitch = tpitch;
+    ca.H = H;
+    ca.W = W;
+    ca.I = I;
+    ca.w = w;
+    ca.h = h;
+    ca.ipitch = ipitch;
+    ca.mode = p.mode;
+    ca.scale_x = p.scale_x;
+    ca.scale_y = p.scale_y;
+    ca.ks = p.ks;
+    std::memcpy(ca.k, p.k, sizeof(float) * p.ks);
+    hipLaunchKernelGGL(fb_colpass_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, ca);
+    return hipGetLastError();
+}
+
+hipError_t launch_polyexp(const float* I, int w, int h, int ipitch, float* R, int rpitch, int64_t rplane, int n,
+                          double sigma, hipStream_t s)
+{
+    FbPolyArgs a;
+    a.I = I;
+    a.w = w;
+    a.h = h;
+    a.ipitch = ipitch;
+    a.R = R;
+    a.rpitch = rpitch;
+    a.rplane = rplane;
+    a.n = n;
+    double ig[4];
+    prepare_gaussian(n, sigma, a.g, a.xg, a.xxg, ig);
+    a.ig11 = ig[0];
+    a.ig03 = ig[1];
+    a.ig33 = ig[2];
+    a.ig55 = ig[3];
+    hipLaunchKernelGGL(fb_polyexp_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+inline int plane_pitch(int w) { return align_up(w, 64); }
+
+// rows per fb_iter workgroup: about 1024 workgroups for the level
+int iter_seg(int w, int h, int m)
+{
+    const int ow = kFbStrip - 2 * m;
+    const int nstrips = (w + ow - 1) / ow;
+    const int nseg = (1024 + nstrips - 1) / nstrips;
+    int seg = (h + nseg - 1) / nseg;
+    return seg < 16 ? 16 : seg;
+}
+
+int fb_reserve(tbdk_ctx* ctx, int64_t px, int64_t tcap)
+{
+    FbScratch* f = ctx->fb;
+    if (!f) {
+        f = new (std::nothrow) FbScratch();
+        if (!f) return TBDK_ENOMEM;
+        ctx->fb = f;
+    }
+    if (px > f->cap_px) {
+        (void)hipFree(f->R0);
+        f->R0 = f->R1 = f->F[0] = f->F[1] = f->I = nullptr;
+        f->cap_px = 0;
+        float* base = nullptr;
+        // R0 (5) + R1 (5) + F0 (2) + F1 (2) + I (1) planes in one allocation
+        if (hipMalloc(&base, sizeof(float) * (size_t)px * 15) != hipSuccess) return TBDK_ENOMEM;
+        f->R0 = base;
+        f->R1 = base + px * 5;
+        f->F[0] = base + px * 10;
+        f->F[1] = base + px * 12;
+        f->I = base + px * 14;
+        f->cap_px = px;
+    }
+    if (tcap > f->cap_T) {
+        (void)hipFree(f->T);
+        f->T = nullptr;
+        f->cap_T = 0;
+        if (hipMalloc(&f->T, sizeof(float) * (size_t)tcap) != hipSuccess) return TBDK_ENOMEM;
+        f->cap_T = tcap;
+    }
+    return TBDK_OK;
+}
+
+struct FbLevel {
+    int w, h, ks;
+    double sigma;
+};
+
+int fb_check(const tbdk_farneback_params* p)
+{
+    if (!p) return TBDK_EINVAL;
+    if (!(p->pyr_scale < 1)) return TBDK_EINVAL;  // CV_Assert(pyrScale_ < 1) (optflowgf.cpp:1113-1114)
+    if (p->fast_pyramids) return TBDK_EINVAL;      // CUDA-only pyrDown pyramids: not provided
+    if (p->win_size < 1 || p->win_size / 2 > kFbMaxHalf) return TBDK_EINVAL;
+    if (p->num_iters < 0) return TBDK_EINVAL;
+    if (p->poly_n < 1 || p->poly_n > kFbMaxPolyN) return TBDK_EINVAL;
+    if (p->flags & ~(TBDK_OPTFLOW_FARNEBACK_GAUSSIAN | TBDK_OPTFLOW_USE_INITIAL_FLOW)) return TBDK_EINVAL;
+    if (p->flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) return TBDK_EINVAL;  // not provided
+    return TBDK_OK;
+}
+
+}  // namespace
+
+void fb_release(tbdk_ctx* ctx)
+{
+    if (!ctx || !ctx->fb) return;
+    (void)hipFree(ctx->fb->R0);
+    (void)hipFree(ctx->fb->T);
+    delete ctx->fb;
+    ctx->fb = nullptr;
+}
+
+}  // namespace tbdk
+
+using namespace tbdk;
+
+extern "C" {
+
+int tbdk_farneback_default_params(tbdk_farneback_params* p)
+{
+    if (!p) return TBDK_EINVAL;
+    // cv::cuda::FarnebackOpticalFlow::create defaults (cudaoptflow.hpp:242-250)
+    p->num_levels = 5;
+    p->pyr_scale = 0.5;
+    p->fast_pyramids = 0;
+    p->win_size = 13;
+    p->num_iters = 10;
+    p->poly_n = 5;
+    p->poly_sigma = 1.1;
+    p->flags = 0;
+    return TBDK_OK;
+}
+
+int tbdk_farneback_levels(int width, int height, const tbdk_farneback_params* p, int* nlevels, int32_t* sizes)
+{
+    if (fb_check(p) != TBDK_OK || width <= 0 || height <= 0 || !nlevels) return TBDK_EINVAL;
+    // FarnebackOpticalFlowImpl::calc level count (optflowgf.cpp:1125-1132)
+    const int min_size = 32;
+    int k;
+    double scale = 1;
+    for (k = 0; k < p->num_levels; k++) {
+        scale *= p->pyr_scale;
+        if (width * scale < min_size || height * scale < min_size) break;
+    }
+    *nlevels = k + 1;
+    if (sizes) {
+        for (int l = 0; l <= k; ++l) {
+            double sc = 1;
+            for (int i = 0; i < l; i++) sc *= p->pyr_scale;
+            sizes[2 * l] = cv_round(width * sc);
+            sizes[2 * l + 1] = cv_round(height * sc);
+        }
+    }
+    return TBDK_OK;
+}
+
+int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int width, int height, int pitch,
+                   float* flow, int flow_pitch, const tbdk_farneback_params* p, void* stream)
+{
+    if (!ctx || !prev || !next || !flow || width <= 0 || height <= 0 || pitch < width) return TBDK_EINVAL;
+    if (flow_pitch < 8 * width || flow_pitch % 8 != 0) return TBDK_EINVAL;
+    int rc = fb_check(p);
+    if (rc != TBDK_OK) return rc;
+    int nl = 0;
+    int32_t sizes[2 * 64];
+    if (p->num_levels > 63) return TBDK_EINVAL;
+    tbdk_farneback_levels(width, height, p, &nl, sizes);
+    const int levels = nl - 1;
+    // per-level smoothing (optflowgf.cpp:1136-1144) and scratch sizes
+    FbLevel lv[64];
+    int64_t tcap = 0;
+    LevelImagePlan plan;
+    for (int k = 0; k <= levels; ++k) {
+        double scale = 1;
+        for (int i = 0; i < k; i++) scale *= p->pyr_scale;
+        const double sigma = (1. / scale - 1) * 0.5;
+        int smooth_sz = cv_round(sigma * 5) | 1;
+        smooth_sz = smooth_sz < 3 ? 3 : smooth_sz;
+        lv[k] = FbLevel{sizes[2 * k], sizes[2 * k + 1], smooth_sz, sigma};
+        if (lv[k].w <= 0 || lv[k].h <= 0) return TBDK_EINVAL;
+        rc = plan_level_image(width, height, lv[k].w, lv[k].h, smooth_sz, sigma, &plan);
+        if (rc != TBDK_OK) return rc;
+        const int64_t t = (int64_t)height * plane_pitch(plan.nc);
+        tcap = t > tcap ? t : tcap;
+    }
+    const int64_t px = (int64_t)plane_pitch(width) * height;
+    DeviceGuard g(ctx->device);
+    rc = fb_reserve(ctx, px, tcap);
+    if (rc != TBDK_OK) return rc;
+    FbScratch* f = ctx->fb;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool gauss = (p->flags & TBDK_OPTFLOW_FARNEBACK_GAUSSIAN) != 0;
+    const int m = p->win_size / 2;
+    hipError_t e = hipSuccess;
+    int cur = 0;  // ping-pong index of the current flow
+    int pw = 0, ph = 0, ppitch = 0;
+    for (int k = levels; k >= 0 && e == hipSuccess; --k) {
+        const int w = lv[k].w, h = lv[k].h, pp = plane_pitch(w);
+        const int64_t plane = (int64_t)pp * h;
+        // level images and polynomial expansion of both frames
+        plan_level_image(width, height, w, h, lv[k].ks, lv[k].sigma, &plan);
+        const int tpitch = plane_pitch(plan.nc);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+            int rec = timing_begin(ctx, "fb_pyr", s);
+            e = launch_level_image(plan, i ? next : prev, width, height, pitch, f->T, tpitch, f->I, w, h, pp, s);
+            timing_end(ctx, rec, s);
+            if (e != hipSuccess) break;
+            rec = timing_begin(ctx, "fb_polyexp", s);
+            e = launch_polyexp(f->I, w, h, pp, i ? f->R1 : f->R0, pp, plane, p->poly_n, p->poly_sigma, s);
+            timing_end(ctx, rec, s);
+        }
+        if (e != hipSuccess) break;
+        // initial flow of the level
+        int rec = timing_begin(ctx, "fb_flow_init", s);
+        if (k == levels) {
+            e = hipMemsetAsync(f->F[cur], 0, sizeof(float) * (size_t)plane * 2, s);
+        } else {
+            FbFlowUpArgs u;
+            u.src = f->F[cur];
+            u.sw = pw;
+            u.sh = ph;
+            u.spitch = ppitch;
+            u.splane = (int64_t)ppitch * ph;
+            u.dst = f->F[cur ^ 1];
+            u.w = w;
+            u.h = h;
+            u.dpitch = pp;
+            u.dplane = plane;
+            u.scale_x = 1. / ((double)w / pw);
+            u.scale_y = 1. / ((double)h / ph);
+            u.alpha = (float)(1. / p->pyr_scale);
+            hipLaunchKernelGGL(fb_flow_up_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, u);
+            e = hipGetLastError();
+            cur ^= 1;
+        }
+        timing_end(ctx, rec, s);
+        if (e != hipSuccess) break;
+        // iterations
+        FbIterArgs a;
+        a.R0 = f->R0;
+        a.R1 = f->R1;
+        a.w = w;
+        a.h = h;
+        a.pitch = pp;
+        a.fplane = plane;
+        a.rplane = plane;
+        a.seg = iter_seg(w, h, m);
+        a.scale = 1. / (p->win_size * p->win_size);
+        // FarnebackUpdateFlow_GaussianBlur kernel (optflowgf.cpp:416-435)
+        {
+            double sg = m * 0.3, sum = 1;
+            a.gk[0] = (float)sum;
+            for (int i = 1; i <= m; i++) {
+                const float t = (float)std::exp(-i * i / (2 * sg * sg));
+                a.gk[i] = t;
+                sum += t * 2;
+            }
+            sum = 1. / sum;
+            for (int i = 0; i <= m; i++) a.gk[i] = (float)(a.gk[i] * sum);
+        }
+        for (int it = 0; it < p->num_iters && e == hipSuccess; ++it) {
+            const bool last = k == 0 && it == p->num_iters - 1;
+            a.fin = f->F[cur];
+            a.fout = last ? flow : f->F[cur ^ 1];
+            a.out_il = last;
+            a.out_pitch = flow_pitch / 4;
+            rec = timing_begin(ctx, "fb_iter", s);
+            e = launch_fb_iter(a, m, gauss, s);
+            timing_end(ctx, rec, s);
+            if (!last) cur ^= 1;
+        }
+        if (e == hipSuccess && k == 0 && p->num_iters == 0) {
+            hipLaunchKernelGGL(fb_interleave_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, f->F[cur], w, h, pp,
+                               plane, flow, flow_pitch / 4);
+            e = hipGetLastError();
+        }
+        pw = w;
+        ph = h;
+        ppitch = pp;
+    }
+    return map_status(e);
+}
+
+int tbdk_fb_level_image(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int dst_width,
+                        int dst_height, int smooth_size, double sigma, float* dst, int dst_pitch, void* stream)
+{
+    if (!ctx || !img || !dst || width <= 0 || height <= 0 || pitch < width || dst_width <= 0 || dst_height <= 0 ||
+        dst_pitch < 4 * dst_width || dst_pitch % 4 != 0)
+        return TBDK_EINVAL;
+    LevelImagePlan plan;
+    int rc = plan_level_image(width, height, dst_width, dst_height, smooth_size, sigma, &plan);
+    if (rc != TBDK_OK) return rc;
+    const int tpitch = plane_pitch(plan.nc);
+    DeviceGuard g(ctx->device);
+    rc = fb_reserve(ctx, ctx->fb ? ctx->fb->cap_px : 0, (int64_t)height * tpitch);
+    if (rc != TBDK_OK) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return map_status(launch_level_image(plan, img, width, height, pitch, ctx->fb->T, tpitch, dst, dst_width,
+                                         dst_height, dst_pitch / 4, s));
+}
+
+int tbdk_fb_poly_exp(tbdk_ctx* ctx, const float* src, int width, int height, int src_pitch, int poly_n,
+                     double poly_sigma, float* dst, int dst_pitch, void* stream)
+{
+    if (!ctx || !src || !dst || width <= 0 || height <= 0 || src_pitch < 4 * width || src_pitch % 4 != 0 ||
+        dst_pitch < 4 * width || dst_pitch % 4 != 0 || poly_n < 1 || poly_n > kFbMaxPolyN)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return map_status(launch_polyexp(src, width, height, src_pitch / 4, dst, dst_pitch / 4,
+                                     (int64_t)(dst_pitch / 4) * height, poly_n, poly_sigma, s));
+}
+
+}  // extern "C"

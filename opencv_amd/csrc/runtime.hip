@@ -49,20 +49,6 @@ static int map_err(hipError_t e)
     return TBDK_EHIP;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev)
-    {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard()
-    {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
 int map_status(hipError_t e) { return map_err(e); }
 
 }  // namespace tbdk
@@ -101,6 +87,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     if (ctx->gftt_blk) (void)hipFree(ctx->gftt_blk);
     if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
     if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
+    fb_release(ctx);
     delete ctx;
     return TBDK_OK;
 }

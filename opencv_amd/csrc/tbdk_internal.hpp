@@ -36,6 +36,23 @@ struct TimingRec {
     hipEvent_t begin, end;
 };
 
+// makes the context's device current for the scope of a C-ABI call
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct FbScratch;  // farneback.hip
+
 }  // namespace tbdk
 
 struct tbdk_ctx {
@@ -52,6 +69,7 @@ struct tbdk_ctx {
     void* gftt_planes = nullptr;  // cap_px floats (eig)
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
+    tbdk::FbScratch* fb = nullptr;  // dense Farneback planes (farneback.hip)
 };
 
 namespace tbdk {
@@ -59,6 +77,9 @@ namespace tbdk {
 // RAII-free helpers used by the C-ABI around each launch.
 int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s);
 void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s);
+
+// frees the context's Farneback scratch (farneback.hip)
+void fb_release(tbdk_ctx* ctx);
 
 // ---- kernels (klt_pyr.hip) ----
 hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& dst, hipStream_t s);

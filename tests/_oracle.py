@@ -264,3 +264,70 @@ def invert_affine(M) -> np.ndarray:
     out = np.zeros(6, np.float64)
     lib.orc_invert_affine(_ptr(m), _ptr(out))
     return out.reshape(2, 3)
+
+
+# ---- dense Farneback (oracle/farneback_oracle.c) ----
+FARNEBACK_GAUSSIAN = 256
+
+
+def _fb_lib():
+    lib = load()
+    lib.orc_fb_calc.restype = C.c_int
+    lib.orc_fb_calc.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_double,
+                                C.c_int, C.c_int, C.c_int, C.c_double, C.c_int]
+    lib.orc_fb_calc_mode.restype = C.c_int
+    lib.orc_fb_calc_mode.argtypes = lib.orc_fb_calc.argtypes + [C.c_int]
+    lib.orc_fb_gauss_blur.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_double]
+    lib.orc_fb_resize_linear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
+    lib.orc_fb_poly_exp.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_void_p]
+    lib.orc_fb_gaussian_kernel.argtypes = [C.c_int, C.c_double, C.c_void_p]
+    return lib
+
+
+def fb_level_image(img: np.ndarray, size, smooth_size: int, sigma: float) -> np.ndarray:
+    """resize(GaussianBlur(float(img), ksize, sigma), size, INTER_LINEAR) (optflowgf.cpp:1170-1172)."""
+    lib = _fb_lib()
+    f = np.ascontiguousarray(img, dtype=np.float32)
+    h, w = f.shape
+    blur = np.empty_like(f)
+    lib.orc_fb_gauss_blur(_ptr(f), w, h, _ptr(blur), int(smooth_size), float(sigma))
+    dw, dh = size
+    if (dw, dh) == (w, h):
+        return blur
+    out = np.empty((dh, dw), np.float32)
+    lib.orc_fb_resize_linear(_ptr(blur), w, h, 1, _ptr(out), dw, dh)
+    return out
+
+
+def fb_poly_exp(src: np.ndarray, n: int, sigma: float) -> np.ndarray:
+    """FarnebackPolyExp -> (H, W, 5) float32."""
+    lib = _fb_lib()
+    s = np.ascontiguousarray(src, dtype=np.float32)
+    h, w = s.shape
+    out = np.empty((h, w, 5), np.float32)
+    lib.orc_fb_poly_exp(_ptr(s), w, h, int(n), float(sigma), _ptr(out))
+    return out
+
+
+def gaussian_kernel(n: int, sigma: float) -> np.ndarray:
+    lib = _fb_lib()
+    out = np.empty(n, np.float32)
+    lib.orc_fb_gaussian_kernel(int(n), float(sigma), _ptr(out))
+    return out
+
+
+def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.5, levels=5, winsize=13, iterations=10, poly_n=5,
+              poly_sigma=1.1, flags=0, box_direct=False) -> np.ndarray:
+    """cv::calcOpticalFlowFarneback -> (H, W, 2) float32.  box_direct: exact-order
+    box window sums (the GPU's order) instead of the reference's running sums."""
+    lib = _fb_lib()
+    a = np.ascontiguousarray(prev, dtype=np.uint8)
+    b = np.ascontiguousarray(nxt, dtype=np.uint8)
+    h, w = a.shape
+    flow = np.zeros((h, w, 2), np.float32)
+    rc = lib.orc_fb_calc_mode(_ptr(a), _ptr(b), w, h, a.strides[0], _ptr(flow), int(levels), float(pyr_scale),
+                              int(winsize), int(iterations), int(poly_n), float(poly_sigma), int(flags),
+                              int(bool(box_direct)))
+    if rc != 0:
+        raise ValueError("unsupported Farneback arguments")
+    return flow
