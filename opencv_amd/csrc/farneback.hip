@@ -19,7 +19,7 @@
 //                            flow) (optflowgf.cpp:217-312) recomputed on the fly
 //                            for a 128-column strip walking down a row segment
 //                            (ring of the last 2m+1 rows of M in registers), the
-//                            vertical window sum (box: exact-order double sum;
+//                            vertical window sum (box: exact-order float sum;
 //                            FARNEBACK_GAUSSIAN: the reference's float weighted
 //                            sum), the horizontal window from LDS, the 2x2 solve
 //                            in double -> next flow (optflowgf.cpp:341-403, 446-569).
@@ -31,10 +31,11 @@
 // Numerics: every float/double expression is written as the reference's (this
 // file is compiled with -ffp-contract=off), so the level images, R, M, the
 // Gaussian-variant blur and the solve round exactly as the reference's scalar/SSE2
-// code.  The box variant's vertical/horizontal sums are exact-order double
-// window sums instead of the reference's running sums (whose float-rounded
-// row differences accumulate over the whole image): that variant is compared to
-// the oracle within a stated tolerance, the Gaussian variant bit for bit.
+// code.  The box variant's vertical/horizontal sums are exact-order float
+// window sums instead of the reference's running double sums, whose
+// float-rounded row differences accumulate over the whole image: bit-exact
+// with the oracle's box_direct mode, which is compared to the reference's
+// running sums within a stated tolerance.
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -61,8 +62,10 @@ namespace {
 constexpr int kFbMaxKs = 255;   // GaussianBlur ksize of the level images
 constexpr int kFbMaxPolyN = 15;
 constexpr int kFbMaxHalf = 10;  // winsize <= 21
-constexpr int kFbStrip = 128;   // fb_iter strip width (lanes, incl. the 2m halo)
-constexpr int kFbRB = 4;        // rows per horizontal batch of fb_iter
+constexpr int kFbStrip = 128;   // fb_iter strip width (columns, incl. the 2m halo)
+// output columns of a strip: a multiple of 4, so every strip starts on an
+// image column divisible by 4 (the box sums restart there)
+__host__ __device__ constexpr int fb_ow(int m) { return (kFbStrip - 2 * m) & ~3; }
 
 enum { kModeNone = 0, kModeArea2 = 1, kModeLinear = 2 };
 
@@ -342,28 +345,80 @@ struct FbIterArgs {
 
 __device__ __forceinline__ float fb_border(int i) { return i < 2 ? 0.14f : 0.4472f; }
 
-// FarnebackUpdateMatrices at pixel (x, y) (optflowgf.cpp:235-309)
-__device__ __forceinline__ void fb_matrices(const FbIterArgs& a, int x, int y, float M[5])
+// FarnebackUpdateMatrices at pixel (x, y) (optflowgf.cpp:235-309), in three
+// phases so a strip can keep two rows of loads in flight: A = the pixel's flow
+// and R0 (7 loads), B = the four R1 neighbours of x + flow (20 loads, their
+// addresses need A), then the arithmetic.
+struct FbRowA {
+    float dx, dy, r0[5];
+};
+struct FbRowB {
+    float q[5][4];  // R1 corners (x1,y1) (x1+1,y1) (x1,y1+1) (x1+1,y1+1) per channel
+    float fx, fy;   // fractional parts
+    bool in;        // (x1, y1) inside [0, w-1) x [0, h-1)
+};
+
+// buffer loads: one VGPR byte offset per pixel, the plane / row offsets in SGPRs
+struct FbRsrc {
+    __amdgpu_buffer_rsrc_t fin, r0, r1;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fb_rsrc(const float* base, int64_t floats)
 {
-    const size_t o = (size_t)y * a.pitch + x;
-    const float dx = a.fin[o], dy = a.fin[o + a.fplane];
-    const float* R0 = a.R0 + o;
-    const float R00 = R0[0], R01 = R0[a.rplane], R02 = R0[2 * a.rplane], R03 = R0[3 * a.rplane],
-                R04 = R0[4 * a.rplane];
-    float fx = (float)x + dx, fy = (float)y + dy;
-    const int x1 = cv_floorf(fx), y1 = cv_floorf(fy);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(floats * 4), 0x00020000);
+}
+__device__ __forceinline__ float fb_bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+__device__ __forceinline__ void fb_load_a(const FbIterArgs& a, const FbRsrc& rs, int x, int y, FbRowA& A)
+{
+    const uint32_t o = (uint32_t)(y * a.pitch + x) * 4u;
+    const int pl = (int)a.fplane * 4, rpl = (int)a.rplane * 4;
+    A.dx = fb_bload(rs.fin, o, 0);
+    A.dy = fb_bload(rs.fin, o, pl);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) A.r0[c] = fb_bload(rs.r0, o, c * rpl);
+}
+
+__device__ __forceinline__ void fb_load_b(const FbIterArgs& a, const FbRsrc& rs, int x, int y, const FbRowA& A,
+                                          FbRowB& B)
+{
+    const float fx = (float)x + A.dx, fy = (float)y + A.dy;
+    const float ffx = floorf(fx), ffy = floorf(fy);
+    // cvFloor (x86: INT_MIN for NaN / out of range); the fraction fx - x1 is
+    // only used in range, where it equals fx - floor(fx)
+    const int x1 = (ffx >= -2147483648.f && ffx < 2147483648.f) ? (int)ffx : INT_MIN;
+    const int y1 = (ffy >= -2147483648.f && ffy < 2147483648.f) ? (int)ffy : INT_MIN;
+    B.fx = fx - ffx;
+    B.fy = fy - ffy;
+    B.in = (unsigned)x1 < (unsigned)(a.w - 1) && (unsigned)y1 < (unsigned)(a.h - 1);
+    // out-of-range lanes load a clamped (unused) neighbourhood: no divergent branch
+    const int xc = clampi(x1, 0, a.w - 2 < 0 ? 0 : a.w - 2), yc = clampi(y1, 0, a.h - 2 < 0 ? 0 : a.h - 2);
+    const uint32_t o = (uint32_t)(yc * a.pitch + xc) * 4u;
+    const uint32_t dx1 = a.w > 1 ? 4u : 0u;
+    const int dy1 = a.h > 1 ? a.pitch * 4 : 0, rpl = (int)a.rplane * 4;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        B.q[c][0] = fb_bload(rs.r1, o, c * rpl);
+        B.q[c][1] = fb_bload(rs.r1, o + dx1, c * rpl);
+        B.q[c][2] = fb_bload(rs.r1, o, c * rpl + dy1);
+        B.q[c][3] = fb_bload(rs.r1, o + dx1, c * rpl + dy1);
+    }
+}
+
+__device__ __forceinline__ void fb_finish(const FbIterArgs& a, int x, int y, const FbRowA& A, const FbRowB& B,
+                                          float M[5])
+{
+    const float dx = A.dx, dy = A.dy;
+    const float R00 = A.r0[0], R01 = A.r0[1], R02 = A.r0[2], R03 = A.r0[3], R04 = A.r0[4];
     float r2, r3, r4, r5, r6;
-    fx -= x1;
-    fy -= y1;
-    if ((unsigned)x1 < (unsigned)(a.w - 1) && (unsigned)y1 < (unsigned)(a.h - 1)) {
+    if (B.in) {
+        const float fx = B.fx, fy = B.fy;
         const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
-        const float* p = a.R1 + (size_t)y1 * a.pitch + x1;
         float r[5];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) {
-            const float* q = p + c * a.rplane;
-            r[c] = a00 * q[0] + a01 * q[1] + a10 * q[a.pitch] + a11 * q[a.pitch + 1];
-        }
+        for (int c = 0; c < 5; ++c) r[c] = a00 * B.q[c][0] + a01 * B.q[c][1] + a10 * B.q[c][2] + a11 * B.q[c][3];
         r2 = r[0];
         r3 = r[1];
         r4 = (R02 + r[2]) * 0.5f;
@@ -407,9 +462,8 @@ __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (
                                               int y, int ox0)
 {
     constexpr int NW = 4 + 2 * M;
-    constexpr int OW = kFbStrip - 2 * M;
-    using ST = typename std::conditional<GAUSS, float, double>::type;
-    ST out[5][4];
+    constexpr int OW = fb_ow(M);
+    float out[5][4];
 #pragma unroll
     for (int ch = 0; ch < 5; ++ch) {
         const float* row = vb[r][ch];
@@ -426,16 +480,17 @@ __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (
                 out[ch][k] = s;
             }
         } else {
-            // window sums in double, left to right, streamed: out[k] = v[k] + ... + v[k+2m]
+            // window of output o0 (image column divisible by 4) summed from the
+            // left, the next three slid: out[k] = (out[k-1] + v[k+2m]) - v[k-1]
+            float win[NW];
 #pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                const double v = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+            float sacc = win[0];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (i == k) out[ch][k] = v;
-                    else if (i > k && i <= k + 2 * M) out[ch][k] += v;
-                }
-            }
+            for (int i = 1; i <= 2 * M; ++i) sacc += win[i];
+            out[ch][0] = sacc;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) out[ch][k] = (out[ch][k - 1] + win[k + 2 * M]) - win[k - 1];
         }
     }
 #pragma unroll
@@ -469,94 +524,133 @@ __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (
     }
 }
 
-// step J of a block (static ring slot J): M of row y0 + m + s into ring[J];
-// for s >= 0 the vertical window of centre row y0 + s into LDS row J
-template <int M, bool GAUSS, int J>
-__device__ __forceinline__ void fb_step(const FbIterArgs& a, float (&ring)[2 * M + 1][5], float (*vb)[5][kFbSlots],
-                                        int x, int y0, int s, int nrows, int sl)
+// workgroup barrier that waits only for LDS traffic
+__device__ __forceinline__ void fb_lds_barrier()
 {
-    constexpr int K = 2 * M + 1;
-    if (s >= nrows) return;
-    fb_matrices(a, x, clampi(y0 + M + s, 0, a.h - 1), ring[J]);
-    if (s < 0) return;
-    constexpr int CS = (J + M + 1) % K;  // ring slot of the centre row; row c+d is slot (CS + d) mod K
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+}
+
+constexpr int kFbRB = 8;        // output rows per batch of fb_iter
+constexpr int kFbThreads = 256; // two threads per strip column
+
+// M of NR rows t0 + half, t0 + half + 2, ... (relative to the segment's first
+// M row) of column x into the LDS ring: every row's loads are issued before
+// any row waits (A loads, then the dependent R1 gathers)
+template <int NR>
+__device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, float* mr, int rr, int x, int col,
+                                        int ybase, int t0, int half)
+{
+    FbRowA A[NR];
+    FbRowB B[NR];
 #pragma unroll
-    for (int ch = 0; ch < 5; ++ch) {
-        float v;
-        if (GAUSS) {
-            // optflowgf.cpp:509-515: s0 = M(c)*k0; s0 += (M(c+i) + M(c-i))*k[i]
-            v = ring[CS][ch] * a.gk[0];
+    for (int i = 0; i < NR; ++i) fb_load_a(a, rs, x, clampi(ybase + t0 + half + 2 * i, 0, a.h - 1), A[i]);
 #pragma unroll
-            for (int i = 1; i <= M; ++i) v += (ring[(CS + i) % K][ch] + ring[(CS + K - i) % K][ch]) * a.gk[i];
-        } else {
-            // exact-order window: rows c-m .. c+m summed in double from the top
-            double sum = 0;
+    for (int i = 0; i < NR; ++i) fb_load_b(a, rs, x, clampi(ybase + t0 + half + 2 * i, 0, a.h - 1), A[i], B[i]);
 #pragma unroll
-            for (int i = -M; i <= M; ++i) sum += ring[(CS + K + i) % K][ch];
-            v = (float)sum;
-        }
-        vb[J][ch][sl] = v;
+    for (int i = 0; i < NR; ++i) {
+        float Mv[5];
+        const int t = t0 + half + 2 * i;
+        fb_finish(a, x, clampi(ybase + t, 0, a.h - 1), A[i], B[i], Mv);
+        float* dst = mr + (t % rr) * kFbStrip + col;
+#pragma unroll
+        for (int ch = 0; ch < 5; ++ch) dst[ch * rr * kFbStrip] = Mv[ch];
     }
 }
 
-template <int M, bool GAUSS, int... J>
-__device__ __forceinline__ void fb_block(std::integer_sequence<int, J...>, const FbIterArgs& a,
-                                         float (&ring)[2 * M + 1][5], float (*vb)[5][kFbSlots], int x, int y0, int s0,
-                                         int nrows, int sl)
-{
-    (fb_step<M, GAUSS, J>(a, ring, vb, x, y0, s0 + J, nrows, sl), ...);
-}
-
-// One workgroup = one 128-column strip (lane = column, m halo lanes per side)
-// walking the output rows [y0, y0 + seg).  Steps s = -2m .. seg-1 each compute
-// M of row y0 + m + s (clamped = BORDER_REPLICATE) into a register ring of
-// 2m+1 rows; a block of 2m+1 steps is expanded at compile time, so every ring
-// slot is static.  Steps s >= 0 store the vertical window of centre row
-// y0 + s (box: exact-order double sum rounded to float; Gaussian: the
-// reference's float weighted sum) in LDS row J of the block; after each block
-// the workgroup sums the horizontal windows and solves.  Every value is a
+// One workgroup = one 128-column strip (m halo columns per side) over the
+// output rows [y0, y0 + seg).  M of the strip's rows lives in an LDS ring of
+// kFbRB + 2m rows; each batch computes kFbRB new rows (two threads per column,
+// all their loads in flight together), then the vertical windows (box: exact-
+// order float sum; Gaussian: the reference's float weighted sum) of kFbRB
+// centre rows, then the horizontal windows and the solve.  Every value is a
 // fixed-order function of the pixel's neighbourhood, independent of the
 // strip/segment split.
 template <int M, bool GAUSS>
-__global__ __launch_bounds__(kFbStrip) void fb_iter_kernel(FbIterArgs a)
+__global__ __launch_bounds__(kFbThreads, 2) void fb_iter_kernel(FbIterArgs a)
 {
     constexpr int K = 2 * M + 1;
-    constexpr int OW = kFbStrip - 2 * M;
-    constexpr int NQ = (OW + 3) / 4;  // 4-column tasks per row
-    __shared__ float vb[K][5][kFbSlots];
+    constexpr int OW = fb_ow(M);
+    constexpr int NQ = (OW + 3) / 4;      // 4-column horizontal tasks per row
+    constexpr int RR = kFbRB + 2 * M;     // M ring rows
+    constexpr int VC = kFbRB / 2;         // centres per thread in the vertical pass
+    __shared__ float mr[5 * RR * kFbStrip];
+    __shared__ float vb[kFbRB][5][kFbSlots];
 
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int col = tid & (kFbStrip - 1), half = tid >> 7;
     const int ox0 = blockIdx.x * OW;
-    const int x = clampi(ox0 - M + lane, 0, a.w - 1);
+    const int x = clampi(ox0 - M + col, 0, a.w - 1);
     const int y0 = blockIdx.y * a.seg;
     const int nrows = min(a.h, y0 + a.seg) - y0;
-    const int sl = fb_slot(lane);
+    const int ybase = y0 - M;  // M row t (relative) is image row ybase + t (clamped)
+    const int sl = fb_slot(col);
 
-    float ring[K][5];
-    for (int s0 = -2 * M; s0 < nrows; s0 += K) {
-        fb_block<M, GAUSS>(std::make_integer_sequence<int, K>{}, a, ring, vb, x, y0, s0, nrows, sl);
-        const int jbeg = s0 < 0 ? -s0 : 0;
-        const int jend = min(K, nrows - s0);
-        __syncthreads();
-        for (int task = threadIdx.x; task < (jend - jbeg) * NQ; task += kFbStrip) {
-            const int r = jbeg + task / NQ, q = task - (task / NQ) * NQ;
+    const int64_t plane_end = (int64_t)a.h * a.pitch;
+    const FbRsrc rs{fb_rsrc(a.fin, a.fplane + plane_end), fb_rsrc(a.R0, 4 * a.rplane + plane_end),
+                    fb_rsrc(a.R1, 4 * a.rplane + plane_end)};
+    // warm-up rows 0 .. 2m-1: batch-sized chunks, then the remainder
+    for (int t = 0; t + kFbRB <= 2 * M; t += kFbRB) fb_rows<kFbRB / 2>(a, rs, mr, RR, x, col, ybase, t, half);
+    if constexpr ((2 * M) % kFbRB != 0)
+        fb_rows<((2 * M) % kFbRB) / 2>(a, rs, mr, RR, x, col, ybase, 2 * M - (2 * M) % kFbRB, half);
+    for (int s0 = 0; s0 < nrows; s0 += kFbRB) {
+        fb_rows<kFbRB / 2>(a, rs, mr, RR, x, col, ybase, 2 * M + s0, half);
+        fb_lds_barrier();
+        // vertical windows of centres s0 + half*VC + j: relative rows c .. c+2m
+#pragma unroll
+        for (int ch = 0; ch < 5; ++ch) {
+            const float* m = mr + ch * RR * kFbStrip + col;
+            float win[VC + 2 * M];
+            float prev = 0.f;
+#pragma unroll
+            for (int i = 0; i < VC + 2 * M; ++i) win[i] = m[((s0 + half * VC + i) % RR) * kFbStrip];
+#pragma unroll
+            for (int j = 0; j < VC; ++j) {
+                float v;
+                if (GAUSS) {
+                    // optflowgf.cpp:509-515: s0 = M(c)*k0; s0 += (M(c+i) + M(c-i))*k[i]
+                    v = win[j + M] * a.gk[0];
+#pragma unroll
+                    for (int i = 1; i <= M; ++i) v += (win[j + M + i] + win[j + M - i]) * a.gk[i];
+                } else {
+                    // rows c-m .. c+m: summed from the top at the batch's first
+                    // centre (image row divisible by 4), then slid
+                    if (j == 0) {
+                        v = win[0];
+#pragma unroll
+                        for (int i = 1; i < K; ++i) v += win[i];
+                    } else {
+                        v = (prev + win[j + 2 * M]) - win[j - 1];
+                    }
+                    prev = v;
+                }
+                vb[half * VC + j][ch][sl] = v;
+            }
+        }
+        fb_lds_barrier();
+        const int nb = min(kFbRB, nrows - s0);
+        if (tid < nb * NQ) {
+            const int r = tid / NQ, q = tid - r * NQ;
             if (ox0 + 4 * q < a.w) fb_horizontal<M, GAUSS>(a, vb, r, 4 * q, y0 + s0 + r, ox0);
         }
-        __syncthreads();
+        // the next batch's M rows overwrite ring rows the vertical pass read,
+        // and its vertical pass vb rows this horizontal pass reads: both are
+        // ordered by the two barriers above (this pass ends before the next
+        // batch's first barrier)
     }
 }
 
 template <int M>
 hipError_t launch_fb_iter_m(const FbIterArgs& a, bool gauss, dim3 grid, hipStream_t s)
 {
-    if (gauss) hipLaunchKernelGGL((fb_iter_kernel<M, true>), grid, dim3(kFbStrip), 0, s, a);
-    else hipLaunchKernelGGL((fb_iter_kernel<M, false>), grid, dim3(kFbStrip), 0, s, a);
+    if (gauss) hipLaunchKernelGGL((fb_iter_kernel<M, true>), grid, dim3(kFbThreads), 0, s, a);
+    else hipLaunchKernelGGL((fb_iter_kernel<M, false>), grid, dim3(kFbThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_fb_iter(const FbIterArgs& a, int m, bool gauss, hipStream_t s)
 {
-    const int ow = kFbStrip - 2 * m;
+    const int ow = fb_ow(m);
     const int nstrips = (a.w + ow - 1) / ow;
     const int nseg = (a.h + a.seg - 1) / a.seg;
     const dim3 grid(nstrips, nseg);
@@ -764,14 +858,17 @@ hipError_t launch_polyexp(const float* I, int w, int h, int ipitch, float* R, in
 
 inline int plane_pitch(int w) { return align_up(w, 64); }
 
-// rows per fb_iter workgroup: about 1024 workgroups for the level
+// rows per fb_iter workgroup (a multiple of the batch): about two rounds of
+// resident workgroups (2 per CU, 256 CUs); small levels get one batch per
+// workgroup so their serial chain of round trips stays short
 int iter_seg(int w, int h, int m)
 {
-    const int ow = kFbStrip - 2 * m;
+    const int ow = fb_ow(m);
     const int nstrips = (w + ow - 1) / ow;
     const int nseg = (1024 + nstrips - 1) / nstrips;
     int seg = (h + nseg - 1) / nseg;
-    return seg < 16 ? 16 : seg;
+    seg = (seg + kFbRB - 1) / kFbRB * kFbRB;
+    return seg < kFbRB ? kFbRB : seg;
 }
 
 int fb_reserve(tbdk_ctx* ctx, int64_t px, int64_t tcap)

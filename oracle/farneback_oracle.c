@@ -23,12 +23,14 @@
  *                              INTER_AREA fast path, :3519-3550, 2479-2500, 2600-2640)
  *
  * The optflowgf.cpp functions are restated literally (running sums, stripe
- * updates).  orc_fb_calc_mode(..., box_direct=1) swaps the box blur's running
- * sums for exact-order window sums (orc_fb_update_flow_blur_direct), the
- * order the GPU kernel uses, so that the GPU is checked bit for bit against
- * it and this mode against the reference's within a tolerance.  Known deviation: the imgproc SIMD paths (GaussianBlur's filter
- * engine, resize) may be built with FMA under AVX2 dispatch on the reference's
- * host; their scalar/SSE orders are restated here.
+ * updates).  orc_fb_calc_mode(..., box_direct=1) swaps the box blur's
+ * image-long running sums for the fixed-order window sums of
+ * orc_fb_update_flow_blur_direct (restarted every 4 rows / columns), the order
+ * the GPU kernel uses, so that the GPU is checked bit for bit against it and
+ * this mode against the reference's within a tolerance.
+ * Known deviation: the imgproc SIMD paths (GaussianBlur's filter engine,
+ * resize) may be built with FMA under AVX2 dispatch on the reference's host;
+ * their scalar/SSE orders are restated here.
  */
 #include <float.h>
 #include <math.h>
@@ -431,38 +433,59 @@ void orc_fb_update_flow_blur(const float* R0, const float* R1, float* flow_, flo
     free(vsum_);
 }
 
-/* The box blur with exact-order window sums, the order libtbdk's fb_iter uses
- * (NOT the reference's): vertical window of rows c-m..c+m (clamped) summed
- * in double from the top, rounded to float; horizontal window of those floats
- * (replicated columns) summed in double from the left; then the reference's
- * scale and solve.  The reference's running sums (orc_fb_update_flow_blur)
- * differ from it only by their float-rounded row differences. */
+/* The box blur in the fixed order libtbdk's fb_iter uses (NOT the
+ * reference's): per column, the vertical window sum of rows c-m..c+m
+ * (clamped) is summed in float from the top at every row c divisible by 4 and
+ * slid from the previous row otherwise, V(c) = (V(c-1) + M(c+m)) - M(c-m-1);
+ * the same along each row of V for the horizontal window (restart at columns
+ * divisible by 4); then the reference's double scale and solve.  The
+ * reference's running double sums (orc_fb_update_flow_blur) slide over the
+ * whole image instead, with float-rounded row differences. */
 void orc_fb_update_flow_blur_direct(const float* R0, const float* R1, float* flow, float* M, int width, int height,
                                     int block_size, int update)
 {
     const int m = block_size / 2;
     const double scale = 1. / (block_size * block_size);
     float* V = malloc(sizeof(float) * (size_t)width * 5);
+    float* Vp = malloc(sizeof(float) * (size_t)width * 5);
+#define MROW(r) (M + (size_t)clampi((r), 0, height - 1) * width * 5)
     for (int y = 0; y < height; y++) {
         for (int x = 0; x < width * 5; x++) {
-            double s = 0;
-            for (int i = -m; i <= m; i++) s += M[(size_t)clampi(y + i, 0, height - 1) * width * 5 + x];
-            V[x] = (float)s;
+            float s;
+            if (y % 4 == 0) {
+                s = MROW(y - m)[x];
+                for (int i = -m + 1; i <= m; i++) s += MROW(y + i)[x];
+            } else {
+                s = (Vp[x] + MROW(y + m)[x]) - MROW(y - m - 1)[x];
+            }
+            V[x] = s;
         }
         float* f = flow + (size_t)y * width * 2;
+        float h[5];
         for (int x = 0; x < width; x++) {
             double g[5];
             for (int c = 0; c < 5; c++) {
-                double s = 0;
-                for (int j = -m; j <= m; j++) s += V[clampi(x + j, 0, width - 1) * 5 + c];
-                g[c] = s * scale;
+#define VCOL(cc) V[clampi((cc), 0, width - 1) * 5 + c]
+                if (x % 4 == 0) {
+                    h[c] = VCOL(x - m);
+                    for (int j = -m + 1; j <= m; j++) h[c] += VCOL(x + j);
+                } else {
+                    h[c] = (h[c] + VCOL(x + m)) - VCOL(x - m - 1);
+                }
+#undef VCOL
+                g[c] = h[c] * scale;
             }
             const double idet = 1. / (g[0] * g[2] - g[1] * g[1] + 1e-3);
             f[x * 2] = (float)((g[0] * g[4] - g[1] * g[3]) * idet);
             f[x * 2 + 1] = (float)((g[2] * g[3] - g[1] * g[4]) * idet);
         }
+        float* t = Vp;
+        Vp = V;
+        V = t;
     }
+#undef MROW
     free(V);
+    free(Vp);
     if (update) orc_fb_update_matrices(R0, R1, flow, width, height, M, 0, height);
 }
 
