@@ -531,22 +531,32 @@ __device__ __forceinline__ void fb_lds_barrier()
     __builtin_amdgcn_s_barrier();
 }
 
-constexpr int kFbRB = 8;        // output rows per batch of fb_iter
+constexpr int kFbRB = 4;        // output rows per batch of fb_iter (4 or 8)
 constexpr int kFbThreads = 256; // two threads per strip column
 
 // M of NR rows t0 + half, t0 + half + 2, ... (relative to the segment's first
 // M row) of column x into the LDS ring: every row's loads are issued before
 // any row waits (A loads, then the dependent R1 gathers)
+// the three phases of M for NR rows t0 + half + 2i of column x, split so a
+// batch's loads can be in flight while the previous batch is summed
 template <int NR>
-__device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, float* mr, int rr, int x, int col,
-                                        int ybase, int t0, int half)
+__device__ __forceinline__ void fb_rows_a(const FbIterArgs& a, const FbRsrc& rs, int x, int ybase, int t0, int half,
+                                          FbRowA (&A)[NR])
 {
-    FbRowA A[NR];
-    FbRowB B[NR];
 #pragma unroll
     for (int i = 0; i < NR; ++i) fb_load_a(a, rs, x, clampi(ybase + t0 + half + 2 * i, 0, a.h - 1), A[i]);
+}
+template <int NR>
+__device__ __forceinline__ void fb_rows_b(const FbIterArgs& a, const FbRsrc& rs, int x, int ybase, int t0, int half,
+                                          const FbRowA (&A)[NR], FbRowB (&B)[NR])
+{
 #pragma unroll
     for (int i = 0; i < NR; ++i) fb_load_b(a, rs, x, clampi(ybase + t0 + half + 2 * i, 0, a.h - 1), A[i], B[i]);
+}
+template <int NR>
+__device__ __forceinline__ void fb_rows_finish(const FbIterArgs& a, float* mr, int rr, int x, int col, int ybase,
+                                               int t0, int half, const FbRowA (&A)[NR], const FbRowB (&B)[NR])
+{
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
         float Mv[5];
@@ -556,6 +566,16 @@ __device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, f
 #pragma unroll
         for (int ch = 0; ch < 5; ++ch) dst[ch * rr * kFbStrip] = Mv[ch];
     }
+}
+template <int NR>
+__device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, float* mr, int rr, int x, int col,
+                                        int ybase, int t0, int half)
+{
+    FbRowA A[NR];
+    FbRowB B[NR];
+    fb_rows_a<NR>(a, rs, x, ybase, t0, half, A);
+    fb_rows_b<NR>(a, rs, x, ybase, t0, half, A, B);
+    fb_rows_finish<NR>(a, mr, rr, x, col, ybase, t0, half, A, B);
 }
 
 // One workgroup = one 128-column strip (m halo columns per side) over the
@@ -567,13 +587,13 @@ __device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, f
 // fixed-order function of the pixel's neighbourhood, independent of the
 // strip/segment split.
 template <int M, bool GAUSS>
-__global__ __launch_bounds__(kFbThreads, 2) void fb_iter_kernel(FbIterArgs a)
+__global__ __launch_bounds__(kFbThreads, (M <= 6 ? (GAUSS ? 2 : 3) : (GAUSS ? 1 : 2))) void fb_iter_kernel(FbIterArgs a)
 {
     constexpr int K = 2 * M + 1;
     constexpr int OW = fb_ow(M);
     constexpr int NQ = (OW + 3) / 4;      // 4-column horizontal tasks per row
     constexpr int RR = kFbRB + 2 * M;     // M ring rows
-    constexpr int VC = kFbRB / 2;         // centres per thread in the vertical pass
+    constexpr int VC = 4;                 // centres per thread in the vertical pass
     __shared__ float mr[5 * RR * kFbStrip];
     __shared__ float vb[kFbRB][5][kFbSlots];
 
@@ -593,17 +613,31 @@ __global__ __launch_bounds__(kFbThreads, 2) void fb_iter_kernel(FbIterArgs a)
     for (int t = 0; t + kFbRB <= 2 * M; t += kFbRB) fb_rows<kFbRB / 2>(a, rs, mr, RR, x, col, ybase, t, half);
     if constexpr ((2 * M) % kFbRB != 0)
         fb_rows<((2 * M) % kFbRB) / 2>(a, rs, mr, RR, x, col, ybase, 2 * M - (2 * M) % kFbRB, half);
+    // batch pipeline: the M rows of batch s0 + kFbRB are loaded (A during the
+    // vertical pass, the dependent R1 gathers B during the horizontal pass of
+    // batch s0) before they are finished at the top of the next iteration
+    constexpr int NR = kFbRB / 2;
+    FbRowA A[NR];
+    FbRowB B[NR];
+    fb_rows_a<NR>(a, rs, x, ybase, 2 * M, half, A);
+    fb_rows_b<NR>(a, rs, x, ybase, 2 * M, half, A, B);
     for (int s0 = 0; s0 < nrows; s0 += kFbRB) {
-        fb_rows<kFbRB / 2>(a, rs, mr, RR, x, col, ybase, 2 * M + s0, half);
+        fb_rows_finish<NR>(a, mr, RR, x, col, ybase, 2 * M + s0, half, A, B);
+        const bool more = s0 + kFbRB < nrows;
+        if (more) fb_rows_a<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A);
         fb_lds_barrier();
-        // vertical windows of centres s0 + half*VC + j: relative rows c .. c+2m
+        // vertical windows of centres s0 + cb + j: relative rows c .. c+2m
+        // (batch of 8: each half takes 4 centres; batch of 4: the halves split
+        // the channels, 0-2 and 3-4)
+        const int cb = kFbRB == 8 ? half * VC : 0;
 #pragma unroll
         for (int ch = 0; ch < 5; ++ch) {
+            if (kFbRB == 4 && (ch < 3) != (half == 0)) continue;
             const float* m = mr + ch * RR * kFbStrip + col;
             float win[VC + 2 * M];
             float prev = 0.f;
 #pragma unroll
-            for (int i = 0; i < VC + 2 * M; ++i) win[i] = m[((s0 + half * VC + i) % RR) * kFbStrip];
+            for (int i = 0; i < VC + 2 * M; ++i) win[i] = m[((s0 + cb + i) % RR) * kFbStrip];
 #pragma unroll
             for (int j = 0; j < VC; ++j) {
                 float v;
@@ -624,9 +658,10 @@ __global__ __launch_bounds__(kFbThreads, 2) void fb_iter_kernel(FbIterArgs a)
                     }
                     prev = v;
                 }
-                vb[half * VC + j][ch][sl] = v;
+                vb[cb + j][ch][sl] = v;
             }
         }
+        if (more) fb_rows_b<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A, B);
         fb_lds_barrier();
         const int nb = min(kFbRB, nrows - s0);
         if (tid < nb * NQ) {
@@ -857,15 +892,16 @@ hipError_t launch_polyexp(const float* I, int w, int h, int ipitch, float* R, in
 }
 
 inline int plane_pitch(int w) { return align_up(w, 64); }
+inline int64_t plane_stride(int pp, int h) { return (int64_t)pp * h; }
 
 // rows per fb_iter workgroup (a multiple of the batch): about two rounds of
-// resident workgroups (2 per CU, 256 CUs); small levels get one batch per
+// resident workgroups (3 per CU, 256 CUs); small levels get one batch per
 // workgroup so their serial chain of round trips stays short
 int iter_seg(int w, int h, int m)
 {
     const int ow = fb_ow(m);
     const int nstrips = (w + ow - 1) / ow;
-    const int nseg = (1024 + nstrips - 1) / nstrips;
+    const int nseg = (1536 + nstrips - 1) / nstrips;
     int seg = (h + nseg - 1) / nseg;
     seg = (seg + kFbRB - 1) / kFbRB * kFbRB;
     return seg < kFbRB ? kFbRB : seg;
@@ -1005,7 +1041,7 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
         const int64_t t = (int64_t)height * plane_pitch(plan.nc);
         tcap = t > tcap ? t : tcap;
     }
-    const int64_t px = (int64_t)plane_pitch(width) * height;
+    const int64_t px = plane_stride(plane_pitch(width), height);
     DeviceGuard g(ctx->device);
     rc = fb_reserve(ctx, px, tcap);
     if (rc != TBDK_OK) return rc;
@@ -1018,7 +1054,7 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
     int pw = 0, ph = 0, ppitch = 0;
     for (int k = levels; k >= 0 && e == hipSuccess; --k) {
         const int w = lv[k].w, h = lv[k].h, pp = plane_pitch(w);
-        const int64_t plane = (int64_t)pp * h;
+        const int64_t plane = plane_stride(pp, h);
         // level images and polynomial expansion of both frames
         plan_level_image(width, height, w, h, lv[k].ks, lv[k].sigma, &plan);
         const int tpitch = plane_pitch(plan.nc);
@@ -1042,7 +1078,7 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
             u.sw = pw;
             u.sh = ph;
             u.spitch = ppitch;
-            u.splane = (int64_t)ppitch * ph;
+            u.splane = plane_stride(ppitch, ph);
             u.dst = f->F[cur ^ 1];
             u.w = w;
             u.h = h;
