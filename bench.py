@@ -127,6 +127,77 @@ def cpu_baseline(frames_host, gt, args, seconds: float):
                       f"PyrLK win {args.win} SSE2-order ({threads} threads); tracker step excluded"}
 
 
+FB_ITER_BYTES_PER_PX = 56  # fb_iter algorithmic bytes per pixel: flow 8 + R0 20 + R1 20 in, flow 8 out
+
+
+def farneback_secondary(ctx, args, device, cpu: bool):
+    """BASELINE configs[4]'s dense Farneback variant on a synthetic 4K pair
+    sequence (3840x2160, 512 objects): frame pairs/s through tbdk_farneback
+    (cv::cuda::FarnebackOpticalFlow defaults), the fb_iter kernel's HBM
+    roofline, and the CPU oracle on one pair.  Reported, never `value`."""
+    import torch
+    from opencv_amd import farneback as F
+    from opencv_amd import klt
+
+    w, h, n = args.fb_width, args.fb_height, args.fb_pairs
+    frames, _ = klt.synth_render(args.seed + 7, w, h, args.fb_objects, 0, n + 3, device=device, ctx=ctx)
+    fb = F.FarnebackOpticalFlow.create(ctx=ctx)
+    flow = torch.empty((h, w, 2), dtype=torch.float32, device=frames.device)
+    for i in range(2):
+        fb.calc(frames[i], frames[i + 1], flow)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n):
+        fb.calc(frames[i], frames[i + 1], flow)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ctx.timing_select(["fb_iter", "fb_pyr", "fb_polyexp", "fb_flow_init"])
+    ctx.timing_enable(True)
+    for i in range(n):
+        fb.calc(frames[i], frames[i + 1], flow)
+    torch.cuda.synchronize()
+    kern = {}
+    for name in ("fb_iter", "fb_pyr", "fb_polyexp", "fb_flow_init"):
+        c, ms = ctx.timing_query(name)
+        kern[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "ms_per_pair": ms / n}
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    levels = fb.levels(w, h)
+    it_bytes = FB_ITER_BYTES_PER_PX * sum(a * b for a, b in levels) * fb.getNumIters() * n
+    gbs = it_bytes / (kern["fb_iter"]["ms_per_pair"] * n * 1e-3) / 1e9 if kern["fb_iter"]["launches"] else 0.0
+    # PMC bytes per fb_iter launch (the committed summary's mean over a pair's
+    # launches, all levels) x launches per pair -> HBM bytes per pair
+    per_launch, traffic_src = pmc_traffic("fb_iter_kernel<6, false>")
+    launches_per_pair = kern["fb_iter"]["launches"] / n
+    traffic = per_launch * launches_per_pair if per_launch is not None else None
+    alg_pair = it_bytes / n
+    out = {"value": round(n / wall, 2), "unit": "pairs/s", "ms_per_pair": round(1000 * wall / n, 3),
+           "config": {"workload": f"Farneback {w}x{h} x {args.fb_objects} objects (BASELINE configs[4] dense "
+                                  "variant, u8 pixels)", "params": "cv::cuda::FarnebackOpticalFlow defaults: "
+                                  "5 levels, pyrScale 0.5, winSize 13, 10 iters, polyN 5, sigma 1.1, box blur",
+                      "levels": [list(l) for l in levels], "pairs": n},
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                        "kernel": "fb_iter", "bytes_per_px": FB_ITER_BYTES_PER_PX,
+                        "algorithmic_bytes_per_pair": alg_pair, "traffic_unit": "bytes per pair (all fb_iter launches)",
+                        "note": "achieved = algorithmic bytes of every level's 10 launches / summed fb_iter time "
+                                "(HIP events on the launch stream)"},
+           "kernels": kern}
+    if cpu:
+        import importlib
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+        O = importlib.import_module("_oracle")
+        a_, b_ = frames[0].cpu().numpy(), frames[1].cpu().numpy()
+        t1 = time.perf_counter()
+        O.farneback(a_, b_)
+        dt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "pairs/s", "cores": 1, "kind": "port",
+                               "sample": f"one {w}x{h} pair through oracle/farneback_oracle.c (the reference's "
+                                         "calcOpticalFlowFarneback restated, running-sum box blur), 1 thread"}
+    del frames
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,6 +222,11 @@ def main():
                          "each timed launch adds two event records to the frame's host work.  The other "
                          "kernels are timed in a separate pass over the same frames (not `value`)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary per-frame tbdk_tbd_step pass")
+    ap.add_argument("--no-farneback", action="store_true", help="skip the secondary dense Farneback measurement")
+    ap.add_argument("--fb-width", type=int, default=3840)
+    ap.add_argument("--fb-height", type=int, default=2160)
+    ap.add_argument("--fb-objects", type=int, default=512)
+    ap.add_argument("--fb-pairs", type=int, default=10)
     args = ap.parse_args()
 
     import numpy as np
@@ -341,6 +417,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(frames[:nb].cpu().numpy(), gtn[:nb], args, args.cpu_baseline_seconds)
     else:
         out["cpu_baseline"] = None
+    if rank == 0 and not args.no_farneback:
+        del frames, frame_list
+        out["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
