@@ -234,6 +234,53 @@ inline void warpAffine(Context& ctx, const GpuImage& src, GpuImage& dst, const d
           "tbdk_warp_affine_u8");
 }
 
+// cv::cuda::FarnebackOpticalFlow (cudaoptflow.hpp:210-252): create() with the
+// reference's defaults, the getters/setters, calc(I0, I1, flow, stream).
+// flow: device CV_32FC2 (dx, dy interleaved), flowPitch in bytes.
+class FarnebackOpticalFlow {
+public:
+    static std::unique_ptr<FarnebackOpticalFlow> create(Context& ctx, int numLevels = 5, double pyrScale = 0.5,
+                                                        bool fastPyramids = false, int winSize = 13,
+                                                        int numIters = 10, int polyN = 5, double polySigma = 1.1,
+                                                        int flags = 0)
+    {
+        std::unique_ptr<FarnebackOpticalFlow> f(new FarnebackOpticalFlow(ctx));
+        f->p_ = tbdk_farneback_params{numLevels, pyrScale, fastPyramids ? 1 : 0, winSize, numIters, polyN,
+                                      polySigma, flags};
+        return f;
+    }
+    int getNumLevels() const { return p_.num_levels; }
+    void setNumLevels(int v) { p_.num_levels = v; }
+    double getPyrScale() const { return p_.pyr_scale; }
+    void setPyrScale(double v) { p_.pyr_scale = v; }
+    bool getFastPyramids() const { return p_.fast_pyramids != 0; }
+    void setFastPyramids(bool v) { p_.fast_pyramids = v ? 1 : 0; }
+    int getWinSize() const { return p_.win_size; }
+    void setWinSize(int v) { p_.win_size = v; }
+    int getNumIters() const { return p_.num_iters; }
+    void setNumIters(int v) { p_.num_iters = v; }
+    int getPolyN() const { return p_.poly_n; }
+    void setPolyN(int v) { p_.poly_n = v; }
+    double getPolySigma() const { return p_.poly_sigma; }
+    void setPolySigma(double v) { p_.poly_sigma = v; }
+    int getFlags() const { return p_.flags; }
+    void setFlags(int v) { p_.flags = v; }
+
+    void calc(const GpuImage& I0, const GpuImage& I1, float* flow, int flowPitch, void* stream = nullptr)
+    {
+        if (I0.width != I1.width || I0.height != I1.height || I0.pitch != I1.pitch)
+            throw Error(TBDK_EINVAL, "FarnebackOpticalFlow::calc");
+        check(tbdk_farneback(ctx_->get(), I0.data, I1.data, I0.width, I0.height, I0.pitch, flow, flowPitch, &p_,
+                             stream),
+              "tbdk_farneback");
+    }
+
+private:
+    explicit FarnebackOpticalFlow(Context& ctx) : ctx_(&ctx) {}
+    Context* ctx_;
+    tbdk_farneback_params p_{};
+};
+
 }  // namespace cuda
 
 // The tracking section of samples/gpu/tbd.cpp:624-706 (cv::tbd::Tracker +

@@ -52,7 +52,22 @@ int main(int argc, char** argv)
             if (s[i] && std::abs(p1[2 * i] - p0[2 * i] - 1.5f) < 0.1f && std::abs(p1[2 * i + 1] - p0[2 * i + 1] + 0.5f) < 0.1f)
                 ++good;
         std::printf("corners %d tracked-correctly %d\n", n, good);
-        return good * 10 >= n * 8 ? 0 : 6;
+        if (good * 10 < n * 8) return 6;
+        // dense Farneback through the facade: the interior flow is the shift
+        float* flow;
+        if (hipMalloc(&flow, (size_t)W * H * 8)) return 4;
+        auto fb = tbdk::cuda::FarnebackOpticalFlow::create(ctx);
+        fb->calc(a, b, flow, W * 8);
+        std::vector<float> fl((size_t)W * H * 2);
+        (void)hipMemcpy(fl.data(), flow, fl.size() * 4, hipMemcpyDeviceToHost);
+        int near = 0, tot = 0;
+        for (int y = 40; y < H - 40; ++y)
+            for (int x = 40; x < W - 40; ++x, ++tot) {
+                const float* f = &fl[((size_t)y * W + x) * 2];
+                near += std::abs(f[0] - 1.5f) < 0.25f && std::abs(f[1] + 0.5f) < 0.25f;
+            }
+        std::printf("farneback interior near-shift %d / %d\n", near, tot);
+        return near * 10 >= tot * 8 ? 0 : 8;
     } catch (const tbdk::Error& e) {
         std::printf("tbdk::Error: %s\n", e.what());
         return (!want_gpu && e.code() == TBDK_ENODEV) ? 0 : 7;
