@@ -143,6 +143,18 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
                    const float* prev_pts, float* next_pts, uint8_t* status, float* err,
                    int32_t* iters, int n, const tbdk_lk_params* params, void* stream);
 
+/* Replaces cv::cuda::DensePyrLKOpticalFlow::calc(I0, I1, flow)
+ * (cudaoptflow/include/opencv2/cudaoptflow.hpp:182-208, impl cudaoptflow/src/pyrlk.cpp:238-299)
+ * with the CPU calcOpticalFlowPyrLK numerics at every pixel (the point grid
+ * (x, y) of level 0 through the tbdk_lk_sparse kernels):
+ *   flow   : device CV_32FC2, (nextPt.x - x, nextPt.y - y) per pixel, flow_pitch in bytes
+ *   status : device u8 plane (status_pitch bytes) or NULL
+ * TBDK_OPTFLOW_USE_INITIAL_FLOW is ignored, as in the reference (dense() never
+ * reads the incoming flow); win_w/win_h <= 2 is TBDK_EINVAL (pyrlk.cpp:243).
+ * Scratch (17 B per pixel) is owned by the context and grown on demand. */
+int tbdk_lk_dense(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, float* flow, int flow_pitch,
+                  uint8_t* status, int status_pitch, const tbdk_lk_params* params, void* stream);
+
 /* ---- good features to track over box ROIs --------------------------------- */
 
 typedef struct tbdk_roi {
@@ -253,7 +265,7 @@ typedef struct tbdk_farneback_params {
     int32_t num_iters;               /* 10 */
     int32_t poly_n;                  /* 5; 1..15 */
     double poly_sigma;               /* 1.1 */
-    int32_t flags;                   /* 0 | TBDK_OPTFLOW_FARNEBACK_GAUSSIAN (USE_INITIAL_FLOW: TBDK_EINVAL) */
+    int32_t flags;                   /* 0 | TBDK_OPTFLOW_FARNEBACK_GAUSSIAN | TBDK_OPTFLOW_USE_INITIAL_FLOW */
 } tbdk_farneback_params;
 
 int tbdk_farneback_default_params(tbdk_farneback_params* p);
@@ -267,7 +279,10 @@ int tbdk_farneback_levels(int width, int height, const tbdk_farneback_params* p,
  * cv::calcOpticalFlowFarneback (video/src/optflowgf.cpp:1096-1190).
  *   prev, next : device u8 frames (width x height, row pitch in bytes)
  *   flow       : device CV_32FC2 output, interleaved (dx, dy) per pixel,
- *                flow_pitch in bytes (multiple of 8)
+ *                flow_pitch in bytes (multiple of 8); with
+ *                TBDK_OPTFLOW_USE_INITIAL_FLOW also the input: the coarsest
+ *                level starts from its INTER_AREA resize times the level scale
+ *                (optflowgf.cpp:1151-1157)
  * Scratch (15 float planes of the frame size + the blur buffer) is owned by
  * the context and grown on demand; the call is asynchronous on `stream`. */
 int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int width, int height, int pitch,

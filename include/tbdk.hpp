@@ -172,6 +172,64 @@ private:
     std::unique_ptr<Pyramid> pyr_[2];
 };
 
+// cv::cuda::DensePyrLKOpticalFlow (cudaoptflow.hpp:182-208; impl pyrlk.cpp:238-299,
+// 352-397): the PyrLK of every level-0 pixel, written as a CV_32FC2 flow field.
+// useInitialFlow is kept for the interface and, as in the reference, has no effect.
+class DensePyrLKOpticalFlow {
+public:
+    static std::unique_ptr<DensePyrLKOpticalFlow> create(Context& ctx, Size winSize = {13, 13}, int maxLevel = 3,
+                                                         int iters = 30, bool useInitialFlow = false)
+    {
+        return std::unique_ptr<DensePyrLKOpticalFlow>(
+            new DensePyrLKOpticalFlow(ctx, winSize, maxLevel, iters, useInitialFlow));
+    }
+
+    Size getWinSize() const { return win_; }
+    void setWinSize(Size s) { win_ = s; pyr_[0].reset(); pyr_[1].reset(); }
+    int getMaxLevel() const { return max_level_; }
+    void setMaxLevel(int v) { max_level_ = v; pyr_[0].reset(); pyr_[1].reset(); }
+    int getNumIters() const { return iters_; }
+    void setNumIters(int v) { iters_ = v; }
+    bool getUseInitialFlow() const { return use_initial_flow_; }
+    void setUseInitialFlow(bool v) { use_initial_flow_ = v; }
+
+    // calc(I0, I1, flow, stream): flow is a device CV_32FC2 image (flowPitch bytes
+    // per row); status, when given, is a device u8 plane of statusPitch bytes per row.
+    void calc(const GpuImage& I0, const GpuImage& I1, float* flow, int flowPitch, void* stream = nullptr,
+              uint8_t* status = nullptr, int statusPitch = 0)
+    {
+        for (int i = 0; i < 2; ++i) {
+            const GpuImage& im = i == 0 ? I0 : I1;
+            if (!pyr_[i] || pyr_[i]->get().lv[0].width != im.width || pyr_[i]->get().lv[0].height != im.height)
+                pyr_[i].reset(new Pyramid(*ctx_, im.width, im.height, max_level_, win_));
+            pyr_[i]->build(im, stream);
+        }
+        tbdk_lk_params p;
+        p.win_w = win_.width;
+        p.win_h = win_.height;
+        p.max_level = max_level_;
+        p.max_count = iters_;
+        p.epsilon = 0.01;
+        p.flags = use_initial_flow_ ? TBDK_OPTFLOW_USE_INITIAL_FLOW : 0;
+        p.min_eig_threshold = 1e-4f;
+        p.impl = 0;
+        check(tbdk_lk_dense(ctx_->get(), &pyr_[0]->get(), &pyr_[1]->get(), flow, flowPitch, status, statusPitch, &p,
+                            stream),
+              "tbdk_lk_dense");
+    }
+
+private:
+    DensePyrLKOpticalFlow(Context& ctx, Size win, int max_level, int iters, bool uif)
+        : ctx_(&ctx), win_(win), max_level_(max_level), iters_(iters), use_initial_flow_(uif)
+    {
+    }
+    Context* ctx_;
+    Size win_;
+    int max_level_, iters_;
+    bool use_initial_flow_;
+    std::unique_ptr<Pyramid> pyr_[2];
+};
+
 // cv::cuda::CornersDetector from createGoodFeaturesToTrackDetector(CV_8UC1,
 // maxCorners, qualityLevel, minDistance, blockSize=3, useHarris=false)
 // (cudaimgproc.hpp:582,603-604).  detect() runs on the whole image; detectRois()

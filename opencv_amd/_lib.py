@@ -241,6 +241,8 @@ SIGNATURES = {
     "tbdk_tbd_predictions": (C.c_int, [C.c_void_p, C.POINTER(Prediction), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "tbdk_lk_dense": (C.c_int, [_P, C.POINTER(Pyr), C.POINTER(Pyr), _P, C.c_int, _P, C.c_int, C.POINTER(LkParams),
+                                _P]),
     "tbdk_farneback_default_params": (C.c_int, [C.POINTER(FarnebackParams)]),
     "tbdk_farneback_levels": (C.c_int, [C.c_int, C.c_int, C.POINTER(FarnebackParams), _PI, C.POINTER(C.c_int32)]),
     "tbdk_farneback": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.POINTER(FarnebackParams), _P]),

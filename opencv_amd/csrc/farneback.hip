@@ -315,6 +315,138 @@ __global__ __launch_bounds__(256) void fb_flow_up_kernel(FbFlowUpArgs a)
     }
 }
 
+// OPTFLOW_USE_INITIAL_FLOW: the coarsest level starts from
+// resize(flow0, INTER_AREA) *= scale (optflowgf.cpp:1151-1157), read from the
+// caller's interleaved CV_32FC2 flow and written to the planar level flow.
+// Modes follow cv::resize (imgproc/src/resize.cpp): same size -> copy (:3745);
+// integer factors -> resizeAreaFast_'s scalar loop for cn 2 (:2626-2640, sums
+// in unrolled groups of 4, then * 1.f/area); otherwise the computeResizeAreaTab
+// tables (:2853-2892), which each thread derives for its own cell in double, and
+// ResizeArea_Invoker's accumulation order (:2724-2813).  `*= scale` is
+// convertTo(alpha = scale, beta = 0), skipped when scale == 1.
+
+enum FbAreaMode { kAreaCopy = 0, kAreaFast = 1, kAreaTable = 2 };
+
+struct FbFlowAreaArgs {
+    const float* src;  // interleaved, spitch floats per row
+    int sw, sh, spitch;
+    float* dst;        // planar: dplane floats between the two components
+    int w, h, dpitch;
+    int64_t dplane;
+    int mode, isx, isy;
+    double scale_x, scale_y;
+    float alpha;
+    int apply_alpha;
+};
+
+// one output cell's source span: the entries (s1-1, a_first), (s, a_mid) for
+// s in [s1, s2), (s2, a_last) that computeResizeAreaTab emits for it
+struct AreaSpan {
+    int s1, s2;
+    float a_first, a_mid, a_last;
+    bool first, last;
+};
+
+__device__ __forceinline__ AreaSpan area_span(int d, double scale, int ss)
+{
+    AreaSpan r;
+    const double f1 = d * scale, f2 = f1 + scale;
+    const double cell = fmin(scale, ss - f1);
+    int s1 = (int)ceil(f1), s2 = (int)floor(f2);
+    s2 = min(s2, ss - 1);
+    s1 = min(s1, s2);
+    r.s1 = s1;
+    r.s2 = s2;
+    r.first = s1 - f1 > 1e-3;
+    r.a_first = (float)((s1 - f1) / cell);
+    r.a_mid = (float)(1.0 / cell);
+    r.last = f2 - s2 > 1e-3;
+    r.a_last = (float)(fmin(fmin(f2 - s2, 1.), cell) / cell);
+    return r;
+}
+
+// buf = sum over the x entries of S[si] * alpha, for both components
+__device__ __forceinline__ float2 area_row(const float* S, const AreaSpan& x)
+{
+    float2 b = make_float2(0.f, 0.f);
+    if (x.first) {
+        const float2 v = *reinterpret_cast<const float2*>(S + 2 * (x.s1 - 1));
+        b.x = b.x + v.x * x.a_first;
+        b.y = b.y + v.y * x.a_first;
+    }
+    for (int sx = x.s1; sx < x.s2; ++sx) {
+        const float2 v = *reinterpret_cast<const float2*>(S + 2 * sx);
+        b.x = b.x + v.x * x.a_mid;
+        b.y = b.y + v.y * x.a_mid;
+    }
+    if (x.last) {
+        const float2 v = *reinterpret_cast<const float2*>(S + 2 * x.s2);
+        b.x = b.x + v.x * x.a_last;
+        b.y = b.y + v.y * x.a_last;
+    }
+    return b;
+}
+
+__global__ __launch_bounds__(256) void fb_flow_area_kernel(FbFlowAreaArgs a)
+{
+    const int dx = blockIdx.x * 256 + threadIdx.x;
+    const int dy = blockIdx.y;
+    if (dx >= a.w) return;
+    float2 r;
+    if (a.mode == kAreaCopy) {
+        r = *reinterpret_cast<const float2*>(a.src + (size_t)dy * a.spitch + 2 * dx);
+    } else if (a.mode == kAreaFast) {
+        const float* S = a.src + (size_t)dy * a.isy * a.spitch + (size_t)2 * dx * a.isx;
+        const int area = a.isx * a.isy;
+        float sx_ = 0.f, sy_ = 0.f;
+        // k enumerates (sy, sx) row-major, as the reference's ofs[] table
+        int k = 0;
+        for (; k <= area - 4; k += 4) {
+            float2 v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int kk = k + t, yy = kk / a.isx, xx = kk - yy * a.isx;
+                v[t] = *reinterpret_cast<const float2*>(S + (size_t)yy * a.spitch + 2 * xx);
+            }
+            sx_ += ((v[0].x + v[1].x) + v[2].x) + v[3].x;
+            sy_ += ((v[0].y + v[1].y) + v[2].y) + v[3].y;
+        }
+        for (; k < area; ++k) {
+            const int yy = k / a.isx, xx = k - yy * a.isx;
+            const float2 v = *reinterpret_cast<const float2*>(S + (size_t)yy * a.spitch + 2 * xx);
+            sx_ += v.x;
+            sy_ += v.y;
+        }
+        const float sc = 1.f / area;
+        r = make_float2(sx_ * sc, sy_ * sc);
+    } else {
+        const AreaSpan x = area_span(dx, a.scale_x, a.sw);
+        const AreaSpan y = area_span(dy, a.scale_y, a.sh);
+        // sum over the y entries in table order; the row's first entry starts it
+        bool started = false;
+        r = make_float2(0.f, 0.f);
+        auto acc = [&](int sy, float beta) {
+            const float2 b = area_row(a.src + (size_t)sy * a.spitch, x);
+            if (!started) {
+                r = make_float2(beta * b.x, beta * b.y);
+                started = true;
+            } else {
+                r.x += beta * b.x;
+                r.y += beta * b.y;
+            }
+        };
+        if (y.first) acc(y.s1 - 1, y.a_first);
+        for (int sy = y.s1; sy < y.s2; ++sy) acc(sy, y.a_mid);
+        if (y.last) acc(y.s2, y.a_last);
+    }
+    if (a.apply_alpha) {
+        r.x = r.x * a.alpha + 0.0f;
+        r.y = r.y * a.alpha + 0.0f;
+    }
+    a.dst[(size_t)dy * a.dpitch + dx] = r.x;
+    a.dst[a.dplane + (size_t)dy * a.dpitch + dx] = r.y;
+}
+
 // planar -> interleaved CV_32FC2 (numIters == 0 at level 0)
 __global__ __launch_bounds__(256) void fb_interleave_kernel(const float* src, int w, int h, int spitch, int64_t splane,
                                                            float* dst, int dpitch)
@@ -953,7 +1085,6 @@ int fb_check(const tbdk_farneback_params* p)
     if (p->num_iters < 0) return TBDK_EINVAL;
     if (p->poly_n < 1 || p->poly_n > kFbMaxPolyN) return TBDK_EINVAL;
     if (p->flags & ~(TBDK_OPTFLOW_FARNEBACK_GAUSSIAN | TBDK_OPTFLOW_USE_INITIAL_FLOW)) return TBDK_EINVAL;
-    if (p->flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) return TBDK_EINVAL;  // not provided
     return TBDK_OK;
 }
 
@@ -1070,7 +1201,32 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
         if (e != hipSuccess) break;
         // initial flow of the level
         int rec = timing_begin(ctx, "fb_flow_init", s);
-        if (k == levels) {
+        if (k == levels && (p->flags & TBDK_OPTFLOW_USE_INITIAL_FLOW)) {
+            double scale = 1;
+            for (int i = 0; i < k; i++) scale *= p->pyr_scale;
+            FbFlowAreaArgs u;
+            u.src = flow;
+            u.sw = width;
+            u.sh = height;
+            u.spitch = flow_pitch / 4;
+            u.dst = f->F[cur];
+            u.w = w;
+            u.h = h;
+            u.dpitch = pp;
+            u.dplane = plane;
+            u.scale_x = 1. / ((double)w / width);
+            u.scale_y = 1. / ((double)h / height);
+            u.isx = cv_round(u.scale_x);
+            u.isy = cv_round(u.scale_y);
+            u.mode = (w == width && h == height) ? kAreaCopy
+                     : (std::fabs(u.scale_x - u.isx) < DBL_EPSILON && std::fabs(u.scale_y - u.isy) < DBL_EPSILON)
+                         ? kAreaFast
+                         : kAreaTable;
+            u.alpha = (float)scale;
+            u.apply_alpha = !(std::fabs(scale - 1) < DBL_EPSILON);
+            hipLaunchKernelGGL(fb_flow_area_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, u);
+            e = hipGetLastError();
+        } else if (k == levels) {
             e = hipMemsetAsync(f->F[cur], 0, sizeof(float) * (size_t)plane * 2, s);
         } else {
             FbFlowUpArgs u;

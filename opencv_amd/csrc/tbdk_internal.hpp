@@ -70,6 +70,8 @@ struct tbdk_ctx {
     int gftt_cap_rois = 0;
     int64_t gftt_cap_px = 0;
     tbdk::FbScratch* fb = nullptr;  // dense Farneback planes (farneback.hip)
+    void* dense_buf = nullptr;      // dense PyrLK grid / next points / status (klt_dense.hip)
+    int64_t dense_cap = 0;          // pixels
 };
 
 namespace tbdk {

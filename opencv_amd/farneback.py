@@ -71,6 +71,9 @@ class FarnebackOpticalFlow:
         if I0.stride(1) != 1 or I1.stride(1) != 1 or I0.stride(0) != I1.stride(0):
             raise _lib.TbdkError("FarnebackOpticalFlow.calc: frames need unit column stride and a common pitch")
         h, w = I0.shape
+        if flow is None and self.p.flags & OPTFLOW_USE_INITIAL_FLOW:
+            # CV_Assert(_flow0.size() == prev0.size() && ...) (optflowgf.cpp:1117-1119)
+            raise _lib.TbdkError("FarnebackOpticalFlow.calc: OPTFLOW_USE_INITIAL_FLOW needs the initial flow")
         if flow is None:
             flow = torch.empty((h, w, 2), dtype=torch.float32, device=I0.device)
         if flow.shape != (h, w, 2) or flow.dtype != torch.float32 or not flow.is_contiguous():

@@ -324,6 +324,36 @@ class SparsePyrLKOpticalFlow:
         return LkResult(out, status, err, iters)
 
 
+class DensePyrLKOpticalFlow(SparsePyrLKOpticalFlow):
+    """cv::cuda::DensePyrLKOpticalFlow (cudaoptflow.hpp:182-208; impl
+    cudaoptflow/src/pyrlk.cpp:238-299): create(winSize=(13,13), maxLevel=3,
+    iters=30, useInitialFlow=False); calc(I0, I1) -> (H, W, 2) float32 flow.
+    Numerics: the CPU calcOpticalFlowPyrLK at every pixel (tbdk_lk_dense)."""
+
+    def __init__(self, winSize=(13, 13), maxLevel: int = 3, iters: int = 30, useInitialFlow: bool = False, **kw):
+        super().__init__(winSize, maxLevel, iters, useInitialFlow, **kw)
+
+    @staticmethod
+    def create(winSize=(13, 13), maxLevel: int = 3, iters: int = 30, useInitialFlow: bool = False, **kw):
+        return DensePyrLKOpticalFlow(winSize, maxLevel, iters, useInitialFlow, **kw)
+
+    def calc(self, prevImg, nextImg, flow: torch.Tensor | None = None, want_status: bool = False, stream=None):
+        P, N = self._as_pyr(prevImg), self._as_pyr(nextImg)
+        w, h = P.pyr.lv[0].width, P.pyr.lv[0].height
+        dev = torch.device("cuda", self.ctx.device)
+        if flow is None:
+            flow = torch.empty((h, w, 2), dtype=torch.float32, device=dev)
+        if flow.shape != (h, w, 2) or flow.dtype != torch.float32 or not flow.is_contiguous():
+            raise _lib.TbdkError("DensePyrLKOpticalFlow.calc: flow must be a contiguous (H, W, 2) float32 tensor")
+        status = torch.empty((h, w), dtype=torch.uint8, device=dev) if want_status else None
+        prm = self.params()
+        _lib.check(self.ctx.lib.tbdk_lk_dense(
+            self.ctx.handle, C.byref(P.pyr), C.byref(N.pyr), C.c_void_p(flow.data_ptr()), 8 * w,
+            C.c_void_p(status.data_ptr()) if status is not None else None, w, C.byref(prm), _stream_ptr(stream)),
+            "tbdk_lk_dense")
+        return (flow, status) if want_status else flow
+
+
 class GoodFeaturesToTrackDetector:
     """cv::cuda::createGoodFeaturesToTrackDetector(CV_8UC1, maxCorners, qualityLevel,
     minDistance, blockSize=3) (cudaimgproc.hpp:603-604) with the CPU

@@ -186,6 +186,118 @@ void orc_fb_resize_linear(const float* src, int sw, int sh, int cn, float* dst, 
     free(alpha);
 }
 
+/* resize(src, dst, Size(dw, dh), 0, 0, INTER_AREA) for a float image of cn
+ * channels, downscaling only (imgproc/src/resize.cpp):
+ *   same size          -> copy (cv::resize, :3745-3750)
+ *   integer factors    -> resizeAreaFast_ (:3530-3553, invoker :2600-2666): the
+ *                         SIMD hook only serves cn 1/4 at 2x2 (:2476), so cn 2 takes
+ *                         the scalar loop, summed in unrolled groups of 4
+ *                         (sum += ((a+b)+c)+d) then * (1.f/area).  The partial-cell
+ *                         branch cannot run: an integer factor means dw*isx == sw.
+ *   otherwise          -> computeResizeAreaTab (:2853-2892) + ResizeArea_Invoker
+ *                         (:2710-2814): per source row, buf += S*alpha over the x
+ *                         table; per output row, sum of beta*buf in table order.
+ * inv_sx/inv_sy are cv::resize's inv_scale (dsize/ssize, or fx/fy when dsize is
+ * empty). */
+void orc_fb_resize_area_fx(const float* src, int sw, int sh, int cn, float* dst, int dw, int dh, double inv_sx,
+                           double inv_sy)
+{
+    if (dw == sw && dh == sh) {
+        if (dst != src) memcpy(dst, src, sizeof(float) * (size_t)sw * sh * cn);
+        return;
+    }
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    const int isx = (int)lrint(scale_x), isy = (int)lrint(scale_y);
+    if (fabs(scale_x - isx) < DBL_EPSILON && fabs(scale_y - isy) < DBL_EPSILON) {
+        const int area = isx * isy;
+        const float sc = 1.f / area;
+        int* ofs = malloc(sizeof(int) * (size_t)area);
+        for (int sy = 0, k = 0; sy < isy; sy++)
+            for (int sx = 0; sx < isx; sx++) ofs[k++] = sy * sw * cn + sx * cn;
+        for (int dy = 0; dy < dh; dy++)
+            for (int dx = 0; dx < dw * cn; dx++) {
+                const float* S = src + (size_t)dy * isy * sw * cn + (dx / cn) * isx * cn + dx % cn;
+                float sum = 0;
+                int k = 0;
+                for (; k <= area - 4; k += 4) sum += S[ofs[k]] + S[ofs[k + 1]] + S[ofs[k + 2]] + S[ofs[k + 3]];
+                for (; k < area; k++) sum += S[ofs[k]];
+                dst[(size_t)dy * dw * cn + dx] = sum * sc;
+            }
+        free(ofs);
+        return;
+    }
+    /* tables: (si, di, alpha) triples in the reference's order */
+    int* xsi = malloc(sizeof(int) * 2 * (size_t)sw);
+    int* xdi = malloc(sizeof(int) * 2 * (size_t)sw);
+    float* xal = malloc(sizeof(float) * 2 * (size_t)sw);
+    int* ysi = malloc(sizeof(int) * 2 * (size_t)sh);
+    int* ydi = malloc(sizeof(int) * 2 * (size_t)sh);
+    float* yal = malloc(sizeof(float) * 2 * (size_t)sh);
+    int nt[2];
+    for (int t = 0; t < 2; t++) {
+        const int ss = t ? sh : sw, ds = t ? dh : dw, c = t ? 1 : cn;
+        const double scale = t ? scale_y : scale_x;
+        int *si = t ? ysi : xsi, *di = t ? ydi : xdi;
+        float* al = t ? yal : xal;
+        int k = 0;
+        for (int d = 0; d < ds; d++) {
+            const double f1 = d * scale, f2 = f1 + scale;
+            const double cell = scale < ss - f1 ? scale : ss - f1;
+            int s1 = (int)ceil(f1), s2 = (int)floor(f2);
+            s2 = s2 < ss - 1 ? s2 : ss - 1;
+            s1 = s1 < s2 ? s1 : s2;
+            if (s1 - f1 > 1e-3) {
+                di[k] = d * c, si[k] = (s1 - 1) * c, al[k++] = (float)((s1 - f1) / cell);
+            }
+            for (int x = s1; x < s2; x++) di[k] = d * c, si[k] = x * c, al[k++] = (float)(1.0 / cell);
+            if (f2 - s2 > 1e-3) {
+                double r = f2 - s2 < 1. ? f2 - s2 : 1.;
+                r = r < cell ? r : cell;
+                di[k] = d * c, si[k] = s2 * c, al[k++] = (float)(r / cell);
+            }
+        }
+        nt[t] = k;
+    }
+    const int W = dw * cn;
+    float* buf = malloc(sizeof(float) * (size_t)W);
+    float* sum = malloc(sizeof(float) * (size_t)W);
+    for (int x = 0; x < W; x++) sum[x] = 0;
+    int prev_dy = ydi[0];
+    for (int j = 0; j < nt[1]; j++) {
+        const float beta = yal[j];
+        const int dy = ydi[j];
+        const float* S = src + (size_t)ysi[j] * sw * cn;
+        for (int x = 0; x < W; x++) buf[x] = 0;
+        for (int k = 0; k < nt[0]; k++)
+            for (int c = 0; c < cn; c++) buf[xdi[k] + c] = buf[xdi[k] + c] + S[xsi[k] + c] * xal[k];
+        if (dy != prev_dy) {
+            float* D = dst + (size_t)prev_dy * W;
+            for (int x = 0; x < W; x++) {
+                D[x] = sum[x];
+                sum[x] = beta * buf[x];
+            }
+            prev_dy = dy;
+        } else {
+            for (int x = 0; x < W; x++) sum[x] += beta * buf[x];
+        }
+    }
+    memcpy(dst + (size_t)prev_dy * W, sum, sizeof(float) * (size_t)W);
+    free(buf);
+    free(sum);
+    free(xsi);
+    free(xdi);
+    free(xal);
+    free(ysi);
+    free(ydi);
+    free(yal);
+}
+
+/* resize with an explicit dsize: inv_scale = dsize / ssize (cv::resize) */
+void orc_fb_resize_area(const float* src, int sw, int sh, int cn, float* dst, int dw, int dh)
+{
+    orc_fb_resize_area_fx(src, sw, sh, cn, dst, dw, dh, (double)dw / sw, (double)dh / sh);
+}
+
 /* FarnebackPrepareGaussian: g, xg, xxg (length 2n+1, centred) and ig11/03/33/55 */
 void orc_fb_prepare_gaussian(int n, double sigma, float* g_, float* xg_, float* xxg_, double* ig)
 {
@@ -542,13 +654,15 @@ void orc_fb_update_flow_gauss(const float* R0, const float* R1, float* flow, flo
 
 static int cv_round(double v) { return (int)lrint(v); }
 
-/* FarnebackOpticalFlowImpl::calc (without OPTFLOW_USE_INITIAL_FLOW).
- * prev/next: u8 (pitch bytes); flow: w*h*2 floats (output). */
+/* FarnebackOpticalFlowImpl::calc.  prev/next: u8 (pitch bytes); flow0: w*h*2
+ * floats, the output, and with FB_USE_INITIAL_FLOW also the input: the coarsest
+ * level starts from resize(flow0, INTER_AREA) *= scale (optflowgf.cpp:1151-1160;
+ * `*=` is convertTo(flow, -1, scale), a plain copy when scale == 1). */
 int orc_fb_calc_mode(const uint8_t* prev, const uint8_t* next, int W, int H, int pitch, float* flow0, int num_levels,
                      double pyr_scale, int win_size, int num_iters, int poly_n, double poly_sigma, int flags,
                      int box_direct)
 {
-    if (pyr_scale >= 1 || (flags & FB_USE_INITIAL_FLOW)) return -1;
+    if (pyr_scale >= 1) return -1;
     const int min_size = 32;
     int k;
     double scale = 1;
@@ -569,7 +683,13 @@ int orc_fb_calc_mode(const uint8_t* prev, const uint8_t* next, int W, int H, int
         if (smooth_sz < 3) smooth_sz = 3;
         const int width = cv_round(W * scale), height = cv_round(H * scale);
         float* flow = k > 0 ? malloc(sizeof(float) * 2 * (size_t)width * height) : flow0;
-        if (!prevFlow) {
+        if (!prevFlow && (flags & FB_USE_INITIAL_FLOW)) {
+            orc_fb_resize_area(flow0, W, H, 2, flow, width, height);
+            if (!(fabs(scale - 1) < DBL_EPSILON)) {
+                const float a = (float)scale;
+                for (size_t i = 0; i < (size_t)width * height * 2; i++) flow[i] = flow[i] * a + 0.0f;
+            }
+        } else if (!prevFlow) {
             memset(flow, 0, sizeof(float) * 2 * (size_t)width * height);
         } else {
             orc_fb_resize_linear(prevFlow, pw, ph, 2, flow, width, height);

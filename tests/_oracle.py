@@ -111,7 +111,9 @@ def scharr(img: np.ndarray) -> np.ndarray:
 
 
 def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01, flags=0,
-       min_eig=1e-4, accum=ACCUM_SSE2, nthreads=8, init: np.ndarray | None = None):
+       min_eig=1e-4, accum=ACCUM_SSE2, nthreads=8, init: np.ndarray | None = None, want_err: bool = True):
+    """calcOpticalFlowPyrLK; want_err=False passes err = noArray(), which also
+    skips the level-0 error pass and its bounds check (lkpyramid.cpp:654-693)."""
     lib = load()
     pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 2)
     n = pts.shape[0]
@@ -121,8 +123,8 @@ def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, 
     iters = np.zeros(n, dtype=np.int32)
     prm = LkParams(win[0], win[1], max_level, max_count, eps, flags, min_eig, accum, nthreads)
     if n:
-        lib.orc_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status), _ptr(err), n,
-                   C.byref(prm), _ptr(iters))
+        lib.orc_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status),
+                   _ptr(err) if want_err else None, n, C.byref(prm), _ptr(iters))
     return nxt_pts, status, err, iters
 
 
@@ -268,6 +270,7 @@ def invert_affine(M) -> np.ndarray:
 
 # ---- dense Farneback (oracle/farneback_oracle.c) ----
 FARNEBACK_GAUSSIAN = 256
+OPTFLOW_USE_INITIAL_FLOW = 4
 
 
 def _fb_lib():
@@ -281,7 +284,23 @@ def _fb_lib():
     lib.orc_fb_resize_linear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
     lib.orc_fb_poly_exp.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_void_p]
     lib.orc_fb_gaussian_kernel.argtypes = [C.c_int, C.c_double, C.c_void_p]
+    lib.orc_fb_resize_area_fx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                          C.c_double, C.c_double]
     return lib
+
+
+def resize_area(src: np.ndarray, size, inv_scale=None) -> np.ndarray:
+    """resize(src, size, INTER_AREA) of a float (H, W) or (H, W, cn) image;
+    inv_scale=(fx, fy) when the reference call passes fx/fy instead of a size."""
+    lib = _fb_lib()
+    s = np.ascontiguousarray(src, dtype=np.float32)
+    h, w = s.shape[:2]
+    cn = 1 if s.ndim == 2 else s.shape[2]
+    dw, dh = size
+    fx, fy = inv_scale if inv_scale is not None else (dw / w, dh / h)
+    out = np.empty((dh, dw) + s.shape[2:], np.float32)
+    lib.orc_fb_resize_area_fx(_ptr(s), w, h, cn, _ptr(out), dw, dh, float(fx), float(fy))
+    return out
 
 
 def fb_level_image(img: np.ndarray, size, smooth_size: int, sigma: float) -> np.ndarray:
@@ -317,14 +336,14 @@ def gaussian_kernel(n: int, sigma: float) -> np.ndarray:
 
 
 def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.5, levels=5, winsize=13, iterations=10, poly_n=5,
-              poly_sigma=1.1, flags=0, box_direct=False) -> np.ndarray:
+              poly_sigma=1.1, flags=0, box_direct=False, init_flow: np.ndarray | None = None) -> np.ndarray:
     """cv::calcOpticalFlowFarneback -> (H, W, 2) float32.  box_direct: exact-order
     box window sums (the GPU's order) instead of the reference's running sums."""
     lib = _fb_lib()
     a = np.ascontiguousarray(prev, dtype=np.uint8)
     b = np.ascontiguousarray(nxt, dtype=np.uint8)
     h, w = a.shape
-    flow = np.zeros((h, w, 2), np.float32)
+    flow = np.zeros((h, w, 2), np.float32) if init_flow is None else np.ascontiguousarray(init_flow, np.float32).copy()
     rc = lib.orc_fb_calc_mode(_ptr(a), _ptr(b), w, h, a.strides[0], _ptr(flow), int(levels), float(pyr_scale),
                               int(winsize), int(iterations), int(poly_n), float(poly_sigma), int(flags),
                               int(bool(box_direct)))

@@ -67,7 +67,19 @@ int main(int argc, char** argv)
                 near += std::abs(f[0] - 1.5f) < 0.25f && std::abs(f[1] + 0.5f) < 0.25f;
             }
         std::printf("farneback interior near-shift %d / %d\n", near, tot);
-        return near * 10 >= tot * 8 ? 0 : 8;
+        if (near * 10 < tot * 8) return 8;
+        // dense PyrLK through the facade
+        auto dlk = tbdk::cuda::DensePyrLKOpticalFlow::create(ctx);
+        dlk->calc(a, b, flow, W * 8);
+        (void)hipMemcpy(fl.data(), flow, fl.size() * 4, hipMemcpyDeviceToHost);
+        near = 0;
+        for (int y = 40; y < H - 40; ++y)
+            for (int x = 40; x < W - 40; ++x) {
+                const float* f = &fl[((size_t)y * W + x) * 2];
+                near += std::abs(f[0] - 1.5f) < 0.25f && std::abs(f[1] + 0.5f) < 0.25f;
+            }
+        std::printf("dense pyrlk interior near-shift %d / %d\n", near, tot);
+        return near * 10 >= tot * 6 ? 0 : 9;
     } catch (const tbdk::Error& e) {
         std::printf("tbdk::Error: %s\n", e.what());
         return (!want_gpu && e.code() == TBDK_ENODEV) ? 0 : 7;

@@ -101,3 +101,77 @@ def test_direct_order_box_sums_vs_running_sums(pyr_scale, poly_n, winsize):
     g0 = O.farneback(fr[0], fr[1], flags=O.FARNEBACK_GAUSSIAN, **kw)
     g1 = O.farneback(fr[0], fr[1], flags=O.FARNEBACK_GAUSSIAN, box_direct=True, **kw)
     assert np.array_equal(g0, g1)
+
+
+# ---- INTER_AREA resize (the USE_INITIAL_FLOW input of the coarsest level) ----
+
+def test_resize_area_matches_reference_known_answer():
+    """Imgproc_resize_area.regression (imgproc/test/test_imgwarp.cpp:1536-1571):
+    16x16 CV_16UC1 at fx = fy = 0.3 through the table path (ResizeArea_Invoker
+    with a float accumulator; ushort -> float is exact, saturate_cast rounds)."""
+    import json
+    import os
+
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "resize_area_regression.json")))
+    src = np.float32(g["input"]).reshape(16, 16)
+    out = np.rint(O.resize_area(src, (5, 5), inv_scale=(0.3, 0.3)))
+    exp = np.float32(g["expected"]).reshape(5, 5)
+    assert np.abs(out - exp).max() <= 1.0  # the reference test's tolerance
+    assert np.array_equal(out, exp)
+
+
+def test_resize_area_half_matches_reference_formula():
+    """Resize.Area_half (test_imgwarp.cpp:1671-1709) for float: within 7e-5 of
+    ((a+b) + (c+d)) * 0.25 on values in [-1000, 1000]; here with 2 channels."""
+    rng = np.random.default_rng(17)
+    src = rng.uniform(-1000, 1000, (100, 100, 2)).astype(np.float32)
+    out = O.resize_area(src, (50, 50))
+    s = src.astype(np.float32)
+    ref = ((s[0::2, 0::2] + s[0::2, 1::2]) + (s[1::2, 0::2] + s[1::2, 1::2])) * np.float32(0.25)
+    assert np.abs(out - ref).max() <= 7e-5
+
+
+@pytest.mark.parametrize("size", [(17, 13), (40, 30), (7, 5)])
+def test_resize_area_general_is_the_cell_average(size):
+    """The table path averages each output cell over the fractional source area:
+    each source pixel [s, s+1) weighs its overlap with the cell [d*scale,
+    (d+1)*scale) (computed here in double, independently of the tables), and a
+    constant image stays constant."""
+    h, w = 60, 80
+    dw, dh = size
+    rng = np.random.default_rng(dw)
+    img = rng.uniform(0, 255, (h, w)).astype(np.float32)
+    out = O.resize_area(img, (dw, dh))
+
+    def weights(ss, ds):
+        sc = ss / ds
+        W = np.zeros((ds, ss))
+        for d in range(ds):
+            lo, hi = d * sc, min((d + 1) * sc, ss)
+            for s_ in range(int(np.floor(lo)), int(np.ceil(hi))):
+                W[d, s_] = max(0.0, min(hi, s_ + 1) - max(lo, s_))
+            W[d] /= W[d].sum()
+        return W
+
+    ref = weights(h, dh) @ img.astype(np.float64) @ weights(w, dw).T
+    assert np.allclose(out, ref, atol=2e-3)
+    const = np.full((h, w, 2), 1.75, np.float32)
+    assert np.allclose(O.resize_area(const, (dw, dh)), 1.75, atol=1e-5)
+
+
+def test_farneback_initial_flow_is_used_and_exact_at_one_level():
+    """OPTFLOW_USE_INITIAL_FLOW: with 0 iterations and one level the output is
+    the input flow (resize to the same size is a copy, *= 1 a no-op); with several
+    levels and 0 iterations it is the area-downscaled, rescaled, then linearly
+    upscaled input; iterating from the true motion keeps it."""
+    rng = np.random.default_rng(3)
+    h, w = 64, 96
+    a = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    init = rng.uniform(-2, 2, (h, w, 2)).astype(np.float32)
+    out = O.farneback(a, a, levels=0, iterations=0, flags=O.OPTFLOW_USE_INITIAL_FLOW, init_flow=init)
+    assert np.array_equal(out, init)
+    zero = O.farneback(a, a, levels=0, iterations=0, flags=0, init_flow=init)
+    assert not zero.any()
+    const = np.full((h, w, 2), 0.5, np.float32)
+    out = O.farneback(a, a, levels=1, iterations=0, flags=O.OPTFLOW_USE_INITIAL_FLOW, init_flow=const)
+    assert np.allclose(out, 0.5, atol=1e-6)  # 0.5 -> area -> *0.5 -> linear up -> *2

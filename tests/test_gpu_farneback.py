@@ -22,12 +22,12 @@ def _frames(seed, w, h, shift=(2.5, -1.25), nobj=6):
     return fr[0], fr[1]
 
 
-def _gpu_flow(gpu, a, b, **kw):
+def _gpu_flow(gpu, a, b, init=None, **kw):
     from opencv_amd import farneback as F
 
     ta, tb = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
     fb = F.FarnebackOpticalFlow.create(ctx=gpu, **kw)
-    out = fb.calc(ta, tb)
+    out = fb.calc(ta, tb, None if init is None else torch.from_numpy(init.copy()).cuda())
     torch.cuda.synchronize()
     return out.cpu().numpy()
 
@@ -135,6 +135,44 @@ def test_1080p_translation(gpu):
     got = _gpu_flow(gpu, a, b)
     inner = got[40:-40, 40:-40]
     assert abs(np.median(inner[..., 0]) - 5) < 0.01 and abs(np.median(inner[..., 1]) + 3) < 0.01
+    assert np.mean(np.abs(inner - np.float32([5, -3])).max(axis=2) < 0.1) > 0.95
+
+
+@pytest.mark.parametrize("w,h,pyr_scale,levels", [
+    (320, 240, 0.5, 5),    # coarsest 80x60: integer factor 4 (resizeAreaFast_, area 16)
+    (96, 64, 0.5, 5),      # coarsest 48x32: factor 2 (area 4)
+    (320, 240, 0.3, 5),    # fractional factors: the computeResizeAreaTab path
+    (1242, 375, 0.5, 5),   # 1242 -> 310 after a .5 rounding: the table path in x
+    (130, 70, 0.5, 0),     # one level: copy, *= 1 skipped
+])
+@pytest.mark.parametrize("iters", [0, 10])
+def test_use_initial_flow_bit_exact(gpu, w, h, pyr_scale, levels, iters):
+    """OPTFLOW_USE_INITIAL_FLOW (optflowgf.cpp:1151-1157): the coarsest level
+    starts from resize(flow0, INTER_AREA) * scale.  Gaussian variant against the
+    reference order, box variant against the exact-order mode."""
+    a, b = _frames(w * 7 + h, w, h, nobj=3)
+    rng = np.random.default_rng(w + levels)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    init = np.stack([2.5 + 0.01 * xx, -1.25 - 0.005 * yy], 2) + rng.uniform(-0.5, 0.5, (h, w, 2))
+    init = init.astype(np.float32)
+    for flags, direct in ((O.FARNEBACK_GAUSSIAN, False), (0, True)):
+        f = flags | O.OPTFLOW_USE_INITIAL_FLOW
+        ref = O.farneback(a, b, pyr_scale=pyr_scale, levels=levels, iterations=iters, flags=f, box_direct=direct,
+                          init_flow=init)
+        got = _gpu_flow(gpu, a, b, init=init, numLevels=levels, pyrScale=pyr_scale, numIters=iters, flags=f)
+        assert np.array_equal(got, ref), (flags, np.abs(got - ref).max())
+
+
+def test_use_initial_flow_converges_from_the_true_motion(gpu):
+    """Seeded with the true shift, one level and a few iterations keep it."""
+    fr, _ = O.synth(77, 640, 480, 12, 0, 1)
+    a = fr[0]
+    b = np.roll(a, (-3, 5), axis=(0, 1))
+    init = np.broadcast_to(np.float32([5, -3]), (480, 640, 2))
+    from opencv_amd import farneback as F
+
+    got = _gpu_flow(gpu, a, b, init=init, numLevels=0, numIters=3, flags=F.OPTFLOW_USE_INITIAL_FLOW)
+    inner = got[40:-40, 40:-40]
     assert np.mean(np.abs(inner - np.float32([5, -3])).max(axis=2) < 0.1) > 0.95
 
 
