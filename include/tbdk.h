@@ -300,6 +300,66 @@ int tbdk_fb_level_image(tbdk_ctx* ctx, const uint8_t* img, int width, int height
 int tbdk_fb_poly_exp(tbdk_ctx* ctx, const float* src, int width, int height, int src_pitch, int poly_n,
                      double poly_sigma, float* dst, int dst_pitch, void* stream);
 
+/* ---- HOG people detector (cv::cuda::HOG / cv::HOGDescriptor) -------------- */
+
+/* cv::cuda::HOG::create(win_size, block_size, block_stride, cell_size, nbins) and
+ * its setters (cudaobjdetect/include/opencv2/cudaobjdetect.hpp:95-180, defaults of
+ * cudaobjdetect/src/hog.cpp:230-250), computed with the CPU HOGDescriptor's
+ * numerics (objdetect/src/hog.cpp) that the sample's CPU mode runs. */
+typedef struct tbdk_hog_params {
+    int32_t win_w, win_h;                   /* 64 x 128 (48 x 96: the Daimler detector) */
+    int32_t block_w, block_h;               /* 16 x 16 */
+    int32_t block_stride_x, block_stride_y; /* 8, 8 */
+    int32_t cell_w, cell_h;                 /* 8, 8 */
+    int32_t nbins;                          /* 9 (1..32) */
+    double win_sigma;                       /* -1: (block_w + block_h) / 8 */
+    double l2hys_threshold;                 /* 0.2 */
+    int32_t gamma_correction;               /* 1 */
+    int32_t signed_gradient;                /* 0 */
+    int32_t nlevels;                        /* 64 */
+    double hit_threshold;                   /* 0 */
+    int32_t win_stride_x, win_stride_y;     /* 8, 8 (= block stride) */
+    double scale0;                          /* 1.05 */
+    int32_t group_threshold;                /* 2 */
+} tbdk_hog_params;
+
+int tbdk_hog_default_params(tbdk_hog_params* p);
+/* descriptor length nbins * cells/block * blocks/window (HOGDescriptor::getDescriptorSize,
+ * hog.cpp:87-99); an SVM detector has this many coefficients, or one more (the bias) */
+int tbdk_hog_descriptor_size(const tbdk_hog_params* p, int* size);
+
+/* Replaces cv::cuda::HOG::detectMultiScale(img, found_locations, confidences)
+ * (cudaobjdetect/src/hog.cpp:415-470) with HOGDescriptor::detectMultiScale(img,
+ * rects, weights, hit_threshold, win_stride, Size(), scale0, group_threshold)
+ * (objdetect/src/hog.cpp:2051-2105), the CPU call of samples/gpu/tbd.cpp:603-605.
+ *   img     : device u8 image, cn 1 (gray), 3 (BGR) or 4 (BGRA, alpha ignored)
+ *   svm     : host float coefficients, svm_len = descriptor size (+ 1 bias)
+ *   rects   : host int32 (x, y, w, h) x max_rects; weights: host double x max_rects
+ *   nrects  : number of grouped, clipped detections (<= max_rects)
+ * Synchronous: returns when the results are in the host buffers. */
+int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                               const tbdk_hog_params* params, const float* svm, int svm_len, int32_t* rects,
+                               double* weights, int max_rects, int* nrects, void* stream);
+/* One level, no resize and no grouping (HOGDescriptor::detect, hog.cpp:1655-1767):
+ * window corners (x, y) and scores in window order; synchronous. */
+int tbdk_hog_detect(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                    const tbdk_hog_params* params, const float* svm, int svm_len, int32_t* xy, double* scores,
+                    int max_hits, int* nhits, void* stream);
+/* Stage entry points (parity tests).  resize(src, dst, (dw, dh), INTER_LINEAR_EXACT)
+ * of a u8 image (imgproc/src/resize.cpp:732-891): */
+int tbdk_hog_resize(tbdk_ctx* ctx, const uint8_t* src, int width, int height, int pitch, int cn, uint8_t* dst,
+                    int dst_width, int dst_height, int dst_pitch, void* stream);
+/* HOGDescriptor::computeGradient (hog.cpp:239-550): grad = 2 floats per pixel
+ * (grad_pitch bytes per row), qangle = 2 bytes per pixel (qangle_pitch). */
+int tbdk_hog_gradient(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                      const tbdk_hog_params* params, float* grad, int grad_pitch, uint8_t* qangle,
+                      int qangle_pitch, void* stream);
+/* normalized block histograms (HOGCache::getBlock + normalizeBlockHistogram,
+ * hog.cpp:860-1248) at every block position of the gcd(win stride, block stride)
+ * grid: blocks[(by * nbx + bx) * hist_size + k], hist_size = nbins * cells/block. */
+int tbdk_hog_blocks(tbdk_ctx* ctx, const float* grad, int grad_pitch, const uint8_t* qangle, int qangle_pitch,
+                    int width, int height, const tbdk_hog_params* params, float* blocks, void* stream);
+
 /* ---- tracking-by-detection loop (one video stream per context) ------------ */
 
 /* Per-stream TBD loop: pyramid -> (GFTT on new / re-detect tracks) -> PyrLK over

@@ -158,6 +158,15 @@ class FarnebackParams(C.Structure):
 
 OPTFLOW_FARNEBACK_GAUSSIAN = 256
 
+
+class HogParams(C.Structure):
+    _fields_ = [("win_w", C.c_int32), ("win_h", C.c_int32), ("block_w", C.c_int32), ("block_h", C.c_int32),
+                ("block_stride_x", C.c_int32), ("block_stride_y", C.c_int32), ("cell_w", C.c_int32),
+                ("cell_h", C.c_int32), ("nbins", C.c_int32), ("win_sigma", C.c_double),
+                ("l2hys_threshold", C.c_double), ("gamma_correction", C.c_int32), ("signed_gradient", C.c_int32),
+                ("nlevels", C.c_int32), ("hit_threshold", C.c_double), ("win_stride_x", C.c_int32),
+                ("win_stride_y", C.c_int32), ("scale0", C.c_double), ("group_threshold", C.c_int32)]
+
 _P = C.c_void_p
 _PI = C.POINTER(C.c_int)
 
@@ -245,6 +254,16 @@ SIGNATURES = {
                                 _P]),
     "tbdk_farneback_default_params": (C.c_int, [C.POINTER(FarnebackParams)]),
     "tbdk_farneback_levels": (C.c_int, [C.c_int, C.c_int, C.POINTER(FarnebackParams), _PI, C.POINTER(C.c_int32)]),
+    "tbdk_hog_default_params": (C.c_int, [C.POINTER(HogParams)]),
+    "tbdk_hog_descriptor_size": (C.c_int, [C.POINTER(HogParams), _PI]),
+    "tbdk_hog_detect_multiscale": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(HogParams), _P,
+                                             C.c_int, _P, _P, C.c_int, _PI, _P]),
+    "tbdk_hog_detect": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(HogParams), _P, C.c_int, _P,
+                                  _P, C.c_int, _PI, _P]),
+    "tbdk_hog_resize": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P]),
+    "tbdk_hog_gradient": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(HogParams), _P, C.c_int,
+                                    _P, C.c_int, _P]),
+    "tbdk_hog_blocks": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.POINTER(HogParams), _P, _P]),
     "tbdk_farneback": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.POINTER(FarnebackParams), _P]),
     "tbdk_fb_level_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, _P,
                                       C.c_int, _P]),

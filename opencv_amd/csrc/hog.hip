@@ -1,0 +1,953 @@
+// hog.hip — HOG people detector: the sample's detection step,
+// cv::cuda::HOG::detectMultiScale (cudaobjdetect/src/hog.cpp), computed with the
+// CPU cv::HOGDescriptor's numerics (objdetect/src/hog.cpp) so that the results
+// equal the CPU detector's.  Per pyramid level:
+//
+//   hog_resize   resize INTER_LINEAR_EXACT (8.8 fixed point, resize.cpp:732-891)
+//   hog_grad     computeGradient: gamma LUT, REFLECT_101, the 3-channel pick,
+//                magnitude / fastAtan (AVX2 dispatch form), bin split (hog.cpp:239-550)
+//   hog_block    one thread per (block, cell): that cell's histogram summed in the
+//                reference's pixData order; the block's L2-Hys normalization in
+//                its 4-lane order via LDS (hog.cpp:860-1248)
+//   hog_window   one thread per window: the SVM dot product in the 4-lane float
+//                order, block by block into a double (hog.cpp:1694-1766); hits are
+//                appended with an atomic counter
+//
+// The host then sorts the hits into window order, scales them to rects, and
+// groups and clips them (groupRectangles, hog.cpp:3783-3861; clipObjects).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "tbdk_internal.hpp"
+
+namespace tbdk {
+
+constexpr int kHogMaxBins = 32;
+constexpr int kHogMaxCells = 16;
+constexpr int kHogMaxLevels = 256;
+
+struct HogScratch {
+    uint8_t* level = nullptr;  // resized level image (u8, cn)
+    float* grad = nullptr;     // 2 floats per pixel
+    uint8_t* qangle = nullptr; // 2 bytes per pixel
+    float* blocks = nullptr;
+    float* svm = nullptr;
+    int4* cells = nullptr;     // per-cell pixel lists: (di, dj, weight bits, 0)
+    int* hits = nullptr;       // [0] count, then (level, x, y) int triples
+    double* scores = nullptr;
+    int64_t cap_px = 0, cap_blocks = 0, cap_svm = 0, cap_cells = 0, cap_hits = 0;
+};
+
+__device__ __forceinline__ int hog_reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// resize INTER_LINEAR_EXACT (u8): interpolationLinear::getCoeffs (resize.cpp:737-761)
+// per output coordinate; ufixedpoint16 horizontal, ufixedpoint32 vertical.
+
+struct ExactCoef {
+    int ofs, c0, c1;
+    int mode;  // 0 inside, 1 left/top (value of 0), 2 right/bottom (value of size - 1)
+};
+
+__device__ __forceinline__ ExactCoef exact_coef(int d, double scale, int ssize)
+{
+    ExactCoef r;
+    const double f = scale * ((double)d + 0.5) - 0.5;
+    const int iv = (int)floor(f);
+    r.ofs = 0, r.c0 = 256, r.c1 = 0, r.mode = 1;
+    if (iv >= 0 && ssize > 1) {
+        if (iv < ssize - 1) {
+            r.mode = 0;
+            r.ofs = iv;
+            r.c1 = (int)rint((f - iv) * 256.0);
+            r.c0 = 256 - r.c1;
+        } else {
+            r.mode = 2;
+        }
+    }
+    return r;
+}
+
+// the reference clamps each side at the first/last index whose interpolation
+// leaves the image (minofst/maxofst), then uses the edge value from there on
+struct ExactAxis {
+    double scale;
+    int ssize, dmin, dmax;
+};
+
+__device__ __forceinline__ uint32_t exact_h(const uint8_t* S, int dx, const ExactCoef& cx, const ExactAxis& ax,
+                                            int cn, int c)
+{
+    if (dx < ax.dmin) return (uint32_t)S[c] << 8;
+    if (dx >= ax.dmax) return (uint32_t)S[(ax.ssize - 1) * cn + c] << 8;
+    return (uint32_t)cx.c0 * S[cx.ofs * cn + c] + (uint32_t)cx.c1 * S[(cx.ofs + 1) * cn + c];
+}
+
+__global__ __launch_bounds__(256) void hog_resize_kernel(const uint8_t* src, int sw, int sh, int spitch, int cn,
+                                                         uint8_t* dst, int dw, int dh, int dpitch, ExactAxis ax,
+                                                         ExactAxis ay)
+{
+    const int dx = blockIdx.x * 256 + threadIdx.x, dy = blockIdx.y;
+    if (dx >= dw) return;
+    const ExactCoef cx = exact_coef(dx, ax.scale, sw);
+    uint8_t* D = dst + (size_t)dy * dpitch + (size_t)dx * cn;
+    if (dy < ay.dmin || dy >= ay.dmax) {
+        const uint8_t* S = src + (size_t)(dy < ay.dmin ? 0 : sh - 1) * spitch;
+        for (int c = 0; c < cn; ++c) D[c] = (uint8_t)((exact_h(S, dx, cx, ax, cn, c) + 128) >> 8);
+        return;
+    }
+    const ExactCoef cy = exact_coef(dy, ay.scale, sh);
+    const uint8_t* S0 = src + (size_t)cy.ofs * spitch;
+    const uint8_t* S1 = S0 + spitch;
+    for (int c = 0; c < cn; ++c) {
+        const uint32_t v = exact_h(S0, dx, cx, ax, cn, c) * (uint32_t)cy.c0 + exact_h(S1, dx, cx, ax, cn, c) * (uint32_t)cy.c1;
+        D[c] = (uint8_t)((v + 32768) >> 16);
+    }
+}
+
+// host: minofst / maxofst of interpolationLinear for one axis
+static ExactAxis exact_axis(int ssize, int dsize)
+{
+    ExactAxis a;
+    a.scale = 1. / ((double)dsize / ssize);
+    a.ssize = ssize;
+    a.dmin = 0;
+    a.dmax = dsize;
+    for (int d = 0; d < dsize; ++d) {
+        const double f = a.scale * ((double)d + 0.5) - 0.5;
+        const int iv = (int)std::floor(f);
+        if (iv >= 0 && ssize > 1) {
+            if (iv >= ssize - 1) a.dmax = std::min(a.dmax, d);
+        } else {
+            a.dmin = std::max(a.dmin, d + 1);
+        }
+    }
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// computeGradient
+
+struct HogGradArgs {
+    const uint8_t* img;
+    int w, h, pitch, cn;
+    float* grad;
+    int gpitch;  // floats
+    uint8_t* qangle;
+    int qpitch;  // bytes
+    int nbins;
+    float angle_scale;
+    int vec_mag;  // magnitude32f / fastAtan32f take the 8-lane path (row >= 16)
+    float lut[256];
+};
+
+__device__ __forceinline__ float hog_fast_atan(float y, float x, bool vec)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (vec) {  // v_atan_f32::compute (mathfuncs_core.simd.hpp:92-103), FMA form
+        const float c = fminf(ax, ay) / (fmaxf(ax, ay) + (float)DBL_EPSILON);
+        const float cc = c * c;
+        a = fmaf(fmaf(fmaf(cc, p7, p5), cc, p3), cc, p1) * c;
+        if (!(ax >= ay)) a = 90.f - a;
+    } else {  // atan_f32 (:50-71)
+        if (ax >= ay) {
+            const float c = ay / (ax + (float)DBL_EPSILON), c2 = c * c;
+            a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+        } else {
+            const float c = ax / (ay + (float)DBL_EPSILON), c2 = c * c;
+            a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+        }
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a * (float)(M_PI / 180);
+}
+
+__global__ __launch_bounds__(256) void hog_grad_kernel(HogGradArgs a)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= a.w) return;
+    const uint8_t* P = a.img + (size_t)y * a.pitch;
+    const uint8_t* Pp = a.img + (size_t)hog_reflect101(y - 1, a.h) * a.pitch;
+    const uint8_t* Pn = a.img + (size_t)hog_reflect101(y + 1, a.h) * a.pitch;
+    const int xl = hog_reflect101(x - 1, a.w), xr = hog_reflect101(x + 1, a.w);
+    float dx, dy;
+    if (a.cn == 1) {
+        dx = a.lut[P[xr]] - a.lut[P[xl]];
+        dy = a.lut[Pn[x]] - a.lut[Pp[x]];
+    } else {
+        float ddx[3], ddy[3], mag[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            ddx[c] = a.lut[P[xr * a.cn + c]] - a.lut[P[xl * a.cn + c]];
+            ddy[c] = a.lut[Pn[x * a.cn + c]] - a.lut[Pp[x * a.cn + c]];
+            mag[c] = ddx[c] * ddx[c] + ddy[c] * ddy[c];
+        }
+        int k;
+        if (x < (a.w & ~3)) {  // SSE2 body (hog.cpp:397-403)
+            k = mag[2] > mag[1] ? 2 : 1;
+            if (!(fmaxf(mag[2], mag[1]) > mag[0])) k = 0;
+        } else {  // scalar tail (hog.cpp:455-477)
+            k = 2;
+            if (mag[k] < mag[1]) k = 1;
+            if (mag[k] < mag[0]) k = 0;
+        }
+        dx = k == 0 ? ddx[0] : k == 1 ? ddx[1] : ddx[2];
+        dy = k == 0 ? ddy[0] : k == 1 ? ddy[1] : ddy[2];
+    }
+    const float m = a.vec_mag ? sqrtf(fmaf(dx, dx, dy * dy)) : sqrtf(dx * dx + dy * dy);
+    float ang = hog_fast_atan(dy, dx, a.vec_mag) * a.angle_scale - 0.5f;
+    int hidx = (int)floorf(ang);
+    ang -= hidx;
+    *reinterpret_cast<float2*>(a.grad + (size_t)y * a.gpitch + 2 * x) = make_float2(m * (1.f - ang), m * ang);
+    if (hidx < 0) hidx += a.nbins;
+    else if (hidx >= a.nbins) hidx -= a.nbins;
+    const int h1 = hidx + 1 < a.nbins ? hidx + 1 : 0;
+    *reinterpret_cast<uchar2*>(a.qangle + (size_t)y * a.qpitch + 2 * x) = make_uchar2((uint8_t)hidx, (uint8_t)h1);
+}
+
+// ---------------------------------------------------------------------------
+// block histograms
+
+struct HogBlockArgs {
+    const float* grad;
+    int gpitch;  // floats
+    const uint8_t* qangle;
+    int qpitch;
+    int nbx, nby, csx, csy;
+    int ncells, nbins, hsz;
+    const int4* cells;  // ncells lists of `cell_cap` entries
+    int cell_cap;
+    int cell_len[kHogMaxCells];
+    float thresh;
+    float* blocks;
+};
+
+// L2-Hys over one block held in LDS (normalizeBlockHistogram's 4-lane sums);
+// every thread of the block computes the same scales, then writes its bins.
+template <int NB>
+__global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
+{
+    extern __shared__ float lds[];
+    const int per_wg = 256 / a.ncells;
+    const int lb = threadIdx.x / a.ncells, cell = threadIdx.x - lb * a.ncells;
+    const int b = blockIdx.x * per_wg + lb;
+    const bool live = lb < per_wg && b < a.nbx * a.nby;
+    float* H = lds + lb * a.hsz;
+    float hist[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) hist[i] = 0.f;
+    if (live) {
+        const int by = b / a.nbx, bx = b - by * a.nbx;
+        const int x0 = bx * a.csx, y0 = by * a.csy;
+        const int4* L = a.cells + (size_t)cell * a.cell_cap;
+        const int n = a.cell_len[cell];
+        for (int k = 0; k < n; ++k) {
+            const int4 e = L[k];
+            const int yy = y0 + e.x, xx = x0 + e.y;
+            const float2 g = *reinterpret_cast<const float2*>(a.grad + (size_t)yy * a.gpitch + 2 * xx);
+            const uchar2 q = *reinterpret_cast<const uchar2*>(a.qangle + (size_t)yy * a.qpitch + 2 * xx);
+            const float w = __int_as_float(e.z);
+            const float t0 = g.x * w, t1 = g.y * w;
+            // exact: every term is >= 0, so adding 0.f to the other bins changes nothing
+#pragma unroll
+            for (int i = 0; i < NB; ++i) hist[i] = hist[i] + (i == q.x ? t0 : (i == q.y ? t1 : 0.f));
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+            if (i < a.nbins) H[cell * a.nbins + i] = hist[i];
+    }
+    __syncthreads();
+    if (!live) return;
+    const int sz = a.hsz;
+    float ps[4];
+    for (int l = 0; l < 4; ++l) ps[l] = H[l] * H[l];
+    int i;
+    for (i = 4; i <= sz - 4; i += 4)
+        for (int l = 0; l < 4; ++l) ps[l] = ps[l] + H[i + l] * H[i + l];
+    float sum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    for (; i < sz; ++i) sum += H[i] * H[i];
+    const float scale = 1.f / (sqrtf(sum) + (float)sz * 0.1f);
+    for (int l = 0; l < 4; ++l) {
+        const float v = fminf(scale * H[l], a.thresh);
+        ps[l] = v * v;
+    }
+    for (i = 4; i <= sz - 4; i += 4)
+        for (int l = 0; l < 4; ++l) {
+            const float v = fminf(H[i + l] * scale, a.thresh);
+            ps[l] = ps[l] + v * v;
+        }
+    sum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    for (; i < sz; ++i) {
+        const float v = fminf(H[i] * scale, a.thresh);
+        sum += v * v;
+    }
+    const float scale2 = 1.f / (sqrtf(sum) + 1e-3f);
+    float* out = a.blocks + (size_t)b * sz + cell * a.nbins;
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+        if (k < a.nbins) out[k] = scale2 * fminf(hist[k] * scale, a.thresh);
+}
+
+// ---------------------------------------------------------------------------
+// windows
+
+struct HogWinArgs {
+    const float* blocks;
+    const float* svm;
+    int nbx, csx, csy;
+    int wbx, wby, bsx, bsy, hsz;
+    int nwx, nwy, wsx, wsy;
+    double rho, hit;
+    int level;
+    int* hits;  // [0] count, then triples
+    double* scores;
+    int cap;
+};
+
+__global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.nwx * a.nwy) return;
+    const int wy = t / a.nwx, wx = t - wy * a.nwx;
+    const int x0 = wx * a.wsx, y0 = wy * a.wsy;
+    double s = a.rho;
+    const float* sv = a.svm;
+    for (int j = 0; j < a.wbx; ++j)
+        for (int i = 0; i < a.wby; ++i, sv += a.hsz) {
+            const int bx = (x0 + j * a.bsx) / a.csx, by = (y0 + i * a.bsy) / a.csy;
+            const float* v = a.blocks + ((size_t)by * a.nbx + bx) * a.hsz;
+            float ps[4];
+            for (int l = 0; l < 4; ++l) ps[l] = sv[l] * v[l];
+            int k;
+            for (k = 4; k <= a.hsz - 4; k += 4)
+                for (int l = 0; l < 4; ++l) ps[l] = ps[l] + v[k + l] * sv[k + l];
+            const double t0 = ps[0] + ps[1], t1 = ps[2] + ps[3];
+            s += t0 + t1;
+            for (; k < a.hsz; ++k) s += v[k] * sv[k];
+        }
+    if (s >= a.hit) {
+        const int slot = atomicAdd(a.hits, 1);
+        if (slot < a.cap) {
+            a.hits[1 + 3 * slot] = a.level;
+            a.hits[2 + 3 * slot] = x0;
+            a.hits[3 + 3 * slot] = y0;
+            a.scores[slot] = s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+
+static int cv_round_d(double v) { return (int)std::lrint(v); }
+
+static int gcd_i(int a, int b)
+{
+    while (b) {
+        const int t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+static int hog_check(const tbdk_hog_params* p)
+{
+    if (!p) return TBDK_EINVAL;
+    if (p->win_w <= 0 || p->win_h <= 0 || p->block_w <= 0 || p->block_h <= 0 || p->cell_w <= 0 || p->cell_h <= 0)
+        return TBDK_EINVAL;
+    if (p->block_stride_x <= 0 || p->block_stride_y <= 0 || p->win_stride_x <= 0 || p->win_stride_y <= 0)
+        return TBDK_EINVAL;
+    // HOG_Impl's asserts (cudaobjdetect/src/hog.cpp:252-256)
+    if ((p->win_w - p->block_w) % p->block_stride_x || (p->win_h - p->block_h) % p->block_stride_y) return TBDK_EINVAL;
+    if (p->block_w % p->cell_w || p->block_h % p->cell_h) return TBDK_EINVAL;
+    if (p->block_w > p->win_w || p->block_h > p->win_h) return TBDK_EINVAL;
+    const int ncells = (p->block_w / p->cell_w) * (p->block_h / p->cell_h);
+    if (p->nbins < 1 || p->nbins > kHogMaxBins || ncells > kHogMaxCells) return TBDK_EINVAL;
+    if (ncells * p->nbins < 4) return TBDK_EINVAL;  // normalizeBlockHistogram reads 4 lanes
+    if (p->block_w * p->block_h > 64 * 64) return TBDK_EINVAL;
+    return TBDK_OK;
+}
+
+static int hist_size(const tbdk_hog_params* p)
+{
+    return (p->block_w / p->cell_w) * (p->block_h / p->cell_h) * p->nbins;
+}
+
+static int descriptor_size(const tbdk_hog_params* p)
+{
+    return hist_size(p) * ((p->win_w - p->block_w) / p->block_stride_x + 1) *
+           ((p->win_h - p->block_h) / p->block_stride_y + 1);
+}
+
+// HOGCache::init's pixData (hog.cpp:656-848), split per cell in pixData order:
+// entry = (di, dj, gradWeight * histWeights[k]) for the k whose histOfs is the cell
+static void cell_lists(const tbdk_hog_params* p, std::vector<std::vector<int4>>& lists)
+{
+    const int bw = p->block_w, bh = p->block_h, ncx = bw / p->cell_w, ncy = bh / p->cell_h;
+    const float sigma = (float)(p->win_sigma > 0 ? p->win_sigma : (bw + bh) / 8.);
+    const float scale = 1.f / (sigma * sigma * 2);
+    const float fbh = bh * 0.5f, fbw = bw * 0.5f;
+    std::vector<float> di(bh), dj(bw);
+    for (int i = 0; i < bh; i++) {
+        di[i] = i - fbh;
+        di[i] *= di[i];
+    }
+    for (int j = 0; j < bw; j++) {
+        dj[j] = j - fbw;
+        dj[j] *= dj[j];
+    }
+    struct Pix {
+        int di, dj, n, cell[4];
+        float hw[4], gw;
+    };
+    std::vector<Pix> g1, g2, g4;
+    for (int j = 0; j < bw; j++)
+        for (int i = 0; i < bh; i++) {
+            Pix d{};
+            float cellX = (j + 0.5f) / p->cell_w - 0.5f;
+            float cellY = (i + 0.5f) / p->cell_h - 0.5f;
+            const int icx0 = (int)std::floor(cellX), icy0 = (int)std::floor(cellY);
+            int icx1 = icx0 + 1, icy1 = icy0 + 1;
+            cellX -= icx0;
+            cellY -= icy0;
+            const bool x0ok = (unsigned)icx0 < (unsigned)ncx, x1ok = (unsigned)icx1 < (unsigned)ncx;
+            const bool y0ok = (unsigned)icy0 < (unsigned)ncy, y1ok = (unsigned)icy1 < (unsigned)ncy;
+            std::vector<Pix>* grp;
+            if (x0ok && x1ok) {
+                if (y0ok && y1ok) {
+                    grp = &g4;
+                    d.n = 4;
+                    d.cell[0] = icx0 * ncy + icy0, d.hw[0] = (1.f - cellX) * (1.f - cellY);
+                    d.cell[1] = icx1 * ncy + icy0, d.hw[1] = cellX * (1.f - cellY);
+                    d.cell[2] = icx0 * ncy + icy1, d.hw[2] = (1.f - cellX) * cellY;
+                    d.cell[3] = icx1 * ncy + icy1, d.hw[3] = cellX * cellY;
+                } else {
+                    grp = &g2;
+                    d.n = 2;
+                    if (y0ok) {
+                        icy1 = icy0;
+                        cellY = 1.f - cellY;
+                    }
+                    d.cell[0] = icx0 * ncy + icy1, d.hw[0] = (1.f - cellX) * cellY;
+                    d.cell[1] = icx1 * ncy + icy1, d.hw[1] = cellX * cellY;
+                }
+            } else {
+                if (x0ok) {
+                    icx1 = icx0;
+                    cellX = 1.f - cellX;
+                }
+                if (y0ok && y1ok) {
+                    grp = &g2;
+                    d.n = 2;
+                    d.cell[0] = icx1 * ncy + icy0, d.hw[0] = cellX * (1.f - cellY);
+                    d.cell[1] = icx1 * ncy + icy1, d.hw[1] = cellX * cellY;
+                } else {
+                    grp = &g1;
+                    d.n = 1;
+                    if (y0ok) {
+                        icy1 = icy0;
+                        cellY = 1.f - cellY;
+                    }
+                    d.cell[0] = icx1 * ncy + icy1, d.hw[0] = cellX * cellY;
+                }
+            }
+            d.di = i, d.dj = j;
+            d.gw = std::exp(-(di[i] + dj[j]) * scale);
+            grp->push_back(d);
+        }
+    lists.assign(ncx * ncy, {});
+    for (const std::vector<Pix>* grp : {&g1, &g2, &g4})
+        for (const Pix& d : *grp)
+            for (int e = 0; e < d.n; e++) {
+                float w = d.gw * d.hw[e];
+                int wb;
+                std::memcpy(&wb, &w, 4);
+                lists[d.cell[e]].push_back(make_int4(d.di, d.dj, wb, 0));
+            }
+}
+
+template <typename T>
+static int grow(T** p, int64_t& cap, int64_t need)
+{
+    if (need <= cap) return TBDK_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)need) != hipSuccess) return TBDK_ENOMEM;
+    cap = need;
+    return TBDK_OK;
+}
+
+struct HogPlan {
+    int hsz, ncells, csx, csy, wbx, wby, dsize;
+    std::vector<std::vector<int4>> lists;
+    int cell_cap;
+};
+
+static void make_plan(const tbdk_hog_params* p, HogPlan& pl)
+{
+    pl.hsz = hist_size(p);
+    pl.ncells = (p->block_w / p->cell_w) * (p->block_h / p->cell_h);
+    pl.csx = gcd_i(p->win_stride_x, p->block_stride_x);
+    pl.csy = gcd_i(p->win_stride_y, p->block_stride_y);
+    pl.wbx = (p->win_w - p->block_w) / p->block_stride_x + 1;
+    pl.wby = (p->win_h - p->block_h) / p->block_stride_y + 1;
+    pl.dsize = descriptor_size(p);
+    cell_lists(p, pl.lists);
+    pl.cell_cap = 0;
+    for (auto& l : pl.lists) pl.cell_cap = std::max(pl.cell_cap, (int)l.size());
+}
+
+static hipError_t upload_plan(HogScratch* S, const HogPlan& pl, hipStream_t s)
+{
+    std::vector<int4> flat((size_t)pl.ncells * pl.cell_cap, make_int4(0, 0, 0, 0));
+    for (int c = 0; c < pl.ncells; ++c)
+        std::copy(pl.lists[c].begin(), pl.lists[c].end(), flat.begin() + (size_t)c * pl.cell_cap);
+    hipError_t e = hipMemcpyAsync(S->cells, flat.data(), sizeof(int4) * flat.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // `flat` is pageable and local
+    return e;
+}
+
+static hipError_t launch_grad(const uint8_t* img, int w, int h, int pitch, int cn, const tbdk_hog_params* p,
+                              float* grad, int gpitch_f, uint8_t* qa, int qpitch, hipStream_t s)
+{
+    HogGradArgs a;
+    a.img = img, a.w = w, a.h = h, a.pitch = pitch, a.cn = cn;
+    a.grad = grad, a.gpitch = gpitch_f, a.qangle = qa, a.qpitch = qpitch;
+    a.nbins = p->nbins;
+    a.angle_scale = p->signed_gradient ? (float)(p->nbins / (2.0 * M_PI)) : (float)(p->nbins / M_PI);
+    a.vec_mag = w >= 16;
+    for (int i = 0; i < 256; ++i) a.lut[i] = p->gamma_correction ? std::sqrt((float)i) : (float)i;
+    hipLaunchKernelGGL(hog_grad_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog_params* p, const float* grad,
+                                int gpitch_f, const uint8_t* qa, int qpitch, int nbx, int nby, float* blocks,
+                                hipStream_t s)
+{
+    HogBlockArgs a;
+    a.grad = grad, a.gpitch = gpitch_f, a.qangle = qa, a.qpitch = qpitch;
+    a.nbx = nbx, a.nby = nby, a.csx = pl.csx, a.csy = pl.csy;
+    a.ncells = pl.ncells, a.nbins = p->nbins, a.hsz = pl.hsz;
+    a.cells = S->cells;
+    a.cell_cap = pl.cell_cap;
+    for (int c = 0; c < kHogMaxCells; ++c) a.cell_len[c] = c < pl.ncells ? (int)pl.lists[c].size() : 0;
+    a.thresh = (float)p->l2hys_threshold;
+    a.blocks = blocks;
+    const int per_wg = 256 / pl.ncells;
+    const int nb = nbx * nby;
+    const dim3 grid((nb + per_wg - 1) / per_wg);
+    const size_t lds = sizeof(float) * per_wg * pl.hsz;
+    if (p->nbins <= 9)
+        hipLaunchKernelGGL(hog_block_kernel<9>, grid, dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL(hog_block_kernel<kHogMaxBins>, grid, dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+// one level: gradients, blocks, windows (hits appended to S->hits)
+static hipError_t run_level(tbdk_ctx* ctx, HogScratch* S, const HogPlan& pl, const tbdk_hog_params* p,
+                            const uint8_t* img, int w, int h, int pitch, int cn, double rho, int level, int hit_cap,
+                            hipStream_t s)
+{
+    const int gpf = 2 * w, qp = 2 * w;
+    int rec = timing_begin(ctx, "hog_grad", s);
+    hipError_t e = launch_grad(img, w, h, pitch, cn, p, S->grad, gpf, S->qangle, qp, s);
+    timing_end(ctx, rec, s);
+    if (e != hipSuccess) return e;
+    const int nbx = (w - p->block_w) / pl.csx + 1, nby = (h - p->block_h) / pl.csy + 1;
+    rec = timing_begin(ctx, "hog_block", s);
+    e = launch_blocks(S, pl, p, S->grad, gpf, S->qangle, qp, nbx, nby, S->blocks, s);
+    timing_end(ctx, rec, s);
+    if (e != hipSuccess) return e;
+    HogWinArgs a;
+    a.blocks = S->blocks, a.svm = S->svm;
+    a.nbx = nbx, a.csx = pl.csx, a.csy = pl.csy;
+    a.wbx = pl.wbx, a.wby = pl.wby, a.bsx = p->block_stride_x, a.bsy = p->block_stride_y, a.hsz = pl.hsz;
+    a.nwx = (w - p->win_w) / p->win_stride_x + 1;
+    a.nwy = (h - p->win_h) / p->win_stride_y + 1;
+    a.wsx = p->win_stride_x, a.wsy = p->win_stride_y;
+    a.rho = rho, a.hit = p->hit_threshold, a.level = level;
+    a.hits = S->hits, a.scores = S->scores, a.cap = hit_cap;
+    rec = timing_begin(ctx, "hog_window", s);
+    hipLaunchKernelGGL(hog_window_kernel, dim3((a.nwx * a.nwy + 255) / 256), dim3(256), 0, s, a);
+    timing_end(ctx, rec, s);
+    return hipGetLastError();
+}
+
+static int reserve(tbdk_ctx* ctx, int w, int h, int cn, const HogPlan& pl, int svm_len, int64_t hit_cap)
+{
+    if (!ctx->hog) ctx->hog = new (std::nothrow) HogScratch();
+    HogScratch* S = ctx->hog;
+    if (!S) return TBDK_ENOMEM;
+    const int64_t px = (int64_t)w * h;
+    int rc = TBDK_OK;
+    if (px > S->cap_px) {
+        int64_t c0 = 0, c1 = 0, c2 = 0;
+        if ((rc = grow(&S->level, c0, px * 4)) || (rc = grow(&S->grad, c1, px * 2)) ||
+            (rc = grow(&S->qangle, c2, px * 2)))
+            return rc;
+        S->cap_px = px;
+    }
+    const int64_t nblk = ((int64_t)w / pl.csx + 1) * (h / pl.csy + 1) * pl.hsz;
+    if ((rc = grow(&S->blocks, S->cap_blocks, nblk))) return rc;
+    if ((rc = grow(&S->svm, S->cap_svm, svm_len))) return rc;
+    if ((rc = grow(&S->cells, S->cap_cells, (int64_t)pl.ncells * pl.cell_cap))) return rc;
+    if (hit_cap > S->cap_hits) {
+        int64_t c = 0;
+        if ((rc = grow(&S->hits, c, 1 + 3 * hit_cap)) || (rc = grow(&S->scores, S->cap_hits, hit_cap))) return rc;
+    }
+    (void)cn;
+    return TBDK_OK;
+}
+
+// groupRectangles(rects, weights, groupThreshold, eps) (hog.cpp:3783-3861) with
+// partition()/SimilarRects, then clipObjects (cascadedetect.cpp:1683-1710)
+static int group_and_clip(std::vector<int>& r, std::vector<double>& wt, int thr, double eps, int W, int H)
+{
+    int n = (int)wt.size();
+    if (thr > 0 && n > 0) {
+        auto similar = [&](int i, int j) {
+            const int* a = &r[4 * i];
+            const int* b = &r[4 * j];
+            const double delta = eps * (std::min(a[2], b[2]) + std::min(a[3], b[3])) * 0.5;
+            return std::abs(a[0] - b[0]) <= delta && std::abs(a[1] - b[1]) <= delta &&
+                   std::abs(a[0] + a[2] - b[0] - b[2]) <= delta && std::abs(a[1] + a[3] - b[1] - b[3]) <= delta;
+        };
+        std::vector<int> parent(n);
+        std::iota(parent.begin(), parent.end(), 0);
+        auto root = [&](int i) {
+            while (parent[i] != i) i = parent[i] = parent[parent[i]];
+            return i;
+        };
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < i; ++j)
+                if (similar(i, j)) {
+                    const int a = root(i), b = root(j);
+                    if (a != b) parent[a] = b;
+                }
+        std::vector<int> cls(n, -1), label(n);
+        int ncls = 0;
+        for (int i = 0; i < n; ++i) {
+            const int rt = root(i);
+            if (cls[rt] < 0) cls[rt] = ncls++;
+            label[i] = cls[rt];
+        }
+        std::vector<double> rr(4 * (size_t)ncls, 0.0), fw(ncls, -DBL_MAX);
+        std::vector<int> cnt(ncls, 0), ri(4 * (size_t)ncls);
+        for (int i = 0; i < n; ++i) {
+            const int c = label[i];
+            for (int t = 0; t < 4; ++t) rr[4 * c + t] += r[4 * i + t];
+            fw[c] = std::max(fw[c], wt[i]);
+            cnt[c]++;
+        }
+        for (int c = 0; c < ncls; ++c) {
+            const double sc = 1.0 / cnt[c];
+            for (int t = 0; t < 4; ++t) ri[4 * c + t] = (int)std::lrint(rr[4 * c + t] * sc);
+        }
+        std::vector<int> out;
+        std::vector<double> ow;
+        for (int i = 0; i < ncls; ++i) {
+            const int* r1 = &ri[4 * i];
+            const int n1 = cnt[i];
+            if (n1 <= thr) continue;
+            int j;
+            for (j = 0; j < ncls; ++j) {
+                const int n2 = cnt[j];
+                if (j == i || n2 <= thr) continue;
+                const int* r2 = &ri[4 * j];
+                const int dx = (int)std::lrint(r2[2] * eps), dy = (int)std::lrint(r2[3] * eps);
+                if (r1[0] >= r2[0] - dx && r1[1] >= r2[1] - dy && r1[0] + r1[2] <= r2[0] + r2[2] + dx &&
+                    r1[1] + r1[3] <= r2[1] + r2[3] + dy && (n2 > std::max(3, n1) || n1 < 3))
+                    break;
+            }
+            if (j == ncls) {
+                out.insert(out.end(), r1, r1 + 4);
+                ow.push_back(fw[i]);
+            }
+        }
+        r.swap(out);
+        wt.swap(ow);
+        n = (int)wt.size();
+    }
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const int x0 = std::max(r[4 * i], 0), y0 = std::max(r[4 * i + 1], 0);
+        const int x1 = std::min(r[4 * i] + r[4 * i + 2], W), y1 = std::min(r[4 * i + 1] + r[4 * i + 3], H);
+        if (x1 <= x0 || y1 <= y0) continue;
+        r[4 * m] = x0, r[4 * m + 1] = y0, r[4 * m + 2] = x1 - x0, r[4 * m + 3] = y1 - y0;
+        wt[m] = wt[i];
+        ++m;
+    }
+    return m;
+}
+
+// shared front half of detect / detectMultiScale: checks, plan, scratch, uploads
+static int prepare(tbdk_ctx* ctx, const uint8_t* img, int w, int h, int pitch, int cn, const tbdk_hog_params* p,
+                   const float* svm, int svm_len, HogPlan& pl, int64_t hit_cap, hipStream_t s)
+{
+    if (!ctx || !img || !svm || w <= 0 || h <= 0 || (cn != 1 && cn != 3 && cn != 4) || pitch < w * cn)
+        return TBDK_EINVAL;
+    int rc = hog_check(p);
+    if (rc != TBDK_OK) return rc;
+    make_plan(p, pl);
+    if (svm_len != pl.dsize && svm_len != pl.dsize + 1) return TBDK_EINVAL;  // checkDetectorSize (hog.cpp:106-112)
+    rc = reserve(ctx, w, h, cn, pl, svm_len, hit_cap);
+    if (rc != TBDK_OK) return rc;
+    HogScratch* S = ctx->hog;
+    hipError_t e = hipMemcpyAsync(S->svm, svm, sizeof(float) * svm_len, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = upload_plan(S, pl, s);
+    if (e == hipSuccess) e = hipMemsetAsync(S->hits, 0, sizeof(int), s);
+    return map_status(e);
+}
+
+struct Hit {
+    int level, x, y;
+    double score;
+};
+
+static int fetch_hits(HogScratch* S, int64_t cap, std::vector<Hit>& out, hipStream_t s)
+{
+    int n = 0;
+    hipError_t e = hipMemcpyAsync(&n, S->hits, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return map_status(e);
+    if (n > cap) return TBDK_ENOMEM;
+    std::vector<int> tri(3 * (size_t)n);
+    std::vector<double> sc(n);
+    if (n) {
+        e = hipMemcpyAsync(tri.data(), S->hits + 1, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(sc.data(), S->scores, sizeof(double) * n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return map_status(e);
+    }
+    out.resize(n);
+    for (int i = 0; i < n; ++i) out[i] = Hit{tri[3 * i], tri[3 * i + 1], tri[3 * i + 2], sc[i]};
+    // window order within a level (the reference's sequential loop)
+    std::sort(out.begin(), out.end(), [](const Hit& a, const Hit& b) {
+        return a.level != b.level ? a.level < b.level : a.y != b.y ? a.y < b.y : a.x < b.x;
+    });
+    return TBDK_OK;
+}
+
+}  // namespace tbdk
+
+using namespace tbdk;
+
+void tbdk::hog_release(tbdk_ctx* ctx)
+{
+    HogScratch* S = ctx->hog;
+    if (!S) return;
+    for (void* p : {(void*)S->level, (void*)S->grad, (void*)S->qangle, (void*)S->blocks, (void*)S->svm,
+                    (void*)S->cells, (void*)S->hits, (void*)S->scores})
+        if (p) (void)hipFree(p);
+    delete S;
+    ctx->hog = nullptr;
+}
+
+extern "C" {
+
+int tbdk_hog_default_params(tbdk_hog_params* p)
+{
+    if (!p) return TBDK_EINVAL;
+    p->win_w = 64, p->win_h = 128;
+    p->block_w = 16, p->block_h = 16;
+    p->block_stride_x = 8, p->block_stride_y = 8;
+    p->cell_w = 8, p->cell_h = 8;
+    p->nbins = 9;
+    p->win_sigma = -1.0;
+    p->l2hys_threshold = 0.2;
+    p->gamma_correction = 1;
+    p->signed_gradient = 0;
+    p->nlevels = 64;
+    p->hit_threshold = 0.0;
+    p->win_stride_x = 8, p->win_stride_y = 8;
+    p->scale0 = 1.05;
+    p->group_threshold = 2;
+    return TBDK_OK;
+}
+
+int tbdk_hog_descriptor_size(const tbdk_hog_params* p, int* size)
+{
+    if (!size || hog_check(p) != TBDK_OK) return TBDK_EINVAL;
+    *size = descriptor_size(p);
+    return TBDK_OK;
+}
+
+int tbdk_hog_resize(tbdk_ctx* ctx, const uint8_t* src, int width, int height, int pitch, int cn, uint8_t* dst,
+                    int dst_width, int dst_height, int dst_pitch, void* stream)
+{
+    if (!ctx || !src || !dst || width <= 0 || height <= 0 || dst_width <= 0 || dst_height <= 0 || cn < 1 || cn > 4 ||
+        pitch < width * cn || dst_pitch < dst_width * cn)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    const ExactAxis ax = exact_axis(width, dst_width), ay = exact_axis(height, dst_height);
+    hipLaunchKernelGGL(hog_resize_kernel, dim3((dst_width + 255) / 256, dst_height), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), src, width, height, pitch, cn, dst, dst_width, dst_height,
+                       dst_pitch, ax, ay);
+    return map_status(hipGetLastError());
+}
+
+int tbdk_hog_gradient(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                      const tbdk_hog_params* params, float* grad, int grad_pitch, uint8_t* qangle,
+                      int qangle_pitch, void* stream)
+{
+    if (!ctx || !img || !grad || !qangle || width <= 0 || height <= 0 || (cn != 1 && cn != 3 && cn != 4) ||
+        pitch < width * cn || grad_pitch < 8 * width || grad_pitch % 8 || qangle_pitch < 2 * width ||
+        qangle_pitch % 2)
+        return TBDK_EINVAL;
+    if (hog_check(params) != TBDK_OK) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    return map_status(launch_grad(img, width, height, pitch, cn, params, grad, grad_pitch / 4, qangle, qangle_pitch,
+                                  static_cast<hipStream_t>(stream)));
+}
+
+int tbdk_hog_blocks(tbdk_ctx* ctx, const float* grad, int grad_pitch, const uint8_t* qangle, int qangle_pitch,
+                    int width, int height, const tbdk_hog_params* params, float* blocks, void* stream)
+{
+    if (!ctx || !grad || !qangle || !blocks || grad_pitch % 8 || grad_pitch < 8 * width || qangle_pitch % 2 ||
+        qangle_pitch < 2 * width)
+        return TBDK_EINVAL;
+    if (hog_check(params) != TBDK_OK) return TBDK_EINVAL;
+    if (width < params->block_w || height < params->block_h) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    HogPlan pl;
+    make_plan(params, pl);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = reserve(ctx, 1, 1, 1, pl, 1, 1);
+    if (rc != TBDK_OK) return rc;
+    hipError_t e = upload_plan(ctx->hog, pl, s);
+    if (e != hipSuccess) return map_status(e);
+    const int nbx = (width - params->block_w) / pl.csx + 1, nby = (height - params->block_h) / pl.csy + 1;
+    return map_status(launch_blocks(ctx->hog, pl, params, grad, grad_pitch / 4, qangle, qangle_pitch, nbx, nby,
+                                    blocks, s));
+}
+
+int tbdk_hog_detect(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                    const tbdk_hog_params* params, const float* svm, int svm_len, int32_t* xy, double* scores,
+                    int max_hits, int* nhits, void* stream)
+{
+    if (!nhits || max_hits < 0 || (max_hits > 0 && (!xy || !scores))) return TBDK_EINVAL;
+    *nhits = 0;
+    if (!ctx) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HogPlan pl;
+    const int64_t cap = (int64_t)(width / std::max(params ? params->win_stride_x : 1, 1) + 1) *
+                        (height / std::max(params ? params->win_stride_y : 1, 1) + 1);
+    int rc = prepare(ctx, img, width, height, pitch, cn, params, svm, svm_len, pl, cap, s);
+    if (rc != TBDK_OK) return rc;
+    if (width < params->win_w || height < params->win_h) return TBDK_OK;
+    const double rho = svm_len > pl.dsize ? svm[pl.dsize] : 0;
+    hipError_t e = run_level(ctx, ctx->hog, pl, params, img, width, height, pitch, cn, rho, 0, (int)cap, s);
+    if (e != hipSuccess) return map_status(e);
+    std::vector<Hit> hits;
+    rc = fetch_hits(ctx->hog, cap, hits, s);
+    if (rc != TBDK_OK) return rc;
+    const int n = std::min((int)hits.size(), max_hits);
+    for (int i = 0; i < n; ++i) {
+        xy[2 * i] = hits[i].x;
+        xy[2 * i + 1] = hits[i].y;
+        scores[i] = hits[i].score;
+    }
+    *nhits = n;
+    return (int)hits.size() > max_hits ? TBDK_ENOMEM : TBDK_OK;
+}
+
+int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
+                               const tbdk_hog_params* params, const float* svm, int svm_len, int32_t* rects,
+                               double* weights, int max_rects, int* nrects, void* stream)
+{
+    if (!nrects || max_rects < 0 || (max_rects > 0 && (!rects || !weights))) return TBDK_EINVAL;
+    *nrects = 0;
+    if (!ctx || !params || params->nlevels < 1) return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // level scales (hog.cpp:2058-2073)
+    std::vector<double> lv;
+    double scale = 1.;
+    for (int l = 0; l < params->nlevels && l < kHogMaxLevels; ++l) {
+        lv.push_back(scale);
+        if (cv_round_d(width / scale) < params->win_w || cv_round_d(height / scale) < params->win_h ||
+            params->scale0 <= 1) {
+            lv.pop_back();
+            break;
+        }
+        scale *= params->scale0;
+    }
+    if (lv.empty()) lv.push_back(1.);
+    // every window of every level can hit: size the hit list for all of them
+    int64_t cap = 1;
+    for (double sc : lv) {
+        const int sw = cv_round_d(width / sc), sh = cv_round_d(height / sc);
+        if (sw >= params->win_w && sh >= params->win_h && params->win_stride_x > 0 && params->win_stride_y > 0)
+            cap += (int64_t)((sw - params->win_w) / params->win_stride_x + 1) *
+                   ((sh - params->win_h) / params->win_stride_y + 1);
+    }
+    HogPlan pl;
+    int rc = prepare(ctx, img, width, height, pitch, cn, params, svm, svm_len, pl, cap, s);
+    if (rc != TBDK_OK) return rc;
+    HogScratch* S = ctx->hog;
+    const double rho = svm_len > pl.dsize ? svm[pl.dsize] : 0;
+    hipError_t e = hipSuccess;
+    for (int l = 0; l < (int)lv.size() && e == hipSuccess; ++l) {
+        const int sw = cv_round_d(width / lv[l]), sh = cv_round_d(height / lv[l]);
+        if (sw < params->win_w || sh < params->win_h) continue;
+        const uint8_t* li = img;
+        int lp = pitch;
+        if (sw != width || sh != height) {
+            const ExactAxis ax = exact_axis(width, sw), ay = exact_axis(height, sh);
+            const int rec = timing_begin(ctx, "hog_resize", s);
+            hipLaunchKernelGGL(hog_resize_kernel, dim3((sw + 255) / 256, sh), dim3(256), 0, s, img, width, height,
+                               pitch, cn, S->level, sw, sh, sw * cn, ax, ay);
+            timing_end(ctx, rec, s);
+            e = hipGetLastError();
+            li = S->level;
+            lp = sw * cn;
+        }
+        if (e == hipSuccess) e = run_level(ctx, S, pl, params, li, sw, sh, lp, cn, rho, l, (int)cap, s);
+    }
+    if (e != hipSuccess) return map_status(e);
+    std::vector<Hit> hits;
+    rc = fetch_hits(S, cap, hits, s);
+    if (rc != TBDK_OK) return rc;
+    // HOGInvoker's rects (hog.cpp:1818-1828)
+    std::vector<int> r;
+    std::vector<double> wt;
+    r.reserve(4 * hits.size());
+    for (const Hit& h : hits) {
+        const double sc = lv[h.level];
+        r.push_back(cv_round_d(h.x * sc));
+        r.push_back(cv_round_d(h.y * sc));
+        r.push_back(cv_round_d(params->win_w * sc));
+        r.push_back(cv_round_d(params->win_h * sc));
+        wt.push_back(h.score);
+    }
+    const int n = group_and_clip(r, wt, params->group_threshold, 0.2, width, height);
+    const int m = std::min(n, max_rects);
+    for (int i = 0; i < m; ++i) {
+        for (int t = 0; t < 4; ++t) rects[4 * i + t] = r[4 * i + t];
+        weights[i] = wt[i];
+    }
+    *nrects = m;
+    return n > max_rects ? TBDK_ENOMEM : TBDK_OK;
+}
+
+}  // extern "C"

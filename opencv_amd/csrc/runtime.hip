@@ -88,6 +88,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
     if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
     fb_release(ctx);
+    hog_release(ctx);
     if (ctx->dense_buf) (void)hipFree(ctx->dense_buf);
     delete ctx;
     return TBDK_OK;

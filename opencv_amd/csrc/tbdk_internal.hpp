@@ -52,6 +52,7 @@ struct DeviceGuard {
 };
 
 struct FbScratch;  // farneback.hip
+struct HogScratch;  // hog.hip
 
 }  // namespace tbdk
 
@@ -71,6 +72,7 @@ struct tbdk_ctx {
     int64_t gftt_cap_px = 0;
     tbdk::FbScratch* fb = nullptr;  // dense Farneback planes (farneback.hip)
     void* dense_buf = nullptr;      // dense PyrLK grid / next points / status (klt_dense.hip)
+    tbdk::HogScratch* hog = nullptr;  // HOG level image, gradients, blocks, hits (hog.hip)
     int64_t dense_cap = 0;          // pixels
 };
 
@@ -82,6 +84,7 @@ void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s);
 
 // frees the context's Farneback scratch (farneback.hip)
 void fb_release(tbdk_ctx* ctx);
+void hog_release(tbdk_ctx* ctx);
 
 // ---- kernels (klt_pyr.hip) ----
 hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& dst, hipStream_t s);

@@ -350,3 +350,107 @@ def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.5, levels=5, winsiz
     if rc != 0:
         raise ValueError("unsupported Farneback arguments")
     return flow
+
+
+# ---- HOG people detector (oracle/hog_oracle.c) ----
+class HogParams(C.Structure):
+    _fields_ = [("win_w", C.c_int), ("win_h", C.c_int), ("block_w", C.c_int), ("block_h", C.c_int),
+                ("bstride_x", C.c_int), ("bstride_y", C.c_int), ("cell_w", C.c_int), ("cell_h", C.c_int),
+                ("nbins", C.c_int), ("win_sigma", C.c_double), ("l2hys", C.c_double), ("gamma", C.c_int),
+                ("signed_grad", C.c_int), ("wstride_x", C.c_int), ("wstride_y", C.c_int)]
+
+
+def hog_params(win=(64, 128), block=(16, 16), bstride=(8, 8), cell=(8, 8), nbins=9, win_sigma=-1.0, l2hys=0.2,
+               gamma=True, signed=False, wstride=(8, 8)) -> HogParams:
+    return HogParams(win[0], win[1], block[0], block[1], bstride[0], bstride[1], cell[0], cell[1], nbins,
+                     win_sigma, l2hys, int(gamma), int(signed), wstride[0], wstride[1])
+
+
+def _hog_lib():
+    lib = load()
+    P = C.POINTER(HogParams)
+    lib.orc_hog_resize_exact.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                         C.c_int, C.c_int]
+    lib.orc_hog_gradient.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_void_p]
+    lib.orc_hog_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, P, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.orc_hog_detect.restype = C.c_int
+    lib.orc_hog_detect.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_void_p, C.c_int,
+                                   C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.orc_hog_group.restype = C.c_int
+    lib.orc_hog_group.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int]
+    lib.orc_hog_detect_multiscale.restype = C.c_int
+    lib.orc_hog_detect_multiscale.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_void_p,
+                                              C.c_int, C.c_double, C.c_int, C.c_double, C.c_int, C.c_void_p,
+                                              C.c_void_p, C.c_int]
+    return lib
+
+
+def _img(img):
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    cn = 1 if a.ndim == 2 else a.shape[2]
+    return a, a.shape[1], a.shape[0], a.strides[0], cn
+
+
+def hog_resize(img: np.ndarray, size) -> np.ndarray:
+    """resize(img, size, 0, 0, INTER_LINEAR_EXACT) of a u8 image."""
+    a, w, h, pitch, cn = _img(img)
+    dw, dh = size
+    out = np.empty((dh, dw) + a.shape[2:], np.uint8)
+    _hog_lib().orc_hog_resize_exact(_ptr(a), w, h, pitch, cn, _ptr(out), dw, dh, out.strides[0])
+    return out
+
+
+def hog_gradient(img: np.ndarray, nbins=9, gamma=True, signed=False):
+    """HOGDescriptor::computeGradient -> (grad (H, W, 2) f32, qangle (H, W, 2) u8)."""
+    a, w, h, pitch, cn = _img(img)
+    grad = np.empty((h, w, 2), np.float32)
+    qa = np.empty((h, w, 2), np.uint8)
+    _hog_lib().orc_hog_gradient(_ptr(a), w, h, pitch, cn, nbins, int(gamma), int(signed), _ptr(grad), _ptr(qa))
+    return grad, qa
+
+
+def hog_blocks(grad: np.ndarray, qangle: np.ndarray, prm: HogParams) -> np.ndarray:
+    """Normalized block histograms on the cache grid -> (nby, nbx, block_hist_size)."""
+    h, w = grad.shape[:2]
+    csx, csy = np.gcd(prm.wstride_x, prm.bstride_x), np.gcd(prm.wstride_y, prm.bstride_y)
+    nbx, nby = (w - prm.block_w) // csx + 1, (h - prm.block_h) // csy + 1
+    sz = (prm.block_w // prm.cell_w) * (prm.block_h // prm.cell_h) * prm.nbins
+    out = np.empty((nby, nbx, sz), np.float32)
+    gx, gy = C.c_int(), C.c_int()
+    _hog_lib().orc_hog_blocks(_ptr(np.ascontiguousarray(grad)), _ptr(np.ascontiguousarray(qangle)), w, h,
+                              C.byref(prm), _ptr(out), C.byref(gx), C.byref(gy))
+    return out
+
+
+def hog_detect(img: np.ndarray, prm: HogParams, svm: np.ndarray, hit_threshold=0.0):
+    """HOGDescriptor::detect (padding 0) -> (xy (n, 2) i32, scores (n,) f64) in window order."""
+    a, w, h, pitch, cn = _img(img)
+    nwin = max((w - prm.win_w) // prm.wstride_x + 1, 0) * max((h - prm.win_h) // prm.wstride_y + 1, 0) + 1
+    xs, ys = np.empty(nwin, np.int32), np.empty(nwin, np.int32)
+    sc = np.empty(nwin, np.float64)
+    s = np.ascontiguousarray(svm, np.float32)
+    n = _hog_lib().orc_hog_detect(_ptr(a), w, h, pitch, cn, C.byref(prm), _ptr(s), s.size, float(hit_threshold),
+                                  _ptr(xs), _ptr(ys), _ptr(sc))
+    return np.stack([xs[:n], ys[:n]], 1), sc[:n]
+
+
+def hog_group(rects: np.ndarray, weights: np.ndarray, group_threshold: int, img_size, eps=0.2):
+    r = np.ascontiguousarray(rects, np.int32).copy()
+    wt = np.ascontiguousarray(weights, np.float64).copy()
+    n = _hog_lib().orc_hog_group(_ptr(r), _ptr(wt), len(r), int(group_threshold), float(eps), img_size[0],
+                                 img_size[1])
+    return r[:n], wt[:n]
+
+
+def hog_detect_multiscale(img: np.ndarray, prm: HogParams, svm: np.ndarray, hit_threshold=0.0, nlevels=64,
+                          scale0=1.05, group_threshold=2, max_rects=1 << 16):
+    """HOGDescriptor::detectMultiScale(img, rects, weights, hit, winStride, Size(), scale0, group) -> (rects, weights)."""
+    a, w, h, pitch, cn = _img(img)
+    rects = np.empty((max_rects, 4), np.int32)
+    wts = np.empty(max_rects, np.float64)
+    s = np.ascontiguousarray(svm, np.float32)
+    n = _hog_lib().orc_hog_detect_multiscale(_ptr(a), w, h, pitch, cn, C.byref(prm), _ptr(s), s.size,
+                                             float(hit_threshold), int(nlevels), float(scale0), int(group_threshold),
+                                             _ptr(rects), _ptr(wts), max_rects)
+    return rects[:n], wts[:n]

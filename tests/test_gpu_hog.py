@@ -1,0 +1,123 @@
+"""HOG people detector on the GPU (libtbdk hog.hip) vs the CPU oracle
+(oracle/hog_oracle.c, the HOGDescriptor restatement): bit-exact at every stage
+(INTER_LINEAR_EXACT levels, gradients and bins, normalized block histograms,
+window scores as doubles) and equal detection sets after grouping."""
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bgr(seed, w, h, cn=3):
+    fr, _ = O.synth(seed, w, h, 8, 0, 1)
+    g = fr[0].astype(np.int32)
+    if cn == 1:
+        return g.astype(np.uint8)
+    rng = np.random.default_rng(seed)
+    chans = [np.clip(g + rng.integers(-30, 30, g.shape), 0, 255) for _ in range(cn)]
+    return np.stack(chans, 2).astype(np.uint8)
+
+
+def _hog(gpu, win=(64, 128), **kw):
+    from opencv_amd import hog
+
+    h = hog.HOG.create(win, ctx=gpu, **kw)
+    h.setSVMDetector(h.getDefaultPeopleDetector())
+    return h
+
+
+def _prm(h):
+    p = h.p
+    return O.hog_params(win=(p.win_w, p.win_h), block=(p.block_w, p.block_h),
+                        bstride=(p.block_stride_x, p.block_stride_y), cell=(p.cell_w, p.cell_h), nbins=p.nbins,
+                        win_sigma=p.win_sigma, l2hys=p.l2hys_threshold, gamma=bool(p.gamma_correction),
+                        signed=bool(p.signed_gradient), wstride=(p.win_stride_x, p.win_stride_y))
+
+
+@pytest.mark.parametrize("cn", [1, 3, 4])
+@pytest.mark.parametrize("src,dst", [((640, 480), (610, 457)), ((1242, 375), (1183, 357)), ((97, 61), (31, 20)),
+                                     ((50, 40), (123, 77))])
+def test_resize_exact_bit_exact(gpu, cn, src, dst):
+    from opencv_amd import hog
+
+    img = _bgr(sum(src) + cn, *src, cn=cn)
+    got = hog.resize_exact(torch.from_numpy(img).cuda(), dst, ctx=gpu).cpu().numpy()
+    assert np.array_equal(got, O.hog_resize(img, dst))
+
+
+@pytest.mark.parametrize("cn", [1, 3, 4])
+@pytest.mark.parametrize("w,h", [(640, 480), (130, 77), (15, 33), (6, 5)])
+@pytest.mark.parametrize("gamma,signed", [(True, False), (False, True)])
+def test_gradient_bit_exact(gpu, cn, w, h, gamma, signed):
+    from opencv_amd import hog
+
+    img = _bgr(w * h + cn, w, h, cn=cn)
+    hg = _hog(gpu)
+    hg.setGammaCorrection(gamma)
+    hg.setSignedGradient(signed)
+    g, q = hog.gradient(torch.from_numpy(img).cuda(), hg, ctx=gpu)
+    og, oq = O.hog_gradient(img[..., :3] if cn == 4 else img, nbins=9, gamma=gamma, signed=signed)
+    assert np.array_equal(q.cpu().numpy(), oq)
+    assert np.array_equal(g.cpu().numpy(), og)
+
+
+@pytest.mark.parametrize("geom", [dict(), dict(block_size=(16, 16), cell_size=(4, 4), nbins=9, win_size=(64, 128)),
+                                  dict(nbins=18, win_size=(64, 128)), dict(block_stride=(4, 4), win_size=(48, 96))])
+def test_blocks_bit_exact(gpu, geom):
+    from opencv_amd import hog
+
+    img = _bgr(7, 200, 150, cn=1)
+    hg = hog.HOG.create(ctx=gpu, **geom)
+    og, oq = O.hog_gradient(img, nbins=hg.p.nbins)
+    B = hog.blocks(torch.from_numpy(og).cuda(), torch.from_numpy(oq).cuda(), hg, ctx=gpu).cpu().numpy()
+    assert np.array_equal(B, O.hog_blocks(og, oq, _prm(hg)))
+
+
+@pytest.mark.parametrize("win", [(64, 128), (48, 96)])
+@pytest.mark.parametrize("cn", [1, 3])
+def test_detect_scores_bit_exact(gpu, win, cn):
+    img = _bgr(11 + cn, 320, 240, cn=cn)
+    hg = _hog(gpu, win)
+    hg.setHitThreshold(-1e9)  # every window
+    xy, sc = hg.detect(torch.from_numpy(img).cuda(), confidences=True)
+    oxy, osc = O.hog_detect(img, _prm(hg), hg.svm, hit_threshold=-1e9)
+    assert len(xy) == len(oxy)
+    assert np.array_equal(np.array(xy), oxy) and np.array_equal(np.array(sc), osc)
+
+
+@pytest.mark.parametrize("win,cn,hit,group", [((64, 128), 3, -2.2, 2), ((48, 96), 3, -1.0, 2), ((64, 128), 1, -1.6, 0),
+                                              ((48, 96), 4, -0.9, 4)])
+def test_detect_multiscale_equals_oracle(gpu, win, cn, hit, group):
+    """The sample's call: 15 levels, scale 1.05, win stride 8 (tbd.cpp:425-431, 596-606)."""
+    img = _bgr(20 + cn, 640, 360, cn=cn)
+    hg = _hog(gpu, win)
+    hg.setNumLevels(15)
+    hg.setHitThreshold(hit)
+    hg.setGroupThreshold(group)
+    rects, wts = hg.detectMultiScale(torch.from_numpy(img).cuda(), confidences=True)
+    ref = img[..., :3] if cn == 4 else img
+    orects, owts = O.hog_detect_multiscale(ref, _prm(hg), hg.svm, hit_threshold=hit, nlevels=15, scale0=1.05,
+                                           group_threshold=group)
+    got = sorted(zip(rects, wts))
+    exp = sorted(zip(map(tuple, orects.tolist()), owts.tolist()))
+    assert len(exp) > 0
+    assert got == exp
+
+
+def test_rejects_bad_arguments(gpu):
+    from opencv_amd import _lib, hog
+
+    with pytest.raises(_lib.TbdkError):
+        hog.HOG.create((60, 128))                        # (win - block) % stride != 0
+    hg = _hog(gpu)
+    with pytest.raises(_lib.TbdkError):
+        hg.setSVMDetector(np.zeros(100, np.float32))     # wrong detector size
+    with pytest.raises(_lib.TbdkError):
+        hg.detectMultiScale(torch.zeros((64, 64, 2), dtype=torch.uint8, device="cuda"))
+    with pytest.raises(_lib.TbdkError):
+        hog.HOG.create((32, 32)).getDefaultPeopleDetector()
+    small = torch.zeros((60, 40), dtype=torch.uint8, device="cuda")  # smaller than the window
+    assert hg.detectMultiScale(small) == []
