@@ -198,6 +198,63 @@ def farneback_secondary(ctx, args, device, cpu: bool):
     return out
 
 
+def hog_secondary(ctx, args, device, cpu: bool):
+    """The sample's detection step in GPU mode (samples/gpu/tbd.cpp:384-443,
+    596-606): cv::cuda::HOG 48x96 people detector, 15 levels, scale 1.05, hit
+    threshold 0.45, win stride 8, group threshold 2, on BGRA frames: frames/s of
+    detectMultiScale through tbdk_hog_detect_multiscale (device levels, host
+    grouping, synchronous), per-kernel times, and the CPU oracle on one frame.
+    Reported, never `value`."""
+    import torch
+    from opencv_amd import hog as H
+    from opencv_amd import klt
+
+    w, h, n = args.hog_width, args.hog_height, args.hog_frames
+    gray, _ = klt.synth_render(args.seed + 11, w, h, args.objects, 0, n, device=device, ctx=ctx)
+    frames = torch.stack([gray, gray.flip(2), gray.flip(1), torch.full_like(gray, 255)], 3).contiguous()
+    hg = H.HOG.create((48, 96), ctx=ctx)
+    hg.setSVMDetector(hg.getDefaultPeopleDetector())
+    hg.setNumLevels(15)
+    hg.setHitThreshold(0.45)
+    found = [len(hg.detectMultiScale(frames[i])) for i in range(min(2, n))]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n):
+        hg.detectMultiScale(frames[i])
+    wall = time.perf_counter() - t0
+    names = ["hog_resize", "hog_grad", "hog_block", "hog_window"]
+    ctx.timing_select(names)
+    ctx.timing_enable(True)
+    for i in range(n):
+        hg.detectMultiScale(frames[i])
+    kern = {}
+    for name in names:
+        c, ms = ctx.timing_query(name)
+        kern[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "ms_per_frame": ms / n}
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    out = {"value": round(n / wall, 2), "unit": "frames/s", "ms_per_frame": round(1000 * wall / n, 3),
+           "config": {"workload": f"HOG detectMultiScale {w}x{h} BGRA synthetic frames ({args.objects} objects)",
+                      "params": "48x96 people detector, nlevels 15, scale 1.05, hit 0.45, win stride 8x8, "
+                                "group threshold 2 (the sample's GPU-mode settings)",
+                      "detections_first_frames": found, "frames": n},
+           "kernels": kern,
+           "note": "wall time includes the per-call detector upload, the hit download and host grouping"}
+    if cpu:
+        import importlib
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+        O = importlib.import_module("_oracle")
+        img = frames[0, ..., :3].cpu().numpy()
+        t1 = time.perf_counter()
+        O.hog_detect_multiscale(img, O.hog_params(win=(48, 96)), hg.svm, hit_threshold=0.45, nlevels=15)
+        dt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"one {w}x{h} BGR frame through oracle/hog_oracle.c (the reference's "
+                                         "HOGDescriptor::detectMultiScale restated), 1 thread"}
+    del frames, gray
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +284,10 @@ def main():
     ap.add_argument("--fb-height", type=int, default=2160)
     ap.add_argument("--fb-objects", type=int, default=512)
     ap.add_argument("--fb-pairs", type=int, default=10)
+    ap.add_argument("--no-hog", action="store_true", help="skip the secondary HOG detector measurement")
+    ap.add_argument("--hog-width", type=int, default=1920)
+    ap.add_argument("--hog-height", type=int, default=1080)
+    ap.add_argument("--hog-frames", type=int, default=10)
     args = ap.parse_args()
 
     import numpy as np
@@ -420,6 +481,8 @@ def main():
     if rank == 0 and not args.no_farneback:
         del frames, frame_list
         out["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+    if rank == 0 and not args.no_hog:
+        out["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -237,9 +237,10 @@ struct HogBlockArgs {
     float* blocks;
 };
 
-// L2-Hys over one block held in LDS (normalizeBlockHistogram's 4-lane sums);
-// every thread of the block computes the same scales, then writes its bins.
-template <int NB>
+// Each thread sums its cell's bins straight into the block's LDS histogram
+// (the reference's read-both-then-write update, hog.cpp:909-911); then every
+// thread of the block computes the same L2-Hys scales in normalizeBlockHistogram's
+// 4-lane order and writes its own bins.
 __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
 {
     extern __shared__ float lds[];
@@ -248,10 +249,9 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
     const int b = blockIdx.x * per_wg + lb;
     const bool live = lb < per_wg && b < a.nbx * a.nby;
     float* H = lds + lb * a.hsz;
-    float hist[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) hist[i] = 0.f;
+    float* hs = H + cell * a.nbins;
     if (live) {
+        for (int i = 0; i < a.nbins; ++i) hs[i] = 0.f;
         const int by = b / a.nbx, bx = b - by * a.nbx;
         const int x0 = bx * a.csx, y0 = by * a.csy;
         const int4* L = a.cells + (size_t)cell * a.cell_cap;
@@ -262,14 +262,11 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
             const float2 g = *reinterpret_cast<const float2*>(a.grad + (size_t)yy * a.gpitch + 2 * xx);
             const uchar2 q = *reinterpret_cast<const uchar2*>(a.qangle + (size_t)yy * a.qpitch + 2 * xx);
             const float w = __int_as_float(e.z);
-            const float t0 = g.x * w, t1 = g.y * w;
-            // exact: every term is >= 0, so adding 0.f to the other bins changes nothing
-#pragma unroll
-            for (int i = 0; i < NB; ++i) hist[i] = hist[i] + (i == q.x ? t0 : (i == q.y ? t1 : 0.f));
+            const float t0 = hs[q.x] + g.x * w;
+            const float t1 = hs[q.y] + g.y * w;
+            hs[q.x] = t0;
+            hs[q.y] = t1;
         }
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-            if (i < a.nbins) H[cell * a.nbins + i] = hist[i];
     }
     __syncthreads();
     if (!live) return;
@@ -298,9 +295,7 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
     }
     const float scale2 = 1.f / (sqrtf(sum) + 1e-3f);
     float* out = a.blocks + (size_t)b * sz + cell * a.nbins;
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-        if (k < a.nbins) out[k] = scale2 * fminf(hist[k] * scale, a.thresh);
+    for (int k = 0; k < a.nbins; ++k) out[k] = scale2 * fminf(hs[k] * scale, a.thresh);
 }
 
 // ---------------------------------------------------------------------------
@@ -319,27 +314,46 @@ struct HogWinArgs {
     int cap;
 };
 
+// One wave per window, one lane per block (blocks x-major as blockData): each
+// lane forms its block's contribution exactly as the reference's loop body
+// (float 4-lane dot, then double t0 + t1, then the tail products), and lane 0
+// adds them to rho in block order (hog.cpp:1709-1760).
+constexpr int kHogWinPerWg = 4;
+
 __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
 {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.nwx * a.nwy) return;
-    const int wy = t / a.nwx, wx = t - wy * a.nwx;
-    const int x0 = wx * a.wsx, y0 = wy * a.wsy;
-    double s = a.rho;
-    const float* sv = a.svm;
-    for (int j = 0; j < a.wbx; ++j)
-        for (int i = 0; i < a.wby; ++i, sv += a.hsz) {
+    extern __shared__ double wl[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * kHogWinPerWg + wave;
+    const int nblk = a.wbx * a.wby, tail = a.hsz & 3;
+    double* main_v = wl + (size_t)wave * nblk * 4;  // per block: main + up to 3 tail products
+    const bool live = t < a.nwx * a.nwy;
+    int x0 = 0, y0 = 0;
+    if (live) {
+        const int wy = t / a.nwx, wx = t - wy * a.nwx;
+        x0 = wx * a.wsx, y0 = wy * a.wsy;
+        for (int k = lane; k < nblk; k += 64) {
+            const int j = k / a.wby, i = k - j * a.wby;
             const int bx = (x0 + j * a.bsx) / a.csx, by = (y0 + i * a.bsy) / a.csy;
             const float* v = a.blocks + ((size_t)by * a.nbx + bx) * a.hsz;
+            const float* sv = a.svm + (size_t)k * a.hsz;
             float ps[4];
             for (int l = 0; l < 4; ++l) ps[l] = sv[l] * v[l];
-            int k;
-            for (k = 4; k <= a.hsz - 4; k += 4)
-                for (int l = 0; l < 4; ++l) ps[l] = ps[l] + v[k + l] * sv[k + l];
+            int q;
+            for (q = 4; q <= a.hsz - 4; q += 4)
+                for (int l = 0; l < 4; ++l) ps[l] = ps[l] + v[q + l] * sv[q + l];
             const double t0 = ps[0] + ps[1], t1 = ps[2] + ps[3];
-            s += t0 + t1;
-            for (; k < a.hsz; ++k) s += v[k] * sv[k];
+            main_v[4 * k] = t0 + t1;
+            for (int r = 0; r < tail; ++r, ++q) main_v[4 * k + 1 + r] = (double)(v[q] * sv[q]);
         }
+    }
+    __syncthreads();
+    if (!live || lane != 0) return;
+    double s = a.rho;
+    for (int k = 0; k < nblk; ++k) {
+        s += main_v[4 * k];
+        for (int r = 0; r < tail; ++r) s += main_v[4 * k + 1 + r];
+    }
     if (s >= a.hit) {
         const int slot = atomicAdd(a.hits, 1);
         if (slot < a.cap) {
@@ -378,7 +392,10 @@ static int hog_check(const tbdk_hog_params* p)
     if (p->block_w % p->cell_w || p->block_h % p->cell_h) return TBDK_EINVAL;
     if (p->block_w > p->win_w || p->block_h > p->win_h) return TBDK_EINVAL;
     const int ncells = (p->block_w / p->cell_w) * (p->block_h / p->cell_h);
-    if (p->nbins < 1 || p->nbins > kHogMaxBins || ncells > kHogMaxCells) return TBDK_EINVAL;
+    if (p->nbins < 2 || p->nbins > kHogMaxBins || ncells > kHogMaxCells) return TBDK_EINVAL;
+    const int64_t wblocks = (int64_t)((p->win_w - p->block_w) / p->block_stride_x + 1) *
+                            ((p->win_h - p->block_h) / p->block_stride_y + 1);
+    if (wblocks * 4 * kHogWinPerWg * (int64_t)sizeof(double) > 64 * 1024) return TBDK_EINVAL;  // window LDS
     if (ncells * p->nbins < 4) return TBDK_EINVAL;  // normalizeBlockHistogram reads 4 lanes
     if (p->block_w * p->block_h > 64 * 64) return TBDK_EINVAL;
     return TBDK_OK;
@@ -555,10 +572,7 @@ static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog
     const int nb = nbx * nby;
     const dim3 grid((nb + per_wg - 1) / per_wg);
     const size_t lds = sizeof(float) * per_wg * pl.hsz;
-    if (p->nbins <= 9)
-        hipLaunchKernelGGL(hog_block_kernel<9>, grid, dim3(256), lds, s, a);
-    else
-        hipLaunchKernelGGL(hog_block_kernel<kHogMaxBins>, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(hog_block_kernel, grid, dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
@@ -587,7 +601,9 @@ static hipError_t run_level(tbdk_ctx* ctx, HogScratch* S, const HogPlan& pl, con
     a.rho = rho, a.hit = p->hit_threshold, a.level = level;
     a.hits = S->hits, a.scores = S->scores, a.cap = hit_cap;
     rec = timing_begin(ctx, "hog_window", s);
-    hipLaunchKernelGGL(hog_window_kernel, dim3((a.nwx * a.nwy + 255) / 256), dim3(256), 0, s, a);
+    const int nwin = a.nwx * a.nwy;
+    const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);
+    hipLaunchKernelGGL(hog_window_kernel, dim3((nwin + kHogWinPerWg - 1) / kHogWinPerWg), dim3(256), lds, s, a);
     timing_end(ctx, rec, s);
     return hipGetLastError();
 }
