@@ -129,7 +129,7 @@ class TbdLoop:
         """Record per-object tracking results of detections with ground-truth ids
         (tbdk_tbd_set_trajectories); keep `traj` alive while attached."""
         self._traj = traj
-        _lib.check(self.ctx.lib.tbdk_tbd_set_trajectories(self.handle, traj.handle if traj else None),
+        _lib.check(self.ctx.lib.tbdk_tbd_set_trajectories(self.handle, traj.handle if traj is not None else None),
                    "tbdk_tbd_set_trajectories")
 
     def write_tracking_output(self, frame_count: int, path: str | None = None, history_ages=None,
@@ -214,7 +214,7 @@ class Tracker:
     def setRand(self, rng: "CRand | None"):
         """Draw new tracks' colours from rng (the reference's global rand())."""
         self._rng = rng
-        _lib.check(self.lib.tbdk_tracker_set_rand(self.handle, rng.handle if rng else None), "tbdk_tracker_set_rand")
+        _lib.check(self.lib.tbdk_tracker_set_rand(self.handle, rng.handle if rng is not None else None), "tbdk_tracker_set_rand")
 
     def storeTracks(self, buf: "TrackBuffer", slot: int):
         """buf[slot] = getTracks() (the sample's track output buffer)."""
@@ -222,7 +222,7 @@ class Tracker:
 
     def setTracks(self, buf: "TrackBuffer | None", slot: int = -1):
         """setTracks(buf[slot]); no buffer or slot < 0 sets no tracks (tbd.cpp:187-190)."""
-        _lib.check(self.lib.tbdk_tracker_load_tracks(self.handle, buf.handle if buf else None, int(slot)),
+        _lib.check(self.lib.tbdk_tracker_load_tracks(self.handle, buf.handle if buf is not None else None, int(slot)),
                    "tbdk_tracker_load_tracks")
 
     def getTracks(self):
