@@ -13,6 +13,7 @@
 #ifndef TBDK_HPP
 #define TBDK_HPP
 
+#include <cstdio>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -340,6 +341,90 @@ private:
 };
 
 }  // namespace cuda
+
+namespace cuda {
+
+// cv::cuda::HOG (cudaobjdetect.hpp:75-180) with the CPU HOGDescriptor's results
+// (objdetect/src/hog.cpp): create / setters / setSVMDetector / detectMultiScale.
+// Detector coefficients stay on the host; getDefaultPeopleDetector's tables ship
+// as opencv_amd/data/hog_people_{64x128,48x96}.f32 (loadDetector reads them).
+class HOG {
+public:
+    static std::unique_ptr<HOG> create(Context& ctx, Size winSize = {64, 128}, Size blockSize = {16, 16},
+                                       Size blockStride = {8, 8}, Size cellSize = {8, 8}, int nbins = 9)
+    {
+        std::unique_ptr<HOG> h(new HOG(ctx));
+        tbdk_hog_default_params(&h->p_);
+        h->p_.win_w = winSize.width, h->p_.win_h = winSize.height;
+        h->p_.block_w = blockSize.width, h->p_.block_h = blockSize.height;
+        h->p_.block_stride_x = blockStride.width, h->p_.block_stride_y = blockStride.height;
+        h->p_.cell_w = cellSize.width, h->p_.cell_h = cellSize.height;
+        h->p_.nbins = nbins;
+        h->p_.win_stride_x = blockStride.width, h->p_.win_stride_y = blockStride.height;
+        h->getDescriptorSize();  // throws on an invalid geometry (HOG_Impl's asserts)
+        return h;
+    }
+    void setGammaCorrection(bool v) { p_.gamma_correction = v; }
+    void setL2HysThreshold(double v) { p_.l2hys_threshold = v; }
+    void setNumLevels(int v) { p_.nlevels = v; }
+    int getNumLevels() const { return p_.nlevels; }
+    void setHitThreshold(double v) { p_.hit_threshold = v; }
+    double getHitThreshold() const { return p_.hit_threshold; }
+    void setWinStride(Size s) { p_.win_stride_x = s.width, p_.win_stride_y = s.height; }
+    void setScaleFactor(double v) { p_.scale0 = v; }
+    double getScaleFactor() const { return p_.scale0; }
+    void setGroupThreshold(int v) { p_.group_threshold = v; }
+    int getGroupThreshold() const { return p_.group_threshold; }
+    void setWinSigma(double v) { p_.win_sigma = v; }
+    int getDescriptorSize() const
+    {
+        int n = 0;
+        check(tbdk_hog_descriptor_size(&p_, &n), "HOG: invalid geometry");
+        return n;
+    }
+    void setSVMDetector(const std::vector<float>& d)
+    {
+        const size_t n = (size_t)getDescriptorSize();
+        if (d.size() != n && d.size() != n + 1) throw Error(TBDK_EINVAL, "HOG::setSVMDetector");
+        svm_ = d;
+    }
+    // reads one of the shipped detector tables (little-endian float32)
+    static std::vector<float> loadDetector(const char* path)
+    {
+        std::vector<float> v;
+        if (FILE* f = std::fopen(path, "rb")) {
+            float x;
+            while (std::fread(&x, 4, 1, f) == 1) v.push_back(x);
+            std::fclose(f);
+        }
+        if (v.empty()) throw Error(TBDK_EINVAL, "HOG::loadDetector");
+        return v;
+    }
+    // img: device u8, 1 (gray), 3 (BGR) or 4 (BGRA) channels; returns (x, y, w, h) rects
+    std::vector<tbdk_roi> detectMultiScale(const GpuImage& img, int channels, std::vector<double>* confidences = nullptr,
+                                           void* stream = nullptr)
+    {
+        std::vector<int32_t> r(4 * 4096);
+        std::vector<double> w(4096);
+        int n = 0;
+        check(tbdk_hog_detect_multiscale(ctx_->get(), img.data, img.width, img.height, img.pitch, channels, &p_,
+                                         svm_.data(), (int)svm_.size(), r.data(), w.data(), 4096, &n, stream),
+              "tbdk_hog_detect_multiscale");
+        std::vector<tbdk_roi> out(n);
+        for (int i = 0; i < n; ++i) out[i] = tbdk_roi{r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]};
+        if (confidences) confidences->assign(w.begin(), w.begin() + n);
+        return out;
+    }
+
+private:
+    explicit HOG(Context& ctx) : ctx_(&ctx) {}
+    Context* ctx_;
+    tbdk_hog_params p_{};
+    std::vector<float> svm_;
+};
+
+}  // namespace cuda
+
 
 // The tracking section of samples/gpu/tbd.cpp:624-706 (cv::tbd::Tracker +
 // KLT box propagation) for one video stream.

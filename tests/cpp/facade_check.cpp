@@ -79,7 +79,17 @@ int main(int argc, char** argv)
                 near += std::abs(f[0] - 1.5f) < 0.25f && std::abs(f[1] + 0.5f) < 0.25f;
             }
         std::printf("dense pyrlk interior near-shift %d / %d\n", near, tot);
-        return near * 10 >= tot * 6 ? 0 : 9;
+        if (near * 10 < tot * 6) return 9;
+        // HOG through the facade: every window of a gray frame scored, grouped
+        auto hog = tbdk::cuda::HOG::create(ctx, {48, 96});
+        std::vector<float> svm(hog->getDescriptorSize() + 1, 0.f);
+        svm.back() = 1.f;  // bias only: every window scores 1 >= the hit threshold
+        hog->setSVMDetector(svm);
+        hog->setNumLevels(3);
+        std::vector<double> conf;
+        const auto rects = hog->detectMultiScale(a, 1, &conf);
+        std::printf("hog rects %zu\n", rects.size());
+        return !rects.empty() && conf.size() == rects.size() && conf[0] == 1.0 ? 0 : 10;
     } catch (const tbdk::Error& e) {
         std::printf("tbdk::Error: %s\n", e.what());
         return (!want_gpu && e.code() == TBDK_ENODEV) ? 0 : 7;
