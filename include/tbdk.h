@@ -311,7 +311,7 @@ typedef struct tbdk_hog_params {
     int32_t block_w, block_h;               /* 16 x 16 */
     int32_t block_stride_x, block_stride_y; /* 8, 8 */
     int32_t cell_w, cell_h;                 /* 8, 8 */
-    int32_t nbins;                          /* 9 (1..32) */
+    int32_t nbins;                          /* 9 (2..32) */
     double win_sigma;                       /* -1: (block_w + block_h) / 8 */
     double l2hys_threshold;                 /* 0.2 */
     int32_t gamma_correction;               /* 1 */
@@ -345,7 +345,10 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
 int tbdk_hog_detect(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, int cn,
                     const tbdk_hog_params* params, const float* svm, int svm_len, int32_t* xy, double* scores,
                     int max_hits, int* nhits, void* stream);
-/* Stage entry points (parity tests).  resize(src, dst, (dw, dh), INTER_LINEAR_EXACT)
+/* The HOG calls of one context share its scratch (cell table, level image,
+ * gradients, hits). A call on a different stream than the context's previous HOG
+ * call first synchronises that previous stream.
+ * Stage entry points (parity tests).  resize(src, dst, (dw, dh), INTER_LINEAR_EXACT)
  * of a u8 image (imgproc/src/resize.cpp:732-891): */
 int tbdk_hog_resize(tbdk_ctx* ctx, const uint8_t* src, int width, int height, int pitch, int cn, uint8_t* dst,
                     int dst_width, int dst_height, int dst_pitch, void* stream);

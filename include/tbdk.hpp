@@ -404,12 +404,19 @@ public:
     std::vector<tbdk_roi> detectMultiScale(const GpuImage& img, int channels, std::vector<double>* confidences = nullptr,
                                            void* stream = nullptr)
     {
-        std::vector<int32_t> r(4 * 4096);
-        std::vector<double> w(4096);
+        std::vector<int32_t> r;
+        std::vector<double> w;
         int n = 0;
-        check(tbdk_hog_detect_multiscale(ctx_->get(), img.data, img.width, img.height, img.pitch, channels, &p_,
-                                         svm_.data(), (int)svm_.size(), r.data(), w.data(), 4096, &n, stream),
-              "tbdk_hog_detect_multiscale");
+        for (int cap = 4096;; cap *= 4) {  // grow and call again while the results overflow
+            r.resize(4 * (size_t)cap);
+            w.resize(cap);
+            const int rc = tbdk_hog_detect_multiscale(ctx_->get(), img.data, img.width, img.height, img.pitch,
+                                                      channels, &p_, svm_.data(), (int)svm_.size(), r.data(),
+                                                      w.data(), cap, &n, stream);
+            if (rc == TBDK_ENOMEM && n == cap) continue;
+            check(rc, "tbdk_hog_detect_multiscale");
+            break;
+        }
         std::vector<tbdk_roi> out(n);
         for (int i = 0; i < n; ++i) out[i] = tbdk_roi{r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]};
         if (confidences) confidences->assign(w.begin(), w.begin() + n);

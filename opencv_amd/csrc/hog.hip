@@ -28,7 +28,6 @@ namespace tbdk {
 
 constexpr int kHogMaxBins = 32;
 constexpr int kHogMaxCells = 16;
-constexpr int kHogMaxLevels = 256;
 
 struct HogScratch {
     uint8_t* level = nullptr;  // resized level image (u8, cn)
@@ -40,7 +39,21 @@ struct HogScratch {
     int* hits = nullptr;       // [0] count, then (level, x, y) int triples
     double* scores = nullptr;
     int64_t cap_px = 0, cap_blocks = 0, cap_svm = 0, cap_cells = 0, cap_hits = 0;
+    hipStream_t stream = nullptr;  // stream of the last call that used this scratch
+    bool used = false;
 };
+
+// The scratch (cell table, level image, gradients, blocks, hits) is rewritten by
+// every call. A call on another stream than the previous one first drains that
+// stream, so kernels still reading the old contents never see the new ones.
+static hipError_t claim(HogScratch* S, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+    if (S->used && S->stream != s) e = hipStreamSynchronize(S->stream);
+    S->stream = s;
+    S->used = true;
+    return e;
+}
 
 __device__ __forceinline__ int hog_reflect101(int p, int len)
 {
@@ -146,7 +159,11 @@ struct HogGradArgs {
     int qpitch;  // bytes
     int nbins;
     float angle_scale;
-    int vec_mag;  // magnitude32f / fastAtan32f take the 8-lane path (row >= 16)
+    // cartToPolar hands each row to magnitude32f / fastAtan32f in chunks of
+    // BLOCK_SIZE = 1024 (core/src/mathfuncs.cpp:285-298, precomp.hpp:269); a chunk
+    // shorter than 2 x 8 lanes takes the scalar forms (mathfuncs_core.simd.hpp:131-138,
+    // 202-207), so the form is chosen per pixel from its chunk's length
+    int vec_min_len;
     float lut[256];
 };
 
@@ -209,8 +226,9 @@ __global__ __launch_bounds__(256) void hog_grad_kernel(HogGradArgs a)
         dx = k == 0 ? ddx[0] : k == 1 ? ddx[1] : ddx[2];
         dy = k == 0 ? ddy[0] : k == 1 ? ddy[1] : ddy[2];
     }
-    const float m = a.vec_mag ? sqrtf(fmaf(dx, dx, dy * dy)) : sqrtf(dx * dx + dy * dy);
-    float ang = hog_fast_atan(dy, dx, a.vec_mag) * a.angle_scale - 0.5f;
+    const int vec = a.w - (x & ~1023) >= a.vec_min_len;  // length of x's 1024-chunk >= 16
+    const float m = vec ? sqrtf(fmaf(dx, dx, dy * dy)) : sqrtf(dx * dx + dy * dy);
+    float ang = hog_fast_atan(dy, dx, vec) * a.angle_scale - 0.5f;
     int hidx = (int)floorf(ang);
     ang -= hidx;
     *reinterpret_cast<float2*>(a.grad + (size_t)y * a.gpitch + 2 * x) = make_float2(m * (1.f - ang), m * ang);
@@ -549,7 +567,7 @@ static hipError_t launch_grad(const uint8_t* img, int w, int h, int pitch, int c
     a.grad = grad, a.gpitch = gpitch_f, a.qangle = qa, a.qpitch = qpitch;
     a.nbins = p->nbins;
     a.angle_scale = p->signed_gradient ? (float)(p->nbins / (2.0 * M_PI)) : (float)(p->nbins / M_PI);
-    a.vec_mag = w >= 16;
+    a.vec_min_len = 16;  // chunk length from which the 8-lane forms run
     for (int i = 0; i < 256; ++i) a.lut[i] = p->gamma_correction ? std::sqrt((float)i) : (float)i;
     hipLaunchKernelGGL(hog_grad_kernel, dim3((w + 255) / 256, h), dim3(256), 0, s, a);
     return hipGetLastError();
@@ -608,11 +626,13 @@ static hipError_t run_level(tbdk_ctx* ctx, HogScratch* S, const HogPlan& pl, con
     return hipGetLastError();
 }
 
-static int reserve(tbdk_ctx* ctx, int w, int h, int cn, const HogPlan& pl, int svm_len, int64_t hit_cap)
+static int reserve(tbdk_ctx* ctx, int w, int h, int cn, const HogPlan& pl, int svm_len, int64_t hit_cap,
+                   hipStream_t s)
 {
     if (!ctx->hog) ctx->hog = new (std::nothrow) HogScratch();
     HogScratch* S = ctx->hog;
     if (!S) return TBDK_ENOMEM;
+    if (claim(S, s) != hipSuccess) return TBDK_EHIP;
     const int64_t px = (int64_t)w * h;
     int rc = TBDK_OK;
     if (px > S->cap_px) {
@@ -725,7 +745,7 @@ static int prepare(tbdk_ctx* ctx, const uint8_t* img, int w, int h, int pitch, i
     if (rc != TBDK_OK) return rc;
     make_plan(p, pl);
     if (svm_len != pl.dsize && svm_len != pl.dsize + 1) return TBDK_EINVAL;  // checkDetectorSize (hog.cpp:106-112)
-    rc = reserve(ctx, w, h, cn, pl, svm_len, hit_cap);
+    rc = reserve(ctx, w, h, cn, pl, svm_len, hit_cap, s);
     if (rc != TBDK_OK) return rc;
     HogScratch* S = ctx->hog;
     hipError_t e = hipMemcpyAsync(S->svm, svm, sizeof(float) * svm_len, hipMemcpyHostToDevice, s);
@@ -847,7 +867,7 @@ int tbdk_hog_blocks(tbdk_ctx* ctx, const float* grad, int grad_pitch, const uint
     HogPlan pl;
     make_plan(params, pl);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    int rc = reserve(ctx, 1, 1, 1, pl, 1, 1);
+    int rc = reserve(ctx, 1, 1, 1, pl, 1, 1, s);
     if (rc != TBDK_OK) return rc;
     hipError_t e = upload_plan(ctx->hog, pl, s);
     if (e != hipSuccess) return map_status(e);
@@ -899,7 +919,7 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
     // level scales (hog.cpp:2058-2073)
     std::vector<double> lv;
     double scale = 1.;
-    for (int l = 0; l < params->nlevels && l < kHogMaxLevels; ++l) {
+    for (int l = 0; l < params->nlevels; ++l) {
         lv.push_back(scale);
         if (cv_round_d(width / scale) < params->win_w || cv_round_d(height / scale) < params->win_h ||
             params->scale0 <= 1) {

@@ -165,7 +165,9 @@ void orc_hog_gradient(const uint8_t* img, int w, int h, int pitch, int cn, int n
     float lut[256];
     for (int i = 0; i < 256; i++) lut[i] = gamma ? sqrtf((float)i) : (float)i;
     const float angle_scale = signed_grad ? (float)(nbins / (2.0 * M_PI)) : (float)(nbins / M_PI);
-    const int vec_mag = w >= 16; /* AVX2 magnitude/atan need 2 x 8 lanes */
+    /* cartToPolar feeds magnitude32f/fastAtan32f 1024-element chunks of the row
+     * (core/src/mathfuncs.cpp:285-298, BLOCK_SIZE precomp.hpp:269); a chunk shorter
+     * than 2 x 8 AVX2 lanes runs the scalar forms (mathfuncs_core.simd.hpp:131-138,202-207) */
     const int simd_w = w & ~3;   /* the SSE2 3-channel body */
     for (int y = 0; y < h; y++) {
         const uint8_t* P = img + (size_t)y * pitch;
@@ -195,6 +197,7 @@ void orc_hog_gradient(const uint8_t* img, int w, int h, int pitch, int cn, int n
                     dx = ddx[k], dy = ddy[k];
                 }
             }
+            const int chunk = w - (x / 1024) * 1024, vec_mag = (chunk < 1024 ? chunk : 1024) >= 16;
             const float m = vec_mag ? sqrtf(fmaf(dx, dx, dy * dy)) : sqrtf(dx * dx + dy * dy);
             float ang = fast_atan(dy, dx, vec_mag) * angle_scale - 0.5f;
             int hidx = (int)floorf(ang);

@@ -89,7 +89,13 @@ int main(int argc, char** argv)
         std::vector<double> conf;
         const auto rects = hog->detectMultiScale(a, 1, &conf);
         std::printf("hog rects %zu\n", rects.size());
-        return !rects.empty() && conf.size() == rects.size() && conf[0] == 1.0 ? 0 : 10;
+        if (rects.empty() || conf.size() != rects.size() || conf[0] != 1.0) return 10;
+        // ungrouped, stride 4: more hits than the first result buffer (4096) holds
+        hog->setGroupThreshold(0);
+        hog->setWinStride({4, 4});
+        const auto all = hog->detectMultiScale(a, 1, &conf);
+        std::printf("hog ungrouped %zu\n", all.size());
+        return all.size() > 4096 && conf.size() == all.size() ? 0 : 11;
     } catch (const tbdk::Error& e) {
         std::printf("tbdk::Error: %s\n", e.what());
         return (!want_gpu && e.code() == TBDK_ENODEV) ? 0 : 7;

@@ -49,7 +49,7 @@ def test_resize_exact_bit_exact(gpu, cn, src, dst):
 
 
 @pytest.mark.parametrize("cn", [1, 3, 4])
-@pytest.mark.parametrize("w,h", [(640, 480), (130, 77), (15, 33), (6, 5)])
+@pytest.mark.parametrize("w,h", [(640, 480), (130, 77), (15, 33), (6, 5), (1031, 9), (2050, 7), (1040, 5)])
 @pytest.mark.parametrize("gamma,signed", [(True, False), (False, True)])
 def test_gradient_bit_exact(gpu, cn, w, h, gamma, signed):
     from opencv_amd import hog

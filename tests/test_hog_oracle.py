@@ -66,6 +66,32 @@ def test_gradient_magnitude_and_bins():
     assert np.array_equal(qa[..., 1], np.where(qa[..., 0] + 1 < 9, qa[..., 0] + 1, 0))
 
 
+@pytest.mark.parametrize("w", [1031, 2050, 1040])
+def test_gradient_form_follows_cartToPolar_chunks(w):
+    """cartToPolar feeds magnitude32f/fastAtan32f 1024-element chunks of each row
+    (core/src/mathfuncs.cpp:285-298); a chunk under 16 elements takes the scalar forms
+    (mathfuncs_core.simd.hpp:131-138,202-207). A column keeps its form when cut out
+    into a crop whose single chunk has the same length class."""
+    rng = np.random.default_rng(w)
+    img = rng.integers(0, 256, (6, w), dtype=np.uint8)
+    g, q = O.hog_gradient(img, nbins=9, gamma=True)
+    base = (w - 1) // 1024 * 1024
+    tail = w - base
+    # the last chunk's interior columns, computed in a crop of the same length class
+    lo = base - 1
+    crop = np.ascontiguousarray(img[:, lo:lo + min(tail, 15) + 1 if tail < 16 else lo + 20])
+    gc, qc = O.hog_gradient(crop, nbins=9, gamma=True)
+    n = crop.shape[1] - 2
+    assert np.array_equal(g[1:-1, base:base + n], gc[1:-1, 1:1 + n])
+    assert np.array_equal(q[1:-1, base:base + n], qc[1:-1, 1:1 + n])
+    # columns of a full chunk run the 8-lane forms: equal to a 20-wide (vector) crop
+    gv, _ = O.hog_gradient(np.ascontiguousarray(img[:, 500:520]), nbins=9, gamma=True)
+    assert np.array_equal(g[1:-1, 501:519], gv[1:-1, 1:19])
+    if tail < 16:  # and the scalar tail differs from the vector form somewhere
+        gs, _ = O.hog_gradient(np.ascontiguousarray(img[:, 500:515]), nbins=9, gamma=True)
+        assert not np.array_equal(gs[1:-1, 1:14], g[1:-1, 501:514])
+
+
 def test_gradient_three_channels_picks_the_strongest():
     rng = np.random.default_rng(2)
     gray = rng.integers(0, 256, (24, 37), dtype=np.uint8)
