@@ -274,6 +274,7 @@ def main():
     ap.add_argument("--api", choices=["run", "ahead", "step"], default="run",
                     help="run: tbdk_tbd_run (native frame loop with look-ahead); ahead: per-frame "
                          "tbdk_tbd_step_ahead; step: per-frame tbdk_tbd_step (no look-ahead)")
+    ap.add_argument("--lk-impl", type=int, default=0, help="PyrLK kernel (ctx option lk_impl; 0 auto)")
     ap.add_argument("--kstats", default="lk_sparse",
                     help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
                          "each timed launch adds two event records to the frame's host work.  The other "
@@ -308,6 +309,8 @@ def main():
     from opencv_amd import klt, tbd
 
     ctx = klt.Context.get(dev)
+    if args.lk_impl:
+        ctx.set_option("lk_impl", args.lk_impl)
     nframes = args.warmup + args.steps
     frames, gt = klt.synth_render(args.seed + rank, args.width, args.height, args.objects, 0, nframes,
                                   device=dev, ctx=ctx)

@@ -67,7 +67,8 @@ typedef struct tbdk_lk_params {
     double epsilon;                  /* default 0.01, clamped to [0, 10] then squared */
     int32_t flags;                   /* TBDK_OPTFLOW_* */
     float min_eig_threshold;         /* default 1e-4 */
-    int32_t impl;                    /* 0 auto; 1 register-strip kernel; 2 generic LDS kernel */
+    int32_t impl;                    /* 0 auto; 1 register-strip kernel; 2 generic LDS kernel;
+                                        3 several points per wave (all bit-identical) */
 } tbdk_lk_params;
 
 /* ---- context ------------------------------------------------------------ */
@@ -79,7 +80,10 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *   "gftt_eig_redo" (0/1): treat every row-segment boundary of the GFTT
  *       eigenvalue strips as a fresh-start mismatch, forcing the re-walk
  *       rounds taken when a segment's fresh start differs from the
- *       reference's running box-filter sum (results equal). */
+ *       reference's running box-filter sum (results equal).
+ *   "lk_impl" (0..3): the PyrLK kernel taken when tbdk_lk_params.impl is 0
+ *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
+ *       (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 
 /* device ordinal of the context */

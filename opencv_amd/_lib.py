@@ -278,7 +278,7 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("TBDK_LIB") or LIB_PATH  # TBDK_LIB: an alternative build (tuning runs)
     if not os.path.exists(p):
         raise TbdkError(
             f"libtbdk.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

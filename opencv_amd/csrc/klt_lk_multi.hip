@@ -1,0 +1,346 @@
+// klt_lk_multi.hip — sparse pyramidal LK with several points per wave (gfx950).
+//
+// Same algorithm and bit-identical results as klt_lk_strip.hip / klt_lk.hip
+// (CPU calcOpticalFlowPyrLK numerics, LKTrackerInvoker video/src/lkpyramid.cpp:178-695,
+// exact integer sums rounded once to float), laid out so that the per-point
+// bookkeeping of a Newton step is shared by P = 64 / WW points:
+//   * lane = one window column x of one point: point k of the wave owns lanes
+//     [k*WW, (k+1)*WW) (win 21: 3 points, lane 63 idle), and each lane keeps all
+//     WH rows of its column (I patch x32, interpolated Scharr Ix/Iy, the J
+//     column pairs) in VGPRs for every Newton iteration of the level;
+//   * the bilinear weights, the 2x2 solve and the stopping tests run once per
+//     lane for all P points at the cost of one (they are per-point values held
+//     by every lane of the point), where the one-point-per-wave kernel spends a
+//     wave-wide instruction on a single point's scalar math;
+//   * per-point sums over the point's WW lanes: every lane partial is split as
+//     hi * 2^15 + lo (|hi| < 2^16, 0 <= lo < 2^15), both halves are scanned over
+//     the wave in int32 with six DPP adds (row_shr 1/2/4/8, row_bcast 15/31; no
+//     overflow), and each lane reads its point's segment (end - start) back by
+//     ds_bpermute; hi * 2^15 + lo in double is the exact integer sum, rounded
+//     once to float — the same value as the exact int64 sum of the other kernels;
+//   * control flow stays wave-uniform (levels, Newton steps while any point is
+//     active, J reloads when any point's integer origin moved), so every DPP and
+//     bpermute runs with all lanes on; a point that stopped keeps its values by
+//     selects.
+#include "lk_device.hpp"
+
+namespace tbdk {
+
+namespace {
+
+using namespace lkdev;
+
+// inclusive prefix sum over the 64 lanes (all lanes active)
+__device__ __forceinline__ int scan64(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Exact per-point sums of N int32 lane partials (|partial| < 2^30): every lane
+// gets its own point's sum, rounded once to float.  e4 / s4: byte addresses of
+// the point's last lane and of the lane before its first (s4 < 0 for point 0).
+template <int N>
+__device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N])
+{
+    int hi[N], lo[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        hi[k] = scan64(v[k] >> 15);
+        lo[k] = scan64(v[k] & 0x7FFF);
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        int h = __builtin_amdgcn_ds_bpermute(e4, hi[k]);
+        int l = __builtin_amdgcn_ds_bpermute(e4, lo[k]);
+        const int hs = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, hi[k]);
+        const int ls = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, lo[k]);
+        if (s4 >= 0) h -= hs, l -= ls;
+        out[k] = (float)((double)h * 32768.0 + (double)l);  // exact in double, one rounding
+    }
+}
+
+// per-point sum of small lane values (no split: |total| < 2^31)
+__device__ __forceinline__ int seg_sum_small(int v, int e4, int s4)
+{
+    v = scan64(v);
+    const int e = __builtin_amdgcn_ds_bpermute(e4, v);
+    const int s = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, v);
+    return s4 < 0 ? e : e - s;
+}
+
+__device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+
+}  // namespace
+
+#ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
+#define TBDK_MULTI_BOUNDS __launch_bounds__(256, TBDK_LK_MULTI_MINW)
+#else
+#define TBDK_MULTI_BOUNDS __launch_bounds__(256)
+#endif
+
+template <int WW, int WH>
+__global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
+{
+    constexpr int P = 64 / WW;         // points per wave
+    constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
+    const int lane = threadIdx.x & 63;
+    const int k = lane / WW;  // point slot of this lane (k == P: idle lane)
+    const int x = lane - k * WW;
+    const int wave = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const int i = k < P ? seg_point(a, wave * P + k) : -1;
+    const bool valid = i >= 0;
+    if (!any_lane(valid)) return;  // wave-uniform
+    const int e4 = 4 * (k * WW + WW - 1), s4 = 4 * (k * WW - 1);
+    const int rnd9 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 5 - 1));
+    const int rnd14 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 1));
+
+    const float FLT_SCALE = 1.f / (1 << 20);
+    const float halfx = (WW - 1) * 0.5f, halfy = (WH - 1) * 0.5f;
+    const float p0x = valid ? a.prev_pts[2 * i] : 0.f, p0y = valid ? a.prev_pts[2 * i + 1] : 0.f;
+    float outx = 0.f, outy = 0.f;
+    if ((a.flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) && valid) {
+        outx = a.next_pts[2 * i];
+        outy = a.next_pts[2 * i + 1];
+    }
+    int status = 1, nit = 0;
+    float errv = 0.f;
+
+    for (int level = a.max_level; level >= 0; --level) {
+        const LkLevel L = a.lv[level];
+        const float sc = (float)(1. / (1 << level));
+        float prevx = p0x * sc, prevy = p0y * sc;
+        float nextx, nexty;
+        if (level == a.max_level) {
+            if (a.flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) {
+                nextx = outx * sc;
+                nexty = outy * sc;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = outx * 2.f;
+            nexty = outy * 2.f;
+        }
+        outx = nextx;
+        outy = nexty;
+
+        prevx -= halfx;
+        prevy -= halfy;
+        const int ipx = (int)floorf(prevx), ipy = (int)floorf(prevy);
+        bool act = valid;
+        if (ipx < -WW || ipx >= L.w || ipy < -WH || ipy >= L.h) {
+            if (level == 0) {
+                status = 0;
+                errv = 0.f;
+            }
+            act = false;
+        }
+        if (!any_lane(act)) continue;
+        uint32_t w0, w1;
+        bilinear_weights(prevx - ipx, prevy - ipy, w0, w1);
+
+        const int hp = L.h + 2 * L.ipad;
+        const __amdgpu_buffer_rsrc_t rI = make_rsrc(L.I, L.ipitch * hp + 256);
+        const __amdgpu_buffer_rsrc_t rD = make_rsrc(L.D, L.dpitch * (L.h + 2 * L.dpad) + 256);
+        const __amdgpu_buffer_rsrc_t rJ = make_rsrc(L.J, L.jpitch * (L.h + 2 * L.jpad) + 256);
+
+        nextx -= halfx;
+        nexty -= halfy;
+        int pinx = (int)floorf(nextx), piny = (int)floorf(nexty);
+        uint32_t jp[WH + 1];
+
+        // ---- I x32 and Ix, Iy of every row, packed by row pairs as int16 x 2
+        uint32_t ipk[NP], gxk[NP], gyk[NP];
+        float A11, A12, A22;
+        {
+            const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
+            const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4) : 0u;
+            uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
+#pragma unroll
+            for (int r = 0; r <= WH; ++r) {
+                ip[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
+                const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);
+                const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);
+                dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
+                dyp[r] = __builtin_amdgcn_perm(d1, d0, 0x07060302u);  // (Iy(x), Iy(x+1))
+            }
+            int acc[3] = {0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const int r = 2 * q;
+                const bool two = r + 1 < WH;
+                const int i0 = bilin_s<W_BITS1 - 5>(ip[r], ip[r + 1], w0, w1, rnd9);
+                const int i1 = two ? bilin_s<W_BITS1 - 5>(ip[r + 1], ip[r + 2], w0, w1, rnd9) : 0;
+                const int x0 = bilin_s<W_BITS1>(dxp[r], dxp[r + 1], w0, w1, rnd14);
+                const int x1 = two ? bilin_s<W_BITS1>(dxp[r + 1], dxp[r + 2], w0, w1, rnd14) : 0;
+                const int y0 = bilin_s<W_BITS1>(dyp[r], dyp[r + 1], w0, w1, rnd14);
+                const int y1 = two ? bilin_s<W_BITS1>(dyp[r + 1], dyp[r + 2], w0, w1, rnd14) : 0;
+                ipk[q] = (uint32_t)i0 | ((uint32_t)i1 << 16);  // both in [0, 8160]
+                gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
+                gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
+                acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
+                acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
+                acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
+            }
+            // J columns at the first Newton position: their loads overlap the G sums
+            {
+                const bool jin = act && !(pinx < -WW || pinx >= L.w || piny < -WH || piny >= L.h);
+                const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + pinx + x + L.jpad) : 0u;
+#pragma unroll
+                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+            }
+            if (k >= P) acc[0] = acc[1] = acc[2] = 0;
+            float s[3];
+            seg_sum_exact<3>(acc, e4, s4, s);
+            // A = float(exact sum) * 2^-20   (lkpyramid.cpp:438-440)
+            A11 = s[0] * FLT_SCALE;
+            A12 = s[1] * FLT_SCALE;
+            A22 = s[2] * FLT_SCALE;
+        }
+        float D = A11 * A22 - A12 * A12;
+        const float minEig =
+            (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+        if (act && (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS)) errv = minEig;
+        if (act && (minEig < a.min_eig || D < 1.19209290e-07F /*FLT_EPSILON*/)) {
+            if (level == 0) status = 0;
+            act = false;
+        }
+        D = 1.f / D;
+
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < a.max_count; ++j) {
+            if (!any_lane(act)) break;
+            const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
+            if (act && (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h)) {
+                if (level == 0) status = 0;
+                act = false;
+            }
+            nit += act ? 1 : 0;
+            const bool moved = act && (inx != pinx || iny != piny);
+            if (any_lane(moved)) {  // uniform: reload the J columns (unchanged for points that did not move)
+                const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
+#pragma unroll
+                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+                pinx = inx;
+                piny = iny;
+            }
+            bilinear_weights(nextx - inx, nexty - iny, w0, w1);
+            int b[2] = {0, 0};
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const int r = 2 * q;
+                const int j0 = bilin_s<W_BITS1 - 5>(jp[r], jp[r + 1], w0, w1, rnd9);
+                const int j1 = r + 1 < WH ? bilin_s<W_BITS1 - 5>(jp[r + 1], jp[r + 2], w0, w1, rnd9) : 0;
+                const s16x2 dk = __builtin_bit_cast(s16x2, (uint32_t)j0 | ((uint32_t)j1 << 16)) -
+                                 __builtin_bit_cast(s16x2, ipk[q]);  // (diff_r, diff_r+1), |diff| <= 8160
+                const uint32_t d = __builtin_bit_cast(uint32_t, dk);
+                b[0] = sdot2(d, gxk[q], b[0]);
+                b[1] = sdot2(d, gyk[q], b[1]);
+            }
+            if (k >= P) b[0] = b[1] = 0;
+            float fb[2];
+            seg_sum_exact<2>(b, e4, s4, fb);
+            const float fb1 = fb[0] * FLT_SCALE;
+            const float fb2 = fb[1] * FLT_SCALE;
+            const float ddx = (A12 * fb2 - A22 * fb1) * D;
+            const float ddy = (A12 * fb1 - A11 * fb2) * D;
+            if (act) {
+                nextx += ddx;
+                nexty += ddy;
+                outx = nextx + halfx;
+                outy = nexty + halfy;
+                if ((double)ddx * ddx + (double)ddy * ddy <= a.eps2) {
+                    act = false;
+                } else if (j > 0 && (double)fabsf(ddx + pdx) < 0.01 && (double)fabsf(ddy + pdy) < 0.01) {
+                    outx -= ddx * 0.5f;
+                    outy -= ddy * 0.5f;
+                    act = false;
+                }
+                pdx = ddx;
+                pdy = ddy;
+            }
+        }
+
+        if (level == 0 && a.err && (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS) == 0) {
+            bool want = valid && status;
+            const float npx = outx - halfx, npy = outy - halfy;
+            const int inx = (int)floorf(npx), iny = (int)floorf(npy);
+            if (want && (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h)) {
+                status = 0;
+                want = false;
+            }
+            if (any_lane(want)) {
+                bilinear_weights(npx - inx, npy - iny, w0, w1);
+                const uint32_t joff = want ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
+#pragma unroll
+                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+                int e = 0;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const int r = 2 * q;
+                    const int i0 = (int)(ipk[q] & 0xFFFFu), i1 = (int)(ipk[q] >> 16);
+                    const int d0 = bilin_s<W_BITS1 - 5>(jp[r], jp[r + 1], w0, w1, rnd9) - i0;
+                    e += d0 < 0 ? -d0 : d0;
+                    if (r + 1 < WH) {
+                        const int d1 = bilin_s<W_BITS1 - 5>(jp[r + 1], jp[r + 2], w0, w1, rnd9) - i1;
+                        e += d1 < 0 ? -d1 : d1;
+                    }
+                }
+                if (k >= P) e = 0;
+                const float errval = (float)seg_sum_small(e, e4, s4);
+                if (want) errv = errval * 1.f / (float)(32 * WW * WH);
+            }
+        }
+    }
+
+    if (valid && x == 0) {
+        a.next_pts[2 * i] = outx;
+        a.next_pts[2 * i + 1] = outy;
+        a.status[i] = (uint8_t)status;
+        if (a.err) a.err[i] = errv;
+        if (a.iters) a.iters[i] = nit;
+    }
+}
+
+#define TBDK_MULTI_WINDOWS(X) X(7) X(9) X(11) X(13) X(15) X(17) X(19) X(21) X(23) X(25) X(27) X(29) X(31)
+
+bool lk_multi_supported(int win_w, int win_h)
+{
+    if (win_w != win_h) return false;
+    switch (win_w) {
+#define TBDK_CASE(W) case W:
+        TBDK_MULTI_WINDOWS(TBDK_CASE)
+#undef TBDK_CASE
+        return true;
+    default:
+        return false;
+    }
+}
+
+hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s)
+{
+    if (!lk_multi_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
+    const int per_wg = 4 * (64 / a.win_w);  // 4 waves of P points
+    const dim3 grid((a.n + per_wg - 1) / per_wg), block(256);
+    switch (a.win_w) {
+#define TBDK_CASE(W)                                                       \
+    case W:                                                                \
+        hipLaunchKernelGGL((lk_multi_kernel<W, W>), grid, block, 0, s, a); \
+        break;
+        TBDK_MULTI_WINDOWS(TBDK_CASE)
+#undef TBDK_CASE
+    default:
+        return hipErrorNotSupported;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace tbdk

@@ -18,26 +18,13 @@
 //     convergence the Newton steps are sub-pixel, so most iterations are pure VALU);
 //   * G / b sums: DPP over 8-lane groups in int32 (cannot overflow), eight
 //     v_readlane into SGPRs, int64 scalar sum -> exact, wave-uniform.
-#include "tbdk_internal.hpp"
+#include "lk_device.hpp"
 
 namespace tbdk {
 
 namespace {
 
-constexpr int W_BITS = 14, W_BITS1 = 14;
-
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
-{
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), c, false);
-}
-
-// bilinear of a packed pixel pair on two rows: (p0 . w0 + p1 . w1 + round) >> shift
-__device__ __forceinline__ int bilin(uint32_t p0, uint32_t p1, uint32_t w0, uint32_t w1, int shift)
-{
-    return sdot2(p0, w0, sdot2(p1, w1, 1 << (shift - 1))) >> shift;
-}
+using namespace lkdev;
 
 template <int CTRL>
 __device__ __forceinline__ int dpp(int v)
@@ -72,30 +59,6 @@ __device__ __forceinline__ void wave_sum_exact(int (&v)[N], long long (&out)[N])
         for (int g = 0; g < 64 / GROUP; ++g) s += (long long)__builtin_amdgcn_readlane(v[k], GROUP * g);
         out[k] = s;
     }
-}
-
-__device__ __forceinline__ void bilinear_weights(float fa, float fb, uint32_t& w0, uint32_t& w1)
-{
-    const int w00 = __float2int_rn((1.f - fa) * (1.f - fb) * (1 << W_BITS));
-    const int w01 = __float2int_rn(fa * (1.f - fb) * (1 << W_BITS));
-    const int w10 = __float2int_rn((1.f - fa) * fb * (1 << W_BITS));
-    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
-    w0 = ((uint32_t)w00 & 0xFFFFu) | ((uint32_t)w01 << 16);
-    w1 = ((uint32_t)w10 & 0xFFFFu) | ((uint32_t)w11 << 16);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-}
-
-// (pixel off, pixel off+1) of the 8 bytes at aligned offset, as an int16 pair
-__device__ __forceinline__ uint32_t load_pair_u8(__amdgpu_buffer_rsrc_t rs, uint32_t aligned, int soff,
-                                                 uint32_t sel)
-{
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned, soff, 0);
-    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned + 4, soff, 0);
-    return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
 }  // namespace
@@ -169,13 +132,11 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
         int ival[R], gx[R], gy[R];
         {
             const uint32_t ioff = (uint32_t)((ipy + row0 + L.ipad) * L.ipitch + ipx + x + L.ipad);
-            const uint32_t isel = 0x0C000C00u | ((ioff & 3u) + (((ioff & 3u) + 1u) << 16));
-            const uint32_t ialn = ioff & ~3u;
             const uint32_t doff = (uint32_t)((ipy + row0 + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4);
             uint32_t ip[R + 1], dxp[R + 1], dyp[R + 1];
 #pragma unroll
             for (int r = 0; r <= R; ++r) {
-                ip[r] = load_pair_u8(rI, ialn, r * L.ipitch, isel);
+                ip[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
                 const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);
                 const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);
                 dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
@@ -227,9 +188,8 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
                 nit++;
                 if (inx != pinx || iny != piny) {  // uniform: reload the J strip
                     const uint32_t joff = (uint32_t)((iny + row0 + L.jpad) * L.jpitch + inx + x + L.jpad);
-                    const uint32_t jsel = 0x0C000C00u | ((joff & 3u) + (((joff & 3u) + 1u) << 16));
 #pragma unroll
-                    for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8(rJ, joff & ~3u, r * L.jpitch, jsel);
+                    for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
                     pinx = inx;
                     piny = iny;
                 }
@@ -270,10 +230,9 @@ __global__ __launch_bounds__(256) void lk_strip_kernel(LkArgs a)
             } else {
                 bilinear_weights(npx - inx, npy - iny, w0, w1);
                 const uint32_t joff = (uint32_t)((iny + row0 + L.jpad) * L.jpitch + inx + x + L.jpad);
-                const uint32_t jsel = 0x0C000C00u | ((joff & 3u) + (((joff & 3u) + 1u) << 16));
                 uint32_t jp[R + 1];
 #pragma unroll
-                for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8(rJ, joff & ~3u, r * L.jpitch, jsel);
+                for (int r = 0; r <= R; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
                 int e[1] = {0};
 #pragma unroll
                 for (int r = 0; r < R; ++r) {

@@ -1,0 +1,80 @@
+// lk_device.hpp — device helpers shared by the register-resident PyrLK kernels
+// (klt_lk_strip.hip, klt_lk_multi.hip): fixed-point bilinear weights and dot
+// products in the reference's integer arithmetic (LKTrackerInvoker,
+// video/src/lkpyramid.cpp:227-303), buffer loads of packed pixel pairs.
+#pragma once
+#include "tbdk_internal.hpp"
+
+namespace tbdk {
+namespace lkdev {
+
+constexpr int W_BITS = 14, W_BITS1 = 14;
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), c, false);
+}
+
+// bilinear of a packed pixel pair on two rows: (p0 . w0 + p1 . w1 + round) >> shift
+// (the reference's _mm_madd_epi16 products and CV_DESCALE, lkpyramid.cpp:288-303)
+__device__ __forceinline__ int bilin(uint32_t p0, uint32_t p1, uint32_t w0, uint32_t w1, int shift)
+{
+    return sdot2(p0, w0, sdot2(p1, w1, 1 << (shift - 1))) >> shift;
+}
+
+// the same with the rounding term taken from an SGPR by the three-operand
+// v_dot2_i32_i16 (the compiler otherwise materialises it with a v_mov per call
+// for the accumulating v_dot2c form)
+template <int SHIFT>
+__device__ __forceinline__ int bilin_s(uint32_t p0, uint32_t p1, uint32_t w0, uint32_t w1, int round_sgpr)
+{
+    int t;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(t) : "v"(p1), "v"(w1), "s"(round_sgpr));
+    return sdot2(p0, w0, t) >> SHIFT;
+}
+
+// iw00..iw11 = cvRound(w * 2^14), iw11 = 2^14 - the others (lkpyramid.cpp:227-234),
+// packed as (w00, w01) and (w10, w11) int16 pairs
+__device__ __forceinline__ void bilinear_weights(float fa, float fb, uint32_t& w0, uint32_t& w1)
+{
+    const int w00 = __float2int_rn((1.f - fa) * (1.f - fb) * (1 << W_BITS));
+    const int w01 = __float2int_rn(fa * (1.f - fb) * (1 << W_BITS));
+    const int w10 = __float2int_rn((1.f - fa) * fb * (1 << W_BITS));
+    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+    w0 = ((uint32_t)w00 & 0xFFFFu) | ((uint32_t)w01 << 16);
+    w1 = ((uint32_t)w10 & 0xFFFFu) | ((uint32_t)w11 << 16);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+
+// (pixel off, pixel off+1) of the 8 bytes at aligned offset, as an int16 pair
+__device__ __forceinline__ uint32_t load_pair_u8(__amdgpu_buffer_rsrc_t rs, uint32_t aligned, int soff, uint32_t sel)
+{
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned, soff, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, aligned + 4, soff, 0);
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// (pixel off, pixel off+1) as an int16 pair from ONE unaligned dword load
+// (gfx950 serves unaligned buffer dword loads; one load and one VGPR per row
+// instead of an aligned dword pair)
+__device__ __forceinline__ uint32_t load_pair_u8_ua(__amdgpu_buffer_rsrc_t rs, uint32_t off, int soff)
+{
+    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, off, soff, 0);
+    return __builtin_amdgcn_perm(v, v, 0x0C010C00u);
+}
+
+// v_perm selector picking bytes (off & 3) and (off & 3) + 1 of the 8 loaded
+// bytes, zero-extended to two int16
+__device__ __forceinline__ uint32_t pair_sel(uint32_t off)
+{
+    return 0x0C000C00u | ((off & 3u) + (((off & 3u) + 1u) << 16));
+}
+
+}  // namespace lkdev
+}  // namespace tbdk

@@ -116,6 +116,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_gftt_eig_redo = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "lk_impl") == 0) {  // kernel used when tbdk_lk_params.impl is 0 (auto)
+        if (value < 0 || value > 3) return TBDK_EINVAL;
+        ctx->opt_lk_impl = (int)value;
+        return TBDK_OK;
+    }
     return TBDK_EINVAL;
 }
 
@@ -323,10 +328,15 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     bool have_d = true;
     for (int l = 0; l <= max_level; ++l)
         if (!a.lv[l].D || a.lv[l].dpad < pad_needed) have_d = false;
-    const bool strip = p->impl != 2 && have_d && lk_strip_supported(p->win_w, p->win_h);
-    if (p->impl == 1 && !strip) return TBDK_EINVAL;
+    // auto: several points per wave when the window has an instantiation, else the
+    // one-point-per-wave strip kernel, else the generic LDS kernel (no derivative planes)
+    if (p->impl < 0 || p->impl > 3) return TBDK_EINVAL;
+    const int impl = p->impl ? p->impl : ctx->opt_lk_impl;
+    const bool multi = (impl == 0 || impl == 3) && have_d && lk_multi_supported(p->win_w, p->win_h);
+    const bool strip = !multi && (impl == 0 || impl == 1) && have_d && lk_strip_supported(p->win_w, p->win_h);
+    if ((p->impl == 1 && !strip) || (p->impl == 3 && !multi)) return TBDK_EINVAL;
     int rec = timing_begin(ctx, "lk_sparse", s);
-    hipError_t e = strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
+    hipError_t e = multi ? launch_lk_multi(a, s) : strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }

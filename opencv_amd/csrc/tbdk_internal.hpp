@@ -60,6 +60,7 @@ struct tbdk_ctx {
     int device = 0;
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
+    int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
@@ -142,6 +143,9 @@ hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);
 // windows without an instantiation (caller falls back to launch_lk_sparse)
 bool lk_strip_supported(int win_w, int win_h);
 hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
+// several points per wave (klt_lk_multi.hip), same results
+bool lk_multi_supported(int win_w, int win_h);
+hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s);
 
 // ---- box propagation (box_fit.hip) ----
 hipError_t launch_box_propagate(const float* prev, const float* next, const uint8_t* status, const int32_t* offsets,

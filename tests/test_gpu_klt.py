@@ -122,7 +122,7 @@ def assert_tolerance(g, sse, frac=0.995, tol=1e-2):
     assert bad.mean() <= 0.01
 
 
-IMPLS = [pytest.param(1, id="strip"), pytest.param(2, id="generic")]
+IMPLS = [pytest.param(3, id="multi"), pytest.param(1, id="strip"), pytest.param(2, id="generic")]
 
 
 @pytest.mark.parametrize("impl", IMPLS)
@@ -152,9 +152,10 @@ def test_lk_window_and_level_variants(gpu, win, maxlev, iters):
     pts = grid_points(240, 320, 7, 0) + np.float32([0.37, 0.61])
     g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters)
     assert_exact(g, ex)
-    if win[0] == win[1] and win[0] <= 31:  # both kernels must agree bit for bit
-        g2, _, _ = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters, impl=2)
-        assert_exact(g2, ex)
+    if win[0] == win[1] and win[0] <= 31:  # every kernel must agree bit for bit
+        for impl in (1, 2):
+            g2, _, _ = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, iters, impl=impl)
+            assert_exact(g2, ex)
 
 
 @pytest.mark.parametrize("impl", IMPLS)

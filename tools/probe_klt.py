@@ -33,11 +33,13 @@ for k in ["pyr_build", "lk_sparse"]:
     print(f"{k}: {c} launches, avg {ms / c * 1000:.1f} us")
 st = r.status.cpu().numpy(); it = r.iters.cpu().numpy()
 print(f"points {n}, tracked {st.mean():.3f}, mean iters {it.mean():.2f}, wall/iter {wall*1e3:.3f} ms")
-# generic kernel for comparison
-lk2 = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30, impl=2)
-ctx.timing_enable(True)
-for _ in range(20):
-    r2 = lk2.calc(P0, P1, pts, want_iters=True)
-torch.cuda.synchronize()
-c, ms = ctx.timing_query("lk_sparse")
-print(f"generic lk_sparse: avg {ms / c * 1000:.1f} us; same result: {torch.equal(r2.next_pts, r.next_pts)}")
+# the other kernels for comparison (impl 1 strip, 2 generic LDS, 3 multi-point)
+for impl in (1, 2, 3):
+    lk2 = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30, impl=impl)
+    ctx.timing_enable(True)
+    for _ in range(20):
+        r2 = lk2.calc(P0, P1, pts, want_iters=True)
+    torch.cuda.synchronize()
+    c, ms = ctx.timing_query("lk_sparse")
+    same = torch.equal(r2.next_pts, r.next_pts) and torch.equal(r2.status, r.status) and torch.equal(r2.iters, r.iters)
+    print(f"impl {impl} lk_sparse: avg {ms / c * 1000:.1f} us; same result: {same}")
