@@ -416,7 +416,10 @@ def main():
         achieved = flops_per_launch / (lk["avg_us"] * 1e-6) / 1e12
     else:
         flops_per_launch, achieved = 0.0, 0.0
-    traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
+    # the auto choice is lk_multi_kernel (several points per wave) for the odd square windows it covers
+    traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}>")
+    if traffic is None:
+        traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic, "kernel": "lk_sparse",
                 "traffic_source": traffic_src,

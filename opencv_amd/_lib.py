@@ -283,6 +283,10 @@ def load(path: str | None = None) -> C.CDLL:
         raise TbdkError(
             f"libtbdk.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP path has no CPU fallback)")
+    # torch carries its own libamdhip64.so.7 (same soname as /opt/rocm's): load it
+    # first so the process holds ONE HIP runtime, whichever of the two is imported
+    # first by the caller (two runtimes -> the second sees no device).
+    import torch  # noqa: F401
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
