@@ -5,19 +5,19 @@
 // exact integer sums rounded once to float), laid out so that the per-point
 // bookkeeping of a Newton step is shared by P = 64 / WW points:
 //   * lane = one window column x of one point: point k of the wave owns lanes
-//     [k*WW, (k+1)*WW) (win 21: 3 points, lane 63 idle), and each lane keeps all
-//     WH rows of its column (I patch x32, interpolated Scharr Ix/Iy, the J
-//     column pairs) in VGPRs for every Newton iteration of the level;
+//     [1 + k*WW, 1 + (k+1)*WW) (win 21: 3 points, lane 0 idle), and each lane
+//     keeps all WH rows of its column (I patch x32, interpolated Scharr Ix/Iy,
+//     the J column pairs) in VGPRs for every Newton iteration of the level;
 //   * the bilinear weights, the 2x2 solve and the stopping tests run once per
 //     lane for all P points at the cost of one (they are per-point values held
 //     by every lane of the point), where the one-point-per-wave kernel spends a
 //     wave-wide instruction on a single point's scalar math;
-//   * per-point sums over the point's WW lanes: every lane partial is split as
-//     hi * 2^15 + lo (|hi| < 2^16, 0 <= lo < 2^15), both halves are scanned over
-//     the wave in int32 with six DPP adds (row_shr 1/2/4/8, row_bcast 15/31; no
-//     overflow), and each lane reads its point's segment (end - start) back by
-//     ds_bpermute; hi * 2^15 + lo in double is the exact integer sum, rounded
-//     once to float — the same value as the exact int64 sum of the other kernels;
+//   * per-point sums over the point's WW lanes: prefix scans over the wave with
+//     six DPP adds (row_shr 1/2/4/8, row_bcast 15/31), each lane reading its
+//     point's segment (end - start) back by ds_bpermute; exact for any window
+//     by a lo/hi split of every partial with the hi parts of up to three sums
+//     packed into one scan (seg_sum_exact), rounded once to float — the same
+//     value as the exact int64 sum of the other kernels;
 //   * control flow stays wave-uniform (levels, Newton steps while any point is
 //     active, J reloads when any point's integer origin moved), so every DPP and
 //     bpermute runs with all lanes on; a point that stopped keeps its values by
@@ -30,48 +30,78 @@ namespace {
 
 using namespace lkdev;
 
-// inclusive prefix sum over the 64 lanes (all lanes active)
-__device__ __forceinline__ int scan64(int v)
+// inclusive prefix sum over the 64 lanes (all lanes active), modulo 2^32
+__device__ __forceinline__ uint32_t scan64(uint32_t v)
 {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
-// Exact per-point sums of N int32 lane partials (|partial| < 2^30): every lane
-// gets its own point's sum, rounded once to float.  e4 / s4: byte addresses of
-// the point's last lane and of the lane before its first (s4 < 0 for point 0).
+// segment total of a scanned value: prefix at the point's last lane minus the
+// prefix at the lane before its first (lane 0 is idle and holds 0, so every
+// point has such a lane)
+__device__ __forceinline__ uint32_t seg_total(uint32_t scanned, int e4, int s4)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(e4, (int)scanned) -
+           (uint32_t)__builtin_amdgcn_ds_bpermute(s4, (int)scanned);
+}
+
+// Exact per-point sums of N <= 3 int32 lane partials (|partial| < 2^30): every
+// lane gets its own point's sum, rounded once to float.  Each partial is split
+// as hi * 2^26 + lo (0 <= lo < 2^26, -16 <= hi < 16).  The lo parts are scanned
+// one per value (a point's lo total is below 21 * 2^26 < 2^31, exact as a
+// modulo-2^32 difference); the hi parts of all N values share ONE scan, packed
+// in 11-bit fields (a point's hi total lies in [-16*21, 15*21] and every field
+// below the top one is recovered by sign extension).  hi * 2^26 + lo in double
+// is the exact integer sum; the one float rounding gives the same value as the
+// exact int64 sum of the other kernels.  e4 / s4: byte addresses of the point's
+// last lane and of the lane before its first.
 template <int N>
 __device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N])
 {
-    int hi[N], lo[N];
+    static_assert(N >= 1 && N <= 3, "three 11-bit fields per packed scan");
+    uint32_t lo[N], hp = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        hi[k] = scan64(v[k] >> 15);
-        lo[k] = scan64(v[k] & 0x7FFF);
+        lo[k] = scan64((uint32_t)v[k] & 0x3FFFFFFu);
+        hp += (uint32_t)(v[k] >> 26) << (11 * k);
     }
+    int h = (int)seg_total(scan64(hp), e4, s4);
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        int h = __builtin_amdgcn_ds_bpermute(e4, hi[k]);
-        int l = __builtin_amdgcn_ds_bpermute(e4, lo[k]);
-        const int hs = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, hi[k]);
-        const int ls = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, lo[k]);
-        if (s4 >= 0) h -= hs, l -= ls;
-        out[k] = (float)((double)h * 32768.0 + (double)l);  // exact in double, one rounding
+        const int hk = k + 1 < N ? (int)((uint32_t)h << 21) >> 21 : h;  // sign-extended low field
+        h = (h - hk) >> 11;
+        const uint32_t l = seg_total(lo[k], e4, s4);
+        out[k] = (float)((double)hk * 67108864.0 + (double)l);  // exact in double, one rounding
     }
 }
 
 // per-point sum of small lane values (no split: |total| < 2^31)
 __device__ __forceinline__ int seg_sum_small(int v, int e4, int s4)
 {
-    v = scan64(v);
-    const int e = __builtin_amdgcn_ds_bpermute(e4, v);
-    const int s = __builtin_amdgcn_ds_bpermute(s4 < 0 ? 0 : s4, v);
-    return s4 < 0 ? e : e - s;
+    return (int)seg_total(scan64((uint32_t)v), e4, s4);
+}
+
+// p0 . w0 + p1 . w1 + c: the reference's bilinear sum started from a per-row
+// VGPR constant (the three-operand v_dot2_i32_i16 keeps c; the compiler
+// otherwise copies c and accumulates with v_dot2c)
+__device__ __forceinline__ int bilin_c(uint32_t p0, uint32_t p1, uint32_t w0, uint32_t w1, int c)
+{
+    int t;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(t) : "v"(p1), "v"(w1), "v"(c));
+    return sdot2(p0, w0, t);
+}
+
+// (t0 >> 9, t1 >> 9) as int16 x 2: bytes 0-1 of t0 >> 9 and bytes 2-3 of
+// t1 << 7 (= the low 16 bits of t1 >> 9 moved up)
+__device__ __forceinline__ uint32_t pack_diff(int t0, int t1)
+{
+    return __builtin_amdgcn_perm((uint32_t)t1 << 7, (uint32_t)(t0 >> 9), 0x07060100u);
 }
 
 __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
@@ -79,10 +109,17 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 
 }  // namespace
 
+// waves per workgroup (tuning builds may change it; the kernel uses no LDS, so
+// one-wave workgroups let a finished wave's slot be refilled at once)
+#ifndef TBDK_LK_MULTI_WAVES
+#define TBDK_LK_MULTI_WAVES 1
+#endif
+constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
+
 #ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
-#define TBDK_MULTI_BOUNDS __launch_bounds__(256, TBDK_LK_MULTI_MINW)
+#define TBDK_MULTI_BOUNDS __launch_bounds__(64 * TBDK_LK_MULTI_WAVES, TBDK_LK_MULTI_MINW)
 #else
-#define TBDK_MULTI_BOUNDS __launch_bounds__(256)
+#define TBDK_MULTI_BOUNDS __launch_bounds__(64 * TBDK_LK_MULTI_WAVES)
 #endif
 
 template <int WW, int WH>
@@ -91,13 +128,15 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     constexpr int P = 64 / WW;         // points per wave
     constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
     const int lane = threadIdx.x & 63;
-    const int k = lane / WW;  // point slot of this lane (k == P: idle lane)
-    const int x = lane - k * WW;
-    const int wave = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    // point k of the wave owns lanes [1 + k*WW, 1 + (k+1)*WW); lane 0 (and any
+    // lane past the last point) is idle with k == P and contributes 0
+    const int k = lane == 0 ? P : (lane - 1) / WW;
+    const int x = k < P ? lane - 1 - k * WW : 0;
+    const int wave = xcd_swizzle(blockIdx.x, gridDim.x) * kMultiWaves + (threadIdx.x >> 6);
     const int i = k < P ? seg_point(a, wave * P + k) : -1;
     const bool valid = i >= 0;
     if (!any_lane(valid)) return;  // wave-uniform
-    const int e4 = 4 * (k * WW + WW - 1), s4 = 4 * (k * WW - 1);
+    const int e4 = 4 * (k * WW + WW), s4 = 4 * (k * WW);  // last lane of the point, lane before its first
     const int rnd9 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 5 - 1));
     const int rnd14 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 1));
 
@@ -157,8 +196,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         int pinx = (int)floorf(nextx), piny = (int)floorf(nexty);
         uint32_t jp[WH + 1];
 
-        // ---- I x32 and Ix, Iy of every row, packed by row pairs as int16 x 2
-        uint32_t ipk[NP], gxk[NP], gyk[NP];
+        // ---- per row: ic = round - I x32 * 2^9, so that the J bilinear sum
+        // started from ic and shifted right by 9 is diff = J x32 - I x32 itself
+        // (2^9 * I is a multiple of the divisor: floor((X - 2^9 I) / 2^9) =
+        // floor(X / 2^9) - I); Ix, Iy packed by row pairs as int16 x 2
+        int ic[WH];
+        uint32_t gxk[NP], gyk[NP];
         float A11, A12, A22;
         {
             const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
@@ -177,13 +220,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             for (int q = 0; q < NP; ++q) {
                 const int r = 2 * q;
                 const bool two = r + 1 < WH;
-                const int i0 = bilin_s<W_BITS1 - 5>(ip[r], ip[r + 1], w0, w1, rnd9);
-                const int i1 = two ? bilin_s<W_BITS1 - 5>(ip[r + 1], ip[r + 2], w0, w1, rnd9) : 0;
+                ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip[r], ip[r + 1], w0, w1, rnd9) << 9);
+                if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip[r + 1], ip[r + 2], w0, w1, rnd9) << 9);
                 const int x0 = bilin_s<W_BITS1>(dxp[r], dxp[r + 1], w0, w1, rnd14);
                 const int x1 = two ? bilin_s<W_BITS1>(dxp[r + 1], dxp[r + 2], w0, w1, rnd14) : 0;
                 const int y0 = bilin_s<W_BITS1>(dyp[r], dyp[r + 1], w0, w1, rnd14);
                 const int y1 = two ? bilin_s<W_BITS1>(dyp[r + 1], dyp[r + 2], w0, w1, rnd14) : 0;
-                ipk[q] = (uint32_t)i0 | ((uint32_t)i1 << 16);  // both in [0, 8160]
                 gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
                 gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
                 acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
@@ -237,11 +279,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 const int r = 2 * q;
-                const int j0 = bilin_s<W_BITS1 - 5>(jp[r], jp[r + 1], w0, w1, rnd9);
-                const int j1 = r + 1 < WH ? bilin_s<W_BITS1 - 5>(jp[r + 1], jp[r + 2], w0, w1, rnd9) : 0;
-                const s16x2 dk = __builtin_bit_cast(s16x2, (uint32_t)j0 | ((uint32_t)j1 << 16)) -
-                                 __builtin_bit_cast(s16x2, ipk[q]);  // (diff_r, diff_r+1), |diff| <= 8160
-                const uint32_t d = __builtin_bit_cast(uint32_t, dk);
+                // (diff_r, diff_r+1) as int16 x 2, |diff| <= 8160
+                const uint32_t d = r + 1 < WH ? pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]),
+                                                          bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]))
+                                              : pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]), 0);
                 b[0] = sdot2(d, gxk[q], b[0]);
                 b[1] = sdot2(d, gyk[q], b[1]);
             }
@@ -286,11 +327,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #pragma unroll
                 for (int q = 0; q < NP; ++q) {
                     const int r = 2 * q;
-                    const int i0 = (int)(ipk[q] & 0xFFFFu), i1 = (int)(ipk[q] >> 16);
-                    const int d0 = bilin_s<W_BITS1 - 5>(jp[r], jp[r + 1], w0, w1, rnd9) - i0;
+                    const int d0 = bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]) >> 9;
                     e += d0 < 0 ? -d0 : d0;
                     if (r + 1 < WH) {
-                        const int d1 = bilin_s<W_BITS1 - 5>(jp[r + 1], jp[r + 2], w0, w1, rnd9) - i1;
+                        const int d1 = bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]) >> 9;
                         e += d1 < 0 ? -d1 : d1;
                     }
                 }
@@ -328,8 +368,8 @@ bool lk_multi_supported(int win_w, int win_h)
 hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s)
 {
     if (!lk_multi_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
-    const int per_wg = 4 * (64 / a.win_w);  // 4 waves of P points
-    const dim3 grid((a.n + per_wg - 1) / per_wg), block(256);
+    const int per_wg = kMultiWaves * (64 / a.win_w);  // waves of P points
+    const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * kMultiWaves);
     switch (a.win_w) {
 #define TBDK_CASE(W)                                                       \
     case W:                                                                \
