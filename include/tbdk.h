@@ -30,6 +30,10 @@ extern "C" {
 
 #define TBDK_MAX_LEVELS 8
 
+/* pixel depths of a pyramid (cv::Mat depth codes: CV_8U = 0; 7 is OpenCV 4's CV_16F) */
+#define TBDK_DEPTH_8U 0
+#define TBDK_DEPTH_16F 7
+
 /* flags, same values as the reference (video/include/opencv2/video/tracking.hpp:56-57) */
 #define TBDK_OPTFLOW_USE_INITIAL_FLOW 4
 #define TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS 8
@@ -53,6 +57,9 @@ typedef struct tbdk_level {
 typedef struct tbdk_pyr {
     int32_t nlevels;                 /* levels built = maxLevel used + 1 */
     int32_t win_w, win_h;            /* window the level count was derived for */
+    int32_t depth;                   /* TBDK_DEPTH_8U (tbdk_pyr_create) or TBDK_DEPTH_16F
+                                        (tbdk_pyr_create_f16: fp16 levels, fp16 (Ix, Iy)
+                                        derivative pairs) */
     tbdk_level lv[TBDK_MAX_LEVELS];
     tbdk_level dv[TBDK_MAX_LEVELS];
     void* storage;                   /* owned by the library; free with tbdk_pyr_destroy */
@@ -116,12 +123,28 @@ int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr);
  * the CPU pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857). */
 int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream);
 
+/* The fp16 pixel path (no reference implementation: the
+ * reference's CPU PyrLK takes 8-bit levels only, lkpyramid.cpp:1272-1276, and
+ * its CUDA class reads CV_32F through textures, cudaoptflow/src/pyrlk.cpp:197-205).
+ * A pyramid of fp16 levels (2 bytes per pixel) and fp16 (Ix, Iy) derivative
+ * pairs (4 bytes per pixel), same padding and level rule as tbdk_pyr_create.
+ * tbdk_pyr_build fills it from a u8 frame (converted exactly);
+ * tbdk_pyr_build_f16 from an fp16 frame (pitch in bytes).  Levels follow
+ * pyrDown_<FltCast<float,8>> (imgproc/src/pyramids.cpp:722-857) in fp32,
+ * rounded to fp16; tbdk_lk_sparse on two such pyramids runs LKTrackerInvoker's
+ * algorithm in fp32. */
+int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level,
+                        int win_w, int win_h, tbdk_pyr* pyr);
+int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream);
+
 /* Synchronous copy of level `level` to host memory (GpuMat::download
  * analogue; not for the hot path).  with_border != 0 copies the padded frame
- * ((height+2*pad) rows of (width+2*pad) bytes), else the interior. */
+ * ((height+2*pad) rows of (width+2*pad) pixels), else the interior; rows of
+ * width * (1 or 2) bytes by depth (fp16 as raw bits). */
 int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
                       int with_border);
-/* Same for the derivative plane of `level` (interior, CV_16SC2, host_pitch in bytes). */
+/* Same for the derivative plane of `level` (interior, CV_16SC2 — fp16 pairs
+ * as raw bits for TBDK_DEPTH_16F — host_pitch in bytes). */
 int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16_t* host, int host_pitch);
 
 /* Single-level cv::cuda::pyrDown replacement: dst = pyrDown(src),
@@ -142,7 +165,8 @@ int tbdk_pyr_down_u8(tbdk_ctx* ctx, const uint8_t* src, int width, int height, i
  *                         minimum eigenvalue with LK_GET_MIN_EIGENVALS; 0 where
  *                         status is 0 and the reference leaves it unset)
  *   iters               : n x i32 or NULL (Newton iterations over all levels)
- * All levels run in one launch; one wave64 per point. */
+ * All levels run in one launch.  prev and next must have the same depth; on
+ * TBDK_DEPTH_16F pyramids the fp16 pixel path runs (impl must be 0). */
 int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
                    const float* prev_pts, float* next_pts, uint8_t* status, float* err,
                    int32_t* iters, int n, const tbdk_lk_params* params, void* stream);

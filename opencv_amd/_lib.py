@@ -48,6 +48,7 @@ class Pyr(C.Structure):
         ("nlevels", C.c_int32),
         ("win_w", C.c_int32),
         ("win_h", C.c_int32),
+        ("depth", C.c_int32),
         ("lv", Level * TBDK_MAX_LEVELS),
         ("dv", Level * TBDK_MAX_LEVELS),
         ("storage", C.c_void_p),
@@ -183,6 +184,8 @@ SIGNATURES = {
     "tbdk_timing_select": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_create_f16": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_build_f16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
     "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_download": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int, C.c_int]),

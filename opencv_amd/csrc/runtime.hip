@@ -158,11 +158,16 @@ int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double
     return TBDK_OK;
 }
 
-int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+}  // extern "C"
+
+// both depths: u8 (1 B/px) levels + int16x2 derivatives, or fp16 (2 B/px) + fp16x2
+static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, int depth,
+                      tbdk_pyr* pyr)
 {
     if (!ctx || !pyr || width <= 0 || height <= 0 || max_level < 0 || win_w <= 2 || win_h <= 2 || win_w > 63 ||
         win_h > 63)
         return TBDK_EINVAL;
+    const int bpp = depth == TBDK_DEPTH_16F ? 2 : 1;
     DeviceGuard g(ctx->device);
     std::memset(pyr, 0, sizeof(*pyr));
     if (max_level >= TBDK_MAX_LEVELS) max_level = TBDK_MAX_LEVELS - 1;
@@ -175,7 +180,7 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win
         L.width = w;
         L.height = h;
         L.pad = pad;
-        L.pitch = align_up(w + 2 * pad, 256);
+        L.pitch = align_up((w + 2 * pad) * bpp, 256);
         offs[level] = total;
         total += (size_t)L.pitch * (h + 2 * pad) + 256;  // +256: aligned over-reads of the last row
         total = (total + 255) & ~(size_t)255;
@@ -205,11 +210,24 @@ int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win
     pyr->nlevels = nlev;
     pyr->win_w = win_w;
     pyr->win_h = win_h;
+    pyr->depth = depth;
     for (int level = 0; level < nlev; ++level) {
         pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
         pyr->dv[level].data = static_cast<uint8_t*>(mem) + doffs[level];
     }
     return TBDK_OK;
+}
+
+extern "C" {
+
+int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+{
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, pyr);
+}
+
+int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+{
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, pyr);
 }
 
 int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr)
@@ -227,10 +245,28 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
-    hipError_t e = launch_pad_copy(img, pitch, pyr->lv[0], s);
-    for (int level = 1; e == hipSuccess && level < pyr->nlevels; ++level)
-        e = launch_pyr_down_padded(pyr->lv[level - 1], pyr->lv[level], s);
-    if (e == hipSuccess) e = launch_scharr_levels(*pyr, s);
+    hipError_t e;
+    if (pyr->depth == TBDK_DEPTH_16F) {
+        e = launch_pyr_build_f16(img, pitch, 0, *pyr, s);
+    } else {
+        e = launch_pad_copy(img, pitch, pyr->lv[0], s);
+        for (int level = 1; e == hipSuccess && level < pyr->nlevels; ++level)
+            e = launch_pyr_down_padded(pyr->lv[level - 1], pyr->lv[level], s);
+        if (e == hipSuccess) e = launch_scharr_levels(*pyr, s);
+    }
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream)
+{
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pyr->depth != TBDK_DEPTH_16F || pitch < 2 * pyr->lv[0].width ||
+        pitch % 2 != 0)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "pyr_build", s);
+    hipError_t e = launch_pyr_build_f16(reinterpret_cast<const uint8_t*>(img), pitch, 1, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }
@@ -240,12 +276,13 @@ int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* ho
 {
     if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
     const tbdk_level& L = pyr->lv[level];
+    const int bpp = pyr->depth == TBDK_DEPTH_16F ? 2 : 1;
     const int w = with_border ? L.width + 2 * L.pad : L.width;
     const int h = with_border ? L.height + 2 * L.pad : L.height;
-    if (host_pitch < w) return TBDK_EINVAL;
-    const uint8_t* src = with_border ? L.data : L.data + (size_t)L.pad * L.pitch + L.pad;
+    if (host_pitch < w * bpp) return TBDK_EINVAL;
+    const uint8_t* src = with_border ? L.data : L.data + (size_t)L.pad * L.pitch + (size_t)L.pad * bpp;
     DeviceGuard g(ctx->device);
-    hipError_t e = hipMemcpy2D(host, host_pitch, src, L.pitch, w, h, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy2D(host, host_pitch, src, L.pitch, (size_t)w * bpp, h, hipMemcpyDeviceToHost);
     return map_err(e);
 }
 
@@ -291,6 +328,9 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     if (!prev_pts || !next_pts || !status) return TBDK_EINVAL;
     if (p->win_w <= 2 || p->win_h <= 2 || p->win_w > 63 || p->win_h > 63 || p->max_level < 0) return TBDK_EINVAL;
     if (prev->nlevels <= 0 || next->nlevels <= 0) return TBDK_EINVAL;
+    if (prev->depth != next->depth || (prev->depth != TBDK_DEPTH_8U && prev->depth != TBDK_DEPTH_16F))
+        return TBDK_EINVAL;
+    const bool f16 = prev->depth == TBDK_DEPTH_16F;
     const int pad_needed = p->win_w > p->win_h ? p->win_w + 2 : p->win_h + 2;
     int max_level = p->max_level;
     if (prev->nlevels - 1 < max_level) max_level = prev->nlevels - 1;
@@ -331,6 +371,13 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     // auto: several points per wave when the window has an instantiation, else the
     // one-point-per-wave strip kernel, else the generic LDS kernel (no derivative planes)
     if (p->impl < 0 || p->impl > 3) return TBDK_EINVAL;
+    if (f16) {  // the fp16 pixel path has one kernel (klt_f16.hip)
+        if (p->impl != 0 || !have_d || !lk_f16_supported(p->win_w, p->win_h)) return TBDK_EINVAL;
+        int rec = timing_begin(ctx, "lk_sparse", s);
+        hipError_t e = launch_lk_f16(a, s);
+        timing_end(ctx, rec, s);
+        return map_err(e);
+    }
     const int impl = p->impl ? p->impl : ctx->opt_lk_impl;
     const bool multi = (impl == 0 || impl == 3) && have_d && lk_multi_supported(p->win_w, p->win_h);
     const bool strip = !multi && (impl == 0 || impl == 1) && have_d && lk_strip_supported(p->win_w, p->win_h);

@@ -94,6 +94,9 @@ hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, u
                                  hipStream_t s);
 // Scharr derivative planes (interior only; the zero frame is written once at allocation)
 hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s);
+// the fp16 pyramid (klt_f16.hip): level 0 from a u8 (img_f16 = 0) or fp16 frame,
+// the fp16 pyrDown levels and the fp16 derivative pairs
+hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s);
 
 // ---- kernels (klt_lk.hip) ----
 struct LkLevel {
@@ -146,6 +149,9 @@ hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 // several points per wave (klt_lk_multi.hip), same results
 bool lk_multi_supported(int win_w, int win_h);
 hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s);
+// the fp16 pixel path (klt_f16.hip)
+bool lk_f16_supported(int win_w, int win_h);
+hipError_t launch_lk_f16(const LkArgs& a, hipStream_t s);
 
 // ---- box propagation (box_fit.hip) ----
 hipError_t launch_box_propagate(const float* prev, const float* next, const uint8_t* status, const int32_t* offsets,

@@ -81,14 +81,24 @@ class Context:
         return int(n.value), float(ms.value)
 
 
-class Pyramid:
-    """A padded u8 pyramid in device memory (tbdk_pyr)."""
+DEPTH_8U, DEPTH_16F = 0, 7  # TBDK_DEPTH_* (cv::Mat depth codes; 7 = OpenCV 4's CV_16F)
 
-    def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21)):
+
+class Pyramid:
+    """A padded pyramid in device memory (tbdk_pyr): u8 levels with int16 Scharr
+    planes, or (dtype=torch.float16) the fp16 pixel path's fp16 levels with fp16
+    (Ix, Iy) planes."""
+
+    def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21),
+                 dtype: torch.dtype = torch.uint8):
+        if dtype not in (torch.uint8, torch.float16):
+            raise _lib.TbdkError("Pyramid dtype must be torch.uint8 or torch.float16")
         self.ctx = ctx
+        self.dtype = dtype
         self.pyr = _lib.Pyr()
-        _lib.check(ctx.lib.tbdk_pyr_create(ctx.handle, int(width), int(height), int(max_level), int(win[0]),
-                                           int(win[1]), C.byref(self.pyr)), "tbdk_pyr_create")
+        create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else ctx.lib.tbdk_pyr_create
+        _lib.check(create(ctx.handle, int(width), int(height), int(max_level), int(win[0]), int(win[1]),
+                          C.byref(self.pyr)), "tbdk_pyr_create")
         self.width, self.height = int(width), int(height)
 
     @property
@@ -96,31 +106,41 @@ class Pyramid:
         return int(self.pyr.nlevels)
 
     def build(self, img: torch.Tensor, stream=None) -> "Pyramid":
-        if img.dtype != torch.uint8 or img.dim() != 2 or not img.is_cuda:
-            raise _lib.TbdkError("Pyramid.build expects a 2-D uint8 device tensor")
+        """From a 2-D uint8 frame (either depth) or, for an fp16 pyramid, a float16 frame."""
+        if img.dim() != 2 or not img.is_cuda or not (img.dtype == torch.uint8 or
+                                                     (img.dtype == torch.float16 and self.dtype == torch.float16)):
+            raise _lib.TbdkError("Pyramid.build expects a 2-D uint8 (or, fp16 pyramid, float16) device tensor")
         if img.shape[0] != self.height or img.shape[1] != self.width or img.stride(1) != 1:
             raise _lib.TbdkError("image size / layout does not match the pyramid")
-        _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
-                                               C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
+        if img.dtype == torch.float16:
+            _lib.check(self.ctx.lib.tbdk_pyr_build_f16(self.ctx.handle, C.c_void_p(img.data_ptr()),
+                                                       int(img.stride(0)) * 2, C.byref(self.pyr),
+                                                       _stream_ptr(stream)), "tbdk_pyr_build_f16")
+        else:
+            _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
+                                                   C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
         return self
 
     def level(self, i: int, with_border: bool = False):
-        """Host copy of level i as a (H, W) uint8 numpy array (test / download helper)."""
+        """Host copy of level i as a (H, W) numpy array, uint8 or float16 (test / download helper)."""
         import numpy as np
         L = self.pyr.lv[i]
         h = L.height + (2 * L.pad if with_border else 0)
         w = L.width + (2 * L.pad if with_border else 0)
-        out = np.empty((h, w), dtype=np.uint8)
+        dt = np.float16 if self.dtype == torch.float16 else np.uint8
+        out = np.empty((h, w), dtype=dt)
         _lib.check(self.ctx.lib.tbdk_pyr_download(self.ctx.handle, C.byref(self.pyr), int(i),
-                                                  out.ctypes.data_as(C.c_void_p), w, int(bool(with_border))),
+                                                  out.ctypes.data_as(C.c_void_p), out.strides[0],
+                                                  int(bool(with_border))),
                    "tbdk_pyr_download")
         return out
 
     def deriv(self, i: int):
-        """Host copy of the Scharr derivative plane of level i: (H, W, 2) int16 (Ix, Iy)."""
+        """Host copy of the Scharr derivative plane of level i: (H, W, 2) (Ix, Iy), int16
+        (or float16 for an fp16 pyramid)."""
         import numpy as np
         L = self.pyr.dv[i]
-        out = np.empty((L.height, L.width, 2), dtype=np.int16)
+        out = np.empty((L.height, L.width, 2), dtype=np.float16 if self.dtype == torch.float16 else np.int16)
         _lib.check(self.ctx.lib.tbdk_pyr_download_deriv(self.ctx.handle, C.byref(self.pyr), int(i),
                                                         out.ctypes.data_as(C.c_void_p), L.width * 4),
                    "tbdk_pyr_download_deriv")
@@ -135,9 +155,12 @@ class Pyramid:
 
 
 def build_pyramid(img: torch.Tensor, win=(21, 21), max_level: int = 3, ctx: Context | None = None,
-                  stream=None) -> Pyramid:
+                  stream=None, dtype: torch.dtype | None = None) -> Pyramid:
+    """cv::buildOpticalFlowPyramid with derivatives; dtype torch.float16 (or a
+    float16 frame) selects the fp16 pixel path."""
     ctx = ctx or Context.get(img.device.index or 0)
-    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win).build(img, stream)
+    dtype = dtype or (torch.float16 if img.dtype == torch.float16 else torch.uint8)
+    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype).build(img, stream)
 
 
 def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torch.Tensor:

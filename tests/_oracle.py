@@ -128,6 +128,87 @@ def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, 
     return nxt_pts, status, err, iters
 
 
+# ---- the fp16 pixel path (oracle/klt16_oracle.c) ------------------------------
+
+class Level16(C.Structure):
+    _fields_ = [("px", C.c_void_p), ("d", C.c_void_p), ("w", C.c_int), ("h", C.c_int)]
+
+
+class OPyr16(C.Structure):
+    _fields_ = [("nlevels", C.c_int), ("lv", Level16 * MAX_LEVELS)]
+
+
+def _lib16():
+    lib = load()
+    if not getattr(lib, "_f16_ready", False):
+        lib.orc16_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        lib.orc16_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.orc16_lk.restype = C.c_int
+        lib.orc16_lk.argtypes = [C.POINTER(OPyr16), C.POINTER(OPyr16), C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_int, C.POINTER(LkParams), C.c_void_p]
+        lib._f16_ready = True
+    return lib
+
+
+def pyr_down16(img: np.ndarray) -> np.ndarray:
+    """pyrDown_<FltCast<float,8>> scalar order in fp32, rounded to fp16 (float16 in / out)."""
+    lib = _lib16()
+    img = np.ascontiguousarray(img, dtype=np.float16)
+    h, w = img.shape
+    out = np.empty(((h + 1) // 2, (w + 1) // 2), dtype=np.float16)
+    lib.orc16_pyr_down(_ptr(img), w, h, w, _ptr(out), out.shape[1], out.shape[0], out.shape[1])
+    return out
+
+
+def scharr16(img: np.ndarray) -> np.ndarray:
+    """calcSharrDeriv's formula in fp32 on an fp16 level: (H, W, 2) float16 (Ix, Iy)."""
+    lib = _lib16()
+    img = np.ascontiguousarray(img, dtype=np.float16)
+    h, w = img.shape
+    out = np.empty((h, w, 2), dtype=np.float16)
+    lib.orc16_scharr(_ptr(img), w, h, w, _ptr(out))
+    return out
+
+
+class Pyramid16:
+    """fp16 oracle pyramid: levels (float16) and their fp16 derivative planes;
+    the level rule of cv::buildOpticalFlowPyramid (lkpyramid.cpp:782-787)."""
+
+    def __init__(self, img: np.ndarray, win=(21, 21), max_level=3):
+        l0 = np.ascontiguousarray(img.astype(np.float16) if img.dtype != np.float16 else img)
+        self.levels = [l0]
+        w, h = l0.shape[1], l0.shape[0]
+        for _ in range(max_level):
+            w, h = (w + 1) // 2, (h + 1) // 2
+            if w <= win[0] or h <= win[1]:
+                break
+            self.levels.append(pyr_down16(self.levels[-1]))
+        self.derivs = [scharr16(L) for L in self.levels]
+        self.nlevels = len(self.levels)
+        self.p = OPyr16()
+        self.p.nlevels = self.nlevels
+        for i, (L, D) in enumerate(zip(self.levels, self.derivs)):
+            self.p.lv[i] = Level16(L.ctypes.data, D.ctypes.data, L.shape[1], L.shape[0])
+
+
+def lk16(prev: Pyramid16, nxt: Pyramid16, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01,
+         flags=0, min_eig=1e-4, nthreads=8, init: np.ndarray | None = None, want_err: bool = True):
+    """sparse LK of the fp16 pixel path (bit-exact definition of klt_f16.hip)."""
+    lib = _lib16()
+    pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 2)
+    n = pts.shape[0]
+    nxt_pts = np.zeros((n, 2), dtype=np.float32) if init is None else np.ascontiguousarray(init, np.float32).copy()
+    status = np.zeros(n, dtype=np.uint8)
+    err = np.zeros(n, dtype=np.float32)
+    iters = np.zeros(n, dtype=np.int32)
+    prm = LkParams(win[0], win[1], max_level, max_count, eps, flags, min_eig, ACCUM_EXACT, nthreads)
+    if n:
+        rc = lib.orc16_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status),
+                          _ptr(err) if want_err else None, n, C.byref(prm), _ptr(iters))
+        assert rc == 0, rc
+    return nxt_pts, status, err, iters
+
+
 def synth(seed: int, W: int, H: int, nobj: int, t0: int, nframes: int):
     lib = load()
     out = np.zeros((nframes, H, W), dtype=np.uint8)
