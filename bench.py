@@ -198,6 +198,106 @@ def farneback_secondary(ctx, args, device, cpu: bool):
     return out
 
 
+def pyr_f16_bytes(w: int, h: int, nlevels: int) -> int:
+    """Algorithmic HBM bytes of one fp16 pyramid build from a u8 frame: frame
+    read (1 B/px) and level 0 written (2 B/px); per further level the previous
+    level read and the level written (2 B/px each); per level its fp16 (Ix, Iy)
+    plane written (4 B/px) from the level read (2 B/px)."""
+    sizes = []
+    for _ in range(nlevels):
+        sizes.append(w * h)
+        w, h = (w + 1) // 2, (h + 1) // 2
+    b = sizes[0] * 3 + sum(2 * sizes[i - 1] + 2 * sizes[i] for i in range(1, nlevels))
+    return b + sum(6 * s for s in sizes)
+
+
+def lk_f16_secondary(ctx, args, device, cpu: bool):
+    """BASELINE configs[4]'s fp16 pixel path: synthetic 4K pairs (3840x2160,
+    512 objects x 256 points), per pair the next frame's fp16 pyramid (3 levels,
+    Scharr planes; the previous pyramid is reused) and sparse PyrLK (win 21) of
+    every point on the fp16 levels (tbdk_lk_sparse on TBDK_DEPTH_16F pyramids).
+    Pairs/s, the LK VALU roofline and the pyramid's HBM roofline, and the fp16
+    oracle on a bounded sample.  Reported, never `value`."""
+    import numpy as np
+    import torch
+    from opencv_amd import klt
+
+    w, h, n, per_box = args.fb_width, args.fb_height, args.f16_pairs, 256
+    win, ml = (args.win, args.win), args.max_level
+    frames, gt = klt.synth_render(args.seed + 13, w, h, args.fb_objects, 0, n + 1, device=device, ctx=ctx)
+    rng = np.random.default_rng(args.seed)
+    pts_h = np.concatenate([np.stack([rng.uniform(x, x + bw, per_box), rng.uniform(y, y + bh, per_box)], 1)
+                            for v, x, y, bw, bh in gt[0].numpy() if v]).astype(np.float32)
+    pts = torch.from_numpy(pts_h).to(frames.device)
+    pyrs = [klt.Pyramid(ctx, w, h, ml, win, torch.float16) for _ in range(2)]
+    lk = klt.SparsePyrLKOpticalFlow(win, ml, 30)
+
+    def run(timing: bool):
+        pyrs[0].build(frames[0])
+        its = 0
+        for i in range(n):
+            pyrs[(i + 1) % 2].build(frames[i + 1])
+            r = lk.calc(pyrs[i % 2], pyrs[(i + 1) % 2], pts, want_err=True, want_iters=timing)
+            if timing:
+                its += int(r.iters.sum().item())
+        return its
+
+    run(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(False)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ctx.timing_select(["pyr_build", "lk_sparse"])
+    ctx.timing_enable(True)
+    iters = run(True)
+    torch.cuda.synchronize()
+    kern = {}
+    for name in ("pyr_build", "lk_sparse"):
+        c, ms = ctx.timing_query(name)
+        kern[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None}
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    nlev = pyrs[0].nlevels
+    npts = len(pts_h)
+    lkk, pk = kern["lk_sparse"], kern["pyr_build"]
+    flops = lk_flops(npts * nlev, iters / n, args.win)  # per launch (one pair)
+    tf = flops / (lkk["avg_us"] * 1e-6) / 1e12
+    pb = pyr_f16_bytes(w, h, nlev)
+    gbs = pb / (pk["avg_us"] * 1e-6) / 1e9
+    out = {"value": round(n / wall, 2), "unit": "pairs/s", "points_per_s": round(n * npts / wall, 1),
+           "ms_per_pair": round(1000 * wall / n, 3), "dtype": "f16 pixels, f32 arithmetic",
+           "config": {"workload": f"sparse PyrLK {w}x{h}, {args.fb_objects} objects x {per_box} points "
+                                  "(BASELINE configs[4] fp16 pixel path)", "points": npts, "levels": nlev,
+                      "win": args.win, "pairs": n, "mean_iters_per_point": iters / n / npts},
+           "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / PEAK_F32_TFLOPS, 4), "traffic": None, "kernel": "lk_sparse (lk_f16_kernel)",
+                        "flops_per_launch": flops,
+                        "note": "VALU-bound (fp32 FMA on fp16 taps, no MFMA); algorithmic flops per SURVEY.md §8(d)"},
+           "roofline_pyramid": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb,
+                                "kernel": "pyr_build (fp16 levels + fp16 Scharr planes)"},
+           "kernels": kern}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        a_, b_ = frames[0].cpu().numpy(), frames[1].cpu().numpy()
+        threads = min(16, os.cpu_count() or 1)
+        sample = pts_h[:: max(1, npts // 8192)]
+        t1 = time.perf_counter()
+        R0, R1 = O.Pyramid16(a_, win, ml), O.Pyramid16(b_, win, ml)
+        tp = (time.perf_counter() - t1) / 2
+        t1 = time.perf_counter()
+        O.lk16(R0, R1, sample, win, ml, nthreads=threads)
+        tl = (time.perf_counter() - t1) * npts / len(sample)
+        out["cpu_baseline"] = {"value": round(1.0 / (tp + tl), 4), "unit": "pairs/s", "cores": threads,
+                               "kind": "port",
+                               "sample": f"oracle/klt16_oracle.c: one fp16 pyramid (1 thread) + LK of {len(sample)} of "
+                                         f"the {npts} points ({threads} threads), LK time scaled to all points"}
+    del frames, pyrs
+    return out
+
+
 def hog_secondary(ctx, args, device, cpu: bool):
     """The sample's detection step in GPU mode (samples/gpu/tbd.cpp:384-443,
     596-606): cv::cuda::HOG 48x96 people detector, 15 levels, scale 1.05, hit
@@ -285,6 +385,8 @@ def main():
     ap.add_argument("--fb-height", type=int, default=2160)
     ap.add_argument("--fb-objects", type=int, default=512)
     ap.add_argument("--fb-pairs", type=int, default=10)
+    ap.add_argument("--no-f16", action="store_true", help="skip the secondary fp16 pixel path measurement")
+    ap.add_argument("--f16-pairs", type=int, default=10)
     ap.add_argument("--no-hog", action="store_true", help="skip the secondary HOG detector measurement")
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
@@ -487,6 +589,8 @@ def main():
     if rank == 0 and not args.no_farneback:
         del frames, frame_list
         out["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+    if rank == 0 and not args.no_f16:
+        out["lk_f16"] = lk_f16_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_hog:
         out["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:

@@ -33,6 +33,15 @@ for k in ["pyr_build", "lk_sparse"]:
     print(f"{k}: {c} launches, avg {ms / c * 1000:.1f} us")
 st = r.status.cpu().numpy(); it = r.iters.cpu().numpy()
 print(f"points {n}, tracked {st.mean():.3f}, mean iters {it.mean():.2f}, wall/iter {wall*1e3:.3f} ms")
+# the fp16 pixel path on the same frames and points
+Q0 = klt.Pyramid(ctx, W, H, 2, dtype=torch.float16).build(frames[0])
+Q1 = klt.Pyramid(ctx, W, H, 2, dtype=torch.float16).build(frames[1])
+ctx.timing_enable(True)
+for _ in range(20):
+    r16 = lk.calc(Q0, Q1, pts, want_iters=True)
+torch.cuda.synchronize()
+c, ms = ctx.timing_query("lk_sparse")
+print(f"fp16 lk_sparse: avg {ms / c * 1000:.1f} us; mean iters {r16.iters.float().mean().item():.2f}")
 # the other kernels for comparison (impl 1 strip, 2 generic LDS, 3 multi-point)
 for impl in (1, 2, 3):
     lk2 = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30, impl=impl)
