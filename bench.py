@@ -375,6 +375,7 @@ def main():
                     help="run: tbdk_tbd_run (native frame loop with look-ahead); ahead: per-frame "
                          "tbdk_tbd_step_ahead; step: per-frame tbdk_tbd_step (no look-ahead)")
     ap.add_argument("--lk-impl", type=int, default=0, help="PyrLK kernel (ctx option lk_impl; 0 auto)")
+    ap.add_argument("--no-early-gftt", action="store_true", help="ctx option tbd_early_gftt = 0 (A/B runs)")
     ap.add_argument("--kstats", default="lk_sparse",
                     help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
                          "each timed launch adds two event records to the frame's host work.  The other "
@@ -413,6 +414,7 @@ def main():
     ctx = klt.Context.get(dev)
     if args.lk_impl:
         ctx.set_option("lk_impl", args.lk_impl)
+    ctx.set_option("tbd_early_gftt", 0 if args.no_early_gftt else 1)
     nframes = args.warmup + args.steps
     frames, gt = klt.synth_render(args.seed + rank, args.width, args.height, args.objects, 0, nframes,
                                   device=dev, ctx=ctx)
@@ -452,7 +454,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = max_over_ranks(el, world, device="cuda")
-    lk_pts = lk_it = klt_pts = ntr = redet = 0
+    lk_pts = lk_it = klt_pts = ntr = redet = early = 0
     h_wait = h_trk = h_step = h_launch = 0.0
     for m in ms:
         lk_pts += m.lk_points
@@ -460,6 +462,7 @@ def main():
         klt_pts += m.klt_points
         ntr += m.ntracks
         redet += m.redetected
+        early += m.early_gftt
         h_wait += m.host_wait_us
         h_trk += m.host_tracker_us
         h_step += m.host_step_us
@@ -578,6 +581,7 @@ def main():
         "kernels_aside": kstats_aside,
         "per_frame": {"lk_points": lk_pts / args.steps, "tracked_points": klt_pts / args.steps,
                       "tracks": ntr / args.steps, "gftt_rois": redet / args.steps,
+                      "gftt_rois_early": early / args.steps,
                       "host_wait_us": h_wait / args.steps, "host_tracker_us": h_trk / args.steps,
                       "host_step_us": h_step / args.steps, "host_launch_us": h_launch / args.steps},
     }

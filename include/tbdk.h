@@ -92,6 +92,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
  *       (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
+/*   "tbd_early_gftt" (0/1, default 1): the TBD loop runs GFTT over the
+ *       detections that will start new tracks at the start of the step, off
+ *       the critical path (results equal). */
 
 /* device ordinal of the context */
 int tbdk_ctx_device(const tbdk_ctx* ctx);
@@ -434,8 +437,8 @@ typedef struct tbdk_frame_metrics {  /* per-frame TP/FN/FP/GT/c/sum d (tbd.hpp:1
     int32_t lk_points;               /* corners that entered PyrLK this frame */
     int32_t klt_points;              /* ... of which tracked (status 1) */
     int32_t klt_predicted;           /* tracks predicted by the KLT fit */
-    int32_t redetected;              /* GFTT ROIs this frame */
-    int32_t pad_;
+    int32_t redetected;              /* point sets refreshed by GFTT this frame */
+    int32_t early_gftt;              /* ... of which served by the early GFTT (tbd_loop.hip) */
     int64_t lk_iters;                /* Newton iterations over all levels (flop accounting) */
     float host_wait_us;              /* host time blocked on the device this step */
     float host_tracker_us;           /* host time in the tracker step (assignment + bookkeeping) */

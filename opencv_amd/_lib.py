@@ -106,7 +106,7 @@ class FrameMetrics(C.Structure):
     _fields_ = [("tp", C.c_int32), ("fn", C.c_int32), ("fp", C.c_int32), ("gt", C.c_int32),
                 ("matches", C.c_int32), ("bbox_overlap", C.c_double), ("ntracks", C.c_int32),
                 ("lk_points", C.c_int32), ("klt_points", C.c_int32), ("klt_predicted", C.c_int32),
-                ("redetected", C.c_int32), ("pad_", C.c_int32), ("lk_iters", C.c_int64),
+                ("redetected", C.c_int32), ("early_gftt", C.c_int32), ("lk_iters", C.c_int64),
                 ("host_wait_us", C.c_float), ("host_tracker_us", C.c_float),
                 ("host_step_us", C.c_float), ("host_launch_us", C.c_float)]
 

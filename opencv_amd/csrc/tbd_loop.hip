@@ -14,6 +14,13 @@
 //   6. GFTT in the boxes of new tracks and of tracks due for re-detection
 //      (every `redetect_every` frames or < min_points corners), written
 //      straight into their point slots                                   [HIP]
+// Early GFTT: a new track's box is its detection's box (tbd.cpp:1043-1055), so
+// GFTT over the detections that will surely start new tracks (boxes beyond the
+// tracker's bounds filter, tbd.cpp:218,306-331: any track on them is deleted
+// before the assignment) is launched at the start of the step, off the
+// critical path; after the tracker step, new tracks whose box equals such a
+// detection box take those corners (the same ROI of the same frame, so the
+// same corners), every other refreshed set runs the post-tracker GFTT.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -111,14 +118,16 @@ __global__ void tbd_clear_kernel(const int* __restrict__ slots, int n, int32_t* 
     if (k < n) slot_counts[slots[k]] = 0;
 }
 
-// GFTT staging -> point slots
+// GFTT staging -> point slots: item k copies corner row rows[k] (k when rows
+// is null) into slot roi_slot[k]
 __global__ void tbd_scatter_kernel(const float2* __restrict__ corners, const int32_t* __restrict__ counts,
-                                   const int* __restrict__ roi_slot, int maxc, float2* __restrict__ slot_pts,
-                                   int32_t* __restrict__ slot_counts)
+                                   const int* __restrict__ rows, const int* __restrict__ roi_slot, int maxc,
+                                   float2* __restrict__ slot_pts, int32_t* __restrict__ slot_counts)
 {
-    const int r = blockIdx.x;
+    const int k = blockIdx.x;
+    const int r = rows ? rows[k] : k;
     const int n = counts[r] < 0 ? 0 : counts[r];
-    const int s = roi_slot[r];
+    const int s = roi_slot[k];
     for (int j = threadIdx.x; j < n; j += blockDim.x)
         slot_pts[(size_t)s * kSlotPts + j] = corners[(size_t)r * maxc + j];
     if (threadIdx.x == 0) slot_counts[s] = n;
@@ -187,11 +196,30 @@ struct tbdk_tbd {
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
     // one pinned block uploaded with a single copy after the tracker step:
-    // [clear slots: S ints][ROI slots: S ints][GFTT ROI table: S GfttRoi]
+    // [clear slots: S ints][ROI slots: S ints][early rows: S ints][early slots: S ints]
+    // [GFTT ROI table: S GfttRoi]
     int* h_post = nullptr;
     int* h_roi_slot = nullptr;
     int* h_clear = nullptr;
+    int* h_erow = nullptr;
+    int* h_eslot = nullptr;
     GfttRoi* h_tab = nullptr;
+
+    int* d_erow = nullptr;
+    int* d_eslot = nullptr;
+    // early GFTT (see the top of the file): ROI tables double-buffered by step
+    // parity (pinned; a table is rewritten two steps later, after a fit sync
+    // that orders its upload), device table, corner rows and counts
+    GfttRoi* h_etab[2] = {nullptr, nullptr};
+    GfttRoi* d_etab = nullptr;
+    float2* d_ecorners = nullptr;
+    int32_t* d_ecounts = nullptr;
+    int epar = 0;
+    std::vector<tbdk_roi> erois;                  // this step's early ROIs
+    std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
+    hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
+    hipStream_t early_s = nullptr;                // lowest priority: off the critical path
+    hipEvent_t early_done = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
     std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
@@ -203,6 +231,12 @@ struct tbdk_tbd {
 };
 
 namespace {
+
+inline uint64_t box_key(int x, int y, int w, int h)
+{
+    return ((uint64_t)(uint16_t)x << 48) | ((uint64_t)(uint16_t)y << 32) | ((uint64_t)(uint16_t)w << 16) |
+           (uint64_t)(uint16_t)h;
+}
 
 int release(tbdk_tbd* t)
 {
@@ -218,11 +252,15 @@ int release(tbdk_tbd* t)
     if (t->side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
-    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre,
-                   t->d_fit,    t->d_corners, t->d_ccounts,   t->d_post,    t->d_la};
+    if (t->pyr_ready) (void)hipEventDestroy(t->pyr_ready);
+    if (t->early_s) (void)hipStreamSynchronize(t->early_s);
+    if (t->early_s) (void)hipStreamDestroy(t->early_s);
+    if (t->early_done) (void)hipEventDestroy(t->early_done);
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre, t->d_fit,
+                   t->d_corners, t->d_ccounts, t->d_post, t->d_la, t->d_etab, t->d_ecorners, t->d_ecounts};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la};
+    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la, t->h_etab[0]};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -304,7 +342,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     dm(reinterpret_cast<void**>(&t->d_fit), sizeof(FitOut) * S);
     dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
     dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
-    const size_t post_bytes = 2 * sizeof(int) * S + sizeof(GfttRoi) * S;
+    const size_t post_bytes = 4 * sizeof(int) * S + sizeof(GfttRoi) * S;
     dm(reinterpret_cast<void**>(&t->d_post), post_bytes);
     hm(&t->h_pre, pre_bytes);
     if (t->h_pre && t->d_pre) {
@@ -315,6 +353,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     }
     t->refreshed.assign((size_t)S, 0);
     t->la_member.assign((size_t)S, 0);
+
     t->b_list.assign((size_t)S, 0);
     dm(reinterpret_cast<void**>(&t->d_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
@@ -323,11 +362,21 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (t->h_post && t->d_post) {
         t->h_clear = t->h_post;
         t->h_roi_slot = t->h_post + S;
-        t->h_tab = reinterpret_cast<GfttRoi*>(t->h_post + 2 * S);
+        t->h_erow = t->h_post + 2 * S;
+        t->h_eslot = t->h_post + 3 * S;
+        t->h_tab = reinterpret_cast<GfttRoi*>(t->h_post + 4 * S);
         t->d_clear = t->d_post;
         t->d_roi_slot = t->d_post + S;
-        t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 2 * S);
+        t->d_erow = t->d_post + 2 * S;
+        t->d_eslot = t->d_post + 3 * S;
+        t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 4 * S);
     }
+    hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
+    if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
+    dm(reinterpret_cast<void**>(&t->d_etab), sizeof(GfttRoi) * S);
+    dm(reinterpret_cast<void**>(&t->d_ecorners), sizeof(float2) * S * cfg->max_corners);
+    dm(reinterpret_cast<void**>(&t->d_ecounts), sizeof(int32_t) * S);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->pyr_ready, hipEventDisableTiming);
     // the post-tracker GFTT heads the next frame's critical path (the refreshed
     // sets' PyrLK waits for it): it gets the highest priority, ahead of the
     // look-ahead PyrLK it shares the device with
@@ -340,6 +389,8 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->la_s, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking, prio_least);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -417,6 +468,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const bool la_valid = t->la_pyr && t->la_frame == frame && t->la_pitch == pitch;
     const bool had_la_lk = t->la_lk;
     const bool la_lk = la_valid && had_la_lk;
+
     if (t->la_pyr && t->la_stream != s) {  // the look-ahead pyramid was built on another stream
         hipError_t e = hipStreamWaitEvent(s, t->la_ready, 0);
         if (e != hipSuccess) return map_status(e);
@@ -429,7 +481,64 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     if (!la_valid) {
         rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, s);
         if (rc != TBDK_OK) return rc;
+        hipError_t e = hipEventRecord(t->pyr_ready, s);
+        if (e != hipSuccess) return map_status(e);
     }
+    const tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
+    if (c.use_klt && t->ctx->opt_tbd_early_gftt) {
+        // the early GFTT stream: behind this frame's pyramid (recorded where it
+        // was built) and the previous step's post-tracker work (the GFTT scratch
+        // and the early corner rows it read); waits taken now, before this step
+        // re-records la_ready for the next frame
+        hipError_t e = hipStreamWaitEvent(t->early_s, la_valid ? t->la_ready : t->pyr_ready, 0);
+        if (e == hipSuccess) e = hipStreamWaitEvent(t->early_s, t->post_done, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
+
+    // ---- early GFTT over the detections that will start new tracks: every
+    // detection before the first tracks exist, else those beyond the tracker's
+    // bounds filter (a track on them is predicted there and deleted before the
+    // assignment).  On the low-priority `early_s`, launched after this step's
+    // PyrLK and fit (it is needed only after the tracker step); the
+    // post-tracker phase takes its corners for every refreshed set whose box
+    // equals one of these ROIs.
+    t->erois.clear();
+    t->erow_of.clear();
+    bool early_launched = false;
+    auto launch_early_gftt = [&]() -> int {
+        if (!c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
+        const bool all_new = t->tracker->getTracks().empty();
+        for (int i = 0; i < ndets && (int)t->erois.size() < c.max_tracks; ++i) {
+            const tbdk_detection& d = dets[i];
+            const bool beyond = d.x >= c.bounds_xmax || d.y >= c.bounds_ymax || d.x + d.width < c.bounds_xmin ||
+                                d.y + d.height < c.bounds_ymin;
+            if (!all_new && !beyond) continue;
+            const int x0 = std::max(d.x, 0), y0 = std::max(d.y, 0);
+            const int x1 = std::min(d.x + d.width, c.width), y1 = std::min(d.y + d.height, c.height);
+            if (x1 - x0 < 3 || y1 - y0 < 3) continue;
+            if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+            t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+        }
+        if (!t->erois.empty()) {
+            GfttPlan eplan;
+            GfttRoi* htab = t->h_etab[t->epar];
+            t->epar ^= 1;
+            int rc2 = gftt_prepare(t->erois.data(), (int)t->erois.size(), c.width, c.height, &gp, htab, &eplan);
+            if (rc2 != TBDK_OK) return rc2;
+            hipStream_t es = t->early_s;  // ordered at the top of the step
+            hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * t->erois.size(), hipMemcpyHostToDevice, es);
+            if (e != hipSuccess) return map_status(e);
+            const tbdk_level& L0 = P.lv[0];
+            rc2 = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_etab, eplan, &gp,
+                              reinterpret_cast<float*>(t->d_ecorners), t->d_ecounts, es);
+            if (rc2 != TBDK_OK) return rc2;
+            e = hipEventRecord(t->early_done, es);
+            if (e != hipSuccess) return map_status(e);
+            early_launched = true;
+        }
+        return TBDK_OK;
+    };
+
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents, h_lists) were last read by uploads issued before the
@@ -483,6 +592,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     if (had_la_lk)
         for (int k = 0; k < t->la_n; ++k) t->la_member[(size_t)t->h_la[k]] = 0;
+
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
     {  // the previous frame's clear / GFTT / scatter (on `side`) before the refreshed sets
         hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
@@ -494,7 +604,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         t->la_pitch = next_pitch;
         t->la_stream = s;
         t->la_pyr = true;
-        return tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, s);
+        const int r = tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, s);
+        if (r != TBDK_OK) return r;
+        return map_status(hipEventRecord(t->la_ready, s));  // the next frame's pyramid (and this fit) done
     };
     if (run_klt) {
         if (nB > 0) {
@@ -519,6 +631,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = enqueue_next_pyr();
             if (rc != TBDK_OK) return rc;
         }
+        rc = launch_early_gftt();
+        if (rc != TBDK_OK) return rc;
         auto ts0 = clk::now();
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
         e = hipEventSynchronize(t->fit_done);
@@ -542,8 +656,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 klt_pred++;
             }
         }
-    } else if (next) {
-        rc = enqueue_next_pyr();
+    } else {
+        if (next) {
+            rc = enqueue_next_pyr();
+            if (rc != TBDK_OK) return rc;
+        }
+        rc = launch_early_gftt();
         if (rc != TBDK_OK) return rc;
     }
 
@@ -577,7 +695,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     // ---- corners for new tracks and tracks due for re-detection
     t->rois.clear();
-    int nroi = 0;
+    int nroi = 0, nearly = 0;
     if (c.use_klt) {
         for (const auto& tr : t->tracker->getTracks()) {
             auto it = t->slot_of.find(tr.id);
@@ -597,14 +715,20 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             const tbd::Rect& b = tr.bboxes.back();
             int x0 = std::max(b.x, 0), y0 = std::max(b.y, 0);
             int x1 = std::min(b.x + b.width, c.width), y1 = std::min(b.y + b.height, c.height);
+            t->refreshed[(size_t)slot] = 1;
+            t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
             if (x1 - x0 < 3 || y1 - y0 < 3) {  // nothing to detect in: empty point set
                 t->rois.push_back(tbdk_roi{0, 0, 1, 1});
             } else {
+                auto er = t->erow_of.find(box_key(x0, y0, x1 - x0, y1 - y0));
+                if (er != t->erow_of.end()) {  // the early GFTT ran on this ROI of this frame
+                    t->h_erow[nearly] = er->second;
+                    t->h_eslot[nearly++] = slot;
+                    continue;
+                }
                 t->rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
             t->h_roi_slot[nroi++] = slot;
-            t->refreshed[(size_t)slot] = 1;
-            t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
         }
     }
     // ---- one upload (clear list, ROI slots, GFTT ROI table), then GFTT / clear / scatter.
@@ -612,16 +736,20 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // enqueued after it (the look-ahead PyrLK): GFTT heads the next frame's
     // critical path, so it is queued first and the PyrLK fills the device
     // around it.
-    tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
     GfttPlan plan;
     if (nroi > 0) {
         rc = gftt_prepare(t->rois.data(), nroi, c.width, c.height, &gp, t->h_tab, &plan);
         if (rc != TBDK_OK) return rc;
     }
-    if (nclear > 0 || nroi > 0) {
-        const size_t bytes = nroi > 0 ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) -
-                                            reinterpret_cast<const uint8_t*>(t->h_post)
-                                      : sizeof(int) * nclear;
+    if (early_launched) {  // its corners, and the GFTT scratch the post-tracker GFTT reuses
+        hipError_t e = hipStreamWaitEvent(t->side, t->early_done, 0);
+        if (e != hipSuccess) return map_status(e);
+    }
+    if (nclear > 0 || nroi > 0 || nearly > 0) {
+        const uint8_t* h0 = reinterpret_cast<const uint8_t*>(t->h_post);
+        const size_t bytes = nroi > 0     ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) - h0
+                             : nearly > 0 ? reinterpret_cast<const uint8_t*>(t->h_eslot + nearly) - h0
+                                          : sizeof(int) * nclear;
         hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
         if (e != hipSuccess) return map_status(e);
     }
@@ -636,8 +764,15 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                            t->slot_counts);
     if (nroi > 0)
         hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, t->side, t->d_corners, t->d_ccounts,
-                           t->d_roi_slot, c.max_corners, t->slot_pts, t->slot_counts);
-    if (nclear > 0 || nroi > 0) {
+                           static_cast<const int*>(nullptr), t->d_roi_slot, c.max_corners, t->slot_pts,
+                           t->slot_counts);
+    if (nearly > 0)
+        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nearly), dim3(256), 0, t->side, t->d_ecorners, t->d_ecounts,
+                           t->d_erow, t->d_eslot, c.max_corners, t->slot_pts, t->slot_counts);
+    // post_done also after an early GFTT none of whose ROIs was used: the next
+    // step's fit sync then orders that GFTT's table upload before the staging
+    // table is rewritten (two steps later)
+    if (nclear > 0 || nroi > 0 || nearly > 0 || !t->erois.empty()) {
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
@@ -645,8 +780,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
     // set was not refreshed just now (exactly the next step's unchanged sets)
     if (next) {
-        hipError_t e = hipEventRecord(t->la_ready, s);
-        if (e != hipSuccess) return map_status(e);
+        hipError_t e = hipSuccess;
         if (c.use_klt && !t->tracker->getTracks().empty()) {
             int n = 0;
             for (const auto& tr : t->tracker->getTracks()) {
@@ -691,9 +825,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         metrics->klt_points = klt_points;
         metrics->lk_points = lk_points;
         metrics->lk_iters = lk_iters;
-        metrics->pad_ = 0;
+        metrics->early_gftt = nearly;
         metrics->klt_predicted = klt_pred;
-        metrics->redetected = nroi;
+        metrics->redetected = nroi + nearly;
         metrics->host_wait_us = (float)wait_us;
         metrics->host_tracker_us = (float)tracker_us;
         metrics->host_launch_us = (float)launch_us;
