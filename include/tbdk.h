@@ -94,7 +94,11 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 /*   "tbd_early_gftt" (0/1, default 1): the TBD loop runs GFTT over the
  *       detections that will start new tracks at the start of the step, off
- *       the critical path (results equal). */
+ *       the critical path (results equal).
+ *   "tbd_spec_lookahead" (0/1, default 1): with a look-ahead frame, the TBD
+ *       loop starts the next frame's PyrLK of the point sets that stay
+ *       unchanged unless their track is deleted before the host tracker step
+ *       (results equal). */
 
 /* device ordinal of the context */
 int tbdk_ctx_device(const tbdk_ctx* ctx);

@@ -178,8 +178,17 @@ struct tbdk_tbd {
     hipEvent_t eig_done = nullptr;   // this step's GFTT eigenvalue kernel complete (on `side`)
     int32_t* h_la = nullptr;         // look-ahead slot list (pinned) / device copy
     int32_t* d_la = nullptr;
-    int la_n = 0;
+    std::vector<int> la_list;        // the la_member slots
     std::vector<char> la_member;     // slot tracked by the look-ahead PyrLK
+    // speculative look-ahead PyrLK, launched before the tracker step for the
+    // sets that will stay unchanged unless the tracker deletes the track (n >=
+    // min_points, KLT prediction inside the bounds filter, no re-detection
+    // frame): [slots] pinned / device, membership
+    int32_t* h_spec = nullptr;
+    int32_t* d_spec = nullptr;
+    std::vector<int> spec_list;
+    std::vector<char> spec_member;
+    std::vector<char> touched;       // scratch: slots cleared this step
     const uint8_t* la_frame = nullptr;
     int la_pitch = 0;
     hipStream_t la_stream = nullptr;
@@ -257,10 +266,11 @@ int release(tbdk_tbd* t)
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre, t->d_fit,
-                   t->d_corners, t->d_ccounts, t->d_post, t->d_la, t->d_etab, t->d_ecorners, t->d_ecounts};
+                   t->d_corners, t->d_ccounts, t->d_post, t->d_la, t->d_etab, t->d_ecorners, t->d_ecounts,
+                   t->d_spec};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la, t->h_etab[0]};
+    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la, t->h_etab[0], t->h_spec};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -353,10 +363,14 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     }
     t->refreshed.assign((size_t)S, 0);
     t->la_member.assign((size_t)S, 0);
+    t->spec_member.assign((size_t)S, 0);
+    t->touched.assign((size_t)S, 0);
 
     t->b_list.assign((size_t)S, 0);
     dm(reinterpret_cast<void**>(&t->d_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
+    dm(reinterpret_cast<void**>(&t->d_spec), sizeof(int32_t) * S);
+    hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
     hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
     if (t->h_post && t->d_post) {
@@ -468,6 +482,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const bool la_valid = t->la_pyr && t->la_frame == frame && t->la_pitch == pitch;
     const bool had_la_lk = t->la_lk;
     const bool la_lk = la_valid && had_la_lk;
+
 
     if (t->la_pyr && t->la_stream != s) {  // the look-ahead pyramid was built on another stream
         hipError_t e = hipStreamWaitEvent(s, t->la_ready, 0);
@@ -590,8 +605,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (rc != TBDK_OK) return rc;
         }
     }
-    if (had_la_lk)
-        for (int k = 0; k < t->la_n; ++k) t->la_member[(size_t)t->h_la[k]] = 0;
+    for (int sl : t->la_list) t->la_member[(size_t)sl] = 0;
+    t->la_list.clear();
+
 
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
     {  // the previous frame's clear / GFTT / scatter (on `side`) before the refreshed sets
@@ -656,6 +672,43 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 klt_pred++;
             }
         }
+        // ---- speculative look-ahead PyrLK (see tbdk_tbd::spec_list): runs while the
+        // host tracks; the post-tracker phase adds the unchanged sets it missed
+        if (next && t->ctx->opt_tbd_spec_la && frame_id % c.redetect_every != 0) {
+            int ns = 0;
+            k = 0;
+            for (const auto& tr : tracks) {
+                auto it = t->slot_of.find(tr.id);
+                if (it == t->slot_of.end()) continue;
+                const FitOut& o = t->h_fit[k++];
+                if (o.n < c.min_points || !o.valid) continue;
+                const tbd::Rect& bb = tr.bboxes.back();  // predictNewLocationsOfTracks + filterTracksOutOfBounds
+                const tbd::Rect r =
+                    tbd::rect_from_point2d(o.cx - bb.width / 2, o.cy - bb.height / 2, bb.width, bb.height);
+                if (r.x + r.width < c.bounds_xmin || r.x >= c.bounds_xmax || r.y + r.height < c.bounds_ymin ||
+                    r.y >= c.bounds_ymax)
+                    continue;
+                t->h_spec[ns++] = it->second;
+            }
+            if (ns > 0) {
+                hipStream_t ls = t->la_s;
+                e = hipStreamWaitEvent(ls, t->la_ready, 0);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
+                if (e != hipSuccess) return map_status(e);
+                rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
+                                 reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                                 ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec);
+                if (rc != TBDK_OK) return rc;
+                e = hipEventRecord(t->la_done, ls);
+                if (e != hipSuccess) return map_status(e);
+                for (int q = 0; q < ns; ++q) {
+                    t->spec_member[(size_t)t->h_spec[q]] = 1;
+                    t->spec_list.push_back(t->h_spec[q]);
+                }
+                t->la_lk = true;
+            }
+        }
     } else {
         if (next) {
             rc = enqueue_next_pyr();
@@ -688,6 +741,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         auto it = t->slot_of.find(id);
         if (it != t->slot_of.end()) {
             t->free_slots.push(it->second);
+            t->touched[(size_t)it->second] = 1;
             t->h_clear[nclear++] = it->second;
             t->slot_of.erase(it);
         }
@@ -741,6 +795,16 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         rc = gftt_prepare(t->rois.data(), nroi, c.width, c.height, &gp, t->h_tab, &plan);
         if (rc != TBDK_OK) return rc;
     }
+    {  // a speculated set the tracker deleted or refreshed: the speculative PyrLK
+       // reads it, so the clear / scatter writing it wait for that PyrLK
+        bool conflict = false;
+        for (int sl : t->spec_list) conflict |= t->touched[(size_t)sl] || t->refreshed[(size_t)sl];
+        for (int k = 0; k < nclear; ++k) t->touched[(size_t)t->h_clear[k]] = 0;
+        if (conflict) {
+            hipError_t e = hipStreamWaitEvent(t->side, t->la_done, 0);
+            if (e != hipSuccess) return map_status(e);
+        }
+    }
     if (early_launched) {  // its corners, and the GFTT scratch the post-tracker GFTT reuses
         hipError_t e = hipStreamWaitEvent(t->side, t->early_done, 0);
         if (e != hipSuccess) return map_status(e);
@@ -782,14 +846,14 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     if (next) {
         hipError_t e = hipSuccess;
         if (c.use_klt && !t->tracker->getTracks().empty()) {
-            int n = 0;
+            int n = 0;  // unchanged sets the speculative PyrLK did not cover
             for (const auto& tr : t->tracker->getTracks()) {
                 auto it = t->slot_of.find(tr.id);
                 if (it == t->slot_of.end() || t->refreshed[(size_t)it->second]) continue;
-                t->h_la[n++] = it->second;
                 t->la_member[(size_t)it->second] = 1;
+                t->la_list.push_back(it->second);
+                if (!t->spec_member[(size_t)it->second]) t->h_la[n++] = it->second;
             }
-            t->la_n = n;
             if (n > 0) {
                 // on la_s, after the fit and the pyramid (la_ready) and behind the
                 // GFTT eigenvalue kernel: its many large workgroups would otherwise
@@ -810,6 +874,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             }
         }
     }
+    for (int sl : t->spec_list) t->spec_member[(size_t)sl] = 0;
+    t->spec_list.clear();
     t->cur ^= 1;
     t->have_prev = true;
 

@@ -176,9 +176,11 @@ def test_tbd_lookahead_discarded_on_other_frame(gpu):
 def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     """The early GFTT (detections beyond the tracker's bounds filter, GFTT'd at
     the start of the step) hands new tracks exactly the corners the
-    post-tracker GFTT computes: same per-frame metrics, predictions and tracks
-    with the option on and off, under the reference's bounds quirk (most new
-    tracks served early) and with re-detection frames mixed in."""
+    post-tracker GFTT computes, and the speculative look-ahead PyrLK (launched
+    before the tracker step) equals the post-tracker one: same per-frame
+    metrics, predictions and tracks with the options on and off, under the
+    reference's bounds quirk (most new tracks served early, speculated sets
+    deleted by the tracker) and with re-detection frames mixed in."""
     from opencv_amd import klt, tbd
 
     W, H, N, F = 960, 540, 40, 16
@@ -187,8 +189,9 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
     res = {}
     try:
-        for early in (1, 0):
+        for early, spec in ((1, 1), (1, 0), (0, 1), (0, 0)):
             gpu.set_option("tbd_early_gftt", early)
+            gpu.set_option("tbd_spec_lookahead", spec)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms, preds = [], []
             if api == "run":
@@ -198,10 +201,12 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
                     nxt = frames[f + 1] if api == "ahead" and f + 1 < F else None
                     ms.append(loop.step(frames[f], f, dets[f], next_frame=nxt))
                     preds.append(loop.predictions())
-            res[early] = ([_mkey(m) for m in ms], preds, loop.tracks(), sum(m.early_gftt for m in ms))
+            res[early, spec] = ([_mkey(m) for m in ms], preds, loop.tracks(), sum(m.early_gftt for m in ms))
     finally:
         gpu.set_option("tbd_early_gftt", 1)
-    assert res[1][0] == res[0][0]
-    assert res[1][1] == res[0][1]
-    assert res[1][2] == res[0][2]
-    assert res[1][3] > 2 * F and res[0][3] == 0  # the early path was taken (and off means off)
+        gpu.set_option("tbd_spec_lookahead", 1)
+    for key in ((1, 1), (1, 0), (0, 1)):
+        assert res[key][0] == res[0, 0][0], key
+        assert res[key][1] == res[0, 0][1], key
+        assert res[key][2] == res[0, 0][2], key
+    assert res[1, 1][3] > 2 * F and res[0, 0][3] == 0  # the early path was taken (and off means off)
