@@ -377,6 +377,7 @@ def main():
     ap.add_argument("--lk-impl", type=int, default=0, help="PyrLK kernel (ctx option lk_impl; 0 auto)")
     ap.add_argument("--no-early-gftt", action="store_true", help="ctx option tbd_early_gftt = 0 (A/B runs)")
     ap.add_argument("--no-spec-lookahead", action="store_true", help="ctx option tbd_spec_lookahead = 0 (A/B runs)")
+    ap.add_argument("--no-zero-copy", action="store_true", help="ctx option tbd_zero_copy = 0 (A/B runs)")
     ap.add_argument("--kstats", default="lk_sparse",
                     help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
                          "each timed launch adds two event records to the frame's host work.  The other "
@@ -417,6 +418,7 @@ def main():
         ctx.set_option("lk_impl", args.lk_impl)
     ctx.set_option("tbd_early_gftt", 0 if args.no_early_gftt else 1)
     ctx.set_option("tbd_spec_lookahead", 0 if args.no_spec_lookahead else 1)
+    ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
     nframes = args.warmup + args.steps
     frames, gt = klt.synth_render(args.seed + rank, args.width, args.height, args.objects, 0, nframes,
                                   device=dev, ctx=ctx)

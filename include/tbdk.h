@@ -98,6 +98,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_spec_lookahead" (0/1, default 1): with a look-ahead frame, the TBD
  *       loop starts the next frame's PyrLK of the point sets that stay
  *       unchanged unless their track is deleted before the host tracker step
+ *       (results equal).
+ *   "tbd_zero_copy" (0/1, default 1; taken by tbdk_tbd_create): the TBD loop's
+ *       kernels read their host tables from, and the fit writes its results
+ *       to, coherent pinned host memory directly instead of through copies
  *       (results equal). */
 
 /* device ordinal of the context */

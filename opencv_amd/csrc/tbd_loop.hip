@@ -227,6 +227,12 @@ struct tbdk_tbd {
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
     hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
+    // zero-copy staging: the kernels read the pinned host tables (fit entries,
+    // slot lists, post-tracker lists, GFTT ROI tables) and the fit kernel
+    // writes its results to pinned host memory directly, through device
+    // mappings of the coherent pinned buffers; no copy is issued (d_pre, d_fit,
+    // d_post, d_la, d_spec, d_etab are those mappings, not device allocations)
+    bool zc = false;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
     hipEvent_t early_done = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
@@ -265,11 +271,15 @@ int release(tbdk_tbd* t)
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
-    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_pre, t->d_fit,
-                   t->d_corners, t->d_ccounts, t->d_post, t->d_la, t->d_etab, t->d_ecorners, t->d_ecounts,
-                   t->d_spec};
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_corners,
+                   t->d_ccounts, t->d_ecorners, t->d_ecounts};
     for (void* p : dev)
         if (p) (void)hipFree(p);
+    if (!t->zc) {
+        void* staged[] = {t->d_pre, t->d_fit, t->d_post, t->d_la, t->d_etab, t->d_spec};
+        for (void* p : staged)
+            if (p) (void)hipFree(p);
+    }
     void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la, t->h_etab[0], t->h_spec};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
@@ -339,8 +349,16 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         if (e == hipSuccess) e = hipMalloc(p, bytes);
         if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
     };
+    t->zc = ctx->opt_tbd_zero_copy != 0;
     auto hm = [&](void** p, size_t bytes) {
-        if (e == hipSuccess) e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+        if (e == hipSuccess)
+            e = hipHostMalloc(p, bytes, t->zc ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault);
+    };
+    // a staged table: its device copy, or (zero-copy) the mapping of the pinned buffer
+    auto sm = [&](void** d, void* h, size_t bytes) {
+        if (e != hipSuccess) return;
+        if (t->zc) e = hipHostGetDevicePointer(d, h, 0);
+        else dm(d, bytes);
     };
     dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * S * kSlotPts);
     dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * S * kSlotPts);
@@ -348,13 +366,22 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * S * kSlotPts);
     dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * S);
     const size_t pre_bytes = (sizeof(FitEntry) + sizeof(int32_t)) * S;
-    dm(&t->d_pre, pre_bytes);
-    dm(reinterpret_cast<void**>(&t->d_fit), sizeof(FitOut) * S);
+    const size_t post_bytes = 4 * sizeof(int) * S + sizeof(GfttRoi) * S;
     dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
     dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
-    const size_t post_bytes = 4 * sizeof(int) * S + sizeof(GfttRoi) * S;
-    dm(reinterpret_cast<void**>(&t->d_post), post_bytes);
     hm(&t->h_pre, pre_bytes);
+    hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
+    hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
+    hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
+    hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
+    hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
+    if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
+    sm(&t->d_pre, t->h_pre, pre_bytes);
+    sm(reinterpret_cast<void**>(&t->d_fit), t->h_fit, sizeof(FitOut) * S);
+    sm(reinterpret_cast<void**>(&t->d_post), t->h_post, post_bytes);
+    sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
+    sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
+    sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
     if (t->h_pre && t->d_pre) {
         t->h_ents = static_cast<FitEntry*>(t->h_pre);
         t->h_lists = reinterpret_cast<int32_t*>(t->h_ents + S);
@@ -367,12 +394,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->touched.assign((size_t)S, 0);
 
     t->b_list.assign((size_t)S, 0);
-    dm(reinterpret_cast<void**>(&t->d_la), sizeof(int32_t) * S);
-    hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
-    dm(reinterpret_cast<void**>(&t->d_spec), sizeof(int32_t) * S);
-    hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
-    hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
-    hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
+
     if (t->h_post && t->d_post) {
         t->h_clear = t->h_post;
         t->h_roi_slot = t->h_post + S;
@@ -385,9 +407,6 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         t->d_eslot = t->d_post + 3 * S;
         t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 4 * S);
     }
-    hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
-    if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
-    dm(reinterpret_cast<void**>(&t->d_etab), sizeof(GfttRoi) * S);
     dm(reinterpret_cast<void**>(&t->d_ecorners), sizeof(float2) * S * cfg->max_corners);
     dm(reinterpret_cast<void**>(&t->d_ecounts), sizeof(int32_t) * S);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->pyr_ready, hipEventDisableTiming);
@@ -541,13 +560,17 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             int rc2 = gftt_prepare(t->erois.data(), (int)t->erois.size(), c.width, c.height, &gp, htab, &eplan);
             if (rc2 != TBDK_OK) return rc2;
             hipStream_t es = t->early_s;  // ordered at the top of the step
-            hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * t->erois.size(), hipMemcpyHostToDevice, es);
-            if (e != hipSuccess) return map_status(e);
+            const GfttRoi* dtab = t->zc ? t->d_etab + (htab - t->h_etab[0]) : t->d_etab;
+            if (!t->zc) {
+                hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * t->erois.size(),
+                                              hipMemcpyHostToDevice, es);
+                if (e != hipSuccess) return map_status(e);
+            }
             const tbdk_level& L0 = P.lv[0];
-            rc2 = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_etab, eplan, &gp,
+            rc2 = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
                               reinterpret_cast<float*>(t->d_ecorners), t->d_ecounts, es);
             if (rc2 != TBDK_OK) return rc2;
-            e = hipEventRecord(t->early_done, es);
+            const hipError_t e = hipEventRecord(t->early_done, es);
             if (e != hipSuccess) return map_status(e);
             early_launched = true;
         }
@@ -596,8 +619,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         // every slot live, nA + nB == S and the two ranges tile h_lists exactly)
         std::copy(t->b_list.begin(), t->b_list.begin() + nB, t->h_lists + nA);
         const size_t bytes = sizeof(FitEntry) * S + sizeof(int32_t) * (size_t)(nA + nB);
-        hipError_t e = hipMemcpyAsync(t->d_pre, t->h_pre, bytes, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return map_status(e);
+        if (!t->zc) {
+            hipError_t e = hipMemcpyAsync(t->d_pre, t->h_pre, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) return map_status(e);
+        }
         if (nA > 0) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
@@ -640,7 +665,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
         timing_end(t->ctx, rec, s);
-        e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
+        if (!t->zc) e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipEventRecord(t->fit_done, s);
         if (e != hipSuccess) return map_status(e);
         if (next) {  // runs on the device while this step waits for the fit and tracks
@@ -693,7 +718,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (ns > 0) {
                 hipStream_t ls = t->la_s;
                 e = hipStreamWaitEvent(ls, t->la_ready, 0);
-                if (e == hipSuccess)
+                if (e == hipSuccess && !t->zc)
                     e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
                 if (e != hipSuccess) return map_status(e);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
@@ -814,8 +839,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         const size_t bytes = nroi > 0     ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) - h0
                              : nearly > 0 ? reinterpret_cast<const uint8_t*>(t->h_eslot + nearly) - h0
                                           : sizeof(int) * nclear;
-        hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
-        if (e != hipSuccess) return map_status(e);
+        if (!t->zc) {
+            hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
+            if (e != hipSuccess) return map_status(e);
+        }
     }
     if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
@@ -861,7 +888,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 hipStream_t ls = t->la_s;
                 e = hipStreamWaitEvent(ls, t->la_ready, 0);
                 if (e == hipSuccess && nroi > 0) e = hipStreamWaitEvent(ls, t->eig_done, 0);
-                if (e == hipSuccess)
+                if (e == hipSuccess && !t->zc)
                     e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
                 if (e != hipSuccess) return map_status(e);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),

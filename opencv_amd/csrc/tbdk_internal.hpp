@@ -63,6 +63,7 @@ struct tbdk_ctx {
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     int opt_tbd_early_gftt = 1;  // tbdk_ctx_set_option("tbd_early_gftt")
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")
+    int opt_tbd_zero_copy = 1;   // tbdk_ctx_set_option("tbd_zero_copy"), read by tbdk_tbd_create
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;

@@ -210,3 +210,24 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
         assert res[key][1] == res[0, 0][1], key
         assert res[key][2] == res[0, 0][2], key
     assert res[1, 1][3] > 2 * F and res[0, 0][3] == 0  # the early path was taken (and off means off)
+
+
+def test_tbd_zero_copy_matches_copies(gpu):
+    """Zero-copy staging (kernels reading the pinned tables, the fit writing to
+    pinned memory) and staged copies give the same frames."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 32, 12
+    frames, gt = klt.synth_render(8, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
+    res = []
+    try:
+        for zc in (1, 0):
+            gpu.set_option("tbd_zero_copy", zc)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            res.append(([_mkey(m) for m in ms], loop.tracks()))
+    finally:
+        gpu.set_option("tbd_zero_copy", 1)
+    assert res[0] == res[1]
