@@ -110,27 +110,44 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
     }
 }
 
-// point sets of deleted tracks: count = 0 (keeps later LK launches from
-// working on stale slots)
-__global__ void tbd_clear_kernel(const int* __restrict__ slots, int n, int32_t* __restrict__ slot_counts)
-{
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) slot_counts[slots[k]] = 0;
-}
+// The post-tracker slot updates in one launch: block k < nroi copies the
+// post-tracker GFTT's corner row k into slot roi_slot[k]; the next nearly
+// blocks copy early-GFTT row erow[k] into eslot[k]; a last block sets the
+// count of every deleted track's slot to 0 (slots handed to a new track in the
+// same step are scattered, not cleared, so no slot is written twice).
+struct PostArgs {
+    const int* clear;
+    int nclear;
+    const float2* corners;
+    const int32_t* counts;
+    const int* roi_slot;
+    int nroi;
+    const float2* ecorners;
+    const int32_t* ecounts;
+    const int* erow;
+    const int* eslot;
+    int nearly;
+    int maxc;
+    float2* slot_pts;
+    int32_t* slot_counts;
+};
 
-// GFTT staging -> point slots: item k copies corner row rows[k] (k when rows
-// is null) into slot roi_slot[k]
-__global__ void tbd_scatter_kernel(const float2* __restrict__ corners, const int32_t* __restrict__ counts,
-                                   const int* __restrict__ rows, const int* __restrict__ roi_slot, int maxc,
-                                   float2* __restrict__ slot_pts, int32_t* __restrict__ slot_counts)
+__global__ void tbd_post_kernel(PostArgs a)
 {
-    const int k = blockIdx.x;
-    const int r = rows ? rows[k] : k;
-    const int n = counts[r] < 0 ? 0 : counts[r];
-    const int s = roi_slot[k];
-    for (int j = threadIdx.x; j < n; j += blockDim.x)
-        slot_pts[(size_t)s * kSlotPts + j] = corners[(size_t)r * maxc + j];
-    if (threadIdx.x == 0) slot_counts[s] = n;
+    int k = blockIdx.x;
+    if (k >= a.nroi + a.nearly) {
+        for (int j = threadIdx.x; j < a.nclear; j += blockDim.x) a.slot_counts[a.clear[j]] = 0;
+        return;
+    }
+    const bool early = k >= a.nroi;
+    if (early) k -= a.nroi;
+    const int r = early ? a.erow[k] : k;
+    const int32_t c = early ? a.ecounts[r] : a.counts[r];
+    const int n = c < 0 ? 0 : c;
+    const int s = early ? a.eslot[k] : a.roi_slot[k];
+    const float2* src = (early ? a.ecorners : a.corners) + (size_t)r * a.maxc;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) a.slot_pts[(size_t)s * kSlotPts + j] = src[j];
+    if (threadIdx.x == 0) a.slot_counts[s] = n;
 }
 
 }  // namespace tbdk
@@ -825,6 +842,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         bool conflict = false;
         for (int sl : t->spec_list) conflict |= t->touched[(size_t)sl] || t->refreshed[(size_t)sl];
         for (int k = 0; k < nclear; ++k) t->touched[(size_t)t->h_clear[k]] = 0;
+        int nc = 0;  // deleted slots handed to a new track are scattered, not cleared
+        for (int k = 0; k < nclear; ++k)
+            if (!t->refreshed[(size_t)t->h_clear[k]]) t->h_clear[nc++] = t->h_clear[k];
+        nclear = nc;
         if (conflict) {
             hipError_t e = hipStreamWaitEvent(t->side, t->la_done, 0);
             if (e != hipSuccess) return map_status(e);
@@ -850,16 +871,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                          reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side, next ? t->eig_done : nullptr);
         if (rc != TBDK_OK) return rc;
     }
-    if (nclear > 0)
-        hipLaunchKernelGGL(tbd_clear_kernel, dim3((nclear + 255) / 256), dim3(256), 0, t->side, t->d_clear, nclear,
-                           t->slot_counts);
-    if (nroi > 0)
-        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nroi), dim3(256), 0, t->side, t->d_corners, t->d_ccounts,
-                           static_cast<const int*>(nullptr), t->d_roi_slot, c.max_corners, t->slot_pts,
-                           t->slot_counts);
-    if (nearly > 0)
-        hipLaunchKernelGGL(tbd_scatter_kernel, dim3(nearly), dim3(256), 0, t->side, t->d_ecorners, t->d_ecounts,
-                           t->d_erow, t->d_eslot, c.max_corners, t->slot_pts, t->slot_counts);
+    if (nclear > 0 || nroi > 0 || nearly > 0) {
+        const PostArgs pa{t->d_clear, nclear, t->d_corners, t->d_ccounts, t->d_roi_slot, nroi,
+                          t->d_ecorners, t->d_ecounts, t->d_erow, t->d_eslot, nearly, c.max_corners,
+                          t->slot_pts, t->slot_counts};
+        hipLaunchKernelGGL(tbd_post_kernel, dim3(nroi + nearly + (nclear > 0 ? 1 : 0)), dim3(256), 0, t->side, pa);
+    }
     // post_done also after an early GFTT none of whose ROIs was used: the next
     // step's fit sync then orders that GFTT's table upload before the staging
     // table is rewritten (two steps later)
