@@ -693,7 +693,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (rc != TBDK_OK) return rc;
         auto ts0 = clk::now();
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
-        e = hipEventSynchronize(t->fit_done);
+        // the one host wait of the frame, on the critical path: poll instead of
+        // a blocking synchronize (its wake-up latency is part of every frame)
+        while ((e = hipEventQuery(t->fit_done)) == hipErrorNotReady) {
+        }
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);
         synced = true;
