@@ -72,12 +72,18 @@ private:
 };
 
 // Padded pyramid with Scharr derivative planes (buildOpticalFlowPyramid with
-// withDerivatives=true, video/src/lkpyramid.cpp:697-793).
+// withDerivatives=true, video/src/lkpyramid.cpp:697-793); depth TBDK_DEPTH_16F
+// gives the fp16 pixel path's pyramid (tbdk_pyr_create_f16).
 class Pyramid {
 public:
-    Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}) : ctx_(&ctx)
+    Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}, int depth = TBDK_DEPTH_8U)
+        : ctx_(&ctx)
     {
-        check(tbdk_pyr_create(ctx.get(), width, height, max_level, win.width, win.height, &p_), "tbdk_pyr_create");
+        if (depth == TBDK_DEPTH_16F)
+            check(tbdk_pyr_create_f16(ctx.get(), width, height, max_level, win.width, win.height, &p_),
+                  "tbdk_pyr_create_f16");
+        else
+            check(tbdk_pyr_create(ctx.get(), width, height, max_level, win.width, win.height, &p_), "tbdk_pyr_create");
     }
     ~Pyramid() { tbdk_pyr_destroy(ctx_->get(), &p_); }
     Pyramid(const Pyramid&) = delete;
@@ -87,6 +93,13 @@ public:
         if (img.width != p_.lv[0].width || img.height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build");
         check(tbdk_pyr_build(ctx_->get(), img.data, img.pitch, &p_, stream), "tbdk_pyr_build");
     }
+    // fp16 frame (pitch in bytes) into an fp16 pyramid
+    void build_f16(const uint16_t* data, int width, int height, int pitch, void* stream = nullptr)
+    {
+        if (width != p_.lv[0].width || height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build_f16");
+        check(tbdk_pyr_build_f16(ctx_->get(), data, pitch, &p_, stream), "tbdk_pyr_build_f16");
+    }
+    int depth() const { return p_.depth; }
     const tbdk_pyr& get() const { return p_; }
     int levels() const { return p_.nlevels; }
 

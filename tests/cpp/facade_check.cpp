@@ -53,6 +53,21 @@ int main(int argc, char** argv)
                 ++good;
         std::printf("corners %d tracked-correctly %d\n", n, good);
         if (good * 10 < n * 8) return 6;
+        {  // the fp16 pixel path through the facade: fp16 pyramids from the u8 frames
+            tbdk::Pyramid P(ctx, W, H, 2, {21, 21}, TBDK_DEPTH_16F), N(ctx, W, H, 2, {21, 21}, TBDK_DEPTH_16F);
+            P.build(a);
+            N.build(b);
+            lk->calc(P, N, pts, nxt, st, nullptr, n);
+            (void)hipMemcpy(p1.data(), nxt, 8 * (size_t)n, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(s.data(), st, n, hipMemcpyDeviceToHost);
+            int good16 = 0;
+            for (int i = 0; i < n; ++i)
+                if (s[i] && std::abs(p1[2 * i] - p0[2 * i] - 1.5f) < 0.1f &&
+                    std::abs(p1[2 * i + 1] - p0[2 * i + 1] + 0.5f) < 0.1f)
+                    ++good16;
+            std::printf("fp16 tracked-correctly %d\n", good16);
+            if (good16 * 10 < n * 8 || P.depth() != TBDK_DEPTH_16F) return 7;
+        }
         // dense Farneback through the facade: the interior flow is the shift
         float* flow;
         if (hipMalloc(&flow, (size_t)W * H * 8)) return 4;

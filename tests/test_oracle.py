@@ -190,3 +190,89 @@ def test_synth_is_deterministic_and_pinned():
     for f in range(3):
         assert hashlib.sha256(fr[f].tobytes()).hexdigest() == golden["640x480x32"][f]
     assert hashlib.sha256(gt.tobytes()).hexdigest() == golden["640x480x32_gt"]
+
+
+# ---- the fp16 pixel path's oracle (oracle/klt16_oracle.c) ----------------------
+
+def _h16():
+    import ctypes as C
+
+    lib = O._lib16()
+    lib.orc16_f2h.restype = C.c_uint16
+    lib.orc16_f2h.argtypes = [C.c_float]
+    lib.orc16_h2f.restype = C.c_float
+    lib.orc16_h2f.argtypes = [C.c_uint16]
+    return lib
+
+
+def test_f16_conversions_match_numpy():
+    """binary16 <-> binary32 (round to nearest even) against numpy's float16:
+    every half value, edge values, random floats over the whole range"""
+    lib = _h16()
+    h = np.arange(65536, dtype=np.uint16)
+    ref = h.view(np.float16).astype(np.float32)
+    got = np.array([lib.orc16_h2f(int(v)) for v in h], dtype=np.float32)
+    nan = np.isnan(ref)
+    assert np.array_equal(np.isnan(got), nan) and np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal(20000) * np.exp(rng.uniform(-20, 11, 20000))).astype(np.float32)
+    x = np.concatenate([x, np.float32([0, -0.0, 2 ** -24, 2 ** -25, 1.5 * 2 ** -25, 6.1e-5, 65504, 65519, 65520,
+                                       1e9, -1e9, 0.1, 1 / 3, 255.0])])
+    with np.errstate(over="ignore"):
+        ref = x.astype(np.float16).view(np.uint16)
+    got = np.array([lib.orc16_f2h(float(v)) for v in x], dtype=np.uint16)
+    assert np.array_equal(got, ref)
+
+
+def test_f16_pyr_down_and_scharr_definitions():
+    """the fp16 pyrDown / Scharr against a numpy statement of the same fp32
+    expression order (reflect-101 borders), rounded to float16"""
+    rng = np.random.default_rng(4)
+    img = (rng.uniform(0, 255, (37, 53)) + rng.uniform(0, 1, (37, 53))).astype(np.float16)
+    f = img.astype(np.float32)
+    h, w = f.shape
+    ry = lambda y: O.load().orc_reflect101(y, h)  # noqa: E731
+    rx = lambda x: O.load().orc_reflect101(x, w)  # noqa: E731
+    dh, dw = (h + 1) // 2, (w + 1) // 2
+    ref = np.empty((dh, dw), np.float16)
+    for y in range(dh):
+        for x in range(dw):
+            r = []
+            for j in range(5):
+                row = f[ry(2 * y + j - 2)]
+                s = [row[rx(2 * x + k - 2)] for k in range(5)]
+                r.append(np.float32(np.float32(np.float32(np.float32(s[2] * np.float32(6)) +
+                                                          np.float32(np.float32(s[1] + s[3]) * np.float32(4))) + s[0]) + s[4]))
+            v = np.float32(np.float32(np.float32(np.float32(r[2] * np.float32(6)) +
+                                                 np.float32(np.float32(r[1] + r[3]) * np.float32(4))) + r[0]) + r[4])
+            ref[y, x] = np.float16(np.float32(v * np.float32(1 / 256)))
+    assert np.array_equal(O.pyr_down16(img).view(np.uint16), ref.view(np.uint16))
+    d = O.scharr16(img)
+    y, x = 7, 11
+    t0 = [np.float32(np.float32((f[y - 1, c] + f[y + 1, c]) * np.float32(3)) + np.float32(f[y, c] * np.float32(10)))
+          for c in (x - 1, x, x + 1)]
+    t1 = [np.float32(f[y + 1, c] - f[y - 1, c]) for c in (x - 1, x, x + 1)]
+    assert d[y, x, 0] == np.float16(np.float32(t0[2] - t0[0]))
+    assert d[y, x, 1] == np.float16(np.float32(np.float32(np.float32(t1[2] + t1[0]) * np.float32(3)) +
+                                               np.float32(t1[1] * np.float32(10))))
+
+
+def test_f16_lk_recovers_translation_and_tracks_u8_path():
+    """the fp16 LK on a known translation, and against the 8-bit path on the
+    same synthetic frames (different arithmetic: a sanity bound, not parity)"""
+    frames, gt = O.synth(20261015, 320, 240, 12, 0, 2)
+    rng = np.random.default_rng(0)
+    pts = np.concatenate([np.stack([rng.uniform(x, x + bw, 24), rng.uniform(y, y + bh, 24)], 1)
+                          for v, x, y, bw, bh in gt[0] if v]).astype(np.float32)
+    nx, st, _, _ = O.lk(O.Pyramid(frames[0]), O.Pyramid(frames[1]), pts, accum=O.ACCUM_EXACT)
+    nx16, st16, err16, _ = O.lk16(O.Pyramid16(frames[0]), O.Pyramid16(frames[1]), pts)
+    both = (st == 1) & (st16 == 1)
+    assert both.mean() > 0.9 and (st == st16).mean() > 0.99
+    assert (np.abs(nx - nx16)[both].max(1) <= 1e-2).mean() >= 0.99
+    # integer translation of a blurred noise image: recovered exactly enough
+    img = frames[0]
+    shifted = np.roll(np.roll(img, 2, axis=1), -1, axis=0)
+    g = np.stack(np.meshgrid(np.arange(40, 280, 20), np.arange(40, 200, 20)), -1).reshape(-1, 2).astype(np.float32)
+    nt, stt, _, _ = O.lk16(O.Pyramid16(img), O.Pyramid16(shifted), g)
+    assert (stt == 1).all()
+    assert np.abs(nt - (g + np.float32([2, -1]))).max() < 0.02
