@@ -190,6 +190,46 @@ static double row_min(const double* row, unsigned n, double init)
     return m;
 }
 
+// The dense passes of the solver, built for AVX2 and baseline x86-64 (picked
+// at load time).  Elementwise IEEE operations only (no contraction: the file is
+// built with -ffp-contract=off), so every value is the same in both builds.
+#define TBDK_SOLVER_CLONES __attribute__((target_clones("avx2", "default")))
+
+// row -= m (step 1, :507-516), fused with step 2's running column minima
+// (:539-561, rows in order): colMin[c] = (row[c] < colMin[c]) ? row[c] : colMin[c]
+TBDK_SOLVER_CLONES static void sub_row_min_and_colmin(double* __restrict row, unsigned n, double m,
+                                                      double* __restrict colMin)
+{
+    for (unsigned c = 0; c < n; ++c) {
+        const double v = row[c] - m;
+        row[c] = v;
+        colMin[c] = (v < colMin[c]) ? v : colMin[c];
+    }
+}
+
+// one row of the zero pattern (equalsZero, tbd.hpp:178-181), optionally after
+// subtracting the column minima (step 2); returns the row's zero count and
+// adds the row to the column counts and "last zero row" of every column
+TBDK_SOLVER_CLONES static unsigned zero_row(double* __restrict row, const double* __restrict colMin, unsigned n,
+                                           uint8_t* __restrict z, unsigned* __restrict colZeros,
+                                           unsigned* __restrict colLast, unsigned r)
+{
+    if (colMin)
+        for (unsigned c = 0; c < n; ++c) row[c] -= colMin[c];
+    unsigned cnt = 0;
+    for (unsigned c = 0; c < n; ++c) {
+        const uint8_t v = std::fabs(row[c]) < 0.00000001 ? 1 : 0;
+        z[c] = v;
+        cnt += v;
+    }
+    if (cnt)
+        for (unsigned c = 0; c < n; ++c) {
+            colZeros[c] += z[c];
+            colLast[c] = z[c] ? r : colLast[c];  // row of a column's single zero
+        }
+    return cnt;
+}
+
 // calculateCostMatrix + solveAssignmentProblem + classifyAssignments
 // (tbd.cpp:333-891) on a flat n x n matrix.  The reference's operation order
 // on every matrix entry is kept (row minima, column minima, the step-4
@@ -224,7 +264,9 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
     for (unsigned k = 0; k < nD; ++k) sortedX0[k] = detX0[detOrder[k]];
     assignmentPerRow.assign(n, n);
     if (n == 0) return;
-    // calculateCostMatrix (:333-351) fused with step 1, the row minima (:494-516)
+    colMin.assign(n, huge);
+    // calculateCostMatrix (:333-351) fused with step 1, the row minima (:494-516),
+    // and step 2's column minima
     for (unsigned r = 0; r < n; ++r) {
         double* row = &cost[(size_t)r * n];
         unsigned c0 = 0;
@@ -248,17 +290,10 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
             c0 = nD;
         }
         for (unsigned c = c0; c < n; ++c) row[c] = pad;
-        const double m = row_min(row, n, huge);
-        for (unsigned k = 0; k < n; ++k) row[k] -= m;
+        sub_row_min_and_colmin(row, n, row_min(row, n, huge), colMin.data());
     }
     {
-        // step 2: column minima (:539-561), scanned in the same r order per column;
-        // their subtraction is fused into the first round's zero pass
-        colMin.assign(n, huge);
-        for (unsigned r = 0; r < n; ++r) {
-            const double* row = &cost[(size_t)r * n];
-            for (unsigned c = 0; c < n; ++c) colMin[c] = (row[c] < colMin[c]) ? row[c] : colMin[c];
-        }
+        // the column minima's subtraction is fused into the first round's zero pass
         zero.resize((size_t)n * n);
         rowZeros.resize(n);
         colZeros.resize(n);
@@ -271,20 +306,9 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
         bool first = true;
         while (true) {  // (:585-887)
             std::fill(colZeros.begin(), colZeros.end(), 0u);
-            for (unsigned r = 0; r < n; ++r) {
-                double* row = &cost[(size_t)r * n];
-                uint8_t* z = &zero[(size_t)r * n];
-                unsigned cnt = 0;
-                if (first)
-                    for (unsigned c = 0; c < n; ++c) row[c] -= colMin[c];
-                for (unsigned c = 0; c < n; ++c) z[c] = std::fabs(row[c]) < 0.00000001 ? 1 : 0;  // == equalsZero
-                for (unsigned c = 0; c < n; ++c) cnt += z[c];
-                if (cnt) {
-                    for (unsigned c = 0; c < n; ++c) colZeros[c] += z[c];
-                    for (unsigned c = 0; c < n; ++c) colLast[c] = z[c] ? r : colLast[c];  // row of a column's single zero
-                }
-                rowZeros[r] = cnt;
-            }
+            for (unsigned r = 0; r < n; ++r)
+                rowZeros[r] = zero_row(&cost[(size_t)r * n], first ? colMin.data() : nullptr, n, &zero[(size_t)r * n],
+                                       colZeros.data(), colLast.data(), r);
             first = false;
             std::fill(rowA.begin(), rowA.end(), 0);
             std::fill(colA.begin(), colA.end(), 0);
