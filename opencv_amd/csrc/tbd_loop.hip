@@ -132,7 +132,7 @@ struct PostArgs {
     int32_t* slot_counts;
 };
 
-__global__ void tbd_post_kernel(PostArgs a)
+__global__ __launch_bounds__(64) void tbd_post_kernel(PostArgs a)
 {
     int k = blockIdx.x;
     if (k >= a.nroi + a.nearly) {
@@ -878,7 +878,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         const PostArgs pa{t->d_clear, nclear, t->d_corners, t->d_ccounts, t->d_roi_slot, nroi,
                           t->d_ecorners, t->d_ecounts, t->d_erow, t->d_eslot, nearly, c.max_corners,
                           t->slot_pts, t->slot_counts};
-        hipLaunchKernelGGL(tbd_post_kernel, dim3(nroi + nearly + (nclear > 0 ? 1 : 0)), dim3(256), 0, t->side, pa);
+        // one wave per block: the launch usually finds the look-ahead PyrLK's waves
+        // holding most wave slots, and single waves fit into the ones they free
+        hipLaunchKernelGGL(tbd_post_kernel, dim3(nroi + nearly + (nclear > 0 ? 1 : 0)), dim3(64), 0, t->side, pa);
     }
     // post_done also after an early GFTT none of whose ROIs was used: the next
     // step's fit sync then orders that GFTT's table upload before the staging
