@@ -375,7 +375,8 @@ def main():
                     help="run: tbdk_tbd_run (native frame loop with look-ahead); ahead: per-frame "
                          "tbdk_tbd_step_ahead; step: per-frame tbdk_tbd_step (no look-ahead)")
     ap.add_argument("--lk-impl", type=int, default=0, help="PyrLK kernel (ctx option lk_impl; 0 auto)")
-    ap.add_argument("--no-early-gftt", action="store_true", help="ctx option tbd_early_gftt = 0 (A/B runs)")
+    ap.add_argument("--early-gftt", type=int, default=2, choices=[0, 1, 2],
+                    help="ctx option tbd_early_gftt (A/B runs; 0 off, 1 new tracks, 2 + re-detection boxes)")
     ap.add_argument("--no-spec-lookahead", action="store_true", help="ctx option tbd_spec_lookahead = 0 (A/B runs)")
     ap.add_argument("--no-zero-copy", action="store_true", help="ctx option tbd_zero_copy = 0 (A/B runs)")
     ap.add_argument("--kstats", default="lk_sparse",
@@ -416,7 +417,7 @@ def main():
     ctx = klt.Context.get(dev)
     if args.lk_impl:
         ctx.set_option("lk_impl", args.lk_impl)
-    ctx.set_option("tbd_early_gftt", 0 if args.no_early_gftt else 1)
+    ctx.set_option("tbd_early_gftt", args.early_gftt)
     ctx.set_option("tbd_spec_lookahead", 0 if args.no_spec_lookahead else 1)
     ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
     nframes = args.warmup + args.steps

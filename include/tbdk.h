@@ -92,9 +92,12 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
  *       (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
-/*   "tbd_early_gftt" (0/1, default 1): the TBD loop runs GFTT over the
+/*   "tbd_early_gftt" (0/1/2, default 2): the TBD loop runs GFTT over the
  *       detections that will start new tracks at the start of the step, off
- *       the critical path (results equal).
+ *       the critical path; 2 also over the box each existing track would get
+ *       on a re-detection frame from the detection overlapping it most (a
+ *       guess: boxes the tracker step does not confirm take the regular GFTT;
+ *       results equal).
  *   "tbd_spec_lookahead" (0/1, default 1): with a look-ahead frame, the TBD
  *       loop starts the next frame's PyrLK of the point sets that stay
  *       unchanged unless their track is deleted before the host tracker step
@@ -220,7 +223,9 @@ typedef struct tbdk_gftt_params {
  *   corners    : device, nroi x max_corners x float2, frame coordinates
  *   counts     : device, nroi int32 (corners found; -1 if a ROI produced more
  *                candidates than the on-chip buffer holds — never truncated)
- * Scratch grows on demand (tbdk_gftt_reserve avoids allocation in the call). */
+ * Scratch grows on demand (tbdk_gftt_reserve avoids allocation in the call);
+ * it is the context's: calls on one context from different streams must be
+ * ordered by the caller (a TBD loop has scratch of its own). */
 int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch,
                    const tbdk_roi* rois, int nroi, const tbdk_gftt_params* params,
                    float* corners, int32_t* counts, void* stream);

@@ -83,10 +83,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
         (void)hipEventDestroy(r.end);
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
-    if (ctx->gftt_rois) (void)hipFree(ctx->gftt_rois);
-    if (ctx->gftt_blk) (void)hipFree(ctx->gftt_blk);
-    if (ctx->gftt_planes) (void)hipFree(ctx->gftt_planes);
-    if (ctx->gftt_cand) (void)hipFree(ctx->gftt_cand);
+    gftt_scratch_free(ctx->gftt);
     fb_release(ctx);
     hog_release(ctx);
     if (ctx->dense_buf) (void)hipFree(ctx->dense_buf);
@@ -117,7 +114,8 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_early_gftt") == 0) {
-        ctx->opt_tbd_early_gftt = value != 0;
+        if (value < 0 || value > 2) return TBDK_EINVAL;
+        ctx->opt_tbd_early_gftt = (int)value;
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_spec_lookahead") == 0) {
@@ -430,10 +428,43 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
     return TBDK_OK;
 }
 
-int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
-                const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s, hipEvent_t after_eig)
+void gftt_scratch_free(GfttScratch& sc)
 {
-    int rc = tbdk_gftt_reserve(ctx, plan.nroi, plan.total);
+    for (void** p : {&sc.rois, reinterpret_cast<void**>(&sc.blk), &sc.planes, &sc.cand}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    sc.cap_rois = 0;
+    sc.cap_px = 0;
+}
+
+int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px)
+{
+    if (max_rois < 0 || max_px < 0) return TBDK_EINVAL;
+    if (max_rois <= sc.cap_rois && max_px <= sc.cap_px) return TBDK_OK;
+    DeviceGuard g(device);
+    const int rois = std::max(max_rois, sc.cap_rois);
+    const int64_t px = std::max(max_px, sc.cap_px);
+    gftt_scratch_free(sc);  // hipFree waits for the device: no launch still reads it
+    const int64_t ncb = gftt_max_cblocks(rois, px), nw = gftt_max_words(px);
+    hipError_t e = hipMalloc(&sc.rois, sizeof(GfttRoi) * (size_t)std::max(rois, 1));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&sc.blk), sizeof(int) * (size_t)ncb);
+    if (e == hipSuccess) e = hipMalloc(&sc.planes, sizeof(float) * (size_t)std::max<int64_t>(px, 1));
+    if (e == hipSuccess) e = hipMalloc(&sc.cand, sizeof(uint64_t) * (size_t)nw);
+    if (e != hipSuccess) {
+        gftt_scratch_free(sc);
+        return map_err(e);
+    }
+    sc.cap_rois = rois;
+    sc.cap_px = px;
+    return TBDK_OK;
+}
+
+int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois,
+                const GfttPlan& plan, const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
+                hipEvent_t after_eig)
+{
+    int rc = gftt_reserve(sc, ctx->device, plan.nroi, plan.total);
     if (rc != TBDK_OK) return rc;
     DeviceGuard g(ctx->device);
     int rec = timing_begin(ctx, "gftt", s);
@@ -443,9 +474,9 @@ int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_r
     a.rois = d_rois;
     a.nroi = plan.nroi;
     a.ncblk = plan.ncblk;
-    a.eig = static_cast<float*>(ctx->gftt_planes);
-    a.blk_max = ctx->gftt_blk;
-    a.lmax = static_cast<uint64_t*>(ctx->gftt_cand);
+    a.eig = static_cast<float*>(sc.planes);
+    a.blk_max = sc.blk;
+    a.lmax = static_cast<uint64_t*>(sc.cand);
     a.max_corners = p->max_corners;
     a.quality = p->quality_level;
     a.min_distance = p->min_distance;
@@ -465,25 +496,7 @@ extern "C" {
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels)
 {
     if (!ctx || max_rois < 0 || max_total_pixels < 0) return TBDK_EINVAL;
-    if (max_rois <= ctx->gftt_cap_rois && max_total_pixels <= ctx->gftt_cap_px) return TBDK_OK;
-    DeviceGuard g(ctx->device);
-    const int rois = std::max(max_rois, ctx->gftt_cap_rois);
-    const int64_t px = std::max(max_total_pixels, ctx->gftt_cap_px);
-    for (void** p : {&ctx->gftt_rois, reinterpret_cast<void**>(&ctx->gftt_blk), &ctx->gftt_planes, &ctx->gftt_cand}) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
-    }
-    ctx->gftt_cap_rois = 0;
-    ctx->gftt_cap_px = 0;
-    const int64_t ncb = gftt_max_cblocks(rois, px), nw = gftt_max_words(px);
-    hipError_t e = hipMalloc(&ctx->gftt_rois, sizeof(GfttRoi) * (size_t)std::max(rois, 1));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->gftt_blk), sizeof(int) * (size_t)ncb);
-    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_planes, sizeof(float) * (size_t)std::max<int64_t>(px, 1));
-    if (e == hipSuccess) e = hipMalloc(&ctx->gftt_cand, sizeof(uint64_t) * (size_t)nw);
-    if (e != hipSuccess) return map_err(e);
-    ctx->gftt_cap_rois = rois;
-    ctx->gftt_cap_px = px;
-    return TBDK_OK;
+    return gftt_reserve(ctx->gftt, ctx->device, max_rois, max_total_pixels);
 }
 
 int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, const tbdk_roi* rois,
@@ -501,9 +514,10 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     // pageable source: the copy is staged and complete when the call returns
-    hipError_t e = hipMemcpyAsync(ctx->gftt_rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(ctx->gftt.rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
-    return gftt_launch(ctx, img, pitch, static_cast<const GfttRoi*>(ctx->gftt_rois), plan, p, corners, counts, s);
+    return gftt_launch(ctx, ctx->gftt, img, pitch, static_cast<const GfttRoi*>(ctx->gftt.rois), plan, p, corners,
+                       counts, s);
 }
 
 int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
@@ -522,23 +536,23 @@ int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int he
     if (rc != TBDK_OK) return rc;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e = hipMemcpyAsync(ctx->gftt_rois, &tab, sizeof(GfttRoi), hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(ctx->gftt.rois, &tab, sizeof(GfttRoi), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
     int rec = timing_begin(ctx, "corner_min_eig", s);
     GfttArgs a{};
     a.img = img;
     a.pitch = pitch;
-    a.rois = static_cast<const GfttRoi*>(ctx->gftt_rois);
+    a.rois = static_cast<const GfttRoi*>(ctx->gftt.rois);
     a.nroi = 1;
     a.ncblk = plan.ncblk;
-    a.eig = static_cast<float*>(ctx->gftt_planes);
-    a.blk_max = ctx->gftt_blk;
-    a.lmax = static_cast<uint64_t*>(ctx->gftt_cand);
+    a.eig = static_cast<float*>(ctx->gftt.planes);
+    a.blk_max = ctx->gftt.blk;
+    a.lmax = static_cast<uint64_t*>(ctx->gftt.cand);
     a.eig_redo = ctx->opt_gftt_eig_redo;
     e = launch_gftt_eig(a, s);
     timing_end(ctx, rec, s);
     if (e == hipSuccess)
-        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt_planes, (size_t)width * 4, (size_t)width * 4, height,
+        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)width * 4, (size_t)width * 4, height,
                              hipMemcpyDeviceToDevice, s);
     return map_err(e);
 }

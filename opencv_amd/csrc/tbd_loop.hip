@@ -243,6 +243,8 @@ struct tbdk_tbd {
     int epar = 0;
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
+    std::vector<int> det_order;
+    GfttScratch gftt;  // this loop's own (early GFTT on early_s, post-tracker GFTT on side)                   // scratch: detections by left edge
     hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
     // zero-copy staging: the kernels read the pinned host tables (fit entries,
     // slot lists, post-tracker lists, GFTT ROI tables) and the fit kernel
@@ -288,6 +290,7 @@ int release(tbdk_tbd* t)
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
+    gftt_scratch_free(t->gftt);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_corners,
                    t->d_ccounts, t->d_ecorners, t->d_ecounts};
     for (void* p : dev)
@@ -462,7 +465,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         return TBDK_ENOMEM;
     }
     for (int s = 0; s < cfg->max_tracks; ++s) t->free_slots.push(s);
-    rc = tbdk_gftt_reserve(ctx, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
+    rc = gftt_reserve(t->gftt, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc != TBDK_OK) {
         release(t);
         return rc;
@@ -570,6 +573,55 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
             t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
         }
+        // re-detection frames: every existing track's set is refreshed in its box
+        // after updateAssignedTracks (tbd.cpp:948-965), which depends only on the
+        // assigned detection and the track's box history; speculate the detection
+        // of largest overlap with the track's last box and GFTT that box early
+        // (a track assigned otherwise, or not at all, takes the post-tracker GFTT)
+        if (t->ctx->opt_tbd_early_gftt >= 2 && !all_new && frame_id % c.redetect_every == 0 && ndets > 0) {
+            auto& order = t->det_order;
+            order.resize((size_t)ndets);
+            int maxw = 0;
+            for (int i = 0; i < ndets; ++i) {
+                order[(size_t)i] = i;
+                maxw = std::max(maxw, dets[i].width);
+            }
+            std::sort(order.begin(), order.end(), [&](int a, int b) { return dets[a].x < dets[b].x; });
+            for (const auto& tr : t->tracker->getTracks()) {
+                if ((int)t->erois.size() >= c.max_tracks) break;
+                if (t->slot_of.find(tr.id) == t->slot_of.end()) continue;
+                const tbd::Rect& lb = tr.bboxes.back();
+                if (lb.x >= c.bounds_xmax || lb.y >= c.bounds_ymax) continue;  // deleted by the bounds filter
+                auto lo = std::lower_bound(order.begin(), order.end(), lb.x - maxw,
+                                           [&](int a, int x) { return dets[a].x < x; });
+                int best = -1;
+                double bo = 0.0;
+                for (auto it = lo; it != order.end() && dets[*it].x <= lb.x + lb.width; ++it) {
+                    const tbdk_detection& d = dets[*it];
+                    const double o = tbd::computeBoundingBoxOverlap(lb, tbd::Rect(d.x, d.y, d.width, d.height));
+                    if (o > bo) {
+                        bo = o;
+                        best = *it;
+                    }
+                }
+                if (best < 0) continue;
+                const tbdk_detection& d = dets[best];
+                const unsigned nprior = tr.historyLength < 4 ? (unsigned)tr.historyLength : 4u;
+                unsigned wsum = 0, hsum = 0;
+                for (unsigned k = tr.bboxes.size() - nprior; k < tr.bboxes.size(); ++k) {
+                    wsum += tr.bboxes[k].width;
+                    hsum += tr.bboxes[k].height;
+                }
+                const int w = (int)((wsum + d.width) / (nprior + 1)), h = (int)((hsum + d.height) / (nprior + 1));
+                const tbd::Rect r = tbd::rect_from_point2d((double)d.x + (d.width / 2 - w / 2),
+                                                           (double)d.y + (d.height / 2 - h / 2), w, h);
+                const int x0 = std::max(r.x, 0), y0 = std::max(r.y, 0);
+                const int x1 = std::min(r.x + r.width, c.width), y1 = std::min(r.y + r.height, c.height);
+                if (x1 - x0 < 3 || y1 - y0 < 3) continue;
+                if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+                t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+            }
+        }
         if (!t->erois.empty()) {
             GfttPlan eplan;
             GfttRoi* htab = t->h_etab[t->epar];
@@ -584,7 +636,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 if (e != hipSuccess) return map_status(e);
             }
             const tbdk_level& L0 = P.lv[0];
-            rc2 = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
+            rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
                               reinterpret_cast<float*>(t->d_ecorners), t->d_ecounts, es);
             if (rc2 != TBDK_OK) return rc2;
             const hipError_t e = hipEventRecord(t->early_done, es);
@@ -870,7 +922,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
-        rc = gftt_launch(t->ctx, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
+        rc = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
                          reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side, next ? t->eig_done : nullptr);
         if (rc != TBDK_OK) return rc;
     }

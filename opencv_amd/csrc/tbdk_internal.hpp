@@ -52,6 +52,16 @@ struct DeviceGuard {
 };
 
 struct FbScratch;  // farneback.hip
+// GFTT scratch: one per context (the standalone calls) and one per TBD loop,
+// so loops sharing a context never share it across their streams
+struct GfttScratch {
+    void* rois = nullptr;    // GfttRoi[cap_rois]
+    int* blk = nullptr;      // per-strip eigenvalue maxima
+    void* cand = nullptr;    // local-maximum words (uint64 per strip row)
+    void* planes = nullptr;  // cap_px floats (eig)
+    int cap_rois = 0;
+    int64_t cap_px = 0;
+};
 struct HogScratch;  // hog.hip
 
 }  // namespace tbdk
@@ -61,19 +71,13 @@ struct tbdk_ctx {
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
-    int opt_tbd_early_gftt = 1;  // tbdk_ctx_set_option("tbd_early_gftt")
+    int opt_tbd_early_gftt = 2;  // tbdk_ctx_set_option("tbd_early_gftt")
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")
     int opt_tbd_zero_copy = 1;   // tbdk_ctx_set_option("tbd_zero_copy"), read by tbdk_tbd_create
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
-    // GFTT scratch (grown on demand, or up front by tbdk_gftt_reserve)
-    void* gftt_rois = nullptr;   // GfttRoi[cap_rois]
-    int* gftt_blk = nullptr;     // per-strip eigenvalue maxima
-    void* gftt_cand = nullptr;   // local-maximum words (uint64 per strip row)
-    void* gftt_planes = nullptr;  // cap_px floats (eig)
-    int gftt_cap_rois = 0;
-    int64_t gftt_cap_px = 0;
+    tbdk::GfttScratch gftt;  // grown on demand, or up front by tbdk_gftt_reserve
     tbdk::FbScratch* fb = nullptr;  // dense Farneback planes (farneback.hip)
     void* dense_buf = nullptr;      // dense PyrLK grid / next points / status (klt_dense.hip)
     tbdk::HogScratch* hog = nullptr;  // HOG level image, gradients, blocks, hits (hog.hip)
@@ -218,7 +222,10 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
                  GfttPlan* plan);
 // launches with a device-resident ROI table (uploaded by the caller on stream s)
 // after_eig (optional): recorded between the eigenvalue and select launches
-int gftt_launch(tbdk_ctx* ctx, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
+// scratch sized for max_rois ROIs of max_px pixels in total (grows only)
+int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px);
+void gftt_scratch_free(GfttScratch& sc);
+int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
                 const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
                 hipEvent_t after_eig = nullptr);
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig = nullptr);

@@ -176,7 +176,9 @@ def test_tbd_lookahead_discarded_on_other_frame(gpu):
 def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     """The early GFTT (detections beyond the tracker's bounds filter, GFTT'd at
     the start of the step) hands new tracks exactly the corners the
-    post-tracker GFTT computes, and the speculative look-ahead PyrLK (launched
+    post-tracker GFTT computes, so do the early GFTTs of the guessed
+    re-detection boxes (option value 2) where the tracker confirms the guess,
+    and the speculative look-ahead PyrLK (launched
     before the tracker step) equals the post-tracker one: same per-frame
     metrics, predictions and tracks with the options on and off, under the
     reference's bounds quirk (most new tracks served early, speculated sets
@@ -189,7 +191,7 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
     res = {}
     try:
-        for early, spec in ((1, 1), (1, 0), (0, 1), (0, 0)):
+        for early, spec in ((2, 1), (2, 0), (1, 1), (1, 0), (0, 1), (0, 0)):
             gpu.set_option("tbd_early_gftt", early)
             gpu.set_option("tbd_spec_lookahead", spec)
             loop = tbd.TbdLoop(c, ctx=gpu)
@@ -203,13 +205,14 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
                     preds.append(loop.predictions())
             res[early, spec] = ([_mkey(m) for m in ms], preds, loop.tracks(), sum(m.early_gftt for m in ms))
     finally:
-        gpu.set_option("tbd_early_gftt", 1)
+        gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
-    for key in ((1, 1), (1, 0), (0, 1)):
+    for key in ((2, 1), (2, 0), (1, 1), (1, 0), (0, 1)):
         assert res[key][0] == res[0, 0][0], key
         assert res[key][1] == res[0, 0][1], key
         assert res[key][2] == res[0, 0][2], key
     assert res[1, 1][3] > 2 * F and res[0, 0][3] == 0  # the early path was taken (and off means off)
+    assert res[2, 1][3] > res[1, 1][3] + F  # re-detection guesses confirmed
 
 
 def test_tbd_zero_copy_matches_copies(gpu):

@@ -1,4 +1,7 @@
 set -o pipefail
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest.log 2>&1 || exit 1
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-bash tools/profile_round.sh r02 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_tbd.py tests/test_gpu_gftt.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_tbd.log 2>&1 || exit 1
+B="python bench.py --steps 480 --no-cpu-baseline --no-step-api --no-farneback --no-hog --no-f16"
+for i in 1 2; do
+timeout -k 10 200 $B --early-gftt 2 > gpurun_out/ab_eg2_$i.json 2>/dev/null || exit 1
+timeout -k 10 200 $B --early-gftt 1 > gpurun_out/ab_eg1_$i.json 2>/dev/null || exit 1
+done
