@@ -243,8 +243,8 @@ struct tbdk_tbd {
     int epar = 0;
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
-    std::vector<int> det_order;
-    GfttScratch gftt;  // this loop's own (early GFTT on early_s, post-tracker GFTT on side)                   // scratch: detections by left edge
+    std::vector<int> det_order;                   // scratch: detections by left edge
+    GfttScratch gftt;  // this loop's own (early GFTT on early_s, post-tracker GFTT on side)
     hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
     // zero-copy staging: the kernels read the pinned host tables (fit entries,
     // slot lists, post-tracker lists, GFTT ROI tables) and the fit kernel
