@@ -42,6 +42,24 @@ __device__ __forceinline__ uint32_t scan64(uint32_t v)
     return v;
 }
 
+// M independent scans advanced step by step together: each DPP reads a value
+// written two or more instructions earlier, so no wait states are needed
+// between the dependent adds of one scan (a lone scan64 needs one per step)
+template <int M>
+__device__ __forceinline__ void scan64_n(uint32_t (&v)[M])
+{
+#define TBDK_SCAN_STEP(ctrl, rmask, bc)                                                                    \
+    _Pragma("unroll") for (int m = 0; m < M; ++m) v[m] +=                                                  \
+        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[m], ctrl, rmask, 0xF, bc);
+    TBDK_SCAN_STEP(0x111, 0xF, true)   // row_shr:1
+    TBDK_SCAN_STEP(0x112, 0xF, true)   // row_shr:2
+    TBDK_SCAN_STEP(0x114, 0xF, true)   // row_shr:4
+    TBDK_SCAN_STEP(0x118, 0xF, true)   // row_shr:8
+    TBDK_SCAN_STEP(0x142, 0xA, false)  // row_bcast:15 -> rows 1, 3
+    TBDK_SCAN_STEP(0x143, 0xC, false)  // row_bcast:31 -> rows 2, 3
+#undef TBDK_SCAN_STEP
+}
+
 // segment total of a scanned value: prefix at the point's last lane minus the
 // prefix at the lane before its first (lane 0 is idle and holds 0, so every
 // point has such a lane)
@@ -65,18 +83,20 @@ template <int N>
 __device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N])
 {
     static_assert(N >= 1 && N <= 3, "three 11-bit fields per packed scan");
-    uint32_t lo[N], hp = 0;
+    uint32_t sc[N + 1];  // lo parts, then the packed hi parts
+    sc[N] = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        lo[k] = scan64((uint32_t)v[k] & 0x3FFFFFFu);
-        hp += (uint32_t)(v[k] >> 26) << (11 * k);
+        sc[k] = (uint32_t)v[k] & 0x3FFFFFFu;
+        sc[N] += (uint32_t)(v[k] >> 26) << (11 * k);
     }
-    int h = (int)seg_total(scan64(hp), e4, s4);
+    scan64_n(sc);
+    int h = (int)seg_total(sc[N], e4, s4);
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         const int hk = k + 1 < N ? (int)((uint32_t)h << 21) >> 21 : h;  // sign-extended low field
         h = (h - hk) >> 11;
-        const uint32_t l = seg_total(lo[k], e4, s4);
+        const uint32_t l = seg_total(sc[k], e4, s4);
         out[k] = (float)((double)hk * 67108864.0 + (double)l);  // exact in double, one rounding
     }
 }
@@ -149,6 +169,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         outy = a.next_pts[2 * i + 1];
     }
     int status = 1, nit = 0;
+#if defined(TBDK_LK_PROBE_RELOADS) && TBDK_LK_PROBE_RELOADS == 2
+    int nrl = 0;
+#endif
     float errv = 0.f;
 
     for (int level = a.max_level; level >= 0; --level) {
@@ -232,16 +255,18 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
                 acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
             }
-            // J columns at the first Newton position: their loads overlap the G sums
+            if (k >= P) acc[0] = acc[1] = acc[2] = 0;
+            float s[3];
+            seg_sum_exact<3>(acc, e4, s4, s);
+            // J columns at the first Newton position, loaded after the G sums (with
+            // the loads in flight during the sums the kernel needs 148 VGPRs, 3
+            // waves per SIMD; this way 116, 4 waves)
             {
                 const bool jin = act && !(pinx < -WW || pinx >= L.w || piny < -WH || piny >= L.h);
                 const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + pinx + x + L.jpad) : 0u;
 #pragma unroll
                 for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
             }
-            if (k >= P) acc[0] = acc[1] = acc[2] = 0;
-            float s[3];
-            seg_sum_exact<3>(acc, e4, s4, s);
             // A = float(exact sum) * 2^-20   (lkpyramid.cpp:438-440)
             A11 = s[0] * FLT_SCALE;
             A12 = s[1] * FLT_SCALE;
@@ -267,7 +292,14 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             }
             nit += act ? 1 : 0;
             const bool moved = act && (inx != pinx || iny != piny);
+#ifdef TBDK_LK_PROBE_RELOADS  // tuning builds: 1 always reloads, 2 counts reloads into iters
+#if TBDK_LK_PROBE_RELOADS == 2
+            nrl += any_lane(moved) ? 1 : 0;
+#endif
+            if (TBDK_LK_PROBE_RELOADS == 1 || any_lane(moved)) {
+#else
             if (any_lane(moved)) {  // uniform: reload the J columns (unchanged for points that did not move)
+#endif
                 const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
 #pragma unroll
                 for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
@@ -346,6 +378,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         a.next_pts[2 * i + 1] = outy;
         a.status[i] = (uint8_t)status;
         if (a.err) a.err[i] = errv;
+#if defined(TBDK_LK_PROBE_RELOADS) && TBDK_LK_PROBE_RELOADS == 2
+        nit += 1000 * nrl;
+#endif
         if (a.iters) a.iters[i] = nit;
     }
 }
