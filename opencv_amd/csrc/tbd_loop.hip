@@ -552,8 +552,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // ---- early GFTT over the detections that will start new tracks: every
     // detection before the first tracks exist, else those beyond the tracker's
     // bounds filter (a track on them is predicted there and deleted before the
-    // assignment).  On the low-priority `early_s`, launched after this step's
-    // PyrLK and fit (it is needed only after the tracker step); the
+    // assignment).  On the low-priority `early_s`, launched first in the step
+    // (it is needed only after the tracker step, and overlaps this step's
+    // PyrLK and fit); the
     // post-tracker phase takes its corners for every refreshed set whose box
     // equals one of these ROIs.
     t->erois.clear();
@@ -645,7 +646,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         return TBDK_OK;
     };
-
+    rc = launch_early_gftt();
+    if (rc != TBDK_OK) return rc;
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents, h_lists) were last read by uploads issued before the
@@ -741,8 +743,6 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = enqueue_next_pyr();
             if (rc != TBDK_OK) return rc;
         }
-        rc = launch_early_gftt();
-        if (rc != TBDK_OK) return rc;
         auto ts0 = clk::now();
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
         // the one host wait of the frame, on the critical path: poll instead of
@@ -811,8 +811,6 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = enqueue_next_pyr();
             if (rc != TBDK_OK) return rc;
         }
-        rc = launch_early_gftt();
-        if (rc != TBDK_OK) return rc;
     }
 
     // ---- host tracker step (cv::tbd::Tracker::performTrackingStep)
