@@ -108,7 +108,10 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
 // by the "gftt_eig_redo" option in the tests) the segments are walked again one
 // after another, each from its predecessor's final SUM: the reference's
 // sequential order.
-constexpr int kEigWaves = 8;  // row segments (waves) per strip
+#ifndef TBDK_GFTT_EIG_WAVES
+#define TBDK_GFTT_EIG_WAVES 8
+#endif
+constexpr int kEigWaves = TBDK_GFTT_EIG_WAVES;  // row segments (waves) per strip
 constexpr int kEigPref = 8;   // pixel rows in flight per wave
 
 struct EigLane {
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     // ---- greedy walk in sorted order (featureselect.cpp:421-503), 64 candidates per step
     const int lane = tid;
     const int maxc = a.max_corners;
-    float2* out = a.corners + (size_t)r * maxc;
+    float2* out = a.corners + (size_t)r * a.corner_stride;
     int n = 0;
     bool done = false;
     GFTT_TDECL;

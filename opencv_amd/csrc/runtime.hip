@@ -462,8 +462,9 @@ int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px)
 
 int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois,
                 const GfttPlan& plan, const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
-                hipEvent_t after_eig)
+                hipEvent_t after_eig, int corner_stride)
 {
+    if (corner_stride != 0 && corner_stride < p->max_corners) return TBDK_EINVAL;
     int rc = gftt_reserve(sc, ctx->device, plan.nroi, plan.total);
     if (rc != TBDK_OK) return rc;
     DeviceGuard g(ctx->device);
@@ -481,6 +482,7 @@ int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, c
     a.quality = p->quality_level;
     a.min_distance = p->min_distance;
     a.corners = reinterpret_cast<float2*>(corners);
+    a.corner_stride = corner_stride ? corner_stride : p->max_corners;
     a.counts = counts;
     a.eig_redo = ctx->opt_gftt_eig_redo;
     gftt_plan(a, plan.max_area);

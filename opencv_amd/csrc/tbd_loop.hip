@@ -12,15 +12,18 @@
 //   5. cv::tbd::Tracker::performTrackingStep restated natively, with the
 //      KLT centroid as Track::motionModel (tbd.hpp:111)                 [host C++]
 //   6. GFTT in the boxes of new tracks and of tracks due for re-detection
-//      (every `redetect_every` frames or < min_points corners), written
-//      straight into their point slots                                   [HIP]
+//      (every `redetect_every` frames or < min_points corners) into GFTT rows
+//      of the slot arrays; the next step tracks such a set from its row and
+//      its fit compacts the tracked points into the slot                  [HIP]
 // Early GFTT: a new track's box is its detection's box (tbd.cpp:1043-1055), so
 // GFTT over the detections that will surely start new tracks (boxes beyond the
 // tracker's bounds filter, tbd.cpp:218,306-331: any track on them is deleted
 // before the assignment) is launched at the start of the step, off the
 // critical path; after the tracker step, new tracks whose box equals such a
 // detection box take those corners (the same ROI of the same frame, so the
-// same corners), every other refreshed set runs the post-tracker GFTT.
+// same corners), every other refreshed set runs the post-tracker GFTT.  On
+// re-detection frames the early GFTT also runs on the box each existing track
+// will get if the tracker assigns it the detection overlapping it most.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -43,6 +46,7 @@ constexpr int kSlotPts = 256;  // corner capacity per track
 struct FitEntry {
     int slot;
     int x, y, w, h;  // the track's last box (centroid convention of tbd.cpp:1064-1065)
+    int src;         // >= 0: a refreshed set, its corners (and PyrLK results) in GFTT row src
 };
 
 struct FitOut {
@@ -70,19 +74,21 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
     if (e >= nents) return;
     const int lane = threadIdx.x;
     const FitEntry E = ents[e];
-    const int cnt = slot_counts[E.slot];
-    const size_t base = (size_t)E.slot * kSlotPts;
+    const int row = E.src >= 0 ? E.src : E.slot;  // where the tracked set and its PyrLK results are
+    const int c0 = slot_counts[row];
+    const int cnt = c0 < 0 ? 0 : c0;  // -1: GFTT candidate overflow, no corners
+    const size_t base = (size_t)E.slot * kSlotPts, rb = (size_t)row * kSlotPts;
     int m = 0, it = 0;
     for (int j0 = 0; j0 < kSlotPts; j0 += 64) {
         const int j = j0 + lane;
-        const bool ok = j < cnt && slot_status[base + j];
-        it += j < cnt ? slot_iters[base + j] : 0;
+        const bool ok = j < cnt && slot_status[rb + j];
+        it += j < cnt ? slot_iters[rb + j] : 0;
         const unsigned long long bal = __ballot(ok);
         if (ok) {
             const int pos = m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-            sa[pos] = slot_pts[base + j];
-            sb[pos] = slot_next[base + j];
+            sa[pos] = slot_pts[rb + j];
+            sb[pos] = slot_next[rb + j];
         }
         m += __popcll(bal);
     }
@@ -110,46 +116,6 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
     }
 }
 
-// The post-tracker slot updates in one launch: block k < nroi copies the
-// post-tracker GFTT's corner row k into slot roi_slot[k]; the next nearly
-// blocks copy early-GFTT row erow[k] into eslot[k]; a last block sets the
-// count of every deleted track's slot to 0 (slots handed to a new track in the
-// same step are scattered, not cleared, so no slot is written twice).
-struct PostArgs {
-    const int* clear;
-    int nclear;
-    const float2* corners;
-    const int32_t* counts;
-    const int* roi_slot;
-    int nroi;
-    const float2* ecorners;
-    const int32_t* ecounts;
-    const int* erow;
-    const int* eslot;
-    int nearly;
-    int maxc;
-    float2* slot_pts;
-    int32_t* slot_counts;
-};
-
-__global__ __launch_bounds__(64) void tbd_post_kernel(PostArgs a)
-{
-    int k = blockIdx.x;
-    if (k >= a.nroi + a.nearly) {
-        for (int j = threadIdx.x; j < a.nclear; j += blockDim.x) a.slot_counts[a.clear[j]] = 0;
-        return;
-    }
-    const bool early = k >= a.nroi;
-    if (early) k -= a.nroi;
-    const int r = early ? a.erow[k] : k;
-    const int32_t c = early ? a.ecounts[r] : a.counts[r];
-    const int n = c < 0 ? 0 : c;
-    const int s = early ? a.eslot[k] : a.roi_slot[k];
-    const float2* src = (early ? a.ecorners : a.corners) + (size_t)r * a.maxc;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) a.slot_pts[(size_t)s * kSlotPts + j] = src[j];
-    if (threadIdx.x == 0) a.slot_counts[s] = n;
-}
-
 }  // namespace tbdk
 
 using namespace tbdk;
@@ -170,13 +136,8 @@ struct tbdk_tbd {
     int32_t* slot_counts = nullptr;
     FitEntry* d_ents = nullptr;
     FitOut* d_fit = nullptr;
-    float2* d_corners = nullptr;
-    int32_t* d_ccounts = nullptr;
-    int* d_post = nullptr;  // device mirror of h_post
-    int* d_roi_slot = nullptr;
-    int* d_clear = nullptr;
-    GfttRoi* d_tab = nullptr;
-    // post-tracker work (clear / GFTT / scatter) runs on `side`, so the next
+    GfttRoi* d_tab = nullptr;  // device mirror of h_tab
+    // post-tracker work (the GFTT of refreshed sets the early GFTT missed) runs on `side`, so the next
     // frame's pyramid, enqueued on the caller's stream, overlaps it; the
     // caller's stream waits for `post_done` before its LK launch
     hipStream_t side = nullptr;
@@ -205,7 +166,6 @@ struct tbdk_tbd {
     int32_t* d_spec = nullptr;
     std::vector<int> spec_list;
     std::vector<char> spec_member;
-    std::vector<char> touched;       // scratch: slots cleared this step
     const uint8_t* la_frame = nullptr;
     int la_pitch = 0;
     hipStream_t la_stream = nullptr;
@@ -221,26 +181,21 @@ struct tbdk_tbd {
     std::vector<int32_t> b_list;  // scratch: refreshed slots in track order
     FitEntry* h_ents = nullptr;
     FitOut* h_fit = nullptr;
-    // one pinned block uploaded with a single copy after the tracker step:
-    // [clear slots: S ints][ROI slots: S ints][early rows: S ints][early slots: S ints]
-    // [GFTT ROI table: S GfttRoi]
-    int* h_post = nullptr;
-    int* h_roi_slot = nullptr;
-    int* h_clear = nullptr;
-    int* h_erow = nullptr;
-    int* h_eslot = nullptr;
+    // the post-tracker GFTT's ROI table (pinned; uploaded, or read in place)
     GfttRoi* h_tab = nullptr;
-
-    int* d_erow = nullptr;
-    int* d_eslot = nullptr;
+    // GFTT rows: the corner sets of refreshed tracks stay where GFTT writes them
+    // and are tracked from there; the next fit compacts the tracked points into
+    // the slot.  Rows of the slot arrays: [0, S) slots, [S, 3S) the early GFTT's
+    // rows (two sets by step parity eb, see early_s), [3S, 4S) the post-tracker
+    // GFTT's rows.  src_row[slot] = the refreshed set's row until the next fit.
+    std::vector<int> src_row;
+    std::vector<int> src_list;
     // early GFTT (see the top of the file): ROI tables double-buffered by step
     // parity (pinned; a table is rewritten two steps later, after a fit sync
     // that orders its upload), device table, corner rows and counts
     GfttRoi* h_etab[2] = {nullptr, nullptr};
     GfttRoi* d_etab = nullptr;
-    float2* d_ecorners = nullptr;
-    int32_t* d_ecounts = nullptr;
-    int epar = 0;
+    int eb = 0;  // early-row set of this step
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
     std::vector<int> det_order;                   // scratch: detections by left edge
@@ -291,16 +246,15 @@ int release(tbdk_tbd* t)
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
     gftt_scratch_free(t->gftt);
-    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_corners,
-                   t->d_ccounts, t->d_ecorners, t->d_ecounts};
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (!t->zc) {
-        void* staged[] = {t->d_pre, t->d_fit, t->d_post, t->d_la, t->d_etab, t->d_spec};
+        void* staged[] = {t->d_pre, t->d_fit, t->d_tab, t->d_la, t->d_etab, t->d_spec};
         for (void* p : staged)
             if (p) (void)hipFree(p);
     }
-    void* host[] = {t->h_pre, t->h_fit, t->h_post, t->h_la, t->h_etab[0], t->h_spec};
+    void* host[] = {t->h_pre, t->h_fit, t->h_tab, t->h_la, t->h_etab[0], t->h_spec};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -380,25 +334,23 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         if (t->zc) e = hipHostGetDevicePointer(d, h, 0);
         else dm(d, bytes);
     };
-    dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_status), S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * S);
+    // 4 S rows: the slots, two sets of early GFTT rows, the post-tracker GFTT rows
+    dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * 4 * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * 4 * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_status), 4 * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * 4 * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * 4 * S);
     const size_t pre_bytes = (sizeof(FitEntry) + sizeof(int32_t)) * S;
-    const size_t post_bytes = 4 * sizeof(int) * S + sizeof(GfttRoi) * S;
-    dm(reinterpret_cast<void**>(&t->d_corners), sizeof(float2) * S * cfg->max_corners);
-    dm(reinterpret_cast<void**>(&t->d_ccounts), sizeof(int32_t) * S);
     hm(&t->h_pre, pre_bytes);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
-    hm(reinterpret_cast<void**>(&t->h_post), post_bytes);
+    hm(reinterpret_cast<void**>(&t->h_tab), sizeof(GfttRoi) * S);
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
     if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
     sm(&t->d_pre, t->h_pre, pre_bytes);
     sm(reinterpret_cast<void**>(&t->d_fit), t->h_fit, sizeof(FitOut) * S);
-    sm(reinterpret_cast<void**>(&t->d_post), t->h_post, post_bytes);
+    sm(reinterpret_cast<void**>(&t->d_tab), t->h_tab, sizeof(GfttRoi) * S);
     sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
@@ -411,24 +363,8 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->refreshed.assign((size_t)S, 0);
     t->la_member.assign((size_t)S, 0);
     t->spec_member.assign((size_t)S, 0);
-    t->touched.assign((size_t)S, 0);
-
     t->b_list.assign((size_t)S, 0);
-
-    if (t->h_post && t->d_post) {
-        t->h_clear = t->h_post;
-        t->h_roi_slot = t->h_post + S;
-        t->h_erow = t->h_post + 2 * S;
-        t->h_eslot = t->h_post + 3 * S;
-        t->h_tab = reinterpret_cast<GfttRoi*>(t->h_post + 4 * S);
-        t->d_clear = t->d_post;
-        t->d_roi_slot = t->d_post + S;
-        t->d_erow = t->d_post + 2 * S;
-        t->d_eslot = t->d_post + 3 * S;
-        t->d_tab = reinterpret_cast<GfttRoi*>(t->d_post + 4 * S);
-    }
-    dm(reinterpret_cast<void**>(&t->d_ecorners), sizeof(float2) * S * cfg->max_corners);
-    dm(reinterpret_cast<void**>(&t->d_ecounts), sizeof(int32_t) * S);
+    t->src_row.assign((size_t)S, -1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->pyr_ready, hipEventDisableTiming);
     // the post-tracker GFTT heads the next frame's critical path (the refreshed
     // sets' PyrLK waits for it): it gets the highest priority, ahead of the
@@ -559,6 +495,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // equals one of these ROIs.
     t->erois.clear();
     t->erow_of.clear();
+    const int S = c.max_tracks;
+    const int erow0 = S * (1 + t->eb);  // this step's early GFTT rows (the previous step's: the other set)
     bool early_launched = false;
     auto launch_early_gftt = [&]() -> int {
         if (!c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
@@ -625,8 +563,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         if (!t->erois.empty()) {
             GfttPlan eplan;
-            GfttRoi* htab = t->h_etab[t->epar];
-            t->epar ^= 1;
+            GfttRoi* htab = t->h_etab[t->eb];
             int rc2 = gftt_prepare(t->erois.data(), (int)t->erois.size(), c.width, c.height, &gp, htab, &eplan);
             if (rc2 != TBDK_OK) return rc2;
             hipStream_t es = t->early_s;  // ordered at the top of the step
@@ -638,7 +575,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             }
             const tbdk_level& L0 = P.lv[0];
             rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
-                              reinterpret_cast<float*>(t->d_ecorners), t->d_ecounts, es);
+                              reinterpret_cast<float*>(t->slot_pts + (size_t)erow0 * kSlotPts), t->slot_counts + erow0,
+                              es, nullptr, kSlotPts);
             if (rc2 != TBDK_OK) return rc2;
             const hipError_t e = hipEventRecord(t->early_done, es);
             if (e != hipSuccess) return map_status(e);
@@ -651,8 +589,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents, h_lists) were last read by uploads issued before the
-    // previous step's sync, and those written after it (h_clear, h_roi_slot,
-    // h_la) are only rewritten after this step's sync, which orders every
+    // previous step's sync, and those written after it (h_tab, h_la) are only
+    // rewritten after this step's sync, which orders every
     // earlier upload.  So this frame's pyramid / LK / fit queue up behind the
     // previous GFTT.
     double wait_us = 0.0;
@@ -675,15 +613,15 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     lp.flags = 0;
     lp.min_eig_threshold = c.min_eig_threshold;
     lp.impl = 0;
-    const int S = c.max_tracks;
     if (run_klt) {
         for (const auto& tr : tracks) {
             auto it = t->slot_of.find(tr.id);
             if (it == t->slot_of.end()) continue;
             const int slot = it->second;
             const tbd::Rect& b = tr.bboxes.back();
-            t->h_ents[nents++] = FitEntry{slot, b.x, b.y, b.width, b.height};
-            if (t->refreshed[(size_t)slot]) t->b_list[nB++] = slot;
+            const int src = t->src_row[(size_t)slot];
+            t->h_ents[nents++] = FitEntry{slot, b.x, b.y, b.width, b.height, src};
+            if (src >= 0) t->b_list[nB++] = src;  // refreshed: tracked from its GFTT row
             else if (!(la_lk && t->la_member[(size_t)slot])) t->h_lists[nA++] = slot;
         }
         // refreshed sets after the unchanged ones (a separate scratch list: with
@@ -703,6 +641,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     for (int sl : t->la_list) t->la_member[(size_t)sl] = 0;
     t->la_list.clear();
+    for (int sl : t->src_list) t->src_row[(size_t)sl] = -1;  // the fit compacts them into their slots
+    t->src_list.clear();
 
 
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
@@ -827,24 +767,24 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size(),
                                     t->traj ? &t->traj->map : nullptr);
     const double tracker_us = std::chrono::duration<double, std::micro>(clk::now() - tt0).count();
-    if (!synced) {  // no fit this step: order the previous step's uploads before reusing h_clear / h_roi_slot
+    if (!synced) {  // no fit this step: order the previous step's uploads before reusing h_tab
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) return map_status(e);
     }
-    int nclear = 0;
     for (unsigned id : t->tracker->deletedIds) {
         auto it = t->slot_of.find(id);
         if (it != t->slot_of.end()) {
             t->free_slots.push(it->second);
-            t->touched[(size_t)it->second] = 1;
-            t->h_clear[nclear++] = it->second;
             t->slot_of.erase(it);
         }
         t->npts_of.erase(id);
     }
-    // ---- corners for new tracks and tracks due for re-detection
+    // ---- corners for new tracks and tracks due for re-detection: each such set
+    // is its GFTT row (an early row when the early GFTT ran on its box, else a
+    // row of the post-tracker GFTT below), tracked from there by the next step
     t->rois.clear();
     int nroi = 0, nearly = 0;
+    const int prow0 = 3 * S;  // the post-tracker GFTT's rows
     if (c.use_klt) {
         for (const auto& tr : t->tracker->getTracks()) {
             auto it = t->slot_of.find(tr.id);
@@ -866,78 +806,49 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             int x1 = std::min(b.x + b.width, c.width), y1 = std::min(b.y + b.height, c.height);
             t->refreshed[(size_t)slot] = 1;
             t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
+            t->src_list.push_back(slot);
             if (x1 - x0 < 3 || y1 - y0 < 3) {  // nothing to detect in: empty point set
                 t->rois.push_back(tbdk_roi{0, 0, 1, 1});
             } else {
                 auto er = t->erow_of.find(box_key(x0, y0, x1 - x0, y1 - y0));
                 if (er != t->erow_of.end()) {  // the early GFTT ran on this ROI of this frame
-                    t->h_erow[nearly] = er->second;
-                    t->h_eslot[nearly++] = slot;
+                    t->src_row[(size_t)slot] = erow0 + er->second;
+                    nearly++;
                     continue;
                 }
                 t->rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
-            t->h_roi_slot[nroi++] = slot;
+            t->src_row[(size_t)slot] = prow0 + nroi++;
         }
     }
-    // ---- one upload (clear list, ROI slots, GFTT ROI table), then GFTT / clear / scatter.
-    // With a next frame, the PyrLK of the point sets this leaves unchanged is
-    // enqueued after it (the look-ahead PyrLK): GFTT heads the next frame's
-    // critical path, so it is queued first and the PyrLK fills the device
-    // around it.
-    GfttPlan plan;
-    if (nroi > 0) {
-        rc = gftt_prepare(t->rois.data(), nroi, c.width, c.height, &gp, t->h_tab, &plan);
-        if (rc != TBDK_OK) return rc;
-    }
-    {  // a speculated set the tracker deleted or refreshed: the speculative PyrLK
-       // reads it, so the clear / scatter writing it wait for that PyrLK
-        bool conflict = false;
-        for (int sl : t->spec_list) conflict |= t->touched[(size_t)sl] || t->refreshed[(size_t)sl];
-        for (int k = 0; k < nclear; ++k) t->touched[(size_t)t->h_clear[k]] = 0;
-        int nc = 0;  // deleted slots handed to a new track are scattered, not cleared
-        for (int k = 0; k < nclear; ++k)
-            if (!t->refreshed[(size_t)t->h_clear[k]]) t->h_clear[nc++] = t->h_clear[k];
-        nclear = nc;
-        if (conflict) {
-            hipError_t e = hipStreamWaitEvent(t->side, t->la_done, 0);
-            if (e != hipSuccess) return map_status(e);
-        }
-    }
-    if (early_launched) {  // its corners, and the GFTT scratch the post-tracker GFTT reuses
+    // ---- the post-tracker GFTT (side stream, behind the early GFTT whose rows
+    // the next step reads and whose scratch it reuses).  With a next frame, the
+    // PyrLK of the point sets this leaves unchanged is enqueued after it (the
+    // look-ahead PyrLK): the GFTT heads the next frame's critical path, so it is
+    // queued first and the PyrLK fills the device around it.
+    if (early_launched) {
         hipError_t e = hipStreamWaitEvent(t->side, t->early_done, 0);
         if (e != hipSuccess) return map_status(e);
     }
-    if (nclear > 0 || nroi > 0 || nearly > 0) {
-        const uint8_t* h0 = reinterpret_cast<const uint8_t*>(t->h_post);
-        const size_t bytes = nroi > 0     ? reinterpret_cast<const uint8_t*>(t->h_tab + nroi) - h0
-                             : nearly > 0 ? reinterpret_cast<const uint8_t*>(t->h_eslot + nearly) - h0
-                                          : sizeof(int) * nclear;
+    if (nroi > 0) {
+        GfttPlan plan;
+        rc = gftt_prepare(t->rois.data(), nroi, c.width, c.height, &gp, t->h_tab, &plan);
+        if (rc != TBDK_OK) return rc;
         if (!t->zc) {
-            hipError_t e = hipMemcpyAsync(t->d_post, t->h_post, bytes, hipMemcpyHostToDevice, t->side);
+            hipError_t e = hipMemcpyAsync(t->d_tab, t->h_tab, sizeof(GfttRoi) * nroi, hipMemcpyHostToDevice, t->side);
             if (e != hipSuccess) return map_status(e);
         }
-    }
-    if (nroi > 0) {
         const tbdk_level& L0 = P.lv[0];
         rc = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
-                         reinterpret_cast<float*>(t->d_corners), t->d_ccounts, t->side, next ? t->eig_done : nullptr);
+                         reinterpret_cast<float*>(t->slot_pts + (size_t)prow0 * kSlotPts), t->slot_counts + prow0,
+                         t->side, next ? t->eig_done : nullptr, kSlotPts);
         if (rc != TBDK_OK) return rc;
-    }
-    if (nclear > 0 || nroi > 0 || nearly > 0) {
-        const PostArgs pa{t->d_clear, nclear, t->d_corners, t->d_ccounts, t->d_roi_slot, nroi,
-                          t->d_ecorners, t->d_ecounts, t->d_erow, t->d_eslot, nearly, c.max_corners,
-                          t->slot_pts, t->slot_counts};
-        // one wave per block: the launch usually finds the look-ahead PyrLK's waves
-        // holding most wave slots, and single waves fit into the ones they free
-        hipLaunchKernelGGL(tbd_post_kernel, dim3(nroi + nearly + (nclear > 0 ? 1 : 0)), dim3(64), 0, t->side, pa);
     }
     // post_done also after an early GFTT none of whose ROIs was used: the next
     // step's fit sync then orders that GFTT's table upload before the staging
     // table is rewritten (two steps later)
-    if (nclear > 0 || nroi > 0 || nearly > 0 || !t->erois.empty()) {
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipEventRecord(t->post_done, t->side);
+    if (nroi > 0 || early_launched) {
+        hipError_t e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
     }
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
@@ -976,6 +887,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     for (int sl : t->spec_list) t->spec_member[(size_t)sl] = 0;
     t->spec_list.clear();
     t->cur ^= 1;
+    t->eb ^= 1;
     t->have_prev = true;
 
     if (metrics) {
@@ -1053,9 +965,9 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
 {
     if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
     const auto& tracks = t->tracker->getTracks();
-    std::vector<int32_t> counts((size_t)t->cfg.max_tracks);
+    std::vector<int32_t> counts(4 * (size_t)t->cfg.max_tracks);  // slots and GFTT rows
     (void)hipSetDevice(t->ctx->device);
-    hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work runs on the side stream
+    hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work (behind the early GFTT) runs on `side`
     if (e == hipSuccess) e = hipMemcpy(counts.data(), t->slot_counts, sizeof(int32_t) * counts.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return map_status(e);
     int k = 0;
@@ -1075,7 +987,12 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
         o.age = (int32_t)tr.age;
         o.total_visible = (int32_t)tr.totalVisibleCount;
         auto it = t->slot_of.find(tr.id);
-        o.npoints = it == t->slot_of.end() ? 0 : counts[(size_t)it->second];
+        if (it == t->slot_of.end()) {
+            o.npoints = 0;
+        } else {  // a refreshed set is still its GFTT row
+            const int src = t->src_row[(size_t)it->second];
+            o.npoints = std::max(0, counts[(size_t)(src >= 0 ? src : it->second)]);
+        }
         o.max_confidence = tr.maxConfidence;
         o.bbox_overlap = tr.bboxOverlap;
     }

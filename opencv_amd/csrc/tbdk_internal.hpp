@@ -201,7 +201,8 @@ struct GfttArgs {
     int img_bytes;   // LDS for the per-ROI byte image of the greedy walk (0: list mode)
     int max_corners;
     double quality, min_distance;
-    float2* corners;  // nroi x max_corners
+    float2* corners;  // nroi rows of corner_stride (>= max_corners) float2
+    int corner_stride;
     int32_t* counts;  // nroi (-1: candidate overflow)
     int eig_redo;     // test option: walk every eig strip segment in sequence
 };
@@ -227,7 +228,7 @@ int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px);
 void gftt_scratch_free(GfttScratch& sc);
 int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
                 const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
-                hipEvent_t after_eig = nullptr);
+                hipEvent_t after_eig = nullptr, int corner_stride = 0);  // 0: max_corners
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig = nullptr);
 hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s);  // eigenvalue planes only
 }  // namespace tbdk
