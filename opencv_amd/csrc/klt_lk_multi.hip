@@ -292,11 +292,11 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             }
             nit += act ? 1 : 0;
             const bool moved = act && (inx != pinx || iny != piny);
-#ifdef TBDK_LK_PROBE_RELOADS  // tuning builds: 1 always reloads, 2 counts reloads into iters
+#ifdef TBDK_LK_PROBE_RELOADS  // tuning builds: 1 always reloads, 2 counts reloads into iters, 3 never reloads
 #if TBDK_LK_PROBE_RELOADS == 2
             nrl += any_lane(moved) ? 1 : 0;
 #endif
-            if (TBDK_LK_PROBE_RELOADS == 1 || any_lane(moved)) {
+            if (TBDK_LK_PROBE_RELOADS == 1 || (TBDK_LK_PROBE_RELOADS != 3 && any_lane(moved))) {
 #else
             if (any_lane(moved)) {  // uniform: reload the J columns (unchanged for points that did not move)
 #endif

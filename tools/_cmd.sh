@@ -1,6 +1,7 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_tbd.py tests/test_gpu_gftt.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_tbd.log 2>&1 || exit 1
-B="python bench.py --steps 480 --no-cpu-baseline --no-step-api --no-farneback --no-hog --no-f16"
+B="python bench.py --steps 1500 --no-cpu-baseline --no-step-api --no-farneback --no-hog --no-f16"
 for i in 1 2 3; do
-timeout -k 10 200 $B > gpurun_out/ab_rows_$i.json 2>/dev/null || exit 1
+for p in 0 1; do
+TBDK_HOST_PROF=1 TBDK_EG_POS=$p timeout -k 10 200 $B > gpurun_out/ab_egpos${p}_$i.json 2>gpurun_out/ab_egpos${p}_$i.err || exit 1
+done
 done

@@ -30,4 +30,6 @@ for n in (3072, 12288):
             r = lk.calc(P0, P1, d, want_iters=True)
         torch.cuda.synchronize()
         c, ms = ctx.timing_query("lk_sparse")
-        print(f"n {n} levels {ml + 1} max_count {mc}: {ms / c * 1000:6.1f} us, mean iters {r.iters.float().mean().item():.2f}")
+        it = r.iters.cpu().numpy()
+        extra = f", J reloads per wave {(it // 1000).mean():.2f}" if it.max() >= 1000 else ""
+        print(f"n {n} levels {ml + 1} max_count {mc}: {ms / c * 1000:6.1f} us, mean iters {(it % 1000).mean():.2f}{extra}")
