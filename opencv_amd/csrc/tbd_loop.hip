@@ -376,7 +376,10 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->la_s, hipStreamNonBlocking);
+    // the look-ahead PyrLK at the lowest priority: when the next step's refreshed
+    // sets' PyrLK (critical) is launched, workgroup slots freed by the look-ahead
+    // waves go to it first (+2 %)
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->la_s, hipStreamNonBlocking, prio_least);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking, prio_least);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
