@@ -376,9 +376,9 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
-    // the look-ahead PyrLK at the lowest priority: when the next step's refreshed
-    // sets' PyrLK (critical) is launched, workgroup slots freed by the look-ahead
-    // waves go to it first (+2 %)
+    // the look-ahead PyrLK at the lowest priority (on gfx950 the range is
+    // normal..high, so this is the default; a high-priority caller stream for
+    // the critical PyrLK measured no difference either)
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->la_s, hipStreamNonBlocking, prio_least);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking, prio_least);
