@@ -199,7 +199,8 @@ struct tbdk_tbd {
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
     std::vector<int> det_order;                   // scratch: detections by left edge
-    GfttScratch gftt;  // this loop's own (early GFTT on early_s, post-tracker GFTT on side)
+    GfttScratch gftt;   // the early GFTT's (early_s); the loop's own, not the context's
+    GfttScratch gftt2;  // the post-tracker GFTT's (side), so the next step's early GFTT need not wait for it
     hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
     // zero-copy staging: the kernels read the pinned host tables (fit entries,
     // slot lists, post-tracker lists, GFTT ROI tables) and the fit kernel
@@ -246,6 +247,7 @@ int release(tbdk_tbd* t)
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
     gftt_scratch_free(t->gftt);
+    gftt_scratch_free(t->gftt2);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts};
     for (void* p : dev)
         if (p) (void)hipFree(p);
@@ -405,6 +407,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     }
     for (int s = 0; s < cfg->max_tracks; ++s) t->free_slots.push(s);
     rc = gftt_reserve(t->gftt, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
+    if (rc == TBDK_OK) rc = gftt_reserve(t->gftt2, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc != TBDK_OK) {
         release(t);
         return rc;
@@ -480,11 +483,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const tbdk_gftt_params gp{c.max_corners, c.quality_level, c.min_distance, 3};
     if (c.use_klt && t->ctx->opt_tbd_early_gftt) {
         // the early GFTT stream: behind this frame's pyramid (recorded where it
-        // was built) and the previous step's post-tracker work (the GFTT scratch
-        // and the early corner rows it read); waits taken now, before this step
-        // re-records la_ready for the next frame
+        // was built; the wait is taken now, before this step re-records la_ready
+        // for the next frame).  It need not wait for the previous step's
+        // post-tracker GFTT (scratch of its own), and the early rows it writes
+        // (set eb) were last read two steps ago, before a fit this host synced.
         hipError_t e = hipStreamWaitEvent(t->early_s, la_valid ? t->la_ready : t->pyr_ready, 0);
-        if (e == hipSuccess) e = hipStreamWaitEvent(t->early_s, t->post_done, 0);
         if (e != hipSuccess) return map_status(e);
     }
 
@@ -842,7 +845,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (e != hipSuccess) return map_status(e);
         }
         const tbdk_level& L0 = P.lv[0];
-        rc = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
+        rc = gftt_launch(t->ctx, t->gftt2, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
                          reinterpret_cast<float*>(t->slot_pts + (size_t)prow0 * kSlotPts), t->slot_counts + prow0,
                          t->side, next ? t->eig_done : nullptr, kSlotPts);
         if (rc != TBDK_OK) return rc;
