@@ -117,11 +117,16 @@ __device__ __forceinline__ int bilin_c(uint32_t p0, uint32_t p1, uint32_t w0, ui
     return sdot2(p0, w0, t);
 }
 
-// (t0 >> 9, t1 >> 9) as int16 x 2: bytes 0-1 of t0 >> 9 and bytes 2-3 of
-// t1 << 7 (= the low 16 bits of t1 >> 9 moved up)
+// (t0 >> 9, t1 >> 9) as int16 x 2 in two instructions: t0 >> 9, then the SDWA
+// form of the second shift writes only the high word (WORD_1) of the result,
+// keeping the low word
 __device__ __forceinline__ uint32_t pack_diff(int t0, int t1)
 {
-    return __builtin_amdgcn_perm((uint32_t)t1 << 7, (uint32_t)(t0 >> 9), 0x07060100u);
+    uint32_t d = (uint32_t)(t0 >> 9);
+    asm("v_ashrrev_i32_sdwa %0, 9, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(d)
+        : "v"(t1));
+    return d;
 }
 
 __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
