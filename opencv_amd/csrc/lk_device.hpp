@@ -36,15 +36,23 @@ __device__ __forceinline__ int bilin_s(uint32_t p0, uint32_t p1, uint32_t w0, ui
 }
 
 // iw00..iw11 = cvRound(w * 2^14), iw11 = 2^14 - the others (lkpyramid.cpp:227-234),
-// packed as (w00, w01) and (w10, w11) int16 pairs
+// packed as (w00, w01) and (w10, w11) int16 pairs.
+// cvRound(p * 2^14) for p = (1-a)(1-b) etc. in [0, 1]: p * 2^14 is exact, so
+// fma(p, 2^14, 1.5 * 2^23) rounds p * 2^14 to the nearest integer, ties to even
+// (the ulp of the sum is 1), and the integer sits in the low mantissa bits of
+// the result (the constant's low 16 bits are zero): no round / convert
+// instructions, and each pair is one byte permute.
 __device__ __forceinline__ void bilinear_weights(float fa, float fb, uint32_t& w0, uint32_t& w1)
 {
-    const int w00 = __float2int_rn((1.f - fa) * (1.f - fb) * (1 << W_BITS));
-    const int w01 = __float2int_rn(fa * (1.f - fb) * (1 << W_BITS));
-    const int w10 = __float2int_rn((1.f - fa) * fb * (1 << W_BITS));
-    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
-    w0 = ((uint32_t)w00 & 0xFFFFu) | ((uint32_t)w01 << 16);
-    w1 = ((uint32_t)w10 & 0xFFFFu) | ((uint32_t)w11 << 16);
+    constexpr float kMagic = 12582912.f;  // 1.5 * 2^23
+    const float ga = 1.f - fa, gb = 1.f - fb;
+    const uint32_t b00 = __float_as_uint(__builtin_fmaf(ga * gb, (float)(1 << W_BITS), kMagic));
+    const uint32_t b01 = __float_as_uint(__builtin_fmaf(fa * gb, (float)(1 << W_BITS), kMagic));
+    const uint32_t b10 = __float_as_uint(__builtin_fmaf(ga * fb, (float)(1 << W_BITS), kMagic));
+    // low 16 bits of 2^14 - w00 - w01 - w10 (the constant's part cancels modulo 2^16)
+    const uint32_t b11 = (uint32_t)(1 << W_BITS) - (b00 + b01 + b10);
+    w0 = __builtin_amdgcn_perm(b01, b00, 0x05040100u);
+    w1 = __builtin_amdgcn_perm(b11, b10, 0x05040100u);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes)
