@@ -79,10 +79,27 @@ __device__ __forceinline__ uint32_t seg_total(uint32_t scanned, int e4, int s4)
 // is the exact integer sum; the one float rounding gives the same value as the
 // exact int64 sum of the other kernels.  e4 / s4: byte addresses of the point's
 // last lane and of the lane before its first.
+//
+// Fast path, taken by the whole wave when every partial lies in (-2^26, 2^26):
+// a point's total is then below 31 * 2^26 < 2^31 in magnitude (windows up to
+// 31 wide), exact as a modulo-2^32 difference of plain scans, and its int ->
+// float conversion is the same single rounding.
 template <int N>
 __device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N])
 {
     static_assert(N >= 1 && N <= 3, "three 11-bit fields per packed scan");
+    bool big = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) big |= (uint32_t)v[k] + (1u << 26) >= (1u << 27);
+    if (__builtin_amdgcn_ballot_w64(big) == 0) {  // wave-uniform
+        uint32_t sv[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) sv[k] = (uint32_t)v[k];
+        scan64_n(sv);
+#pragma unroll
+        for (int k = 0; k < N; ++k) out[k] = (float)(int)seg_total(sv[k], e4, s4);
+        return;
+    }
     uint32_t sc[N + 1];  // lo parts, then the packed hi parts
     sc[N] = 0;
 #pragma unroll

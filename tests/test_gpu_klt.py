@@ -172,6 +172,22 @@ def test_lk_edge_points_and_flags(gpu, impl):
     assert_exact(g, ex)
 
 
+@pytest.mark.parametrize("impl", IMPLS)
+def test_lk_high_contrast_exact_sums(gpu, impl):
+    """binary 0/255 noise in 2x2 cells: per-column partial sums of diff * Ix reach
+    ~1e8 > 2^26, so the multi-point kernel leaves its plain-scan fast path for the
+    lo/hi-split exact sums; every kernel still equals the oracle bit for bit"""
+    rng = np.random.default_rng(5)
+    a = (rng.integers(0, 2, (120, 160)) * 255).astype(np.uint8).repeat(2, 0).repeat(2, 1)
+    b = np.roll(a, (1, -2), (0, 1))
+    b[rng.random(b.shape) < 0.1] ^= 255
+    pts = grid_points(240, 320, 9, 0) + np.float32([0.43, 0.27])
+    for win, maxlev in (((21, 21), 2), ((31, 31), 1), ((9, 9), 0)):
+        g, ex, _ = run_pair(gpu, a, b, pts, win, maxlev, 30, impl=impl)
+        assert_exact(g, ex)
+        assert (g[1] == 1).mean() > 0.2
+
+
 def test_lk_empty_input(gpu):
     K = klt()
     lk = K.SparsePyrLKOpticalFlow()
