@@ -43,6 +43,7 @@
 #include <type_traits>
 #include <utility>
 
+#include <cstdlib>
 #include "tbdk_internal.hpp"
 
 namespace tbdk {
@@ -815,6 +816,34 @@ hipError_t launch_fb_iter_m(const FbIterArgs& a, bool gauss, dim3 grid, hipStrea
     return hipGetLastError();
 }
 
+// resident fb_iter workgroups per CU (occupancy of the instance for m, gauss)
+template <int M>
+int fb_iter_occ_m(bool gauss)
+{
+    int n = 0;
+    hipError_t e = gauss ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_iter_kernel<M, true>, kFbThreads, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_iter_kernel<M, false>, kFbThreads, 0);
+    return e == hipSuccess && n > 0 ? n : 1;
+}
+
+int fb_iter_occupancy(int m, bool gauss)
+{
+    switch (m) {
+    case 0: return fb_iter_occ_m<0>(gauss);
+    case 1: return fb_iter_occ_m<1>(gauss);
+    case 2: return fb_iter_occ_m<2>(gauss);
+    case 3: return fb_iter_occ_m<3>(gauss);
+    case 4: return fb_iter_occ_m<4>(gauss);
+    case 5: return fb_iter_occ_m<5>(gauss);
+    case 6: return fb_iter_occ_m<6>(gauss);
+    case 7: return fb_iter_occ_m<7>(gauss);
+    case 8: return fb_iter_occ_m<8>(gauss);
+    case 9: return fb_iter_occ_m<9>(gauss);
+    case 10: return fb_iter_occ_m<10>(gauss);
+    default: return 1;
+    }
+}
+
 hipError_t launch_fb_iter(const FbIterArgs& a, int m, bool gauss, hipStream_t s)
 {
     const int ow = fb_ow(m);
@@ -1026,14 +1055,19 @@ hipError_t launch_polyexp(const float* I, int w, int h, int ipitch, float* R, in
 inline int plane_pitch(int w) { return align_up(w, 64); }
 inline int64_t plane_stride(int pp, int h) { return (int64_t)pp * h; }
 
-// rows per fb_iter workgroup (a multiple of the batch): about two rounds of
-// resident workgroups (3 per CU, 256 CUs); small levels get one batch per
-// workgroup so their serial chain of round trips stays short
-int iter_seg(int w, int h, int m)
+// rows per fb_iter workgroup (a multiple of the batch) for `wgs` workgroups in
+// total.  Longer segments pay the 2m warm-up rows of M less often, fewer
+// workgroups hide less latency: the caller asks for whole rounds of resident
+// workgroups, at least 3 per CU (4K, win 13: box 768 = one round of 3 per CU
+// beat 512 / 1024 / 1536 by 4-13 %; Gaussian 1024 = two rounds of 2 per CU
+// beat 512 / 768 / 1536 by 1-13 %).  Small levels get one batch per workgroup
+// so their serial chain of round trips stays short.
+int iter_seg(int w, int h, int m, int wgs)
 {
     const int ow = fb_ow(m);
     const int nstrips = (w + ow - 1) / ow;
-    const int nseg = (1536 + nstrips - 1) / nstrips;
+    const int target = wgs;
+    const int nseg = (target + nstrips - 1) / nstrips;
     int seg = (h + nseg - 1) / nseg;
     seg = (seg + kFbRB - 1) / kFbRB * kFbRB;
     return seg < kFbRB ? kFbRB : seg;
@@ -1179,7 +1213,12 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
     FbScratch* f = ctx->fb;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool gauss = (p->flags & TBDK_OPTFLOW_FARNEBACK_GAUSSIAN) != 0;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+        cus = 256;
     const int m = p->win_size / 2;
+    const int round_wgs = cus * fb_iter_occupancy(m, gauss);  // one round of resident fb_iter workgroups
+    const int iter_wgs = round_wgs * ((3 * cus + round_wgs - 1) / round_wgs);
     hipError_t e = hipSuccess;
     int cur = 0;  // ping-pong index of the current flow
     int pw = 0, ph = 0, ppitch = 0;
@@ -1258,7 +1297,7 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
         a.pitch = pp;
         a.fplane = plane;
         a.rplane = plane;
-        a.seg = iter_seg(w, h, m);
+        a.seg = iter_seg(w, h, m, iter_wgs);
         a.scale = 1. / (p->win_size * p->win_size);
         // FarnebackUpdateFlow_GaussianBlur kernel (optflowgf.cpp:416-435)
         {

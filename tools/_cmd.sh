@@ -1,8 +1,6 @@
 set -o pipefail
-B="python bench.py --steps 1500 --no-cpu-baseline --no-step-api --no-farneback --no-hog --no-f16"
-for i in 1 2 3; do
-timeout -k 10 200 $B > gpurun_out/ab_fast_$i.json 2>/dev/null || exit 1
-TBDK_LIB=opencv_amd/lib/var_head.so timeout -k 10 200 $B > gpurun_out/ab_head_$i.json 2>/dev/null || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_farneback.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_fb.log 2>&1 || exit 1
+for f in 0 256; do
+timeout -k 10 200 python tools/bench_farneback.py --pairs 10 --flags $f > gpurun_out/fbn_$f.json 2>/dev/null || exit 1
+TBDK_LIB=opencv_amd/lib/var_head.so timeout -k 10 200 python tools/bench_farneback.py --pairs 10 --flags $f > gpurun_out/fbh_$f.json 2>/dev/null || exit 1
 done
-timeout -k 10 120 python tools/probe_lk_scale.py > gpurun_out/probe_scale_fast.txt 2>&1 || exit 1
-TBDK_LIB=opencv_amd/lib/var_head.so timeout -k 10 120 python tools/probe_lk_scale.py > gpurun_out/probe_scale_head.txt 2>&1 || exit 1
