@@ -122,20 +122,43 @@ struct FbRowArgs {
     float k[kFbMaxKs];
 };
 
+// source column of sample j of a row
+__device__ __forceinline__ int fb_row_col(const FbRowArgs& a, int j)
+{
+    if (a.mode != kModeLinear) return j;
+    const LinX lx = lin_x(j >> 1, a.scale_x, a.W);
+    return (j & 1) && lx.inner ? lx.sx + 1 : lx.sx;
+}
+
 // row filter of row y at source column c (filter.simd.hpp SymmRowSmallFilter /
-// RowFilter scalar and SSE orders, see oracle/farneback_oracle.c)
+// RowFilter scalar and SSE orders, see oracle/farneback_oracle.c).  Kernels
+// wider than 5 taps (the coarse levels: up to ~90 taps) read the block's span of
+// the row from LDS, staged once with its reflect-101 border, instead of one
+// global byte load and one reflect per tap.
 __global__ __launch_bounds__(256) void fb_rowpass_kernel(FbRowArgs a)
 {
     const int j = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
-    if (j >= a.nc) return;
-    int c = j;
-    if (a.mode == kModeLinear) {
-        const LinX lx = lin_x(j >> 1, a.scale_x, a.W);
-        c = (j & 1) && lx.inner ? lx.sx + 1 : lx.sx;
-    }
     const uint8_t* S = a.img + (size_t)y * a.pitch;
     const int r = a.ks >> 1;
+    if (a.ks > 5) {
+        extern __shared__ uint8_t srow[];
+        // the samples of this block read columns [c0 - r, c1 + r] (columns are
+        // monotonic in j)
+        const int j0 = blockIdx.x * 256, j1 = min(j0 + 255, a.nc - 1);
+        const int c0 = fb_row_col(a, j0 & ~1), c1 = fb_row_col(a, (j1 | 1) < a.nc ? (j1 | 1) : j1);
+        const int base = c0 - r, len = c1 - c0 + 1 + 2 * r;
+        for (int i = threadIdx.x; i < len; i += 256) srow[i] = S[reflect101(base + i, a.W)];
+        __syncthreads();
+        if (j >= a.nc) return;
+        const uint8_t* R = srow + (fb_row_col(a, j) - r - base);  // R[t] = column c - r + t
+        float s = a.k[0] * (float)R[0];
+        for (int t = 1; t < a.ks; ++t) s += a.k[t] * (float)R[t];
+        a.T[(size_t)y * a.tpitch + j] = s;
+        return;
+    }
+    if (j >= a.nc) return;
+    const int c = fb_row_col(a, j);
 #define SX(o) ((float)S[reflect101(c + (o), a.W)])
     float s;
     if (a.ks == 3) {
@@ -1009,7 +1032,10 @@ hipError_t launch_level_image(const LevelImagePlan& p, const uint8_t* img, int W
     ra.scale_x = p.scale_x;
     ra.ks = p.ks;
     std::memcpy(ra.k, p.k, sizeof(float) * p.ks);
-    hipLaunchKernelGGL(fb_rowpass_kernel, dim3((p.nc + 255) / 256, H), dim3(256), 0, s, ra);
+    // LDS for the wide-kernel path: one block's column span plus the border
+    const size_t span = p.mode == kModeLinear ? (size_t)std::ceil(128.0 * p.scale_x) + 4 : 256;
+    const size_t smem = p.ks > 5 ? (span + 2 * (p.ks >> 1) + 16 + 15) & ~(size_t)15 : 0;
+    hipLaunchKernelGGL(fb_rowpass_kernel, dim3((p.nc + 255) / 256, H), dim3(256), smem, s, ra);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     FbColArgs ca;
