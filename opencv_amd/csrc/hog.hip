@@ -29,6 +29,16 @@ namespace tbdk {
 constexpr int kHogMaxBins = 32;
 constexpr int kHogMaxCells = 16;
 
+// one pyramid level of a batched detectMultiScale: its regions of the
+// multi-level gradient / block buffers and its first workgroup in the batched
+// block and window launches
+struct HogLevelEnt {
+    int64_t goff, qoff, boff;  // floats, bytes, floats
+    int gpitch, qpitch;        // floats, bytes
+    int nbx, nby, nwx, nwy;
+    int level, b0, w0;
+};
+
 struct HogScratch {
     uint8_t* level = nullptr;  // resized level image (u8, cn)
     float* grad = nullptr;     // 2 floats per pixel
@@ -39,6 +49,13 @@ struct HogScratch {
     int* hits = nullptr;       // [0] count, then (level, x, y) int triples
     double* scores = nullptr;
     int64_t cap_px = 0, cap_blocks = 0, cap_svm = 0, cap_cells = 0, cap_hits = 0;
+    // detectMultiScale: every level's gradients and blocks at once (one block
+    // and one window launch for all levels)
+    float* mgrad = nullptr;
+    uint8_t* mqa = nullptr;
+    float* mblocks = nullptr;
+    HogLevelEnt* lvtab = nullptr;
+    int64_t cap_mgrad = 0, cap_mqa = 0, cap_mblocks = 0, cap_lvtab = 0;
     hipStream_t stream = nullptr;  // stream of the last call that used this scratch
     bool used = false;
 };
@@ -253,7 +270,18 @@ struct HogBlockArgs {
     int cell_len[kHogMaxCells];
     float thresh;
     float* blocks;
+    const HogLevelEnt* lv;  // nlv > 0: all levels in one launch (grad, qangle, blocks are the multi-level buffers)
+    int nlv;
 };
+
+// the level of workgroup wg of a batched launch (first-workgroup field b0 or w0)
+template <bool WIN>
+__device__ __forceinline__ int hog_level_of(const HogLevelEnt* lv, int nlv, int wg)
+{
+    int L = 0;
+    while (L + 1 < nlv && (WIN ? lv[L + 1].w0 : lv[L + 1].b0) <= wg) ++L;
+    return L;
+}
 
 // Each thread sums its cell's bins straight into the block's LDS histogram
 // (the reference's read-both-then-write update, hog.cpp:909-911); then every
@@ -264,21 +292,33 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
     extern __shared__ float lds[];
     const int per_wg = 256 / a.ncells;
     const int lb = threadIdx.x / a.ncells, cell = threadIdx.x - lb * a.ncells;
-    const int b = blockIdx.x * per_wg + lb;
-    const bool live = lb < per_wg && b < a.nbx * a.nby;
+    int wg = blockIdx.x, nbx = a.nbx, nby = a.nby;
+    const float* grad = a.grad;
+    const uint8_t* qangle = a.qangle;
+    int gpitch = a.gpitch, qpitch = a.qpitch;
+    float* blocks = a.blocks;
+    if (a.nlv > 0) {
+        const HogLevelEnt& e = a.lv[hog_level_of<false>(a.lv, a.nlv, wg)];
+        wg -= e.b0;
+        nbx = e.nbx, nby = e.nby;
+        grad += e.goff, qangle += e.qoff, blocks += e.boff;
+        gpitch = e.gpitch, qpitch = e.qpitch;
+    }
+    const int b = wg * per_wg + lb;
+    const bool live = lb < per_wg && b < nbx * nby;
     float* H = lds + lb * a.hsz;
     float* hs = H + cell * a.nbins;
     if (live) {
         for (int i = 0; i < a.nbins; ++i) hs[i] = 0.f;
-        const int by = b / a.nbx, bx = b - by * a.nbx;
+        const int by = b / nbx, bx = b - by * nbx;
         const int x0 = bx * a.csx, y0 = by * a.csy;
         const int4* L = a.cells + (size_t)cell * a.cell_cap;
         const int n = a.cell_len[cell];
         for (int k = 0; k < n; ++k) {
             const int4 e = L[k];
             const int yy = y0 + e.x, xx = x0 + e.y;
-            const float2 g = *reinterpret_cast<const float2*>(a.grad + (size_t)yy * a.gpitch + 2 * xx);
-            const uchar2 q = *reinterpret_cast<const uchar2*>(a.qangle + (size_t)yy * a.qpitch + 2 * xx);
+            const float2 g = *reinterpret_cast<const float2*>(grad + (size_t)yy * gpitch + 2 * xx);
+            const uchar2 q = *reinterpret_cast<const uchar2*>(qangle + (size_t)yy * qpitch + 2 * xx);
             const float w = __int_as_float(e.z);
             const float t0 = hs[q.x] + g.x * w;
             const float t1 = hs[q.y] + g.y * w;
@@ -312,7 +352,7 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
         sum += v * v;
     }
     const float scale2 = 1.f / (sqrtf(sum) + 1e-3f);
-    float* out = a.blocks + (size_t)b * sz + cell * a.nbins;
+    float* out = blocks + (size_t)b * sz + cell * a.nbins;
     for (int k = 0; k < a.nbins; ++k) out[k] = scale2 * fminf(hs[k] * scale, a.thresh);
 }
 
@@ -330,6 +370,8 @@ struct HogWinArgs {
     int* hits;  // [0] count, then triples
     double* scores;
     int cap;
+    const HogLevelEnt* lv;  // nlv > 0: all levels in one launch (blocks is the multi-level buffer)
+    int nlv;
 };
 
 // One wave per window, one lane per block (blocks x-major as blockData): each
@@ -342,18 +384,26 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
 {
     extern __shared__ double wl[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * kHogWinPerWg + wave;
+    int wg = blockIdx.x, nwx = a.nwx, nwy = a.nwy, nbx = a.nbx, level = a.level;
+    const float* blocks = a.blocks;
+    if (a.nlv > 0) {
+        const HogLevelEnt& e = a.lv[hog_level_of<true>(a.lv, a.nlv, wg)];
+        wg -= e.w0;
+        nwx = e.nwx, nwy = e.nwy, nbx = e.nbx, level = e.level;
+        blocks += e.boff;
+    }
+    const int t = wg * kHogWinPerWg + wave;
     const int nblk = a.wbx * a.wby, tail = a.hsz & 3;
     double* main_v = wl + (size_t)wave * nblk * 4;  // per block: main + up to 3 tail products
-    const bool live = t < a.nwx * a.nwy;
+    const bool live = t < nwx * nwy;
     int x0 = 0, y0 = 0;
     if (live) {
-        const int wy = t / a.nwx, wx = t - wy * a.nwx;
+        const int wy = t / nwx, wx = t - wy * nwx;
         x0 = wx * a.wsx, y0 = wy * a.wsy;
         for (int k = lane; k < nblk; k += 64) {
             const int j = k / a.wby, i = k - j * a.wby;
             const int bx = (x0 + j * a.bsx) / a.csx, by = (y0 + i * a.bsy) / a.csy;
-            const float* v = a.blocks + ((size_t)by * a.nbx + bx) * a.hsz;
+            const float* v = blocks + ((size_t)by * nbx + bx) * a.hsz;
             const float* sv = a.svm + (size_t)k * a.hsz;
             float ps[4];
             for (int l = 0; l < 4; ++l) ps[l] = sv[l] * v[l];
@@ -375,7 +425,7 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
     if (s >= a.hit) {
         const int slot = atomicAdd(a.hits, 1);
         if (slot < a.cap) {
-            a.hits[1 + 3 * slot] = a.level;
+            a.hits[1 + 3 * slot] = level;
             a.hits[2 + 3 * slot] = x0;
             a.hits[3 + 3 * slot] = y0;
             a.scores[slot] = s;
@@ -586,6 +636,8 @@ static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog
     for (int c = 0; c < kHogMaxCells; ++c) a.cell_len[c] = c < pl.ncells ? (int)pl.lists[c].size() : 0;
     a.thresh = (float)p->l2hys_threshold;
     a.blocks = blocks;
+    a.lv = nullptr;
+    a.nlv = 0;
     const int per_wg = 256 / pl.ncells;
     const int nb = nbx * nby;
     const dim3 grid((nb + per_wg - 1) / per_wg);
@@ -618,6 +670,7 @@ static hipError_t run_level(tbdk_ctx* ctx, HogScratch* S, const HogPlan& pl, con
     a.wsx = p->win_stride_x, a.wsy = p->win_stride_y;
     a.rho = rho, a.hit = p->hit_threshold, a.level = level;
     a.hits = S->hits, a.scores = S->scores, a.cap = hit_cap;
+    a.lv = nullptr, a.nlv = 0;
     rec = timing_begin(ctx, "hog_window", s);
     const int nwin = a.nwx * a.nwy;
     const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);
@@ -792,7 +845,8 @@ void tbdk::hog_release(tbdk_ctx* ctx)
     HogScratch* S = ctx->hog;
     if (!S) return;
     for (void* p : {(void*)S->level, (void*)S->grad, (void*)S->qangle, (void*)S->blocks, (void*)S->svm,
-                    (void*)S->cells, (void*)S->hits, (void*)S->scores})
+                    (void*)S->cells, (void*)S->hits, (void*)S->scores, (void*)S->mgrad, (void*)S->mqa,
+                    (void*)S->mblocks, (void*)S->lvtab})
         if (p) (void)hipFree(p);
     delete S;
     ctx->hog = nullptr;
@@ -942,10 +996,35 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
     if (rc != TBDK_OK) return rc;
     HogScratch* S = ctx->hog;
     const double rho = svm_len > pl.dsize ? svm[pl.dsize] : 0;
-    hipError_t e = hipSuccess;
-    for (int l = 0; l < (int)lv.size() && e == hipSuccess; ++l) {
+    // every level's blocks get their own region of one buffer, so the window
+    // pass runs once over all levels (small levels alone fill a fraction of the
+    // device; batching the block pass as well measured 14 % slower for it)
+    std::vector<HogLevelEnt> ents;
+    int64_t boff = 0;
+    int nwwg = 0;
+    for (int l = 0; l < (int)lv.size(); ++l) {
         const int sw = cv_round_d(width / lv[l]), sh = cv_round_d(height / lv[l]);
         if (sw < params->win_w || sh < params->win_h) continue;
+        HogLevelEnt en;
+        en.goff = 0, en.qoff = 0, en.boff = boff;
+        en.gpitch = 2 * sw, en.qpitch = 2 * sw;
+        en.nbx = (sw - params->block_w) / pl.csx + 1, en.nby = (sh - params->block_h) / pl.csy + 1;
+        en.nwx = (sw - params->win_w) / params->win_stride_x + 1;
+        en.nwy = (sh - params->win_h) / params->win_stride_y + 1;
+        en.level = l, en.b0 = 0, en.w0 = nwwg;
+        ents.push_back(en);
+        boff += (int64_t)en.nbx * en.nby * pl.hsz;
+        nwwg += (en.nwx * en.nwy + kHogWinPerWg - 1) / kHogWinPerWg;
+    }
+    if ((rc = grow(&S->mblocks, S->cap_mblocks, std::max<int64_t>(boff, 1))) ||
+        (rc = grow(&S->lvtab, S->cap_lvtab, std::max<int64_t>((int64_t)ents.size(), 1))))
+        return rc;
+    hipError_t e = ents.empty() ? hipSuccess
+                                : hipMemcpyAsync(S->lvtab, ents.data(), sizeof(HogLevelEnt) * ents.size(),
+                                                 hipMemcpyHostToDevice, s);
+    for (size_t k = 0; k < ents.size() && e == hipSuccess; ++k) {
+        const HogLevelEnt& en = ents[k];
+        const int sw = en.gpitch / 2, sh = cv_round_d(height / lv[en.level]);
         const uint8_t* li = img;
         int lp = pitch;
         if (sw != width || sh != height) {
@@ -958,7 +1037,33 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
             li = S->level;
             lp = sw * cn;
         }
-        if (e == hipSuccess) e = run_level(ctx, S, pl, params, li, sw, sh, lp, cn, rho, l, (int)cap, s);
+        if (e != hipSuccess) break;
+        int rec = timing_begin(ctx, "hog_grad", s);
+        e = launch_grad(li, sw, sh, lp, cn, params, S->grad, en.gpitch, S->qangle, en.qpitch, s);
+        timing_end(ctx, rec, s);
+        if (e != hipSuccess) break;
+        rec = timing_begin(ctx, "hog_block", s);
+        e = launch_blocks(S, pl, params, S->grad, en.gpitch, S->qangle, en.qpitch, en.nbx, en.nby,
+                          S->mblocks + en.boff, s);
+        timing_end(ctx, rec, s);
+    }
+    if (e == hipSuccess && !ents.empty()) {
+        {
+            HogWinArgs w;
+            w.blocks = S->mblocks, w.svm = S->svm;
+            w.nbx = 0, w.csx = pl.csx, w.csy = pl.csy;
+            w.wbx = pl.wbx, w.wby = pl.wby, w.bsx = params->block_stride_x, w.bsy = params->block_stride_y;
+            w.hsz = pl.hsz;
+            w.nwx = 0, w.nwy = 0, w.wsx = params->win_stride_x, w.wsy = params->win_stride_y;
+            w.rho = rho, w.hit = params->hit_threshold, w.level = 0;
+            w.hits = S->hits, w.scores = S->scores, w.cap = (int)cap;
+            w.lv = S->lvtab, w.nlv = (int)ents.size();
+            const int rec = timing_begin(ctx, "hog_window", s);
+            const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);
+            hipLaunchKernelGGL(hog_window_kernel, dim3(nwwg), dim3(256), lds, s, w);
+            timing_end(ctx, rec, s);
+            e = hipGetLastError();
+        }
     }
     if (e != hipSuccess) return map_status(e);
     std::vector<Hit> hits;
