@@ -49,13 +49,11 @@ struct HogScratch {
     int* hits = nullptr;       // [0] count, then (level, x, y) int triples
     double* scores = nullptr;
     int64_t cap_px = 0, cap_blocks = 0, cap_svm = 0, cap_cells = 0, cap_hits = 0;
-    // detectMultiScale: every level's gradients and blocks at once (one block
-    // and one window launch for all levels)
-    float* mgrad = nullptr;
-    uint8_t* mqa = nullptr;
+    // detectMultiScale: every level's blocks at once (one window launch for
+    // all levels)
     float* mblocks = nullptr;
     HogLevelEnt* lvtab = nullptr;
-    int64_t cap_mgrad = 0, cap_mqa = 0, cap_mblocks = 0, cap_lvtab = 0;
+    int64_t cap_mblocks = 0, cap_lvtab = 0;
     hipStream_t stream = nullptr;  // stream of the last call that used this scratch
     bool used = false;
 };
@@ -845,8 +843,8 @@ void tbdk::hog_release(tbdk_ctx* ctx)
     HogScratch* S = ctx->hog;
     if (!S) return;
     for (void* p : {(void*)S->level, (void*)S->grad, (void*)S->qangle, (void*)S->blocks, (void*)S->svm,
-                    (void*)S->cells, (void*)S->hits, (void*)S->scores, (void*)S->mgrad, (void*)S->mqa,
-                    (void*)S->mblocks, (void*)S->lvtab})
+                    (void*)S->cells, (void*)S->hits, (void*)S->scores, (void*)S->mblocks,
+                    (void*)S->lvtab})
         if (p) (void)hipFree(p);
     delete S;
     ctx->hog = nullptr;
