@@ -29,14 +29,13 @@ namespace tbdk {
 constexpr int kHogMaxBins = 32;
 constexpr int kHogMaxCells = 16;
 
-// one pyramid level of a batched detectMultiScale: its regions of the
-// multi-level gradient / block buffers and its first workgroup in the batched
-// block and window launches
+// one pyramid level of a batched detectMultiScale: its region of the
+// multi-level block buffer and its first workgroup in the batched window launch
 struct HogLevelEnt {
-    int64_t goff, qoff, boff;  // floats, bytes, floats
-    int gpitch, qpitch;        // floats, bytes
+    int64_t boff;        // floats
+    int gpitch, qpitch;  // floats, bytes
     int nbx, nby, nwx, nwy;
-    int level, b0, w0;
+    int level, w0;
 };
 
 struct HogScratch {
@@ -268,16 +267,13 @@ struct HogBlockArgs {
     int cell_len[kHogMaxCells];
     float thresh;
     float* blocks;
-    const HogLevelEnt* lv;  // nlv > 0: all levels in one launch (grad, qangle, blocks are the multi-level buffers)
-    int nlv;
 };
 
-// the level of workgroup wg of a batched launch (first-workgroup field b0 or w0)
-template <bool WIN>
+// the level of workgroup wg of the batched window launch
 __device__ __forceinline__ int hog_level_of(const HogLevelEnt* lv, int nlv, int wg)
 {
     int L = 0;
-    while (L + 1 < nlv && (WIN ? lv[L + 1].w0 : lv[L + 1].b0) <= wg) ++L;
+    while (L + 1 < nlv && lv[L + 1].w0 <= wg) ++L;
     return L;
 }
 
@@ -290,19 +286,12 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
     extern __shared__ float lds[];
     const int per_wg = 256 / a.ncells;
     const int lb = threadIdx.x / a.ncells, cell = threadIdx.x - lb * a.ncells;
-    int wg = blockIdx.x, nbx = a.nbx, nby = a.nby;
+    const int nbx = a.nbx, nby = a.nby;
     const float* grad = a.grad;
     const uint8_t* qangle = a.qangle;
-    int gpitch = a.gpitch, qpitch = a.qpitch;
+    const int gpitch = a.gpitch, qpitch = a.qpitch;
     float* blocks = a.blocks;
-    if (a.nlv > 0) {
-        const HogLevelEnt& e = a.lv[hog_level_of<false>(a.lv, a.nlv, wg)];
-        wg -= e.b0;
-        nbx = e.nbx, nby = e.nby;
-        grad += e.goff, qangle += e.qoff, blocks += e.boff;
-        gpitch = e.gpitch, qpitch = e.qpitch;
-    }
-    const int b = wg * per_wg + lb;
+    const int b = blockIdx.x * per_wg + lb;
     const bool live = lb < per_wg && b < nbx * nby;
     float* H = lds + lb * a.hsz;
     float* hs = H + cell * a.nbins;
@@ -385,7 +374,7 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
     int wg = blockIdx.x, nwx = a.nwx, nwy = a.nwy, nbx = a.nbx, level = a.level;
     const float* blocks = a.blocks;
     if (a.nlv > 0) {
-        const HogLevelEnt& e = a.lv[hog_level_of<true>(a.lv, a.nlv, wg)];
+        const HogLevelEnt& e = a.lv[hog_level_of(a.lv, a.nlv, wg)];
         wg -= e.w0;
         nwx = e.nwx, nwy = e.nwy, nbx = e.nbx, level = e.level;
         blocks += e.boff;
@@ -634,8 +623,6 @@ static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog
     for (int c = 0; c < kHogMaxCells; ++c) a.cell_len[c] = c < pl.ncells ? (int)pl.lists[c].size() : 0;
     a.thresh = (float)p->l2hys_threshold;
     a.blocks = blocks;
-    a.lv = nullptr;
-    a.nlv = 0;
     const int per_wg = 256 / pl.ncells;
     const int nb = nbx * nby;
     const dim3 grid((nb + per_wg - 1) / per_wg);
@@ -1004,12 +991,12 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
         const int sw = cv_round_d(width / lv[l]), sh = cv_round_d(height / lv[l]);
         if (sw < params->win_w || sh < params->win_h) continue;
         HogLevelEnt en;
-        en.goff = 0, en.qoff = 0, en.boff = boff;
+        en.boff = boff;
         en.gpitch = 2 * sw, en.qpitch = 2 * sw;
         en.nbx = (sw - params->block_w) / pl.csx + 1, en.nby = (sh - params->block_h) / pl.csy + 1;
         en.nwx = (sw - params->win_w) / params->win_stride_x + 1;
         en.nwy = (sh - params->win_h) / params->win_stride_y + 1;
-        en.level = l, en.b0 = 0, en.w0 = nwwg;
+        en.level = l, en.w0 = nwwg;
         ents.push_back(en);
         boff += (int64_t)en.nbx * en.nby * pl.hsz;
         nwwg += (en.nwx * en.nwy + kHogWinPerWg - 1) / kHogWinPerWg;
