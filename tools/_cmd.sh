@@ -1,2 +1,4 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_hog.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_hog.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_all.log 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+bash tools/profile_round.sh r02 > gpurun_out/prof.log 2>&1 || exit 1
