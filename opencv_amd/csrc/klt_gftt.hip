@@ -24,6 +24,7 @@
 //                   corners are accepted.
 #include <atomic>
 #include <cfloat>
+#include <cmath>
 
 #include "tbdk_internal.hpp"
 
@@ -441,6 +442,29 @@ __device__ __forceinline__ void sort_keys(uint64_t* keys, int np2, int tid)
     __syncthreads();
 }
 
+// Bitonic sort of np2 keys in LDS only (every stage a compare-exchange pass
+// over LDS pairs): the path for ROIs with more than 4 * kSelThreads candidates.
+// Slower than sort_keys, but it keeps the kernel's register footprint at that
+// of sort_keys<4> (the register-resident sorts of 8-32 keys per thread needed
+// 169 VGPRs, which made every select workgroup wait for PyrLK waves to drain).
+__device__ __forceinline__ void sort_keys_lds(uint64_t* keys, int np2, int tid)
+{
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = tid; p < np2 / 2; p += kSelThreads) {
+                const int e = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // lower element of the pair
+                const uint64_t x = keys[e], y = keys[e | j];
+                const bool desc = (e & k) == 0;
+                if (desc ? x < y : x > y) {
+                    keys[e] = y;
+                    keys[e | j] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // Greedy-walk distance test of one candidate against the byte image (image
 // mode): for every window pixel closer than min_distance, 255 = an accepted
 // corner (the candidate is rejected), 1..64 = a candidate of this step in lane
@@ -519,6 +543,11 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
 //   acc   : max_corners float2 accepted positions + 64 float2 (list mode)
 //   img   : img_bytes, one byte per ROI pixel (image mode): 0 empty,
 //           1..64 candidate of the current step (lane + 1), 255 accepted corner
+// RMAX: the largest distance-window radius this instance handles (the walk's
+// window rows are register arrays: radius 6 needs 156 VGPRs, radius 2 68, and
+// a select workgroup's eight waves only find room next to PyrLK waves at the
+// smaller size); the host picks the instance from min_distance.
+template <int RMAX>
 __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -622,9 +651,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     case 1: sort_keys<1>(keys, np2, tid); break;
     case 2: sort_keys<2>(keys, np2, tid); break;
     case 4: sort_keys<4>(keys, np2, tid); break;
-    case 8: sort_keys<8>(keys, np2, tid); break;
-    case 16: sort_keys<16>(keys, np2, tid); break;
-    default: sort_keys<32>(keys, np2, tid); break;
+    default: sort_keys_lds(keys, np2, tid); break;
     }
     GFTT_STAMP(2);
     if (tid >= 64) return;
@@ -651,14 +678,20 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
             __builtin_amdgcn_wave_barrier();
             GFTT_T(1);
             if (valid) {
-                switch (rad) {  // uniform
+                switch (rad) {  // uniform; rad <= RMAX (host)
                 case 0: window_test<0>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
                 case 1: window_test<1>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
                 case 2: window_test<2>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
-                case 3: window_test<3>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
-                case 4: window_test<4>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
-                case 5: window_test<5>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
-                default: window_test<6>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                default:
+                    if constexpr (RMAX > 2) {
+                        switch (rad) {
+                        case 3: window_test<3>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                        case 4: window_test<4>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                        case 5: window_test<5>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                        default: window_test<6>(img, R.w, R.h, ix, iy, fx, fy, lane, md2, good, inb); break;
+                        }
+                    }
+                    break;
                 }
             }
         } else if (use_dist) {  // list mode: every accepted corner, then this step's pairs
@@ -769,16 +802,25 @@ hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig)
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(opted.load(std::memory_order_acquire) & bit)) {
-        hipFuncAttributes fa;
-        e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&gftt_select_kernel));
-        if (e != hipSuccess) return e;
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gftt_select_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(160L * 1024 - (long)fa.sharedSizeBytes));
-        if (e != hipSuccess) return e;
+        for (const void* k : {reinterpret_cast<const void*>(&gftt_select_kernel<2>),
+                              reinterpret_cast<const void*>(&gftt_select_kernel<6>)}) {
+            hipFuncAttributes fa;
+            e = hipFuncGetAttributes(&fa, k);
+            if (e != hipSuccess) return e;
+            e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(160L * 1024 - (long)fa.sharedSizeBytes));
+            if (e != hipSuccess) return e;
+        }
         opted.fetch_or(bit, std::memory_order_acq_rel);
     }
-    hipLaunchKernelGGL(gftt_select_kernel, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
+    // the distance window's radius, as the kernel derives it
+    const double md2 = a.min_distance * a.min_distance;
+    int rad = (int)ceil(a.min_distance) - 1;
+    if ((double)(rad + 1) * (rad + 1) < md2) rad++;
+    if (a.min_distance >= 1.0 && rad > 2)
+        hipLaunchKernelGGL(gftt_select_kernel<6>, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
+    else
+        hipLaunchKernelGGL(gftt_select_kernel<2>, dim3(a.nroi), dim3(kSelThreads), smem, s, a);
     return hipGetLastError();
 }
 

@@ -1,4 +1,6 @@
 set -o pipefail
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_all.log 2>&1 || exit 1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-bash tools/profile_round.sh r02 > gpurun_out/prof.log 2>&1 || exit 1
+B="python bench.py --steps 1500 --no-cpu-baseline --no-step-api --no-farneback --no-hog --no-f16"
+for i in 1 2 3 4; do
+timeout -k 10 200 $B > gpurun_out/ab_new_$i.json 2>/dev/null || exit 1
+TBDK_LIB=opencv_amd/lib/var_head.so timeout -k 10 200 $B > gpurun_out/ab_head_$i.json 2>/dev/null || exit 1
+done
