@@ -379,6 +379,8 @@ def main():
                     help="ctx option tbd_early_gftt (A/B runs; 0 off, 1 new tracks, 2 + re-detection boxes)")
     ap.add_argument("--no-spec-lookahead", action="store_true", help="ctx option tbd_spec_lookahead = 0 (A/B runs)")
     ap.add_argument("--no-zero-copy", action="store_true", help="ctx option tbd_zero_copy = 0 (A/B runs)")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="HIP events on every Nth launch of the timed kernels in the timed region")
     ap.add_argument("--kstats", default="lk_sparse",
                     help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
                          "each timed launch adds two event records to the frame's host work.  The other "
@@ -442,6 +444,10 @@ def main():
     timed = ["pyr_build", "lk_sparse", "gftt", "tbd_fit"] if args.kstats == "all" else \
         [] if args.kstats == "none" else [k for k in args.kstats.split(",") if k]
     ctx.timing_select(timed or None)
+    # events on every 5th timed launch: each timed launch costs two event records of
+    # host work on the frame's critical path (~5 % of the frame when every launch is
+    # timed); 5 is odd, so a frame's alternating launch kinds are sampled alike
+    ctx.set_option("timing_every", args.timing_every)
     ctx.timing_enable(bool(timed))
     if world > 1:
         dist.barrier()
@@ -476,9 +482,11 @@ def main():
     kstats = {}
     for name in timed:
         c, ms = ctx.timing_query(name)
-        kstats[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "total_ms": ms}
+        kstats[name] = {"launches": ctx.timing_calls(name), "timed_launches": c,
+                        "avg_us": (ms / c * 1000.0) if c else None, "total_ms_timed": ms}
     ctx.timing_enable(False)
     ctx.timing_select(None)
+    ctx.set_option("timing_every", 1)
     nolaunch = {"launches": 0, "avg_us": None, "total_ms": 0.0}
 
     # secondary: the same frames through the per-frame tbdk_tbd_step API (no
@@ -534,7 +542,8 @@ def main():
                 "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic, "kernel": "lk_sparse",
                 "traffic_source": traffic_src,
                 "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA use; peak = fp32 vector rate; "
-                        "algorithmic flops per SURVEY.md §8(d) with the measured iteration count",
+                        "algorithmic flops per SURVEY.md §8(d) with the measured iteration count; "
+                        f"launch duration = HIP events on every {args.timing_every}th launch of the timed region",
                 "flops_per_launch": flops_per_launch,
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}

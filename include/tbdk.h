@@ -105,7 +105,9 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_zero_copy" (0/1, default 1; taken by tbdk_tbd_create): the TBD loop's
  *       kernels read their host tables from, and the fit writes its results
  *       to, coherent pinned host memory directly instead of through copies
- *       (results equal). */
+ *       (results equal).
+ *   "timing_every" (>= 1, default 1): HIP events on every Nth launch of each
+ *       kernel selected for timing (see tbdk_timing_calls). */
 
 /* device ordinal of the context */
 int tbdk_ctx_device(const tbdk_ctx* ctx);
@@ -120,6 +122,11 @@ int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double
 /* Restrict recording to the comma-separated kernel names in `names` (NULL or
  * "" = all).  Each timed launch costs two event records on the host. */
 int tbdk_timing_select(tbdk_ctx* ctx, const char* names);
+/* Selected launches of kernel `name` since tbdk_timing_enable, timed or not:
+ * with the ctx option "timing_every" = N only every Nth of them records events
+ * (tbdk_timing_query counts those), to keep the event records' host cost out
+ * of a measured loop. */
+int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls);
 
 /* ---- pyramids ------------------------------------------------------------ */
 

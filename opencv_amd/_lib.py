@@ -183,6 +183,7 @@ SIGNATURES = {
     "tbdk_ctx_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     "tbdk_timing_select": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    "tbdk_timing_calls": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_f16": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_build_f16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),

@@ -28,6 +28,14 @@ int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
     if (!ctx->timing_only.empty() &&
         ctx->timing_only.find("," + std::string(name) + ",") == std::string::npos)
         return -1;
+    int64_t* calls = nullptr;
+    for (auto& c : ctx->timing_calls)
+        if (c.first == name) calls = &c.second;
+    if (!calls) {
+        ctx->timing_calls.emplace_back(name, 0);
+        calls = &ctx->timing_calls.back().second;
+    }
+    if ((*calls)++ % ctx->timing_every != 0) return -1;  // sampled: this launch is not timed
     TimingRec r{name, take_event(ctx), take_event(ctx)};
     if (!r.begin || !r.end) return -1;
     (void)hipEventRecord(r.begin, s);
@@ -102,6 +110,7 @@ int tbdk_timing_enable(tbdk_ctx* ctx, int enable)
         ctx->free_events.push_back(r.end);
     }
     ctx->recs.clear();
+    ctx->timing_calls.clear();
     ctx->timing = enable != 0;
     return TBDK_OK;
 }
@@ -111,6 +120,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
     if (!ctx || !name) return TBDK_EINVAL;
     if (std::strcmp(name, "gftt_eig_redo") == 0) {
         ctx->opt_gftt_eig_redo = value != 0;
+        return TBDK_OK;
+    }
+    if (std::strcmp(name, "timing_every") == 0) {
+        if (value < 1 || value > (1 << 20)) return TBDK_EINVAL;
+        ctx->timing_every = (int)value;
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_early_gftt") == 0) {
@@ -165,6 +179,15 @@ int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double
     }
     if (launches) *launches = cnt;
     if (total_ms) *total_ms = tot;
+    return TBDK_OK;
+}
+
+int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls)
+{
+    if (!ctx || !name || !calls) return TBDK_EINVAL;
+    *calls = 0;
+    for (auto& c : ctx->timing_calls)
+        if (c.first == name) *calls = c.second;
     return TBDK_OK;
 }
 

@@ -75,6 +75,8 @@ struct tbdk_ctx {
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")
     int opt_tbd_zero_copy = 1;   // tbdk_ctx_set_option("tbd_zero_copy"), read by tbdk_tbd_create
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
+    int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
+    std::vector<std::pair<std::string, int64_t>> timing_calls;  // selected launches per name (sampled or not)
     std::vector<tbdk::TimingRec> recs;
     std::vector<hipEvent_t> free_events;
     tbdk::GfttScratch gftt;  // grown on demand, or up front by tbdk_gftt_reserve

@@ -73,6 +73,12 @@ class Context:
         arg = ",".join(names).encode() if names else None
         _lib.check(self.lib.tbdk_timing_select(self.handle, arg), "tbdk_timing_select")
 
+    def timing_calls(self, name: str) -> int:
+        """Selected launches of `name` since timing_enable, timed or not (ctx option timing_every)."""
+        n = C.c_int64()
+        _lib.check(self.lib.tbdk_timing_calls(self.handle, name.encode(), C.byref(n)), "tbdk_timing_calls")
+        return int(n.value)
+
     def timing_query(self, name: str) -> tuple[int, float]:
         n = C.c_int64()
         ms = C.c_double()
