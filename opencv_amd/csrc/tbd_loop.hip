@@ -203,10 +203,10 @@ struct tbdk_tbd {
     GfttScratch gftt2;  // the post-tracker GFTT's (side), so the next step's early GFTT need not wait for it
     hipEvent_t pyr_ready = nullptr;               // this step's pyramid built on the step's stream
     // zero-copy staging: the kernels read the pinned host tables (fit entries,
-    // slot lists, post-tracker lists, GFTT ROI tables) and the fit kernel
+    // slot lists, GFTT ROI tables) and the fit kernel
     // writes its results to pinned host memory directly, through device
     // mappings of the coherent pinned buffers; no copy is issued (d_pre, d_fit,
-    // d_post, d_la, d_spec, d_etab are those mappings, not device allocations)
+    // d_tab, d_la, d_spec, d_etab are those mappings, not device allocations)
     bool zc = false;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
     hipEvent_t early_done = nullptr;
@@ -652,7 +652,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
 
 
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
-    {  // the previous frame's clear / GFTT / scatter (on `side`) before the refreshed sets
+    {  // the previous step's early and post-tracker GFTT (their rows) before the refreshed sets
         hipError_t e = hipStreamWaitEvent(s, t->post_done, 0);
         if (e != hipSuccess) return map_status(e);
     }
