@@ -205,3 +205,30 @@ def test_lk_1080p_full_size(gpu, impl):
     g, ex, sse = run_pair(gpu, fr[0], fr[1], pts, maxlev=2, impl=impl)
     assert_exact(g, ex)
     assert_tolerance(g, sse)
+
+
+def test_timing_sampling(gpu):
+    """ctx option timing_every: events on every Nth selected launch; tbdk_timing_calls
+    counts all of them (bench.py's roofline uses both)"""
+    K = klt()
+    fr, _ = O.synth(3, 320, 240, 8, 0, 2)
+    pts = to_dev(grid_points(240, 320, 16, 8))
+    P0 = K.build_pyramid(to_dev(fr[0]), (21, 21), 2, ctx=gpu)
+    P1 = K.build_pyramid(to_dev(fr[1]), (21, 21), 2, ctx=gpu)
+    lk = K.SparsePyrLKOpticalFlow((21, 21), 2)
+    try:
+        gpu.timing_select(["lk_sparse"])
+        gpu.set_option("timing_every", 3)
+        gpu.timing_enable(True)
+        for _ in range(7):
+            lk.calc(P0, P1, pts)
+        torch.cuda.synchronize()
+        c, ms = gpu.timing_query("lk_sparse")
+        assert gpu.timing_calls("lk_sparse") == 7
+        assert c == 3 and ms > 0  # launches 0, 3, 6
+    finally:
+        gpu.timing_enable(False)
+        gpu.timing_select(None)
+        gpu.set_option("timing_every", 1)
+    with pytest.raises(Exception):
+        gpu.set_option("timing_every", 0)
