@@ -90,7 +90,11 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       reference's running box-filter sum (results equal).
  *   "lk_impl" (0..3): the PyrLK kernel taken when tbdk_lk_params.impl is 0
  *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
- *       (results equal). */
+ *       (results equal).
+ *   "hog_block_tiled" (0..2, default 1): HOG block histograms of 2x2-cell,
+ *       9-bin geometries by the LDS-tiled kernel, its histograms in LDS (1)
+ *       or in registers (2); 0 forces the per-cell kernel of every other
+ *       geometry (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 /*   "tbd_early_gftt" (0/1/2, default 2): the TBD loop runs GFTT over the
  *       detections that will start new tracks at the start of the step, off

@@ -16,6 +16,7 @@
 // The host then sorts the hits into window order, scales them to rects, and
 // groups and clips them (groupRectangles, hog.cpp:3783-3861; clipObjects).
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -55,6 +56,7 @@ struct HogScratch {
     int64_t cap_mblocks = 0, cap_lvtab = 0;
     hipStream_t stream = nullptr;  // stream of the last call that used this scratch
     bool used = false;
+    int block_tiled = 1;  // tbdk_ctx_set_option("hog_block_tiled"), copied by reserve()
 };
 
 // The scratch (cell table, level image, gradients, blocks, hits) is rewritten by
@@ -343,6 +345,142 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
     for (int k = 0; k < a.nbins; ++k) out[k] = scale2 * fminf(hs[k] * scale, a.thresh);
 }
 
+// Tiled variant for 2x2-cell blocks with 9 bins (the detectors' geometry): a
+// workgroup owns 16 x 4 blocks and first stages their pixel footprint (gx, gy,
+// bins) and the four cells' pixData lists into LDS, coalesced, so no per-entry
+// load leaves the CU (lists read from L2 per entry group measured as slow as
+// the untiled kernel).  Each thread then sums its
+// cell's entries in pixData order, the reference's read-both-then-write update
+// (hog.cpp:909-911), into
+//   BINS_LDS = true:  its own histogram in LDS, bin-major (hs[bin * 256 + tid]),
+//                     so the lanes' data-dependent bins never share a bank;
+//   BINS_LDS = false: nine registers, every bin adding its entry term or +0.0f
+//                     (leaves a value >= +0 unchanged; b0 != b1 for nbins >= 2).
+// Pixel planes are skewed by one word per csx columns, so the 16 blocks of a
+// wave (csx apart) read 16 different banks: s(y, x) = y * twp + x + x / csx.
+struct HogTile {
+    int bw, bh;            // block size in pixels
+    int ntx;               // tiles per row of blocks
+    int twp, npx;          // skewed plane pitch and plane size (words)
+    int off_q;             // word offset of the bin plane (u16)
+    int off_h;             // word offset of the LDS histograms (BINS_LDS)
+    int off_l, lstride;    // word offset of the cell lists (int2), entries per list
+};
+constexpr int kHogTileBx = 16, kHogTileBy = 4;
+
+template <bool BINS_LDS>
+__global__ __launch_bounds__(256) void hog_block_tile_kernel(HogBlockArgs a, HogTile t)
+{
+    constexpr int NB = 9, U = 4;
+    extern __shared__ float lds[];
+    float* gxs = lds;
+    float* gys = lds + t.npx;
+    uint16_t* qs = reinterpret_cast<uint16_t*>(lds + t.off_q);
+    float* hs = lds + t.off_h + threadIdx.x;
+    int2* lst = reinterpret_cast<int2*>(lds + t.off_l);
+    const int tid = threadIdx.x, csx = a.csx, csy = a.csy;
+    const int tby = blockIdx.x / t.ntx, tbx = blockIdx.x - tby * t.ntx;
+    const int bx0 = tbx * kHogTileBx, by0 = tby * kHogTileBy;
+    const int px0 = bx0 * csx, py0 = by0 * csy;
+    const int tw = (min(bx0 + kHogTileBx, a.nbx) - 1 - bx0) * csx + t.bw;
+    const int th = (min(by0 + kHogTileBy, a.nby) - 1 - by0) * csy + t.bh;
+    // the footprint, one wave per row, lanes along x
+    for (int y = tid >> 6; y < th; y += 4) {
+        const float* gr = a.grad + (size_t)(py0 + y) * a.gpitch + 2 * px0;
+        const uint16_t* qr = reinterpret_cast<const uint16_t*>(a.qangle + (size_t)(py0 + y) * a.qpitch) + px0;
+        for (int x = tid & 63; x < tw; x += 64) {
+            const float2 g = *reinterpret_cast<const float2*>(gr + 2 * x);
+            const int s = y * t.twp + x + x / csx;
+            gxs[s] = g.x;
+            gys[s] = g.y;
+            qs[s] = qr[x];
+        }
+    }
+    // the four cell lists as (skewed offset, weight bits)
+    for (int i = tid; i < 4 * t.lstride; i += 256) {
+        const int c = i / t.lstride, k = i - c * t.lstride;
+        if (k < a.cell_cap) {
+            const int4 e = a.cells[(size_t)c * a.cell_cap + k];
+            lst[i] = make_int2(e.w, e.z);
+        }
+    }
+    if (BINS_LDS)
+        for (int i = 0; i < NB; ++i) hs[i * 256] = 0.f;
+    __syncthreads();
+    const int lb = tid >> 2, cell = tid & 3;
+    const int lbx = lb & (kHogTileBx - 1), lby = lb / kHogTileBx;
+    const int bx = bx0 + lbx, by = by0 + lby;
+    const bool live = bx < a.nbx && by < a.nby;
+    float h[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) h[i] = 0.f;
+    if (live) {
+        const int base = lby * csy * t.twp + lbx * csx + lbx;
+        const int2* L = lst + cell * t.lstride;
+        const int n = cell == 0 ? a.cell_len[0] : cell == 1 ? a.cell_len[1] : cell == 2 ? a.cell_len[2] : a.cell_len[3];
+        for (int k = 0; k < n; k += U) {
+            // U entries' pixels read ahead of their (ordered) updates
+            uint32_t q[U];
+            float a0[U], a1[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int2 e = L[min(k + u, n - 1)];
+                const int s = base + e.x;
+                const float w = __int_as_float(e.y);
+                q[u] = qs[s];
+                a0[u] = gxs[s] * w;
+                a1[u] = gys[s] * w;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (k + u >= n) break;
+                const uint32_t q0 = q[u] & 0xffu, q1 = q[u] >> 8;
+                if (BINS_LDS) {
+                    const float t0 = hs[q0 * 256] + a0[u];
+                    const float t1 = hs[q1 * 256] + a1[u];
+                    hs[q0 * 256] = t0;
+                    hs[q1 * 256] = t1;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NB; ++i)
+                        h[i] = h[i] + (q0 == (uint32_t)i ? a0[u] : (q1 == (uint32_t)i ? a1[u] : 0.f));
+                }
+            }
+        }
+    }
+    if (BINS_LDS)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) h[i] = hs[i * 256];
+    __syncthreads();  // the pixel planes become the blocks' histograms
+    const int sz = 4 * NB;
+    float* H = lds + lb * sz;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) H[cell * NB + i] = h[i];
+    __syncthreads();
+    if (!live) return;
+    // normalizeBlockHistogram, as in hog_block_kernel (sz = 36: nine 4-lane steps)
+    float ps[4];
+    for (int l = 0; l < 4; ++l) ps[l] = H[l] * H[l];
+    for (int i = 4; i <= sz - 4; i += 4)
+        for (int l = 0; l < 4; ++l) ps[l] = ps[l] + H[i + l] * H[i + l];
+    float sum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    const float scale = 1.f / (sqrtf(sum) + (float)sz * 0.1f);
+    for (int l = 0; l < 4; ++l) {
+        const float v = fminf(scale * H[l], a.thresh);
+        ps[l] = v * v;
+    }
+    for (int i = 4; i <= sz - 4; i += 4)
+        for (int l = 0; l < 4; ++l) {
+            const float v = fminf(H[i + l] * scale, a.thresh);
+            ps[l] = ps[l] + v * v;
+        }
+    sum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    const float scale2 = 1.f / (sqrtf(sum) + 1e-3f);
+    float* out = a.blocks + ((size_t)by * a.nbx + bx) * sz + cell * NB;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) out[k] = scale2 * fminf(h[k] * scale, a.thresh);
+}
+
 // ---------------------------------------------------------------------------
 // windows
 
@@ -568,8 +706,9 @@ static int grow(T** p, int64_t& cap, int64_t need)
 
 struct HogPlan {
     int hsz, ncells, csx, csy, wbx, wby, dsize;
-    std::vector<std::vector<int4>> lists;
+    std::vector<std::vector<int4>> lists;  // entry .w: offset in hog_block_tile_kernel's skewed tile
     int cell_cap;
+    int tile_twp;
 };
 
 static void make_plan(const tbdk_hog_params* p, HogPlan& pl)
@@ -582,6 +721,10 @@ static void make_plan(const tbdk_hog_params* p, HogPlan& pl)
     pl.wby = (p->win_h - p->block_h) / p->block_stride_y + 1;
     pl.dsize = descriptor_size(p);
     cell_lists(p, pl.lists);
+    const int tw = (kHogTileBx - 1) * pl.csx + p->block_w;
+    pl.tile_twp = tw + (tw - 1) / pl.csx + 1;
+    for (auto& l : pl.lists)
+        for (int4& e : l) e.w = e.x * pl.tile_twp + e.y + e.y / pl.csx;
     pl.cell_cap = 0;
     for (auto& l : pl.lists) pl.cell_cap = std::max(pl.cell_cap, (int)l.size());
 }
@@ -610,6 +753,27 @@ static hipError_t launch_grad(const uint8_t* img, int w, int h, int pitch, int c
     return hipGetLastError();
 }
 
+// dynamic LDS of the tiled block kernels: two workgroups per CU (the default
+// geometry takes 75 KB); above 64 KB the kernels opt in once per device
+constexpr size_t kHogTileLds = 80 * 1024;
+
+static hipError_t tile_lds_opt_in()
+{
+    static std::atomic<unsigned long long> opted{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (opted.load(std::memory_order_acquire) & bit) return hipSuccess;
+    for (const void* k : {reinterpret_cast<const void*>(&hog_block_tile_kernel<true>),
+                          reinterpret_cast<const void*>(&hog_block_tile_kernel<false>)}) {
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHogTileLds);
+        if (e != hipSuccess) return e;
+    }
+    opted.fetch_or(bit, std::memory_order_acq_rel);
+    return hipSuccess;
+}
+
 static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog_params* p, const float* grad,
                                 int gpitch_f, const uint8_t* qa, int qpitch, int nbx, int nby, float* blocks,
                                 hipStream_t s)
@@ -623,6 +787,30 @@ static hipError_t launch_blocks(HogScratch* S, const HogPlan& pl, const tbdk_hog
     for (int c = 0; c < kHogMaxCells; ++c) a.cell_len[c] = c < pl.ncells ? (int)pl.lists[c].size() : 0;
     a.thresh = (float)p->l2hys_threshold;
     a.blocks = blocks;
+    if (S->block_tiled && pl.ncells == 4 && p->nbins == 9) {
+        HogTile t;
+        t.bw = p->block_w, t.bh = p->block_h;
+        t.ntx = (nbx + kHogTileBx - 1) / kHogTileBx;
+        t.twp = pl.tile_twp;
+        t.npx = ((kHogTileBy - 1) * pl.csy + t.bh) * t.twp;
+        t.off_q = 2 * t.npx;
+        t.off_h = t.off_q + (t.npx + 1) / 2;
+        const bool bins_lds = S->block_tiled == 1;
+        t.off_l = (t.off_h + (bins_lds ? 9 * 256 : 0) + 1) & ~1;
+        t.lstride = (pl.cell_cap + 31) / 32 * 32 + 4;  // the four lists' heads 8 banks apart
+        const size_t words = std::max<size_t>((size_t)t.off_l + 2 * 4 * (size_t)t.lstride, 64 * 36);
+        if (words * sizeof(float) <= kHogTileLds) {
+            const hipError_t e = tile_lds_opt_in();
+            if (e != hipSuccess) return e;
+            const int nty = (nby + kHogTileBy - 1) / kHogTileBy;
+            const dim3 grid(t.ntx * nty);
+            if (bins_lds)
+                hipLaunchKernelGGL(hog_block_tile_kernel<true>, grid, dim3(256), words * sizeof(float), s, a, t);
+            else
+                hipLaunchKernelGGL(hog_block_tile_kernel<false>, grid, dim3(256), words * sizeof(float), s, a, t);
+            return hipGetLastError();
+        }
+    }
     const int per_wg = 256 / pl.ncells;
     const int nb = nbx * nby;
     const dim3 grid((nb + per_wg - 1) / per_wg);
@@ -671,6 +859,7 @@ static int reserve(tbdk_ctx* ctx, int w, int h, int cn, const HogPlan& pl, int s
     HogScratch* S = ctx->hog;
     if (!S) return TBDK_ENOMEM;
     if (claim(S, s) != hipSuccess) return TBDK_EHIP;
+    S->block_tiled = ctx->opt_hog_block_tiled;
     const int64_t px = (int64_t)w * h;
     int rc = TBDK_OK;
     if (px > S->cap_px) {

@@ -140,6 +140,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_zero_copy = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "hog_block_tiled") == 0) {
+        if (value < 0 || value > 2) return TBDK_EINVAL;
+        ctx->opt_hog_block_tiled = (int)value;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "lk_impl") == 0) {  // kernel used when tbdk_lk_params.impl is 0 (auto)
         if (value < 0 || value > 3) return TBDK_EINVAL;
         ctx->opt_lk_impl = (int)value;

@@ -76,6 +76,27 @@ def test_blocks_bit_exact(gpu, geom):
     assert np.array_equal(B, O.hog_blocks(og, oq, _prm(hg)))
 
 
+@pytest.mark.parametrize("w,h,bstride", [(300, 170, (8, 8)), (16, 16, (8, 8)), (151, 97, (4, 4)), (777, 41, (8, 8))])
+def test_blocks_tiled_kernel_bit_exact(gpu, w, h, bstride):
+    """hog_block_tile_kernel (2x2 cells, 9 bins): ragged last tiles in x and y, a single
+    block, block stride 4; equal to the oracle, to the register-bin variant (option 2) and
+    to the per-cell kernel (option 0)"""
+    from opencv_amd import hog
+
+    img = _bgr(w + 3 * h, w, h, cn=1)
+    hg = hog.HOG.create(ctx=gpu, block_stride=bstride, win_size=(48, 96) if bstride[0] == 4 else (64, 128))
+    og, oq = O.hog_gradient(img, nbins=9)
+    G, Q = torch.from_numpy(og).cuda(), torch.from_numpy(oq).cuda()
+    B = hog.blocks(G, Q, hg, ctx=gpu).cpu().numpy()
+    assert np.array_equal(B, O.hog_blocks(og, oq, _prm(hg)))
+    try:
+        for opt in (0, 2):
+            gpu.set_option("hog_block_tiled", opt)
+            assert np.array_equal(B, hog.blocks(G, Q, hg, ctx=gpu).cpu().numpy()), opt
+    finally:
+        gpu.set_option("hog_block_tiled", 1)
+
+
 @pytest.mark.parametrize("win", [(64, 128), (48, 96)])
 @pytest.mark.parametrize("cn", [1, 3])
 def test_detect_scores_bit_exact(gpu, win, cn):
