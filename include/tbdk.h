@@ -94,7 +94,11 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *   "hog_block_tiled" (0..2, default 1): HOG block histograms of 2x2-cell,
  *       9-bin geometries by the LDS-tiled kernel, its histograms in LDS (1)
  *       or in registers (2); 0 forces the per-cell kernel of every other
- *       geometry (results equal). */
+ *       geometry (results equal).
+ *   "hog_level_streams" (1..4, default 4): tbdk_hog_detect_multiscale runs
+ *       the levels' resize/gradient/block chains on this many streams (the
+ *       caller's and internal ones, joined back before the window pass;
+ *       results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 /*   "tbd_early_gftt" (0/1/2, default 2): the TBD loop runs GFTT over the
  *       detections that will start new tracks at the start of the step, off

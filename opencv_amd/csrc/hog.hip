@@ -57,6 +57,16 @@ struct HogScratch {
     hipStream_t stream = nullptr;  // stream of the last call that used this scratch
     bool used = false;
     int block_tiled = 1;  // tbdk_ctx_set_option("hog_block_tiled"), copied by reserve()
+    // detectMultiScale's level lanes: level k's resize -> gradient -> block
+    // chain runs on lane k % nlanes; lane 0 is the caller's stream with the
+    // buffers above, lanes 1.. own a stream and a level image / gradient set
+    static constexpr int kMaxLanes = 4;
+    hipStream_t lane_stream[kMaxLanes] = {};
+    hipEvent_t fork = nullptr, join[kMaxLanes] = {};
+    uint8_t* lane_level[kMaxLanes] = {};
+    float* lane_grad[kMaxLanes] = {};
+    uint8_t* lane_qangle[kMaxLanes] = {};
+    int64_t lane_cap_px[kMaxLanes] = {};
 };
 
 // The scratch (cell table, level image, gradients, blocks, hits) is rewritten by
@@ -981,6 +991,30 @@ static int prepare(tbdk_ctx* ctx, const uint8_t* img, int w, int h, int pitch, i
     return map_status(e);
 }
 
+// lanes 1..n-1 of a multi-level call: streams, events and level buffers for
+// images of up to px pixels
+static int reserve_lanes(HogScratch* S, int n, int64_t px)
+{
+    int rc = TBDK_OK;
+    if (!S->fork && hipEventCreateWithFlags(&S->fork, hipEventDisableTiming) != hipSuccess) return TBDK_EHIP;
+    for (int k = 1; k < n; ++k) {
+        if (!S->lane_stream[k] && hipStreamCreateWithFlags(&S->lane_stream[k], hipStreamNonBlocking) != hipSuccess)
+            return TBDK_EHIP;
+        if (!S->join[k] && hipEventCreateWithFlags(&S->join[k], hipEventDisableTiming) != hipSuccess)
+            return TBDK_EHIP;
+    }
+    for (int k = 1; k < n; ++k) {
+        if (px <= S->lane_cap_px[k]) continue;
+        int64_t c0 = 0, c1 = 0, c2 = 0;
+        S->lane_cap_px[k] = 0;
+        if ((rc = grow(&S->lane_level[k], c0, px * 4)) || (rc = grow(&S->lane_grad[k], c1, px * 2)) ||
+            (rc = grow(&S->lane_qangle[k], c2, px * 2)))
+            return rc;
+        S->lane_cap_px[k] = px;
+    }
+    return TBDK_OK;
+}
+
 struct Hit {
     int level, x, y;
     double score;
@@ -1022,6 +1056,13 @@ void tbdk::hog_release(tbdk_ctx* ctx)
                     (void*)S->cells, (void*)S->hits, (void*)S->scores, (void*)S->mblocks,
                     (void*)S->lvtab})
         if (p) (void)hipFree(p);
+    for (int k = 1; k < HogScratch::kMaxLanes; ++k) {
+        for (void* p : {(void*)S->lane_level[k], (void*)S->lane_grad[k], (void*)S->lane_qangle[k]})
+            if (p) (void)hipFree(p);
+        if (S->lane_stream[k]) (void)hipStreamDestroy(S->lane_stream[k]);
+        if (S->join[k]) (void)hipEventDestroy(S->join[k]);
+    }
+    if (S->fork) (void)hipEventDestroy(S->fork);
     delete S;
     ctx->hog = nullptr;
 }
@@ -1196,30 +1237,48 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
     hipError_t e = ents.empty() ? hipSuccess
                                 : hipMemcpyAsync(S->lvtab, ents.data(), sizeof(HogLevelEnt) * ents.size(),
                                                  hipMemcpyHostToDevice, s);
+    // the levels' chains are independent until the window pass: spread them
+    // over lanes (streams) so the latency-bound launches of several levels overlap
+    const int nlanes = std::max(1, std::min<int>(ctx->opt_hog_level_streams, (int)ents.size()));
+    if (nlanes > 1) {
+        if ((rc = reserve_lanes(S, nlanes, (int64_t)width * height)) != TBDK_OK) return rc;
+        if (e == hipSuccess) e = hipEventRecord(S->fork, s);
+        for (int k = 1; k < nlanes && e == hipSuccess; ++k) e = hipStreamWaitEvent(S->lane_stream[k], S->fork, 0);
+    }
     for (size_t k = 0; k < ents.size() && e == hipSuccess; ++k) {
         const HogLevelEnt& en = ents[k];
+        const int ln = (int)(k % nlanes);
+        hipStream_t ls = ln ? S->lane_stream[ln] : s;
+        uint8_t* lvl = ln ? S->lane_level[ln] : S->level;
+        float* grd = ln ? S->lane_grad[ln] : S->grad;
+        uint8_t* qa = ln ? S->lane_qangle[ln] : S->qangle;
         const int sw = en.gpitch / 2, sh = cv_round_d(height / lv[en.level]);
         const uint8_t* li = img;
         int lp = pitch;
         if (sw != width || sh != height) {
             const ExactAxis ax = exact_axis(width, sw), ay = exact_axis(height, sh);
-            const int rec = timing_begin(ctx, "hog_resize", s);
-            hipLaunchKernelGGL(hog_resize_kernel, dim3((sw + 255) / 256, sh), dim3(256), 0, s, img, width, height,
-                               pitch, cn, S->level, sw, sh, sw * cn, ax, ay);
-            timing_end(ctx, rec, s);
+            const int rec = timing_begin(ctx, "hog_resize", ls);
+            hipLaunchKernelGGL(hog_resize_kernel, dim3((sw + 255) / 256, sh), dim3(256), 0, ls, img, width, height,
+                               pitch, cn, lvl, sw, sh, sw * cn, ax, ay);
+            timing_end(ctx, rec, ls);
             e = hipGetLastError();
-            li = S->level;
+            li = lvl;
             lp = sw * cn;
         }
         if (e != hipSuccess) break;
-        int rec = timing_begin(ctx, "hog_grad", s);
-        e = launch_grad(li, sw, sh, lp, cn, params, S->grad, en.gpitch, S->qangle, en.qpitch, s);
-        timing_end(ctx, rec, s);
+        int rec = timing_begin(ctx, "hog_grad", ls);
+        e = launch_grad(li, sw, sh, lp, cn, params, grd, en.gpitch, qa, en.qpitch, ls);
+        timing_end(ctx, rec, ls);
         if (e != hipSuccess) break;
-        rec = timing_begin(ctx, "hog_block", s);
-        e = launch_blocks(S, pl, params, S->grad, en.gpitch, S->qangle, en.qpitch, en.nbx, en.nby,
-                          S->mblocks + en.boff, s);
-        timing_end(ctx, rec, s);
+        rec = timing_begin(ctx, "hog_block", ls);
+        e = launch_blocks(S, pl, params, grd, en.gpitch, qa, en.qpitch, en.nbx, en.nby, S->mblocks + en.boff, ls);
+        timing_end(ctx, rec, ls);
+    }
+    // join every lane (also on failure: later calls order behind `s` only)
+    for (int k = 1; k < nlanes; ++k) {
+        hipError_t j = hipEventRecord(S->join[k], S->lane_stream[k]);
+        if (j == hipSuccess) j = hipStreamWaitEvent(s, S->join[k], 0);
+        if (e == hipSuccess) e = j;
     }
     if (e == hipSuccess && !ents.empty()) {
         {

@@ -128,6 +128,26 @@ def test_detect_multiscale_equals_oracle(gpu, win, cn, hit, group):
     assert got == exp
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_detect_multiscale_level_streams_equal(gpu, lanes):
+    """ctx option hog_level_streams: the levels' chains on 1..3 streams give the
+    default (4 streams) result, here on frames of two sizes back to back"""
+    hg = _hog(gpu, (48, 96))
+    hg.setNumLevels(15)
+    hg.setHitThreshold(-0.5)
+    imgs = [torch.from_numpy(_bgr(31, 640, 360, cn=4)).cuda(), torch.from_numpy(_bgr(32, 800, 450, cn=4)).cuda()]
+    ref = [hg.detectMultiScale(im, confidences=True) for im in imgs]
+    assert sum(len(r[0]) for r in ref) > 0
+    try:
+        gpu.set_option("hog_level_streams", lanes)
+        got = [hg.detectMultiScale(im, confidences=True) for im in imgs]
+    finally:
+        gpu.set_option("hog_level_streams", 4)
+    assert got == ref
+    with pytest.raises(Exception):
+        gpu.set_option("hog_level_streams", 5)
+
+
 def test_rejects_bad_arguments(gpu):
     from opencv_amd import _lib, hog
 
