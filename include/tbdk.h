@@ -98,7 +98,11 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *   "hog_level_streams" (1..4, default 4): tbdk_hog_detect_multiscale runs
  *       the levels' resize/gradient/block chains on this many streams (the
  *       caller's and internal ones, joined back before the window pass;
- *       results equal). */
+ *       results equal).
+ *   "fb_prep_ahead" (0/1, default 1): tbdk_farneback computes every level's
+ *       images and polynomial expansions on an internal stream, coarse to
+ *       fine, while the coarser levels iterate on the caller's stream
+ *       (results equal). */
 int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
 /*   "tbd_early_gftt" (0/1/2, default 2): the TBD loop runs GFTT over the
  *       detections that will start new tracks at the start of the step, off

@@ -56,6 +56,13 @@ struct FbScratch {
     float* I = nullptr;   // level image
     int64_t cap_px = 0;   // floats per plane
     int64_t cap_T = 0;
+    // prep-ahead (ctx option fb_prep_ahead): every level's R0 / R1 in its own
+    // region of Rl, computed on the prep stream while coarser levels iterate
+    float* Rl = nullptr;
+    int64_t cap_Rl = 0;
+    hipStream_t prep = nullptr;
+    hipEvent_t fork = nullptr;
+    hipEvent_t lev_ev[64] = {};
 };
 
 namespace {
@@ -1136,6 +1143,24 @@ struct FbLevel {
     double sigma;
 };
 
+// the prep stream, its events and the per-level R planes (rfloats in all)
+int fb_reserve_ahead(FbScratch* f, int64_t rfloats, int nlev)
+{
+    if (!f->prep && hipStreamCreateWithFlags(&f->prep, hipStreamNonBlocking) != hipSuccess) return TBDK_EHIP;
+    if (!f->fork && hipEventCreateWithFlags(&f->fork, hipEventDisableTiming) != hipSuccess) return TBDK_EHIP;
+    for (int k = 0; k < nlev; ++k)
+        if (!f->lev_ev[k] && hipEventCreateWithFlags(&f->lev_ev[k], hipEventDisableTiming) != hipSuccess)
+            return TBDK_EHIP;
+    if (rfloats > f->cap_Rl) {
+        (void)hipFree(f->Rl);
+        f->Rl = nullptr;
+        f->cap_Rl = 0;
+        if (hipMalloc(&f->Rl, sizeof(float) * (size_t)rfloats) != hipSuccess) return TBDK_ENOMEM;
+        f->cap_Rl = rfloats;
+    }
+    return TBDK_OK;
+}
+
 int fb_check(const tbdk_farneback_params* p)
 {
     if (!p) return TBDK_EINVAL;
@@ -1155,6 +1180,11 @@ void fb_release(tbdk_ctx* ctx)
     if (!ctx || !ctx->fb) return;
     (void)hipFree(ctx->fb->R0);
     (void)hipFree(ctx->fb->T);
+    if (ctx->fb->Rl) (void)hipFree(ctx->fb->Rl);
+    if (ctx->fb->prep) (void)hipStreamDestroy(ctx->fb->prep);
+    if (ctx->fb->fork) (void)hipEventDestroy(ctx->fb->fork);
+    for (hipEvent_t ev : ctx->fb->lev_ev)
+        if (ev) (void)hipEventDestroy(ev);
     delete ctx->fb;
     ctx->fb = nullptr;
 }
@@ -1246,23 +1276,52 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
     const int round_wgs = cus * fb_iter_occupancy(m, gauss);  // one round of resident fb_iter workgroups
     const int iter_wgs = round_wgs * ((3 * cus + round_wgs - 1) / round_wgs);
     hipError_t e = hipSuccess;
+    // level images and polynomial expansion of both frames (the flow does not
+    // enter them): with prep-ahead every level's R0 / R1 is its own region,
+    // computed on the prep stream coarse to fine while the coarser levels iterate
+    const bool ahead = ctx->opt_fb_prep_ahead && levels > 0;
+    int64_t roff[64];
+    int64_t rtot = 0;
+    for (int k = 0; k <= levels; ++k) {
+        roff[k] = rtot;
+        rtot += 10 * plane_stride(plane_pitch(lv[k].w), lv[k].h);
+    }
+    if (ahead) {
+        if ((rc = fb_reserve_ahead(f, rtot, levels + 1)) != TBDK_OK) return rc;
+        e = hipEventRecord(f->fork, s);  // the previous call's readers of Rl, T, I are done
+        if (e == hipSuccess) e = hipStreamWaitEvent(f->prep, f->fork, 0);
+    }
+    auto prep_level = [&](int k, hipStream_t ps, float* R0, float* R1) {
+        const int w = lv[k].w, h = lv[k].h, pp = plane_pitch(w);
+        const int64_t plane = plane_stride(pp, h);
+        LevelImagePlan pl;
+        plan_level_image(width, height, w, h, lv[k].ks, lv[k].sigma, &pl);
+        const int tpitch = plane_pitch(pl.nc);
+        hipError_t r = hipSuccess;
+        for (int i = 0; i < 2 && r == hipSuccess; ++i) {
+            int rec = timing_begin(ctx, "fb_pyr", ps);
+            r = launch_level_image(pl, i ? next : prev, width, height, pitch, f->T, tpitch, f->I, w, h, pp, ps);
+            timing_end(ctx, rec, ps);
+            if (r != hipSuccess) break;
+            rec = timing_begin(ctx, "fb_polyexp", ps);
+            r = launch_polyexp(f->I, w, h, pp, i ? R1 : R0, pp, plane, p->poly_n, p->poly_sigma, ps);
+            timing_end(ctx, rec, ps);
+        }
+        return r;
+    };
+    for (int k = levels; ahead && k >= 0 && e == hipSuccess; --k) {
+        const int64_t plane = plane_stride(plane_pitch(lv[k].w), lv[k].h);
+        e = prep_level(k, f->prep, f->Rl + roff[k], f->Rl + roff[k] + 5 * plane);
+        if (e == hipSuccess) e = hipEventRecord(f->lev_ev[k], f->prep);
+    }
     int cur = 0;  // ping-pong index of the current flow
     int pw = 0, ph = 0, ppitch = 0;
     for (int k = levels; k >= 0 && e == hipSuccess; --k) {
         const int w = lv[k].w, h = lv[k].h, pp = plane_pitch(w);
         const int64_t plane = plane_stride(pp, h);
-        // level images and polynomial expansion of both frames
-        plan_level_image(width, height, w, h, lv[k].ks, lv[k].sigma, &plan);
-        const int tpitch = plane_pitch(plan.nc);
-        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-            int rec = timing_begin(ctx, "fb_pyr", s);
-            e = launch_level_image(plan, i ? next : prev, width, height, pitch, f->T, tpitch, f->I, w, h, pp, s);
-            timing_end(ctx, rec, s);
-            if (e != hipSuccess) break;
-            rec = timing_begin(ctx, "fb_polyexp", s);
-            e = launch_polyexp(f->I, w, h, pp, i ? f->R1 : f->R0, pp, plane, p->poly_n, p->poly_sigma, s);
-            timing_end(ctx, rec, s);
-        }
+        float* R0 = ahead ? f->Rl + roff[k] : f->R0;
+        float* R1 = ahead ? R0 + 5 * plane : f->R1;
+        e = ahead ? hipStreamWaitEvent(s, f->lev_ev[k], 0) : prep_level(k, s, R0, R1);
         if (e != hipSuccess) break;
         // initial flow of the level
         int rec = timing_begin(ctx, "fb_flow_init", s);
@@ -1316,8 +1375,8 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
         if (e != hipSuccess) break;
         // iterations
         FbIterArgs a;
-        a.R0 = f->R0;
-        a.R1 = f->R1;
+        a.R0 = R0;
+        a.R1 = R1;
         a.w = w;
         a.h = h;
         a.pitch = pp;

@@ -140,6 +140,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_zero_copy = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "fb_prep_ahead") == 0) {
+        ctx->opt_fb_prep_ahead = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "hog_level_streams") == 0) {
         if (value < 1 || value > 4) return TBDK_EINVAL;
         ctx->opt_hog_level_streams = (int)value;

@@ -127,6 +127,26 @@ def test_odd_sizes_and_iterations(gpu, w, h):
             assert np.array_equal(got, ref), (iters, flags)
 
 
+def test_prep_ahead_equal(gpu):
+    """ctx option fb_prep_ahead: the level preps on the side stream (default) and inline
+    give identical flows, at two sizes back to back (the per-level regions and events
+    are reused) and for one level (no side stream)"""
+    runs = []
+    for ahead in (1, 0):
+        gpu.set_option("fb_prep_ahead", ahead)
+        try:
+            out = []
+            for (w, h), kw in (((641, 359), {}), ((333, 250), dict(flags=O.FARNEBACK_GAUSSIAN)),
+                               ((200, 120), dict(numLevels=0))):
+                a, b = _frames(w * h, w, h, nobj=3)
+                out.append(_gpu_flow(gpu, a, b, **kw))
+            runs.append(out)
+        finally:
+            gpu.set_option("fb_prep_ahead", 1)
+    for x, y in zip(*runs):
+        assert np.array_equal(x, y)
+
+
 def test_1080p_translation(gpu):
     """Full-size known motion: a 1080p synthetic frame shifted by (5, -3)."""
     fr, _ = O.synth(20261015, 1920, 1080, 24, 0, 1)

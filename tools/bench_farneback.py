@@ -39,8 +39,10 @@ def main():
     ap.add_argument("--pairs", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--prep-ahead", type=int, default=1, help="ctx option fb_prep_ahead")
     a = ap.parse_args()
     ctx = Context.get(0)
+    ctx.set_option("fb_prep_ahead", a.prep_ahead)
     frames = render(ctx, a.width, a.height, a.objects, a.pairs + 1)
     fb = F.FarnebackOpticalFlow.create(flags=a.flags, ctx=ctx)
     flow = torch.empty((a.height, a.width, 2), dtype=torch.float32, device="cuda")
