@@ -95,7 +95,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       9-bin geometries by the LDS-tiled kernel, its histograms in LDS (1)
  *       or in registers (2); 0 forces the per-cell kernel of every other
  *       geometry (results equal).
- *   "hog_level_streams" (1..4, default 4): tbdk_hog_detect_multiscale runs
+ *   "hog_level_streams" (1..4, default 3): tbdk_hog_detect_multiscale runs
  *       the levels' resize/gradient/block chains on this many streams (the
  *       caller's and internal ones, joined back before the window pass;
  *       results equal).

@@ -128,10 +128,10 @@ def test_detect_multiscale_equals_oracle(gpu, win, cn, hit, group):
     assert got == exp
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 3])
+@pytest.mark.parametrize("lanes", [1, 2, 4])
 def test_detect_multiscale_level_streams_equal(gpu, lanes):
-    """ctx option hog_level_streams: the levels' chains on 1..3 streams give the
-    default (4 streams) result, here on frames of two sizes back to back"""
+    """ctx option hog_level_streams: the levels' chains on 1, 2 or 4 streams give the
+    default (3 streams) result, here on frames of two sizes back to back"""
     hg = _hog(gpu, (48, 96))
     hg.setNumLevels(15)
     hg.setHitThreshold(-0.5)
@@ -142,7 +142,7 @@ def test_detect_multiscale_level_streams_equal(gpu, lanes):
         gpu.set_option("hog_level_streams", lanes)
         got = [hg.detectMultiScale(im, confidences=True) for im in imgs]
     finally:
-        gpu.set_option("hog_level_streams", 4)
+        gpu.set_option("hog_level_streams", 3)
     assert got == ref
     with pytest.raises(Exception):
         gpu.set_option("hog_level_streams", 5)
