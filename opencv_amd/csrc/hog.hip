@@ -1010,11 +1010,9 @@ static int prepare(tbdk_ctx* ctx, const uint8_t* img, int w, int h, int pitch, i
     return map_status(e);
 }
 
-// lanes 1..n-1 of a multi-level call: streams, events and level buffers for
-// images of up to px pixels
-static int reserve_lanes(HogScratch* S, int n, int64_t px)
+// the lanes' streams and events (1..n-1)
+static int create_lanes(HogScratch* S, int n)
 {
-    int rc = TBDK_OK;
     if (!S->fork && hipEventCreateWithFlags(&S->fork, hipEventDisableTiming) != hipSuccess) return TBDK_EHIP;
     for (int k = 1; k < n; ++k) {
         if (!S->lane_stream[k] && hipStreamCreateWithFlags(&S->lane_stream[k], hipStreamNonBlocking) != hipSuccess)
@@ -1022,6 +1020,15 @@ static int reserve_lanes(HogScratch* S, int n, int64_t px)
         if (!S->join[k] && hipEventCreateWithFlags(&S->join[k], hipEventDisableTiming) != hipSuccess)
             return TBDK_EHIP;
     }
+    return TBDK_OK;
+}
+
+// lanes 1..n-1 of a multi-level call: streams, events and level buffers for
+// images of up to px pixels
+static int reserve_lanes(HogScratch* S, int n, int64_t px)
+{
+    int rc = create_lanes(S, n);
+    if (rc != TBDK_OK) return rc;
     for (int k = 1; k < n; ++k) {
         if (px <= S->lane_cap_px[k]) continue;
         int64_t c0 = 0, c1 = 0, c2 = 0;
@@ -1066,6 +1073,17 @@ static int fetch_hits(HogScratch* S, int64_t cap, std::vector<Hit>& out, hipStre
 }  // namespace tbdk
 
 using namespace tbdk;
+
+// Called by tbdk_ctx_create: the lanes' streams exist before any stream the
+// caller creates afterwards.  HIP maps streams onto a few hardware queues in
+// creation order; lanes created after, e.g., a TBD loop's four streams shared
+// queues with the caller's stream and overlapped nothing (1080p HOG 780 instead
+// of 1130 frames/s, tools/probe_hog_after_loop.py).
+void tbdk::hog_create_lanes(tbdk_ctx* ctx)
+{
+    if (!ctx->hog) ctx->hog = new (std::nothrow) HogScratch();
+    if (ctx->hog) (void)create_lanes(ctx->hog, std::min(ctx->opt_hog_level_streams, HogScratch::kMaxLanes));
+}
 
 void tbdk::hog_release(tbdk_ctx* ctx)
 {

@@ -78,6 +78,14 @@ int tbdk_ctx_create(int device, tbdk_ctx** out)
     tbdk_ctx* c = new (std::nothrow) tbdk_ctx();
     if (!c) return TBDK_ENOMEM;
     c->device = device;
+    {
+        DeviceGuard g(device);
+        // best effort, side streams first (HOG and Farneback create what is missing
+        // on first use): Farneback's prep stream, then the default HOG lanes, so
+        // that with 4 hardware queues neither shares one with the caller's stream
+        fb_create_streams(c);
+        hog_create_lanes(c);
+    }
     *out = c;
     return TBDK_OK;
 }

@@ -98,6 +98,8 @@ void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s);
 // frees the context's Farneback scratch (farneback.hip)
 void fb_release(tbdk_ctx* ctx);
 void hog_release(tbdk_ctx* ctx);
+void hog_create_lanes(tbdk_ctx* ctx);
+void fb_create_streams(tbdk_ctx* ctx);
 
 // ---- kernels (klt_pyr.hip) ----
 hipError_t launch_pad_copy(const uint8_t* src, int spitch, const tbdk_level& dst, hipStream_t s);
