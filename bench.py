@@ -396,7 +396,7 @@ def main():
     ap.add_argument("--no-hog", action="store_true", help="skip the secondary HOG detector measurement")
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
-    ap.add_argument("--hog-frames", type=int, default=10)
+    ap.add_argument("--hog-frames", type=int, default=60)
     args = ap.parse_args()
 
     import numpy as np
