@@ -57,6 +57,10 @@ struct HogScratch {
     hipStream_t stream = nullptr;  // stream of the last call that used this scratch
     bool used = false;
     int block_tiled = 1;  // tbdk_ctx_set_option("hog_block_tiled"), copied by reserve()
+    // host copies of what `cells` and `svm` hold (empty: unknown), so repeated
+    // calls with the same detector skip the uploads and their stream sync
+    std::vector<int4> cells_host;
+    std::vector<float> svm_host;
     // detectMultiScale's level lanes: level k's resize -> gradient -> block
     // chain runs on lane k % nlanes; lane 0 is the caller's stream with the
     // buffers above, lanes 1.. own a stream and a level image / gradient set
@@ -758,13 +762,21 @@ static void make_plan(const tbdk_hog_params* p, HogPlan& pl)
     for (auto& l : pl.lists) pl.cell_cap = std::max(pl.cell_cap, (int)l.size());
 }
 
+static bool same_int4(const std::vector<int4>& a, const std::vector<int4>& b)
+{
+    return a.size() == b.size() && std::memcmp(a.data(), b.data(), sizeof(int4) * a.size()) == 0;
+}
+
 static hipError_t upload_plan(HogScratch* S, const HogPlan& pl, hipStream_t s)
 {
     std::vector<int4> flat((size_t)pl.ncells * pl.cell_cap, make_int4(0, 0, 0, 0));
     for (int c = 0; c < pl.ncells; ++c)
         std::copy(pl.lists[c].begin(), pl.lists[c].end(), flat.begin() + (size_t)c * pl.cell_cap);
+    if (same_int4(flat, S->cells_host)) return hipSuccess;
+    S->cells_host.clear();
     hipError_t e = hipMemcpyAsync(S->cells, flat.data(), sizeof(int4) * flat.size(), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);  // `flat` is pageable and local
+    if (e == hipSuccess) S->cells_host.swap(flat);
     return e;
 }
 
@@ -900,7 +912,9 @@ static int reserve(tbdk_ctx* ctx, int w, int h, int cn, const HogPlan& pl, int s
     }
     const int64_t nblk = ((int64_t)w / pl.csx + 1) * (h / pl.csy + 1) * pl.hsz;
     if ((rc = grow(&S->blocks, S->cap_blocks, nblk))) return rc;
+    if (svm_len > S->cap_svm) S->svm_host.clear();  // reallocated below: contents unknown
     if ((rc = grow(&S->svm, S->cap_svm, svm_len))) return rc;
+    if ((int64_t)pl.ncells * pl.cell_cap > S->cap_cells) S->cells_host.clear();
     if ((rc = grow(&S->cells, S->cap_cells, (int64_t)pl.ncells * pl.cell_cap))) return rc;
     if (hit_cap > S->cap_hits) {
         int64_t c = 0;
@@ -1004,7 +1018,13 @@ static int prepare(tbdk_ctx* ctx, const uint8_t* img, int w, int h, int pitch, i
     rc = reserve(ctx, w, h, cn, pl, svm_len, hit_cap, s);
     if (rc != TBDK_OK) return rc;
     HogScratch* S = ctx->hog;
-    hipError_t e = hipMemcpyAsync(S->svm, svm, sizeof(float) * svm_len, hipMemcpyHostToDevice, s);
+    hipError_t e = hipSuccess;
+    if (S->svm_host.size() != (size_t)svm_len || std::memcmp(S->svm_host.data(), svm, sizeof(float) * svm_len) != 0) {
+        S->svm_host.clear();
+        e = hipMemcpyAsync(S->svm, svm, sizeof(float) * svm_len, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // `svm` is the caller's pageable memory
+        if (e == hipSuccess) S->svm_host.assign(svm, svm + svm_len);
+    }
     if (e == hipSuccess) e = upload_plan(S, pl, s);
     if (e == hipSuccess) e = hipMemsetAsync(S->hits, 0, sizeof(int), s);
     return map_status(e);

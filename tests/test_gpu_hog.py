@@ -128,6 +128,22 @@ def test_detect_multiscale_equals_oracle(gpu, win, cn, hit, group):
     assert got == exp
 
 
+def test_detector_change_between_calls(gpu):
+    """The detector and the cell plan are uploaded only when they change (host copies
+    compared): a new detector of the same size, then the old one again, each equal to
+    the oracle's scores"""
+    img = _bgr(5, 320, 240, cn=3)
+    hg = _hog(gpu)
+    hg.setHitThreshold(-1e9)
+    d0 = list(hg.svm)
+    d1 = [v * 0.5 for v in d0]
+    for d in (d0, d1, d0):
+        hg.setSVMDetector(d)
+        xy, sc = hg.detect(torch.from_numpy(img).cuda(), confidences=True)
+        oxy, osc = O.hog_detect(img, _prm(hg), hg.svm, hit_threshold=-1e9)
+        assert np.array_equal(np.array(xy), oxy) and np.array_equal(np.array(sc), osc)
+
+
 @pytest.mark.parametrize("lanes", [1, 2, 4])
 def test_detect_multiscale_level_streams_equal(gpu, lanes):
     """ctx option hog_level_streams: the levels' chains on 1, 2 or 4 streams give the
