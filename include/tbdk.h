@@ -99,6 +99,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       the levels' resize/gradient/block chains on this many streams (the
  *       caller's and internal ones, joined back before the window pass;
  *       results equal).
+ *   "hog_window_tiled" (0/1, default 1): tbdk_hog_detect_multiscale's window
+ *       pass stages each row of 16 windows' blocks and the detector in LDS
+ *       (36-float blocks); 0 reads them per window from L2 (results equal).
  *   "fb_prep_ahead" (0/1, default 1): tbdk_farneback computes every level's
  *       images and polynomial expansions on an internal stream, coarse to
  *       fine, while the coarser levels iterate on the caller's stream

@@ -591,6 +591,82 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
     }
 }
 
+// Batched window pass over 36-float blocks, one row of kHogWinTile windows per
+// workgroup: the blocks those windows share (their union: 20 x 11 at the
+// defaults instead of 16 x 55 block reads) and the detector are staged in LDS
+// once, coalesced; each wave then scores every fourth window exactly as
+// hog_window_kernel does (same products, sums and order).
+constexpr int kHogWinTile = 16;
+
+struct HogWinTile {
+    int cols, rows;        // staged block columns / rows (full tile)
+    int cstep, rstep;      // window step in block columns / rows (win stride / cell grid)
+    int bstepx, bstepy;    // block step inside a window (block stride / cell grid)
+    int off_svm, off_d;    // float offsets of the staged detector and the per-wave doubles
+};
+
+__global__ __launch_bounds__(256) void hog_window_tile_kernel(HogWinArgs a, HogWinTile t)
+{
+    extern __shared__ float wt[];
+    float4* B4 = reinterpret_cast<float4*>(wt);
+    float4* S4 = reinterpret_cast<float4*>(wt + t.off_svm);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const HogLevelEnt& e = a.lv[hog_level_of(a.lv, a.nlv, blockIdx.x)];
+    const int wg = blockIdx.x - e.w0, nwx = e.nwx, nbx = e.nbx;
+    const float* blocks = a.blocks + e.boff;
+    const int per_row = (nwx + kHogWinTile - 1) / kHogWinTile;
+    const int wy = wg / per_row, wx0 = (wg - wy * per_row) * kHogWinTile;
+    const int nwin = min(kHogWinTile, nwx - wx0);
+    const int bc0 = wx0 * t.cstep, br0 = wy * t.rstep;
+    const int cols = (nwin - 1) * t.cstep + (a.wbx - 1) * t.bstepx + 1;
+    const int nblk = a.wbx * a.wby;
+    for (int idx = tid; idx < t.rows * cols * 9; idx += 256) {
+        const int r = idx / (cols * 9), rem = idx - r * cols * 9, c = rem / 9, q = rem - c * 9;
+        B4[(r * t.cols + c) * 9 + q] =
+            reinterpret_cast<const float4*>(blocks + ((size_t)(br0 + r) * nbx + bc0 + c) * 36)[q];
+    }
+    for (int idx = tid; idx < nblk * 9; idx += 256) S4[idx] = reinterpret_cast<const float4*>(a.svm)[idx];
+    double* main_v = reinterpret_cast<double*>(wt + t.off_d) + wave * nblk;
+    for (int w0 = 0; w0 < nwin; w0 += 4) {
+        __syncthreads();  // staging done / the previous round's sums read
+        const int w = w0 + wave;
+        if (w < nwin)
+            for (int k = lane; k < nblk; k += 64) {
+                const int j = k / a.wby, i = k - j * a.wby;
+                const float4* v4 = B4 + ((i * t.bstepy) * t.cols + w * t.cstep + j * t.bstepx) * 9;
+                const float4* s4 = S4 + k * 9;
+                float4 x[9], y[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) x[q] = v4[q], y[q] = s4[q];
+                float ps[4];
+                ps[0] = y[0].x * x[0].x, ps[1] = y[0].y * x[0].y, ps[2] = y[0].z * x[0].z, ps[3] = y[0].w * x[0].w;
+#pragma unroll
+                for (int q = 1; q < 9; ++q) {
+                    ps[0] = ps[0] + x[q].x * y[q].x;
+                    ps[1] = ps[1] + x[q].y * y[q].y;
+                    ps[2] = ps[2] + x[q].z * y[q].z;
+                    ps[3] = ps[3] + x[q].w * y[q].w;
+                }
+                const double t0 = ps[0] + ps[1], t1 = ps[2] + ps[3];
+                main_v[k] = t0 + t1;
+            }
+        __syncthreads();
+        if (w < nwin && lane == 0) {
+            double sc = a.rho;
+            for (int k = 0; k < nblk; ++k) sc += main_v[k];
+            if (sc >= a.hit) {
+                const int slot = atomicAdd(a.hits, 1);
+                if (slot < a.cap) {
+                    a.hits[1 + 3 * slot] = e.level;
+                    a.hits[2 + 3 * slot] = (wx0 + w) * a.wsx;
+                    a.hits[3 + 3 * slot] = wy * a.wsy;
+                    a.scores[slot] = sc;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 
@@ -1268,6 +1344,21 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
     if (rc != TBDK_OK) return rc;
     HogScratch* S = ctx->hog;
     const double rho = svm_len > pl.dsize ? svm[pl.dsize] : 0;
+    // the window pass: tiled (blocks and detector staged in LDS) for 36-float
+    // blocks when the tile fits, else one wave per window from L2
+    HogWinTile wtile{};
+    size_t wtile_lds = 0;
+    bool win_tiled = false;
+    if (ctx->opt_hog_window_tiled && pl.hsz == 36) {
+        wtile.cstep = params->win_stride_x / pl.csx, wtile.rstep = params->win_stride_y / pl.csy;
+        wtile.bstepx = params->block_stride_x / pl.csx, wtile.bstepy = params->block_stride_y / pl.csy;
+        wtile.cols = (kHogWinTile - 1) * wtile.cstep + (pl.wbx - 1) * wtile.bstepx + 1;
+        wtile.rows = (pl.wby - 1) * wtile.bstepy + 1;
+        wtile.off_svm = wtile.rows * wtile.cols * 36;
+        wtile.off_d = (wtile.off_svm + pl.wbx * pl.wby * 36 + 1) & ~1;
+        wtile_lds = sizeof(float) * ((size_t)wtile.off_d + 2 * 4 * (size_t)(pl.wbx * pl.wby));
+        win_tiled = wtile_lds <= 64 * 1024;
+    }
     // every level's blocks get their own region of one buffer, so the window
     // pass runs once over all levels (small levels alone fill a fraction of the
     // device; batching the block pass as well measured 14 % slower for it)
@@ -1286,7 +1377,8 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
         en.level = l, en.w0 = nwwg;
         ents.push_back(en);
         boff += (int64_t)en.nbx * en.nby * pl.hsz;
-        nwwg += (en.nwx * en.nwy + kHogWinPerWg - 1) / kHogWinPerWg;
+        nwwg += win_tiled ? en.nwy * ((en.nwx + kHogWinTile - 1) / kHogWinTile)
+                          : (en.nwx * en.nwy + kHogWinPerWg - 1) / kHogWinPerWg;
     }
     if ((rc = grow(&S->mblocks, S->cap_mblocks, std::max<int64_t>(boff, 1))) ||
         (rc = grow(&S->lvtab, S->cap_lvtab, std::max<int64_t>((int64_t)ents.size(), 1))))
@@ -1349,8 +1441,12 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
             w.hits = S->hits, w.scores = S->scores, w.cap = (int)cap;
             w.lv = S->lvtab, w.nlv = (int)ents.size();
             const int rec = timing_begin(ctx, "hog_window", s);
-            const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);
-            hipLaunchKernelGGL(hog_window_kernel, dim3(nwwg), dim3(256), lds, s, w);
+            if (win_tiled) {
+                hipLaunchKernelGGL(hog_window_tile_kernel, dim3(nwwg), dim3(256), wtile_lds, s, w, wtile);
+            } else {
+                const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);
+                hipLaunchKernelGGL(hog_window_kernel, dim3(nwwg), dim3(256), lds, s, w);
+            }
             timing_end(ctx, rec, s);
             e = hipGetLastError();
         }

@@ -157,6 +157,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_hog_level_streams = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "hog_window_tiled") == 0) {
+        ctx->opt_hog_window_tiled = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "hog_block_tiled") == 0) {
         if (value < 0 || value > 2) return TBDK_EINVAL;
         ctx->opt_hog_block_tiled = (int)value;

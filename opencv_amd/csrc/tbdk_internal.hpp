@@ -73,6 +73,7 @@ struct tbdk_ctx {
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     int opt_fb_prep_ahead = 1;  // tbdk_ctx_set_option("fb_prep_ahead"): Farneback level prep on a side stream
     int opt_hog_level_streams = 3;  // tbdk_ctx_set_option("hog_level_streams"): lanes of detectMultiScale
+    int opt_hog_window_tiled = 1;  // tbdk_ctx_set_option("hog_window_tiled"): LDS-tiled window pass
     int opt_hog_block_tiled = 1;  // tbdk_ctx_set_option("hog_block_tiled"): LDS-tiled block kernel where it applies
     int opt_tbd_early_gftt = 2;  // tbdk_ctx_set_option("tbd_early_gftt")
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")

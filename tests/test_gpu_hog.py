@@ -164,6 +164,25 @@ def test_detect_multiscale_level_streams_equal(gpu, lanes):
         gpu.set_option("hog_level_streams", 5)
 
 
+@pytest.mark.parametrize("win", [(64, 128), (48, 96)])
+def test_window_pass_tiled_equals_per_window(gpu, win):
+    """ctx option hog_window_tiled: the LDS-tiled window pass (rows of 16 windows,
+    ragged last tiles) and the per-window pass give the same rects and weights"""
+    hg = _hog(gpu, win)
+    hg.setNumLevels(15)
+    hg.setHitThreshold(-1.5)
+    hg.setGroupThreshold(0)
+    im = torch.from_numpy(_bgr(41, 700, 420, cn=3)).cuda()
+    ref = hg.detectMultiScale(im, confidences=True)
+    assert len(ref[0]) > 0
+    try:
+        gpu.set_option("hog_window_tiled", 0)
+        got = hg.detectMultiScale(im, confidences=True)
+    finally:
+        gpu.set_option("hog_window_tiled", 1)
+    assert got == ref
+
+
 def test_rejects_bad_arguments(gpu):
     from opencv_amd import _lib, hog
 
