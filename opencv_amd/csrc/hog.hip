@@ -595,7 +595,8 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
 // workgroup: the blocks those windows share (their union: 20 x 11 at the
 // defaults instead of 16 x 55 block reads) and the detector are staged in LDS
 // once, coalesced; each wave then scores every fourth window exactly as
-// hog_window_kernel does (same products, sums and order).
+// hog_window_kernel does (same products, sums and order), one lane per window
+// for the serial sums.
 constexpr int kHogWinTile = 16;
 
 struct HogWinTile {
@@ -626,42 +627,46 @@ __global__ __launch_bounds__(256) void hog_window_tile_kernel(HogWinArgs a, HogW
             reinterpret_cast<const float4*>(blocks + ((size_t)(br0 + r) * nbx + bc0 + c) * 36)[q];
     }
     for (int idx = tid; idx < nblk * 9; idx += 256) S4[idx] = reinterpret_cast<const float4*>(a.svm)[idx];
-    double* main_v = reinterpret_cast<double*>(wt + t.off_d) + wave * nblk;
-    for (int w0 = 0; w0 < nwin; w0 += 4) {
-        __syncthreads();  // staging done / the previous round's sums read
-        const int w = w0 + wave;
-        if (w < nwin)
-            for (int k = lane; k < nblk; k += 64) {
-                const int j = k / a.wby, i = k - j * a.wby;
-                const float4* v4 = B4 + ((i * t.bstepy) * t.cols + w * t.cstep + j * t.bstepx) * 9;
-                const float4* s4 = S4 + k * 9;
-                float4 x[9], y[9];
+    // wave `wave` scores windows wave, wave + 4, ... (kHogWinTile / 4 rounds); the
+    // block terms of all its windows first, then one lane per window sums them
+    double* main_v = reinterpret_cast<double*>(wt + t.off_d) + wave * (kHogWinTile / 4) * nblk;
+    __syncthreads();  // staging done
+    for (int r = 0; r < kHogWinTile / 4; ++r) {
+        const int w = wave + 4 * r;
+        if (w >= nwin) break;
+        for (int k = lane; k < nblk; k += 64) {
+            const int j = k / a.wby, i = k - j * a.wby;
+            const float4* v4 = B4 + ((i * t.bstepy) * t.cols + w * t.cstep + j * t.bstepx) * 9;
+            const float4* s4 = S4 + k * 9;
+            float4 x[9], y[9];
 #pragma unroll
-                for (int q = 0; q < 9; ++q) x[q] = v4[q], y[q] = s4[q];
-                float ps[4];
-                ps[0] = y[0].x * x[0].x, ps[1] = y[0].y * x[0].y, ps[2] = y[0].z * x[0].z, ps[3] = y[0].w * x[0].w;
+            for (int q = 0; q < 9; ++q) x[q] = v4[q], y[q] = s4[q];
+            float ps[4];
+            ps[0] = y[0].x * x[0].x, ps[1] = y[0].y * x[0].y, ps[2] = y[0].z * x[0].z, ps[3] = y[0].w * x[0].w;
 #pragma unroll
-                for (int q = 1; q < 9; ++q) {
-                    ps[0] = ps[0] + x[q].x * y[q].x;
-                    ps[1] = ps[1] + x[q].y * y[q].y;
-                    ps[2] = ps[2] + x[q].z * y[q].z;
-                    ps[3] = ps[3] + x[q].w * y[q].w;
-                }
-                const double t0 = ps[0] + ps[1], t1 = ps[2] + ps[3];
-                main_v[k] = t0 + t1;
+            for (int q = 1; q < 9; ++q) {
+                ps[0] = ps[0] + x[q].x * y[q].x;
+                ps[1] = ps[1] + x[q].y * y[q].y;
+                ps[2] = ps[2] + x[q].z * y[q].z;
+                ps[3] = ps[3] + x[q].w * y[q].w;
             }
-        __syncthreads();
-        if (w < nwin && lane == 0) {
-            double sc = a.rho;
-            for (int k = 0; k < nblk; ++k) sc += main_v[k];
-            if (sc >= a.hit) {
-                const int slot = atomicAdd(a.hits, 1);
-                if (slot < a.cap) {
-                    a.hits[1 + 3 * slot] = e.level;
-                    a.hits[2 + 3 * slot] = (wx0 + w) * a.wsx;
-                    a.hits[3 + 3 * slot] = wy * a.wsy;
-                    a.scores[slot] = sc;
-                }
+            const double t0 = ps[0] + ps[1], t1 = ps[2] + ps[3];
+            main_v[r * nblk + k] = t0 + t1;
+        }
+    }
+    __syncthreads();
+    const int w = wave + 4 * lane;
+    if (lane < kHogWinTile / 4 && w < nwin) {
+        const double* m = main_v + lane * nblk;
+        double sc = a.rho;
+        for (int k = 0; k < nblk; ++k) sc += m[k];
+        if (sc >= a.hit) {
+            const int slot = atomicAdd(a.hits, 1);
+            if (slot < a.cap) {
+                a.hits[1 + 3 * slot] = e.level;
+                a.hits[2 + 3 * slot] = (wx0 + w) * a.wsx;
+                a.hits[3 + 3 * slot] = wy * a.wsy;
+                a.scores[slot] = sc;
             }
         }
     }
@@ -1356,7 +1361,7 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
         wtile.rows = (pl.wby - 1) * wtile.bstepy + 1;
         wtile.off_svm = wtile.rows * wtile.cols * 36;
         wtile.off_d = (wtile.off_svm + pl.wbx * pl.wby * 36 + 1) & ~1;
-        wtile_lds = sizeof(float) * ((size_t)wtile.off_d + 2 * 4 * (size_t)(pl.wbx * pl.wby));
+        wtile_lds = sizeof(float) * ((size_t)wtile.off_d + 2 * kHogWinTile * (size_t)(pl.wbx * pl.wby));
         win_tiled = wtile_lds <= 64 * 1024;
     }
     // every level's blocks get their own region of one buffer, so the window
