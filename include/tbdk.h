@@ -80,7 +80,11 @@ typedef struct tbdk_lk_params {
 
 /* ---- context ------------------------------------------------------------ */
 
-/* Creates a context bound to HIP device `device` (one per thread x device). */
+/* Creates a context bound to HIP device `device` (one per thread x device).
+ * It also creates the library's side streams (Farneback's level prep, the HOG
+ * level lanes): HIP maps streams onto a few hardware queues in creation order,
+ * so creating the context before the caller's own streams keeps those side
+ * streams off the caller's queue (HOG "Side streams"). */
 int tbdk_ctx_create(int device, tbdk_ctx** out);
 int tbdk_ctx_destroy(tbdk_ctx* ctx);
 /* Context options (test and tuning knobs; TBDK_EINVAL for unknown names):
