@@ -362,10 +362,10 @@ __global__ __launch_bounds__(256) void hog_block_kernel(HogBlockArgs a)
 // Tiled variant for 2x2-cell blocks with 9 bins (the detectors' geometry): a
 // workgroup owns 16 x 4 blocks and first stages their pixel footprint (gx, gy,
 // bins) and the four cells' pixData lists into LDS, coalesced, so no per-entry
-// load leaves the CU (lists read from L2 per entry group measured as slow as
-// the untiled kernel).  Each thread then sums its
-// cell's entries in pixData order, the reference's read-both-then-write update
-// (hog.cpp:909-911), into
+// load leaves the CU (with the lists read from L2 per entry group: 0.63 instead
+// of 0.50 ms per 1080p frame).  Each thread then sums its cell's entries in
+// pixData order, the reference's read-both-then-write update (hog.cpp:909-911),
+// into
 //   BINS_LDS = true:  its own histogram in LDS, bin-major (hs[bin * 256 + tid]),
 //                     so the lanes' data-dependent bins never share a bank;
 //   BINS_LDS = false: nine registers, every bin adding its entry term or +0.0f
