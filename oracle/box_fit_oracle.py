@@ -14,17 +14,21 @@ import numpy as np
 
 def rt_sums(a: np.ndarray, b: np.ndarray):
     """sa (4x4) and sb (4) of getRTMatrix (:1441-1461) for float32 pairs a -> b."""
-    a = np.asarray(a, np.float32)
-    b = np.asarray(b, np.float32)
-    s00 = s02 = s03 = b0 = b1 = b2 = b3 = 0.0
-    for (ax, ay), (bx, by) in zip(a, b):
-        s00 += float(np.float32(ax * ax) + np.float32(ay * ay))
-        s02 += float(ax)
-        s03 += float(ay)
-        b0 += float(np.float32(ax * bx) + np.float32(ay * by))
-        b1 += float(np.float32(ax * by) - np.float32(ay * bx))
-        b2 += float(bx)
-        b3 += float(by)
+    a = np.asarray(a, np.float32).reshape(-1, 2)
+    b = np.asarray(b, np.float32).reshape(-1, 2)
+    ax, ay, bx, by = a[:, 0], a[:, 1], b[:, 0], b[:, 1]
+
+    def seq(v):  # float terms promoted to double and added in point order (np.cumsum is sequential)
+        v = np.asarray(v).astype(np.float64)
+        return float(np.cumsum(v)[-1]) if len(v) else 0.0
+
+    # each product and the float add / subtract round to float32 (numpy applies
+    # one ufunc per operator, never a fused multiply-add)
+    s00 = seq(ax * ax + ay * ay)
+    s02, s03 = seq(ax), seq(ay)
+    b0 = seq(ax * bx + ay * by)
+    b1 = seq(ax * by - ay * bx)
+    b2, b3 = seq(bx), seq(by)
     n = float(len(a))
     sa = np.array([[s00, 0.0, s02, s03],
                    [0.0, s00, -s03, s02],
