@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """bench.py — tracked frames/sec of the 1080p x 128-object TBD loop on MI355X.
 
-Workload (BASELINE.json configs[2]): one synthetic 1920x1080 sequence of
-`warmup + steps` frames with 128 moving textured objects per GPU, rendered
-into HBM before timing (tbdk_synth_render).  A "step" is one frame through the
-full loop of libtbdk (tbdk_tbd_run over the timed frames: per frame the same
-work as tbdk_tbd_step, with the next frame's pyramid and tracker-independent
-PyrLK enqueued before the host tracker step): 3-level pyramid + Scharr planes, GFTT in
-the boxes of new / re-detect tracks, sparse PyrLK (win 21) over every track's
-corners, per-track similarity fit (KLT box propagation), and the native
-cv::tbd::Tracker step on the frame's ground-truth detections.
+Workload (BASELINE.json configs[2]): one synthetic 1920x1080 sequence of 500
+frames (or warmup + steps, if more) with 128 moving textured objects per GPU,
+rendered into HBM before timing (tbdk_synth_render).  A "step" is one frame
+through the full loop of libtbdk: frames [0, warmup) go through tbdk_tbd_step
+untimed, frames [warmup, warmup + steps) through tbdk_tbd_run (per frame the
+same work as tbdk_tbd_step, with the next frame's pyramid and the
+tracker-independent PyrLK enqueued before the host tracker step): 3-level
+pyramid + Scharr planes, GFTT in the boxes of new / re-detect tracks, sparse
+PyrLK (win 21) over every track's corners, per-track similarity fit (KLT box
+propagation), and the native cv::tbd::Tracker step on the frame's
+ground-truth detections.
+
+Secondary objects (never `value`): the whole sequence in steady state, median
+of 5 runs (`sequence`); the same frames uploaded from pinned host memory
+(`with_h2d`); KITTI-shaped configs[3] (`kitti`); per-frame API (`step_api`);
+dense Farneback and the fp16 pixel path (configs[4]); the HOG detector.
 
 Multi-GPU: one process per GPU (torchrun), one independent sequence per GPU
 (seed + rank), no data-path collective; value = frames of all ranks / max
@@ -89,42 +96,193 @@ def pmc_traffic(kernel_substr: str):
     return None, None
 
 
-def cpu_baseline(frames_host, gt, args, seconds: float):
-    """The oracle (CPU restatement of the reference path) running the same
-    per-frame KLT work: pyramid, GFTT in every box every `redetect` frames
-    (single-threaded, as the reference's goodFeaturesToTrack), multithreaded
-    LK over the tracked corners (the reference's parallel_for_ over points).
-    The host tracker step (~1 ms, identical code on both sides) is excluded."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import numpy as np
-    import _oracle as O
+# ---- host cores and rank pinning --------------------------------------------------------------
 
-    threads = min(16, os.cpu_count() or 1)
-    pts = None
-    prev = None
+
+def parse_cpulist(s: str) -> list:
+    out = []
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def host_cores():
+    """CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU
+    quota when one is set (the GPU box gives each GPU a share of a larger host)."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    n = len(aff) if quota is None else min(len(aff), quota)
+    return n, {"affinity_cpus": len(aff), "cgroup_cpu_quota": quota}
+
+
+def gpu_numa_cpus(local_rank: int):
+    """(numa node, cpus) of the host CPUs local to the local_rank-th visible GPU,
+    read from sysfs (KFD topology nodes, in HIP device order, and the GPU's PCI
+    device) without touching the GPU; None when the topology does not say."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        gpus = []
+        for n in sorted(os.listdir(root), key=int):
+            props = {}
+            for line in open(os.path.join(root, n, "properties")):
+                kv = line.split()
+                if len(kv) == 2:
+                    props[kv[0]] = int(kv[1])
+            if props.get("simd_count", 0) > 0 and "location_id" in props:
+                gpus.append((props.get("domain", 0), props["location_id"]))
+        vis = os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
+        if vis:
+            gpus = [gpus[int(i)] for i in vis.split(",")]
+        dom, loc = gpus[local_rank]
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if node < 0:
+            return None
+        return node, parse_cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read())
+    except (OSError, ValueError, IndexError, KeyError):
+        return None
+
+
+def pin_rank(local_rank: int):
+    """Pin this rank (before any GPU call, so the HIP runtime's threads inherit
+    it) to the CPUs NUMA-local to its GPU: each rank's host loop and tracker then
+    run next to their device and off the other ranks' cores.
+    Returns what was done, for the JSON line."""
+    got = gpu_numa_cpus(local_rank)
+    if got is None:
+        return {"pinned": False, "reason": "no NUMA information for the GPU"}
+    node, cpus = got
+    allowed = sorted(set(cpus) & os.sched_getaffinity(0))
+    if not allowed:
+        return {"pinned": False, "numa_node": node, "reason": "NUMA-local CPUs outside the affinity mask"}
+    os.sched_setaffinity(0, allowed)
+    return {"pinned": True, "numa_node": node, "cpus": len(allowed)}
+
+
+# ---- CPU baseline -----------------------------------------------------------------------------
+
+
+def native_oracle():
+    """Build the oracle's sources -O3 -march=native for THIS host (the CPU
+    baseline of SURVEY.md §8d; -ffp-contract=off keeps its results identical to
+    the test build) and point tests/_oracle.py at it.  Must run before the first
+    import of _oracle.  Returns the library path, or None (the shipped -O2 build
+    is used)."""
+    import subprocess
+    import tempfile
+
+    if "_oracle" in sys.modules:
+        return os.environ.get("TBDK_ORACLE_LIB")
+    out = os.path.join(tempfile.mkdtemp(prefix="tbdk_oracle_"), "liboracle_native.so")
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE_OUT={out}"],
+                       check=True, capture_output=True, timeout=300)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    os.environ["TBDK_ORACLE_LIB"] = out
+    return out
+
+
+class _NativeTracker:
+    """tbd_oracle.Tracker's interface over libtbdk's host tracker (tbdk_tracker_*:
+    host C++, the same code the GPU loop's tracker step runs), so the CPU
+    baseline's tracker step costs what the reference's C++ tracker costs, not
+    what the pure-Python checker costs."""
+
+    def __init__(self, bounds):
+        import numpy as np
+        from opencv_amd import tbd
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import tbd_oracle as T
+
+        self.np, self.tbd, self.T = np, tbd, T
+        self.t = tbd.Tracker(bounds=bounds)
+        self.tracks = []
+        self.true_positives, self.false_negatives, self.false_positives, self.ground_truths = [], [], [], []
+
+    def step(self, dets, frame_id, preds):
+        d = self.np.zeros(len(dets), self.tbd.DET_DTYPE)
+        for i, x in enumerate(dets):
+            d[i] = (x.id, x.bbox.x, x.bbox.y, x.bbox.width, x.bbox.height, x.confidence)
+        m = self.t.performTrackingStep(d, frame_id, preds)
+        self.true_positives.append(m.tp)
+        self.false_negatives.append(m.fn)
+        self.false_positives.append(m.fp)
+        self.ground_truths.append(m.gt)
+        T = self.T
+        self.tracks = [T.Track(id=r.id, bboxes=[T.Rect(r.x, r.y, r.width, r.height)], age=r.age,
+                               totalVisibleCount=r.total_visible,
+                               predPosition=T.Rect(r.pred_x, r.pred_y, r.pred_w, r.pred_h))
+                       for r in self.t.getTracks()]
+
+
+def cpu_baseline(frames_host, gt, args, seconds: float, threads: int, max_frames=None):
+    """The CPU loop of the same workload on this host: oracle/tbd_loop_oracle.py
+    (the reference's primitives composed as the GPU loop composes them: pyramid,
+    GFTT(256/box, q 0.01, minDist 3) on new / re-detect / depleted tracks, PyrLK
+    win 21 3 levels in the reference's SSE2 accumulation order, getRTMatrix fit,
+    the tracker step) with `threads` threads: PyrLK over points (the
+    reference's parallel_for_), the boxes' goodFeaturesToTrack calls concurrently
+    (one ROI per call, as the reference's single-threaded GFTT), and the C++
+    tracker.  Frame 0 (no tracking yet) runs untimed; frames 1.. are timed until
+    `seconds` have passed (at least 3)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tbd_loop_oracle as L
+
+    W, H = frames_host.shape[2], frames_host.shape[1]
+    bounds = (0, W, 0, H) if args.bounds == "frame" else (0, 1280, 0, 720)
+    pool = ThreadPoolExecutor(threads) if threads > 1 else None
+    lp = L.KltTbdLoop(W, H, win=args.win, max_level=args.max_level, redetect_every=args.redetect,
+                      accum=L.O.ACCUM_SSE2, nthreads=threads, tracker=_NativeTracker(bounds), gftt_pool=pool)
+    lp.step(frames_host[0], 0, L.detections(gt[0], 0))
+    n = frames_host.shape[0] if max_frames is None else min(max_frames, frames_host.shape[0])
     done = 0
     t0 = time.perf_counter()
-    n = frames_host.shape[0]
-    for f in range(n):
-        img = frames_host[f]
-        P = O.Pyramid(img, (args.win, args.win), args.max_level)
-        if prev is not None and pts is not None and len(pts):
-            nxt, st, _, _ = O.lk(prev, P, pts, (args.win, args.win), args.max_level, 30, 0.01, 0, 1e-4,
-                                 O.ACCUM_SSE2, threads)
-            pts = nxt[st == 1]
-        if f % args.redetect == 0 or pts is None:
-            rois = [tuple(int(v) for v in g[1:]) for g in gt[f] if g[0]]
-            got = O.gftt_rois(img, rois, 256, 0.01, 3.0)
-            pts = np.concatenate(got).astype(np.float32) if got else np.zeros((0, 2), np.float32)
-        prev = P
+    for f in range(1, n):
+        lp.step(frames_host[f], f, L.detections(gt[f], f))
         done += 1
         if time.perf_counter() - t0 > seconds and done >= 3:
             break
     el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} frames of the rank-0 sequence, {args.width}x{args.height}x{args.objects} "
-                      f"objects: oracle pyramid + GFTT(256/box, every {args.redetect} frames, 1 thread) + "
-                      f"PyrLK win {args.win} SSE2-order ({threads} threads); tracker step excluded"}
+    if pool is not None:
+        pool.shutdown()
+    return done / el, done
+
+
+def cpu_baseline_line(frames_host, gt, args, restore_affinity=None):
+    """cpu_baseline object: every CPU this process may use (the rank's pinning
+    undone for the measurement), plus a 1-thread figure on a shorter sample."""
+    pinned = os.sched_getaffinity(0)
+    if restore_affinity:
+        os.sched_setaffinity(0, restore_affinity)
+    try:
+        lib = native_oracle()
+        cores, info = host_cores()
+        fps, n = cpu_baseline(frames_host, gt, args, args.cpu_baseline_seconds, cores)
+        fps1, n1 = cpu_baseline(frames_host, gt, args, args.cpu_baseline_seconds_1t, 1)
+    finally:
+        os.sched_setaffinity(0, pinned)
+    return {"value": round(fps, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "value_1_thread": round(fps1, 4), "frames_1_thread": n1, "host": info,
+            "build": "oracle/ sources -O3 -march=native -ffp-contract=off, built on this host" if lib else
+                     "oracle/liboracle.so as shipped (-O2; the native build failed)",
+            "sample": f"frames 1..{n} of the rank-0 sequence ({args.width}x{args.height} x {args.objects} objects, "
+                      f"frame 0 untimed) through oracle/tbd_loop_oracle.py: pyramid, GFTT(256/box, every "
+                      f"{args.redetect} frames or < 32 points, the boxes' calls on {cores} threads), PyrLK win "
+                      f"{args.win} {args.max_level + 1} levels in the reference's SSE2 accumulation order "
+                      f"({cores} threads), getRTMatrix fit, and the C++ tracker step; the 1-thread figure over "
+                      f"frames 1..{n1 + 1}"}
 
 
 FB_ITER_BYTES_PER_PX = 56  # fb_iter algorithmic bytes per pixel: flow 8 + R0 20 + R1 20 in, flow 8 out
@@ -270,7 +428,7 @@ def lk_f16_secondary(ctx, args, device, cpu: bool):
            "config": {"workload": f"sparse PyrLK {w}x{h}, {args.fb_objects} objects x {per_box} points "
                                   "(BASELINE configs[4] fp16 pixel path)", "points": npts, "levels": nlev,
                       "win": args.win, "pairs": n, "mean_iters_per_point": iters / n / npts},
-           "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+           "roofline": {"bound": "valu", "achieved": round(tf, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(tf / PEAK_F32_TFLOPS, 4), "traffic": None, "kernel": "lk_sparse (lk_f16_kernel)",
                         "flops_per_launch": flops,
                         "note": "VALU-bound (fp32 FMA on fp16 taps, no MFMA); algorithmic flops per SURVEY.md §8(d)"},
@@ -355,11 +513,229 @@ def hog_secondary(ctx, args, device, cpu: bool):
     return out
 
 
-def main():
+# ---- the contract ----------------------------------------------------------------------------
+
+
+def rank_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_leg=None):
+    """The bench contract, independent of what a step is: the rank's own
+    sequence (seed + rank), W untimed warm-up steps, then EXACTLY K steps
+    bracketed by a barrier + device sync on both sides, the max time over ranks,
+    value = steps of all ranks / that time (replicas, weak scaling), and the CPU
+    baseline on rank 0 at N = 1 only.  Returns (line, per-step results)."""
+    import torch.distributed as dist
+
+    measure.prepare(args.seed + rank)
+    measure.warmup(args.warmup)
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    per_step = measure.timed(args.steps)
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    el = max_over_ranks(el, world, device=dist_device)
+    line = {
+        "metric": METRIC,
+        "value": round(replica_throughput(args.steps, world, el), 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1000.0, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+    }
+    line["cpu_baseline"] = cpu_leg() if (cpu_leg is not None and rank == 0 and world == 1) else None
+    return line, per_step
+
+
+class TbdMeasure:
+    """BASELINE configs[2]: the rank's synthetic 1080p x 128-object sequence of
+    max(sequence_frames, W + K) frames rendered into HBM; warm-up = frames
+    [0, W) one tbdk_tbd_step at a time, the timed steps = frames [W, W + K)
+    through tbdk_tbd_run (or the per-frame APIs, --api)."""
+
+    def __init__(self, args, ctx, dev):
+        self.args, self.ctx, self.dev = args, ctx, dev
+
+    def prepare(self, seed: int):
+        import torch
+        from opencv_amd import klt, tbd
+
+        a = self.args
+        self.nseq = max(a.sequence_frames, a.warmup + a.steps)
+        self.frames, gt = klt.synth_render(seed, a.width, a.height, a.objects, 0, self.nseq, device=self.dev,
+                                           ctx=self.ctx)
+        self.gtn = gt.numpy()
+        self.dets = [tbd.detections_from_gt(self.gtn[f]) for f in range(self.nseq)]
+        over = dict(bounds_xmax=a.width, bounds_ymax=a.height) if a.bounds == "frame" else {}
+        self.cfg = tbd.default_config(a.width, a.height, win=a.win, max_level=a.max_level,
+                                      redetect_every=a.redetect, **over)
+        self.stream = torch.cuda.current_stream()
+        self.loop = tbd.TbdLoop(self.cfg, ctx=self.ctx)
+        torch.cuda.synchronize()
+
+    def new_loop(self, warmup: int):
+        from opencv_amd import tbd
+
+        loop = tbd.TbdLoop(self.cfg, ctx=self.ctx)
+        for f in range(warmup):
+            loop.step(self.frames[f], f, self.dets[f], self.stream)
+        return loop
+
+    def warmup(self, w: int):
+        from opencv_amd import tbd
+
+        a, ctx = self.args, self.ctx
+        for f in range(w):
+            self.loop.step(self.frames[f], f, self.dets[f], self.stream)
+        self.w = w
+        self.frame_list = [self.frames[f] for f in range(w, w + a.steps)]
+        self.packed = tbd.TbdLoop.pack_detections(self.dets[w:w + a.steps])  # staged like the frames
+        self.timed_kernels = ["pyr_build", "lk_sparse", "gftt", "tbd_fit"] if a.kstats == "all" else \
+            [] if a.kstats == "none" else [k for k in a.kstats.split(",") if k]
+        ctx.timing_select(self.timed_kernels or None)
+        # events on every Nth timed launch: each costs two event records of host
+        # work on the frame's critical path (~5 % of the frame when every launch is timed)
+        ctx.set_option("timing_every", a.timing_every)
+        ctx.timing_enable(bool(self.timed_kernels))
+
+    def timed(self, k: int):
+        a, w = self.args, self.w
+        if a.api == "run":
+            return list(self.loop.run(self.frame_list, w, None, self.stream, packed=self.packed))
+        out = []
+        for f in range(w, w + k):
+            nxt = self.frames[f + 1] if a.api == "ahead" and f + 1 < self.nseq else None
+            out.append(self.loop.step(self.frames[f], f, self.dets[f], self.stream, next_frame=nxt))
+        return out
+
+
+def timed_on_all_ranks(fn, world):
+    """Barrier + sync, fn(), sync, barrier; the max wall time over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    return max_over_ranks(el, world, device="cuda")
+
+
+def sequence_repeats(m: TbdMeasure, world: int, runs: int, skip: int):
+    """the whole sequence in steady state (frames [skip, nseq)
+    after `skip` warm-up frames), a fresh loop per run, median of `runs` runs."""
+    from opencv_amd import tbd
+
+    frames = [m.frames[f] for f in range(skip, m.nseq)]
+    packed = tbd.TbdLoop.pack_detections(m.dets[skip:m.nseq])
+    fps = []
+    for _ in range(runs):
+        loop = m.new_loop(skip)
+        el = timed_on_all_ranks(lambda: loop.run(frames, skip, None, m.stream, packed=packed), world)
+        fps.append(replica_throughput(len(frames), world, el))
+        del loop
+    return {"frames": len(frames), "skip": skip, "runs_fps": [round(v, 1) for v in fps],
+            "median_fps": round(sorted(fps)[len(fps) // 2], 2), "unit": "frames/s",
+            "api": "tbdk_tbd_run", "note": "whole 500-frame sequence after 20 warm-up frames, fresh loop per run"}
+
+
+def with_h2d(m: TbdMeasure, world: int, runs: int, skip: int):
+    """§8d's with-H2D variant: the same frames from page-locked host memory
+    through tbdk_tbd_run_host (each frame uploaded into a device ring two
+    frames ahead, on its own stream).  Never `value`."""
+    from opencv_amd import tbd
+
+    host = m.frames.cpu().pin_memory()
+    packed = tbd.TbdLoop.pack_detections(m.dets[skip:m.nseq])
+    fps = []
+    for _ in range(runs):
+        loop = m.new_loop(skip)
+        el = timed_on_all_ranks(lambda: loop.run_host(host[skip:], skip, None, m.stream, packed=packed), world)
+        fps.append(replica_throughput(m.nseq - skip, world, el))
+        del loop
+    px = m.args.width * m.args.height
+    med = sorted(fps)[len(fps) // 2]
+    del host
+    return {"frames": m.nseq - skip, "runs_fps": [round(v, 1) for v in fps], "median_fps": round(med, 2),
+            "unit": "frames/s", "h2d_bytes_per_frame": px, "h2d_gbs": round(med / world * px / 1e9, 3),
+            "api": "tbdk_tbd_run_host (pinned host frames, upload ring)"}
+
+
+def kitti_leg(args, ctx, dev, world: int, rank: int):
+    """BASELINE configs[3]: KITTI-shaped 1242x375 sequences, one per GPU (seed
+    s + rank, sequences s..s+7 at 8 GPUs), 128 objects, the full loop; frames of
+    all ranks / max time.  Reported, never `value`."""
+    import torch
+    from opencv_amd import klt, tbd
+
+    w, h, n, skip = 1242, 375, args.kitti_frames, 20
+    frames, gt = klt.synth_render(args.seed + rank, w, h, args.objects, 0, n, device=dev, ctx=ctx)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(n)]
+    cfg = tbd.default_config(w, h, win=args.win, max_level=args.max_level, redetect_every=args.redetect)
+    stream = torch.cuda.current_stream()
+    fl = [frames[f] for f in range(skip, n)]
+    packed = tbd.TbdLoop.pack_detections(dets[skip:])
+    fps = []
+    for _ in range(3):
+        loop = tbd.TbdLoop(cfg, ctx=ctx)
+        for f in range(skip):
+            loop.step(frames[f], f, dets[f], stream)
+        el = timed_on_all_ranks(lambda: loop.run(fl, skip, None, stream, packed=packed), world)
+        fps.append(replica_throughput(len(fl), world, el))
+        del loop
+    del frames
+    return {"value": round(sorted(fps)[1], 2), "unit": "frames/s", "runs_fps": [round(v, 1) for v in fps],
+            "n_gpus": world, "config": {"workload": f"TBD loop {w}x{h} x {args.objects} objects (BASELINE configs[3]),"
+                                                    f" one sequence per GPU (seeds s..s+{world - 1})",
+                                        "frames_timed": len(fl), "tracker_bounds": "reference"}}
+
+
+PYR_KERNELS = ("pyr_build_kernel", "pad_copy_kernel", "pyr_down_padded_kernel", "scharr_levels_kernel")
+
+
+def pmc_bytes(kernel_substrs):
+    """Sum over kernels of the committed PMC summary's per-launch bytes (raw
+    FETCH_SIZE, FETCH_SIZE x2 as the guide's wide-read correction, WRITE_SIZE);
+    None when no summary covers them."""
+    d = os.path.join(ROOT, "profiles")
+    try:
+        files = sorted(f for f in os.listdir(d) if f.endswith("_pmc.json"))
+    except OSError:
+        return None
+    for f in reversed(files):
+        k = json.load(open(os.path.join(d, f)))["kernels"]
+        hit = [(n, v) for n, v in k.items() if any(s in n for s in kernel_substrs)
+               and v.get("fetch_bytes") is not None and v.get("write_bytes") is not None]
+        if hit:
+            raw = sum(v["fetch_size_kib"] * 1024 for _, v in hit)
+            return {"source": f, "kernels": [n.split("(")[0] for n, _ in hit], "fetch_raw": raw,
+                    "fetch_x2": 2 * raw, "write": sum(v["write_bytes"] for _, v in hit)}
+    return None
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--sequence-frames", type=int, default=500,
+                    help="frames rendered per GPU (configs[2]'s sequence); the timed steps are frames "
+                         "[warmup, warmup + steps) of it")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--objects", type=int, default=128)
@@ -370,7 +746,9 @@ def main():
     ap.add_argument("--bounds", choices=["reference", "frame"], default="reference",
                     help="reference: the tracker's hard-coded 1280x720 filter (tbd.cpp:218); frame: W x H")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds-1t", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pin", action="store_true", help="do not pin the rank to its GPU's NUMA-local CPUs")
     ap.add_argument("--api", choices=["run", "ahead", "step"], default="run",
                     help="run: tbdk_tbd_run (native frame loop with look-ahead); ahead: per-frame "
                          "tbdk_tbd_step_ahead; step: per-frame tbdk_tbd_step (no look-ahead)")
@@ -385,7 +763,12 @@ def main():
                     help="kernels timed with HIP events in the timed region (comma list, 'all' or 'none'); "
                          "each timed launch adds two event records to the frame's host work.  The other "
                          "kernels are timed in a separate pass over the same frames (not `value`)")
+    ap.add_argument("--repeats", type=int, default=5, help="runs of the whole sequence (median reported)")
+    ap.add_argument("--no-secondary", action="store_true", help="only the contract line (A/B runs)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary per-frame tbdk_tbd_step pass")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (tbdk_tbd_run_host) variant")
+    ap.add_argument("--no-kitti", action="store_true", help="skip the KITTI-shaped configs[3] measurement")
+    ap.add_argument("--kitti-frames", type=int, default=500)
     ap.add_argument("--no-farneback", action="store_true", help="skip the secondary dense Farneback measurement")
     ap.add_argument("--fb-width", type=int, default=3840)
     ap.add_argument("--fb-height", type=int, default=2160)
@@ -397,15 +780,18 @@ def main():
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
     ap.add_argument("--hog-frames", type=int, default=60)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.no_secondary:
+        args.no_step_api = args.no_h2d = args.no_kitti = args.no_farneback = args.no_f16 = args.no_hog = True
+        args.repeats = 0
 
-    import numpy as np
+    world, rank, local = rank_env()
+    full_affinity = os.sched_getaffinity(0)
+    pin = {"pinned": False, "reason": "--no-pin"} if args.no_pin else pin_rank(local)  # before any GPU call
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -422,112 +808,67 @@ def main():
     ctx.set_option("tbd_early_gftt", args.early_gftt)
     ctx.set_option("tbd_spec_lookahead", 0 if args.no_spec_lookahead else 1)
     ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
-    nframes = args.warmup + args.steps
-    frames, gt = klt.synth_render(args.seed + rank, args.width, args.height, args.objects, 0, nframes,
-                                  device=dev, ctx=ctx)
-    gtn = gt.numpy()
-    dets = [tbd.detections_from_gt(gtn[f]) for f in range(nframes)]
-    over = {}
-    if args.bounds == "frame":
-        over = dict(bounds_xmax=args.width, bounds_ymax=args.height)
-    cfg = tbd.default_config(args.width, args.height, win=args.win, max_level=args.max_level,
-                             redetect_every=args.redetect, **over)
-    loop = tbd.TbdLoop(cfg, ctx=ctx)
-    stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()
 
-    for f in range(args.warmup):
-        loop.step(frames[f], f, dets[f], stream)
-    frame_list = [frames[f] for f in range(args.warmup, nframes)]
-    packed = tbd.TbdLoop.pack_detections(dets[args.warmup:])  # host detections staged like the frames
-
-    timed = ["pyr_build", "lk_sparse", "gftt", "tbd_fit"] if args.kstats == "all" else \
-        [] if args.kstats == "none" else [k for k in args.kstats.split(",") if k]
-    ctx.timing_select(timed or None)
-    # events on every 5th timed launch: each timed launch costs two event records of
-    # host work on the frame's critical path (~5 % of the frame when every launch is
-    # timed); 5 is odd, so a frame's alternating launch kinds are sampled alike
-    ctx.set_option("timing_every", args.timing_every)
-    ctx.timing_enable(bool(timed))
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if args.api == "run":
-        ms = loop.run(frame_list, args.warmup, None, stream, packed=packed)
-    else:
-        ms = []
-        for f in range(args.warmup, nframes):
-            nxt = frames[f + 1] if args.api == "ahead" and f + 1 < nframes else None
-            ms.append(loop.step(frames[f], f, dets[f], stream, next_frame=nxt))
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    el = max_over_ranks(el, world, device="cuda")
+    m = TbdMeasure(args, ctx, dev)
+    nb = 60  # frames handed to the CPU baseline (it stops at its time budget)
+    cpu_leg = None if args.no_cpu_baseline else \
+        (lambda: cpu_baseline_line(m.frames[:nb].cpu().numpy(), m.gtn[:nb], args, restore_affinity=full_affinity))
+    line, ms = run_contract(args, world, rank, m, torch.cuda.synchronize, "cuda", cpu_leg=cpu_leg)
+    stream, cfg, frames, dets = m.stream, m.cfg, m.frames, m.dets
+    timed = m.timed_kernels
     lk_pts = lk_it = klt_pts = ntr = redet = early = 0
     h_wait = h_trk = h_step = h_launch = 0.0
-    for m in ms:
-        lk_pts += m.lk_points
-        lk_it += m.lk_iters
-        klt_pts += m.klt_points
-        ntr += m.ntracks
-        redet += m.redetected
-        early += m.early_gftt
-        h_wait += m.host_wait_us
-        h_trk += m.host_tracker_us
-        h_step += m.host_step_us
-        h_launch += m.host_launch_us
-
+    for x in ms:
+        lk_pts += x.lk_points
+        lk_it += x.lk_iters
+        klt_pts += x.klt_points
+        ntr += x.ntracks
+        redet += x.redetected
+        early += x.early_gftt
+        h_wait += x.host_wait_us
+        h_trk += x.host_tracker_us
+        h_step += x.host_step_us
+        h_launch += x.host_launch_us
     kstats = {}
     for name in timed:
-        c, ms = ctx.timing_query(name)
+        c, t_ms = ctx.timing_query(name)
         kstats[name] = {"launches": ctx.timing_calls(name), "timed_launches": c,
-                        "avg_us": (ms / c * 1000.0) if c else None, "total_ms_timed": ms}
+                        "avg_us": (t_ms / c * 1000.0) if c else None, "total_ms_timed": t_ms}
     ctx.timing_enable(False)
     ctx.timing_select(None)
     ctx.set_option("timing_every", 1)
     nolaunch = {"launches": 0, "avg_us": None, "total_ms": 0.0}
+    w0, nframes = args.warmup, args.warmup + args.steps
 
     # secondary: the same frames through the per-frame tbdk_tbd_step API (no
     # look-ahead), a fresh loop, no timing events; reported, never `value`
     step_api = None
     if args.api != "step" and not args.no_step_api:
-        loop2 = tbd.TbdLoop(cfg, ctx=ctx)
-        for f in range(args.warmup):
-            loop2.step(frames[f], f, dets[f], stream)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for f in range(args.warmup, nframes):
-            loop2.step(frames[f], f, dets[f], stream)
-        torch.cuda.synchronize()
-        el2 = max_over_ranks(time.perf_counter() - t1, world, device="cuda")
+        loop2 = m.new_loop(w0)
+        el2 = timed_on_all_ranks(lambda: [loop2.step(frames[f], f, dets[f], stream) for f in range(w0, nframes)],
+                                 world)
         step_api = {"value": round(replica_throughput(args.steps, world, el2), 2), "unit": "frames/s",
                     "api": "tbdk_tbd_step per frame from Python"}
         del loop2
 
     # the kernels not timed in the timed region: a separate pass over the same
-    # frames with events on them (a fresh loop; its wall time is not reported)
+    # frames with events on every launch (a fresh loop; its wall time is not reported)
     rest = [k for k in ("pyr_build", "lk_sparse", "gftt", "tbd_fit") if k not in timed]
     kstats_aside = {}
     if rest:
-        loop3 = tbd.TbdLoop(cfg, ctx=ctx)
-        for f in range(args.warmup):
-            loop3.step(frames[f], f, dets[f], stream)
+        loop3 = m.new_loop(w0)
         ctx.timing_select(rest)
         ctx.timing_enable(True)
-        loop3.run(frame_list, args.warmup, None, stream, packed=packed)
+        loop3.run(m.frame_list, w0, None, stream, packed=m.packed)
         torch.cuda.synchronize()
         for name in rest:
-            c, ms = ctx.timing_query(name)
-            kstats_aside[name] = {"launches": c, "avg_us": (ms / c * 1000.0) if c else None, "total_ms": ms}
+            c, t_ms = ctx.timing_query(name)
+            kstats_aside[name] = {"launches": c, "avg_us": (t_ms / c * 1000.0) if c else None, "total_ms": t_ms}
         ctx.timing_enable(False)
         ctx.timing_select(None)
         del loop3
 
-    lk = kstats.get("lk_sparse", nolaunch)
+    lk = kstats.get("lk_sparse", kstats_aside.get("lk_sparse", nolaunch))
     nlev = args.max_level + 1
     if lk["launches"]:
         flops_per_launch = lk_flops(lk_pts * nlev, lk_it, args.win) / lk["launches"]
@@ -538,20 +879,28 @@ def main():
     traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}>")
     if traffic is None:
         traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
-    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic, "kernel": "lk_sparse",
                 "traffic_source": traffic_src,
-                "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA use; peak = fp32 vector rate; "
-                        "algorithmic flops per SURVEY.md §8(d) with the measured iteration count; "
-                        f"launch duration = HIP events on every {args.timing_every}th launch of the timed region",
+                "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA (no contraction on this path); peak = "
+                        "fp32 vector rate; algorithmic flops per SURVEY.md §8(d) with the measured iteration "
+                        f"count; launch duration = HIP events on every {args.timing_every}th launch of the timed "
+                        "region; traffic = FETCH_SIZE x2 + WRITE_SIZE per launch (committed PMC summary)",
                 "flops_per_launch": flops_per_launch,
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}
     pb = pyr_bytes(args.width, args.height, nlev)
     pyr = kstats.get("pyr_build", kstats_aside.get("pyr_build", nolaunch))
     pyr_gbs = pb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
+    cnt = pmc_bytes(PYR_KERNELS)
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build"}
+                "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build",
+                "traffic": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,
+                "traffic_raw": (cnt["fetch_raw"] + cnt["write"]) if cnt else None,
+                "traffic_kernels": cnt["kernels"] if cnt else None, "traffic_source": cnt["source"] if cnt else None,
+                "note": "achieved = SURVEY §8d algorithmic bytes (new frame read, levels 1.. written and re-read) / "
+                        "the build's HIP-event time; traffic = counter bytes per build (FETCH_SIZE x2 and raw, "
+                        "+ WRITE_SIZE), which include the Scharr planes the algorithmic count leaves out"}
     # north_star's "HBM-read roofline on pyramid+PyrLK": SURVEY §8d bytes B_pyr + B_lk + N*21,
     # with B_lk at its upper bound (2 full pyramids), over the two stages' summed time
     w_, h_, lv_bytes = args.width, args.height, 0
@@ -567,26 +916,17 @@ def main():
                "note": "B_lk taken at its SURVEY §8d upper bound (2 full pyramids); PyrLK is compute-bound "
                        "(~360 flop/B vs ridge ~20), so this fraction is structurally small (DESIGN.md §3)"}
 
-
-    out = {
-        "metric": METRIC,
-        "value": round(replica_throughput(args.steps, world, el), 2),
-        "unit": "frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1000.0, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
+    line.update({
         "dtype": "u8",
         "data": "synthetic (deterministic in-repo generator, opencv_amd/csrc/synth_spec.h)",
         "config": {"workload": f"TBD loop {args.width}x{args.height} x {args.objects} objects "
-                               f"(BASELINE configs[2]), {nframes}-frame sequence per GPU",
+                               f"(BASELINE configs[2]), frames [{w0}, {nframes}) of a {m.nseq}-frame sequence "
+                               "per GPU",
                    "levels": nlev, "win": args.win, "gftt": f"256/box, q 0.01, minDist 3, every {args.redetect}",
                    "tracker_bounds": args.bounds, "parallelism": f"replicas x{world} (one sequence per GPU)",
                    "api": {"run": "tbdk_tbd_run (native frame loop, look-ahead)",
                            "ahead": "tbdk_tbd_step_ahead per frame", "step": "tbdk_tbd_step per frame"}[args.api]},
+        "host_pinning": pin,
         "step_api": step_api,
         "roofline": roofline,
         "roofline_pyramid": roof_pyr,
@@ -598,22 +938,24 @@ def main():
                       "gftt_rois_early": early / args.steps,
                       "host_wait_us": h_wait / args.steps, "host_tracker_us": h_trk / args.steps,
                       "host_step_us": h_step / args.steps, "host_launch_us": h_launch / args.steps},
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        nb = min(nframes, 40)
-        out["cpu_baseline"] = cpu_baseline(frames[:nb].cpu().numpy(), gtn[:nb], args, args.cpu_baseline_seconds)
-    else:
-        out["cpu_baseline"] = None
+    })
+    if args.repeats > 0:
+        line["sequence"] = sequence_repeats(m, world, args.repeats, 20)
+    if not args.no_h2d:
+        line["with_h2d"] = with_h2d(m, world, 3, 20)
+    del m.frames, frames, m.loop
+    if not args.no_kitti:
+        line["kitti"] = kitti_leg(args, ctx, dev, world, rank)
     if rank == 0 and not args.no_farneback:
-        del frames, frame_list
-        out["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+        line["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_f16:
-        out["lk_f16"] = lk_f16_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+        line["lk_f16"] = lk_f16_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_hog:
-        out["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+        line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

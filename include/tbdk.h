@@ -653,6 +653,15 @@ int tbdk_tbd_step_ahead(tbdk_tbd* tbd, const uint8_t* frame, int pitch, int fram
 int tbdk_tbd_run(tbdk_tbd* tbd, const uint8_t* const* frames, int pitch, int first_frame_id,
                  const tbdk_detection* dets, const int32_t* det_offsets, int nframes, tbdk_frame_metrics* metrics,
                  void* stream);
+/* tbdk_tbd_run over frames in HOST memory (the sample's frame source,
+ * samples/gpu/tbd.cpp:568-599: a decoded frame is uploaded, then processed):
+ * frames = host pointers (same pitch; page-locked memory lets the uploads
+ * overlap the loop).  Each frame is uploaded into a ring of three device
+ * frames on a copy stream two frames ahead of its use, so frame i+2's upload
+ * runs during frame i's work; results are identical to tbdk_tbd_run's. */
+int tbdk_tbd_run_host(tbdk_tbd* tbd, const uint8_t* const* frames, int pitch, int first_frame_id,
+                      const tbdk_detection* dets, const int32_t* det_offsets, int nframes,
+                      tbdk_frame_metrics* metrics, void* stream);
 int tbdk_tbd_tracks(tbdk_tbd* tbd, tbdk_track_info* out, int cap, int* n);
 /* Attach a trajectory map (NULL detaches): every later step records, for each
  * detection with a ground-truth id (id >= 0), its position (parseDetections,

@@ -247,6 +247,8 @@ SIGNATURES = {
                                       C.c_void_p, C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
     "tbdk_tbd_run": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(Detection),
                                C.POINTER(C.c_int32), C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
+    "tbdk_tbd_run_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(Detection),
+                                    C.POINTER(C.c_int32), C.c_int, C.POINTER(FrameMetrics), C.c_void_p]),
     "tbdk_tbd_set_trajectories": (C.c_int, [_P, _P]),
     "tbdk_tbd_tracking_write": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_char_p, C.c_int,
                                           C.POINTER(ScenarioMetrics)]),

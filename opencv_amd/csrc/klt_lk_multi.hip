@@ -164,7 +164,10 @@ constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 #define TBDK_MULTI_BOUNDS __launch_bounds__(64 * TBDK_LK_MULTI_WAVES)
 #endif
 
-template <int WW, int WH>
+// FLY: the Scharr derivatives of the window are computed from the u8 level in
+// the level setup instead of read from the pyramid's derivative planes (same
+// values; the planes need not exist)
+template <int WW, int WH, bool FLY>
 __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 {
     constexpr int P = 64 / WW;         // points per wave
@@ -249,16 +252,60 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         uint32_t gxk[NP], gyk[NP];
         float A11, A12, A22;
         {
-            const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
-            const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4) : 0u;
             uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
+            if constexpr (FLY) {
+                // calcSharrDeriv (lkpyramid.cpp:55-144) of the window, from the
+                // padded u8 level: one unaligned dword per row holds columns
+                // x-1 .. x+2, rows -1 .. WH; unpacked as int16 pairs (x-1, x) and
+                // (x+1, x+2), the vertical pass t0 = 3(a+c) + 10b, t1 = c - a runs
+                // on both pairs, and the horizontal pass gives (Ix(x), Ix(x+1)) =
+                // hi - lo and (Iy(x), Iy(x+1)) = 3 (lo + hi) + 10 (t1(x), t1(x+1))
+                // directly as the pairs the bilinear sums take.  Integer and exact
+                // in 16 bits (|Ix|, |Iy| <= 4080); the level's reflect-101 frame is
+                // the reference's row / column reflection.
+                const uint32_t ioff = act ? (uint32_t)((ipy - 1 + L.ipad) * L.ipitch + ipx + x - 1 + L.ipad) : 0u;
+                uint32_t u[WH + 3];
 #pragma unroll
-            for (int r = 0; r <= WH; ++r) {
-                ip[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
-                const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);
-                const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);
-                dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
-                dyp[r] = __builtin_amdgcn_perm(d1, d0, 0x07060302u);  // (Iy(x), Iy(x+1))
+                for (int r = 0; r < WH + 3; ++r) u[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);
+                // outside the level the derivative planes hold BORDER_CONSTANT 0
+                // (lkpyramid.cpp:1357): masked only in waves with a window at an edge
+                const bool edge = any_lane(act && (ipx < 0 || ipx + WW > L.w - 1 || ipy < 0 || ipy + WH > L.h - 1));
+                const uint32_t cm = ((unsigned)(ipx + x) < (unsigned)L.w ? 0x0000FFFFu : 0u) |
+                                    ((unsigned)(ipx + x + 1) < (unsigned)L.w ? 0xFFFF0000u : 0u);
+#pragma unroll
+                for (int r = 0; r <= WH; ++r) {
+                    const u16x2 al = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C010C00u));
+                    const u16x2 ah = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C030C02u));
+                    const u16x2 bl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C010C00u));
+                    const u16x2 bh = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C030C02u));
+                    const u16x2 cl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C010C00u));
+                    const u16x2 ch = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C030C02u));
+                    ip[r] = __builtin_amdgcn_perm(0u, u[r + 1], 0x0C020C01u);  // (I(x), I(x+1))
+                    const u16x2 t0l = (al + cl) * (unsigned short)3 + bl * (unsigned short)10;
+                    const u16x2 t0h = (ah + ch) * (unsigned short)3 + bh * (unsigned short)10;
+                    const uint32_t t1l = as_u32(cl - al), t1h = as_u32(ch - ah);
+                    const u16x2 mid = as_u16x2(__builtin_amdgcn_perm(t1h, t1l, 0x05040302u));  // (t1(x), t1(x+1))
+                    uint32_t dx = as_u32(t0h - t0l);
+                    uint32_t dy = as_u32((as_u16x2(t1l) + as_u16x2(t1h)) * (unsigned short)3 + mid * (unsigned short)10);
+                    if (edge) {
+                        const uint32_t m = (unsigned)(ipy + r) < (unsigned)L.h ? cm : 0u;
+                        dx &= m;
+                        dy &= m;
+                    }
+                    dxp[r] = dx;
+                    dyp[r] = dy;
+                }
+            } else {
+                const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
+                const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4) : 0u;
+#pragma unroll
+                for (int r = 0; r <= WH; ++r) {
+                    ip[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
+                    const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);
+                    const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);
+                    dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
+                    dyp[r] = __builtin_amdgcn_perm(d1, d0, 0x07060302u);  // (Iy(x), Iy(x+1))
+                }
             }
             int acc[3] = {0, 0, 0};
 #pragma unroll
@@ -422,15 +469,16 @@ bool lk_multi_supported(int win_w, int win_h)
     }
 }
 
-hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s)
+hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s)
 {
     if (!lk_multi_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
     const int per_wg = kMultiWaves * (64 / a.win_w);  // waves of P points
     const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * kMultiWaves);
     switch (a.win_w) {
-#define TBDK_CASE(W)                                                       \
-    case W:                                                                \
-        hipLaunchKernelGGL((lk_multi_kernel<W, W>), grid, block, 0, s, a); \
+#define TBDK_CASE(W)                                                                   \
+    case W:                                                                            \
+        if (fly) hipLaunchKernelGGL((lk_multi_kernel<W, W, true>), grid, block, 0, s, a);  \
+        else hipLaunchKernelGGL((lk_multi_kernel<W, W, false>), grid, block, 0, s, a); \
         break;
         TBDK_MULTI_WINDOWS(TBDK_CASE)
 #undef TBDK_CASE

@@ -11,6 +11,10 @@ namespace lkdev {
 constexpr int W_BITS = 14, W_BITS1 = 14;
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // packed 16-bit VALU ops (v_pk_*_u16)
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 __device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
 {

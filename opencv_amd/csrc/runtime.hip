@@ -166,6 +166,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_hog_block_tiled = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "lk_scharr_fly") == 0) {
+        ctx->opt_lk_scharr_fly = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "lk_impl") == 0) {  // kernel used when tbdk_lk_params.impl is 0 (auto)
         if (value < 0 || value > 3) return TBDK_EINVAL;
         ctx->opt_lk_impl = (int)value;
@@ -438,11 +442,14 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
         return map_err(e);
     }
     const int impl = p->impl ? p->impl : ctx->opt_lk_impl;
-    const bool multi = (impl == 0 || impl == 3) && have_d && lk_multi_supported(p->win_w, p->win_h);
+    // the multi kernel derives the window's Scharr values itself when the
+    // pyramid has no derivative planes, or when asked to (ctx option lk_scharr_fly)
+    const bool fly = !have_d || ctx->opt_lk_scharr_fly;
+    const bool multi = (impl == 0 || impl == 3) && lk_multi_supported(p->win_w, p->win_h);
     const bool strip = !multi && (impl == 0 || impl == 1) && have_d && lk_strip_supported(p->win_w, p->win_h);
     if ((p->impl == 1 && !strip) || (p->impl == 3 && !multi)) return TBDK_EINVAL;
     int rec = timing_begin(ctx, "lk_sparse", s);
-    hipError_t e = multi ? launch_lk_multi(a, s) : strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
+    hipError_t e = multi ? launch_lk_multi(a, fly, s) : strip ? launch_lk_strip(a, s) : launch_lk_sparse(a, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }

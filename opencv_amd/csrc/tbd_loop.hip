@@ -218,6 +218,14 @@ struct tbdk_tbd {
     std::vector<tbd::Detection> dets;
     std::vector<tbd::Prediction> preds;
     std::vector<tbdk_roi> rois;
+    // tbdk_tbd_run_host: uploaded frames, a ring of three device frames filled
+    // on `up_s` two frames ahead; copied[k] = ring[k] holds its frame,
+    // freed[k] = the steps that read ring[k] (its pyramid) are enqueued before it
+    uint8_t* ring[3] = {nullptr, nullptr, nullptr};
+    int ring_pitch = 0;
+    hipStream_t up_s = nullptr;
+    hipEvent_t copied[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t freed[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -248,6 +256,14 @@ int release(tbdk_tbd* t)
     if (t->early_done) (void)hipEventDestroy(t->early_done);
     gftt_scratch_free(t->gftt);
     gftt_scratch_free(t->gftt2);
+    if (t->up_s) (void)hipStreamSynchronize(t->up_s);
+    for (int k = 0; k < 3; ++k) {
+        if (t->freed[k]) (void)hipEventSynchronize(t->freed[k]);
+        if (t->ring[k]) (void)hipFree(t->ring[k]);
+        if (t->copied[k]) (void)hipEventDestroy(t->copied[k]);
+        if (t->freed[k]) (void)hipEventDestroy(t->freed[k]);
+    }
+    if (t->up_s) (void)hipStreamDestroy(t->up_s);
     void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts};
     for (void* p : dev)
         if (p) (void)hipFree(p);
@@ -951,6 +967,63 @@ int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first
                            det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr,
                            static_cast<hipStream_t>(stream));
         if (rc != TBDK_OK) return rc;
+    }
+    return TBDK_OK;
+}
+
+int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,
+                      const tbdk_detection* dets, const int32_t* det_offsets, int nframes,
+                      tbdk_frame_metrics* metrics, void* stream)
+{
+    if (!t || nframes < 0 || (nframes > 0 && (!frames || !det_offsets || pitch < t->cfg.width))) return TBDK_EINVAL;
+    for (int i = 0; i < nframes; ++i)
+        if (!frames[i] || det_offsets[i + 1] < det_offsets[i] || det_offsets[i] < 0) return TBDK_EINVAL;
+    if (nframes > 0 && det_offsets[nframes] > det_offsets[0] && !dets) return TBDK_EINVAL;
+    if (nframes == 0) return TBDK_OK;
+    (void)hipSetDevice(t->ctx->device);
+    const int W = t->cfg.width, H = t->cfg.height;
+    hipError_t e = hipSuccess;
+    if (!t->up_s) {  // the ring, its stream and events: once per loop
+        t->ring_pitch = (W + 255) & ~255;
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) {
+            e = hipMalloc(reinterpret_cast<void**>(&t->ring[k]), (size_t)t->ring_pitch * H + 256);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&t->copied[k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&t->freed[k], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->up_s, hipStreamNonBlocking);
+        if (e != hipSuccess) return map_status(e);
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // upload of frame j into ring[j % 3], behind the steps that last read that
+    // buffer (freed: recorded after step j - 3, whose look-ahead built frame
+    // j - 2's pyramid from ring[(j - 2) % 3], and whose own pyramid came from
+    // ring[(j - 3) % 3])
+    auto upload = [&](int j) -> hipError_t {
+        const int k = j % 3;
+        hipError_t r = hipStreamWaitEvent(t->up_s, t->freed[k], 0);
+        if (r == hipSuccess)
+            r = hipMemcpy2DAsync(t->ring[k], (size_t)t->ring_pitch, frames[j], (size_t)pitch, (size_t)W, (size_t)H,
+                                 hipMemcpyHostToDevice, t->up_s);
+        if (r == hipSuccess) r = hipEventRecord(t->copied[k], t->up_s);
+        return r;
+    };
+    e = upload(0);
+    if (e == hipSuccess && nframes > 1) e = upload(1);
+    if (e != hipSuccess) return map_status(e);
+    for (int i = 0; i < nframes; ++i) {
+        // this step reads frame i (its pyramid, unless the previous step built
+        // it) and frame i + 1 (the look-ahead pyramid)
+        e = hipStreamWaitEvent(s, t->copied[i % 3], 0);
+        if (e == hipSuccess && i + 1 < nframes) e = hipStreamWaitEvent(s, t->copied[(i + 1) % 3], 0);
+        if (e == hipSuccess && i + 2 < nframes) e = upload(i + 2);  // ring[(i + 2) % 3] held frame i - 1
+        if (e != hipSuccess) return map_status(e);
+        const uint8_t* next = i + 1 < nframes ? t->ring[(i + 1) % 3] : nullptr;
+        int rc = step_impl(t, t->ring[i % 3], t->ring_pitch, first_frame_id + i,
+                           dets ? dets + det_offsets[i] : nullptr, det_offsets[i + 1] - det_offsets[i], next,
+                           t->ring_pitch, metrics ? metrics + i : nullptr, s);
+        if (rc != TBDK_OK) return rc;
+        e = hipEventRecord(t->freed[i % 3], s);
+        if (e != hipSuccess) return map_status(e);
     }
     return TBDK_OK;
 }

@@ -70,6 +70,7 @@ struct tbdk_ctx {
     int device = 0;
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
+    int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     int opt_fb_prep_ahead = 1;  // tbdk_ctx_set_option("fb_prep_ahead"): Farneback level prep on a side stream
     int opt_hog_level_streams = 3;  // tbdk_ctx_set_option("hog_level_streams"): lanes of detectMultiScale
@@ -163,7 +164,8 @@ bool lk_strip_supported(int win_w, int win_h);
 hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 // several points per wave (klt_lk_multi.hip), same results
 bool lk_multi_supported(int win_w, int win_h);
-hipError_t launch_lk_multi(const LkArgs& a, hipStream_t s);
+// fly: Scharr derivatives computed in the kernel (no derivative planes read)
+hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s);
 // the fp16 pixel path (klt_f16.hip)
 bool lk_f16_supported(int win_w, int win_h);
 hipError_t launch_lk_f16(const LkArgs& a, hipStream_t s);

@@ -125,6 +125,26 @@ class TbdLoop:
             C.cast(offs.ctypes.data, C.POINTER(C.c_int32)), nf, ms, _stream_ptr(stream)), "tbdk_tbd_run")
         return ms[:nf]
 
+    def run_host(self, frames: torch.Tensor, first_frame_id: int, dets, stream=None, packed=None):
+        """tbdk_tbd_run_host: the frame loop over frames in host memory, uploaded
+        into a device ring two frames ahead of their use (frames: a CPU uint8
+        tensor (n, H, W) with unit column stride, ideally pinned).  Returns the
+        per-frame FrameMetrics array, identical to run()'s on the same frames."""
+        if frames.is_cuda or frames.dtype != torch.uint8 or frames.dim() != 3 or frames.stride(2) != 1:
+            raise _lib.TbdkError("frames must be a (n, H, W) uint8 host tensor")
+        nf = frames.shape[0]
+        cat, offs = packed if packed is not None else self.pack_detections(dets)
+        if len(offs) != nf + 1:
+            raise _lib.TbdkError("one detection list per frame")
+        base, step = frames.data_ptr(), frames.stride(0)
+        ptrs = (C.c_void_p * max(1, nf))(*[base + i * step for i in range(nf)])
+        ms = (_lib.FrameMetrics * max(1, nf))()
+        _lib.check(self.ctx.lib.tbdk_tbd_run_host(
+            self.handle, ptrs, int(frames.stride(1)), int(first_frame_id),
+            C.cast(cat.ctypes.data, C.POINTER(_lib.Detection)),
+            C.cast(offs.ctypes.data, C.POINTER(C.c_int32)), nf, ms, _stream_ptr(stream)), "tbdk_tbd_run_host")
+        return ms[:nf]
+
     def set_trajectories(self, traj: "Trajectories | None"):
         """Record per-object tracking results of detections with ground-truth ids
         (tbdk_tbd_set_trajectories); keep `traj` alive while attached."""

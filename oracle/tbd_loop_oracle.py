@@ -60,14 +60,18 @@ class KltTbdLoop:
     def __init__(self, width, height, win=21, max_level=2, lk_iters=30, lk_epsilon=0.01, min_eig=1e-4,
                  max_corners=256, quality=0.01, min_distance=3.0, redetect_every=5, min_points=32,
                  min_fit_points=4, bounds=(0, 1280, 0, 720), max_tracks=1024, accum=None, nthreads=16,
-                 **tracker_args):
+                 tracker=None, gftt_pool=None, **tracker_args):
+        """tracker: an object with tbd_oracle.Tracker's step / tracks / metric lists
+        (default: tbd_oracle.Tracker); gftt_pool: an executor running the ROIs'
+        goodFeaturesToTrack calls concurrently (default: one after another)."""
         self.W, self.H = width, height
         self.win, self.ml, self.iters, self.eps, self.min_eig = win, max_level, lk_iters, lk_epsilon, min_eig
         self.max_corners, self.quality, self.min_distance = max_corners, quality, min_distance
         self.redetect, self.min_points, self.min_fit = redetect_every, min_points, min_fit_points
         self.accum = O.ACCUM_EXACT if accum is None else accum
         self.nthreads = nthreads
-        self.tracker = T.Tracker(bounds=bounds, **tracker_args)
+        self.tracker = tracker if tracker is not None else T.Tracker(bounds=bounds, **tracker_args)
+        self.gftt_pool = gftt_pool
         self.prev = None
         self.sets = {}     # track id -> float32 (n, 2) corners of the last frame
         self.npts = {}     # track id -> corners left after the last fit
@@ -137,7 +141,12 @@ class KltTbdLoop:
                 continue
             rois.append((x0, y0, x1 - x0, y1 - y0))
             owners.append(t.id)
-        for i, c in zip(owners, O.gftt_rois(frame, rois, self.max_corners, self.quality, self.min_distance)):
+        if self.gftt_pool is not None:
+            found = list(self.gftt_pool.map(lambda r: O.gftt_rois(frame, [r], self.max_corners, self.quality,
+                                                                   self.min_distance)[0], rois))
+        else:
+            found = O.gftt_rois(frame, rois, self.max_corners, self.quality, self.min_distance)
+        for i, c in zip(owners, found):
             self.sets[i] = np.ascontiguousarray(c, np.float32)
         self.prev = P
         self.preds = preds

@@ -12,7 +12,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+# TBDK_ORACLE_LIB: another build of the same sources (bench.py's CPU baseline
+# builds one with -O3 -march=native on the host it runs on)
+ORACLE_LIB = os.environ.get("TBDK_ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle.so")
 
 ACCUM_SSE2 = 0
 ACCUM_EXACT = 1

@@ -55,3 +55,88 @@ def test_single_rank_needs_no_collective():
 
     assert bench.max_over_ranks(3.0, 1) == 3.0
     assert bench.replica_throughput(100, 1, 0.5) == 200.0
+
+
+class _FakeMeasure:
+    """Stands in for bench.TbdMeasure: records the seed, sleeps per step."""
+
+    def __init__(self, per_step):
+        self.per_step, self.seed, self.warm = per_step, None, None
+
+    def prepare(self, seed):
+        self.seed = seed
+
+    def warmup(self, w):
+        self.warm = w
+
+    def timed(self, k):
+        import time
+
+        time.sleep(self.per_step * k)
+        return list(range(k))
+
+
+def _contract_worker(rank, world, port, q):
+    import argparse
+
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = argparse.Namespace(seed=100, warmup=3, steps=10)
+    calls = []
+    m = _FakeMeasure([0.01, 0.03][rank])  # rank 1 is the straggler
+    line, per = bench.run_contract(args, world, rank, m, lambda: None, "cpu", cpu_leg=lambda: calls.append(1) or 1)
+    q.put((rank, m.seed, m.warm, len(per), line["value"], line["ms_per_step"], line["cpu_baseline"], len(calls)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_contract_rank_plumbing_world_size_2():
+    """bench.run_contract under gloo, world size 2, GPU legs stubbed: each rank
+    runs its own sequence (seed + rank), the job time is the slower rank's, the
+    value counts both ranks' steps, and no CPU baseline runs at N > 1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_contract_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [100, 101] and all(r[2] == 3 and r[3] == 10 for r in res)
+    assert res[0][4] == res[1][4] and res[0][5] == res[1][5]  # one job time on every rank
+    el = res[0][5] * 10 / 1000.0
+    assert el >= 0.3 and abs(res[0][4] - 2 * 10 / el) < 1e-6 * res[0][4] + 0.02  # slowest rank's 0.3 s
+    assert all(r[6] is None and r[7] == 0 for r in res)
+
+
+def test_run_contract_single_rank_runs_cpu_baseline():
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    calls = []
+    args = argparse.Namespace(seed=7, warmup=1, steps=4)
+    line, per = bench.run_contract(args, 1, 0, _FakeMeasure(0.001), lambda: None, "cpu",
+                                   cpu_leg=lambda: calls.append(1) or {"value": 1.0})
+    assert calls == [1] and line["cpu_baseline"] == {"value": 1.0}
+    assert line["n_gpus"] == 1 and line["steps"] == 4 and len(per) == 4
+    assert abs(line["value"] - 4 / (line["ms_per_step"] * 4 / 1000.0)) < 0.05 * line["value"]
+
+
+def test_host_topology_helpers():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    n, info = bench.host_cores()
+    assert 1 <= n <= info["affinity_cpus"]
+    r = bench.pin_rank(0)  # no KFD topology here: nothing pinned, nothing changed
+    assert isinstance(r, dict) and "pinned" in r

@@ -207,3 +207,19 @@ def test_rejects_bad_arguments(gpu):
             F.FarnebackOpticalFlow.create(ctx=gpu, **kw).calc(a, a)
     with pytest.raises(_lib.TbdkError):
         F.FarnebackOpticalFlow.create(ctx=gpu).calc(a, a[:32])
+
+
+@pytest.mark.parametrize("flags,direct", [(0, True), ("gauss", False)])
+def test_4k_pair_bit_exact(gpu, flags, direct):
+    """BASELINE configs[4] at its full size: the bench's 3840x2160 synthetic pair
+    (seed + 7, 512 objects) with cv::cuda::FarnebackOpticalFlow's defaults
+    (5 levels, pyrScale 0.5, winSize 13, 10 iterations, polyN 5, sigma 1.1).
+    Box variant (the bench's) against the oracle's exact-order mode, the
+    Gaussian variant against the reference order: bit-exact over all 8.3 Mpx
+    (optflowgf.cpp:1096-1191)."""
+    f = O.FARNEBACK_GAUSSIAN if flags == "gauss" else 0
+    fr, _ = O.synth(20261015 + 7, 3840, 2160, 512, 0, 2)
+    ref = O.farneback(fr[0], fr[1], flags=f, box_direct=direct)
+    got = _gpu_flow(gpu, fr[0], fr[1], flags=f)
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
+    assert np.isfinite(ref).all() and np.abs(ref).max() > 0.5  # real motion, not a trivial field

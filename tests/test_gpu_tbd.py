@@ -234,3 +234,25 @@ def test_tbd_zero_copy_matches_copies(gpu):
     finally:
         gpu.set_option("tbd_zero_copy", 1)
     assert res[0] == res[1]
+
+
+def test_tbd_run_host_matches_run(gpu):
+    """tbdk_tbd_run_host (frames uploaded from pinned host memory through the
+    three-frame device ring) gives the same frames as tbdk_tbd_run on the same
+    frames resident in HBM, over two calls on one loop (the ring is reused)
+    and from pageable memory too."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 32, 14
+    frames, gt = klt.synth_render(12, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
+    ref = tbd.TbdLoop(c, ctx=gpu)
+    want = [_mkey(m) for m in ref.run(frames, 0, dets)]
+    host = frames.cpu().pin_memory()
+    for src in (host, frames.cpu()):
+        loop = tbd.TbdLoop(c, ctx=gpu)
+        got = [_mkey(m) for m in loop.run_host(src[:9], 0, dets[:9])]
+        got += [_mkey(m) for m in loop.run_host(src[9:], 9, dets[9:])]
+        assert got == want
+        assert loop.tracks() == ref.tracks()

@@ -97,6 +97,6 @@ def test_tbd_loop_equals_oracle_pipeline_1080p_128(gpu, seed, drop):
 
 @pytest.mark.parametrize("k", range(8))
 def test_tbd_loop_equals_oracle_pipeline_kitti(gpu, k):
-    """BASELINE configs[3]: the KITTI-shaped 1242x375 sequences s..s+7 (one per GPU in the bench)."""
-    s = run_pair(gpu, 1242, 375, 48, 12, SEED + k)
+    """BASELINE configs[3]: the KITTI-shaped 1242x375 sequences s..s+7, 128 objects (one per GPU in the bench)."""
+    s = run_pair(gpu, 1242, 375, 128, 12, SEED + k)
     assert s["preds"] > 0

@@ -50,3 +50,26 @@ def test_loop_oracle_slot_pool_exhaustion():
             assert m["klt_predicted"] <= 4
     rows = lp.track_rows()
     assert sum(1 for r in rows if r[-1] > 0) <= 4
+
+
+def test_bench_cpu_baseline_leg_runs_on_cpu():
+    """bench.py's CPU baseline (the loop oracle with the C++ host tracker and
+    concurrent GFTT calls) runs and matches the pure-Python tracker's frames."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    fr, gt = L.O.synth(5, 640, 480, 8, 0, 6)
+    args = argparse.Namespace(bounds="frame", win=21, max_level=2, redetect=5)
+    fps, n = bench.cpu_baseline(fr, gt, args, 0.05, 2)
+    assert fps > 0 and n >= 3
+    # the native tracker adapter gives the same loop as the pure-Python tracker
+    from concurrent.futures import ThreadPoolExecutor
+
+    a = L.KltTbdLoop(640, 480, bounds=(0, 640, 0, 480), nthreads=2)
+    with ThreadPoolExecutor(2) as pool:
+        b = L.KltTbdLoop(640, 480, nthreads=2, tracker=bench._NativeTracker((0, 640, 0, 480)), gftt_pool=pool)
+        for f in range(6):
+            assert a.step(fr[f], f, L.detections(gt[f], f)) == b.step(fr[f], f, L.detections(gt[f], f))
+            assert a.track_rows() == b.track_rows()
