@@ -49,21 +49,31 @@ typedef struct tbdk_level {
     int32_t width, height, pitch, pad;
 } tbdk_level;
 
-/* A pyramid with derivatives, the layout of
- * cv::buildOpticalFlowPyramid(..., withDerivatives=true) (lkpyramid.cpp:765-780):
- * lv[i] are the u8 levels; dv[i] the Scharr derivative planes of calcSharrDeriv
- * (lkpyramid.cpp:55-144), CV_16SC2 interleaved (Ix, Iy) per pixel (4 bytes; pitch
- * in bytes) with a zero (BORDER_CONSTANT) frame of `pad` pixels. */
+/* A pyramid, the layout of cv::buildOpticalFlowPyramid (lkpyramid.cpp:697-793):
+ * lv[i] are the u8 levels, each with a reflect-101 frame of `pad` pixels; with
+ * derivatives (tbdk_pyr_create, withDerivatives=true, lkpyramid.cpp:765-780)
+ * dv[i] are the Scharr planes of calcSharrDeriv (lkpyramid.cpp:55-144), CV_16SC2
+ * interleaved (Ix, Iy) per pixel (4 bytes; pitch in bytes) with a zero
+ * (BORDER_CONSTANT) frame of `pad` pixels; without (tbdk_pyr_create_levels)
+ * dv[i].data is NULL and tbdk_lk_sparse derives the window's Scharr values
+ * itself (same results).  A tbdk_pyr must come from tbdk_pyr_create* (which
+ * fill every field); callers never fill one themselves.
+ * ABI 2 (TBDK_ABI_VERSION): `depth` and `flags` follow `storage`, so every
+ * field before them has its offset of the original (depth-less) layout. */
 typedef struct tbdk_pyr {
     int32_t nlevels;                 /* levels built = maxLevel used + 1 */
     int32_t win_w, win_h;            /* window the level count was derived for */
-    int32_t depth;                   /* TBDK_DEPTH_8U (tbdk_pyr_create) or TBDK_DEPTH_16F
-                                        (tbdk_pyr_create_f16: fp16 levels, fp16 (Ix, Iy)
-                                        derivative pairs) */
     tbdk_level lv[TBDK_MAX_LEVELS];
     tbdk_level dv[TBDK_MAX_LEVELS];
     void* storage;                   /* owned by the library; free with tbdk_pyr_destroy */
+    int32_t depth;                   /* TBDK_DEPTH_8U (tbdk_pyr_create*) or TBDK_DEPTH_16F
+                                        (tbdk_pyr_create_f16: fp16 levels, fp16 (Ix, Iy)
+                                        derivative pairs) */
+    int32_t flags;                   /* TBDK_PYR_NO_DERIVS: levels only */
 } tbdk_pyr;
+
+#define TBDK_ABI_VERSION 2
+#define TBDK_PYR_NO_DERIVS 1
 
 /* cv::TermCriteria(COUNT+EPS, maxCount, epsilon) + flags + minEigThreshold of
  * cv::calcOpticalFlowPyrLK (video/include/opencv2/video/tracking.hpp:178-183) */
@@ -92,6 +102,13 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       eigenvalue strips as a fresh-start mismatch, forcing the re-walk
  *       rounds taken when a segment's fresh start differs from the
  *       reference's running box-filter sum (results equal).
+ *   "pyr_fuse" (0/1, default 1): tbdk_pyr_build computes the level copy and
+ *       two levels below it per launch (levels of at least pad + 1 pixels);
+ *       0: one launch per level (results equal).
+ *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
+ *       kernel derives the window's Scharr values from the u8 level even when
+ *       the pyramid has derivative planes (it always does without them;
+ *       results equal).
  *   "lk_impl" (0..3): the PyrLK kernel taken when tbdk_lk_params.impl is 0
  *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
  *       (results equal).
@@ -162,6 +179,13 @@ int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr);
  * (modules/cudawarping/include/opencv2/cudawarping.hpp:201) — bit-exact with
  * the CPU pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857). */
 int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream);
+/* A u8 pyramid without derivative planes (flags TBDK_PYR_NO_DERIVS, dv[i].data
+ * NULL): levels only, built by tbdk_pyr_build in one fused launch for levels of
+ * at least pad + 1 pixels each way (the level copy and two levels below it per
+ * launch).  PyrLK on it derives the window's Scharr values in the kernel
+ * (identical results); the TBD loop's pyramids are of this kind. */
+int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h,
+                           tbdk_pyr* pyr);
 
 /* The fp16 pixel path (no reference implementation: the
  * reference's CPU PyrLK takes 8-bit levels only, lkpyramid.cpp:1272-1276, and
@@ -685,6 +709,8 @@ int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int n
 
 /* Library version string */
 const char* tbdk_version(void);
+/* TBDK_ABI_VERSION of the library (struct layouts of this header) */
+int tbdk_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,7 @@ TBDK_EHIP = -2
 TBDK_ENOMEM = -3
 TBDK_ENODEV = -4
 TBDK_MAX_LEVELS = 8
+TBDK_ABI_VERSION = 2  # include/tbdk.h: the struct layouts below
 OPTFLOW_USE_INITIAL_FLOW = 4
 OPTFLOW_LK_GET_MIN_EIGENVALS = 8
 
@@ -48,10 +49,11 @@ class Pyr(C.Structure):
         ("nlevels", C.c_int32),
         ("win_w", C.c_int32),
         ("win_h", C.c_int32),
-        ("depth", C.c_int32),
         ("lv", Level * TBDK_MAX_LEVELS),
         ("dv", Level * TBDK_MAX_LEVELS),
         ("storage", C.c_void_p),
+        ("depth", C.c_int32),
+        ("flags", C.c_int32),
     ]
 
 
@@ -174,6 +176,7 @@ _PI = C.POINTER(C.c_int)
 # name -> (restype, argtypes); every symbol include/tbdk.h declares
 SIGNATURES = {
     "tbdk_version": (C.c_char_p, []),
+    "tbdk_abi_version": (C.c_int, []),
     "tbdk_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "tbdk_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tbdk_ctx_device": (C.c_int, [C.c_void_p]),
@@ -186,6 +189,7 @@ SIGNATURES = {
     "tbdk_timing_calls": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_f16": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_create_levels": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_build_f16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
     "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
@@ -289,12 +293,19 @@ def load(path: str | None = None) -> C.CDLL:
         raise TbdkError(
             f"libtbdk.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP path has no CPU fallback)")
-    # torch carries its own libamdhip64.so.7 (same soname as /opt/rocm's): load it
-    # first so the process holds ONE HIP runtime, whichever of the two is imported
-    # first by the caller (two runtimes -> the second sees no device).
-    import torch  # noqa: F401
+    # TBDK_HOST_ONLY: TBDK_LIB is the host-only C++ build (tracker, sample
+    # driver; make host-asan), which exports only the host entry points and
+    # needs no HIP runtime (tests/test_host_sanitizers.py)
+    host_only = os.environ.get("TBDK_HOST_ONLY") == "1"
+    if not host_only:
+        # torch carries its own libamdhip64.so.7 (same soname as /opt/rocm's): load it
+        # first so the process holds ONE HIP runtime, whichever of the two is imported
+        # first by the caller (two runtimes -> the second sees no device).
+        import torch  # noqa: F401
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
+        if host_only and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

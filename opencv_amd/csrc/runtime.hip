@@ -67,6 +67,8 @@ extern "C" {
 
 const char* tbdk_version(void) { return "tbdk 0.1 (gfx950)"; }
 
+int tbdk_abi_version(void) { return TBDK_ABI_VERSION; }
+
 int tbdk_ctx_create(int device, tbdk_ctx** out)
 {
     if (!out) return TBDK_EINVAL;
@@ -166,6 +168,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_hog_block_tiled = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "pyr_fuse") == 0) {
+        ctx->opt_pyr_fuse = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "lk_scharr_fly") == 0) {
         ctx->opt_lk_scharr_fly = value != 0;
         return TBDK_OK;
@@ -225,7 +231,7 @@ int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls)
 
 // both depths: u8 (1 B/px) levels + int16x2 derivatives, or fp16 (2 B/px) + fp16x2
 static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, int depth,
-                      tbdk_pyr* pyr)
+                      int flags, tbdk_pyr* pyr)
 {
     if (!ctx || !pyr || width <= 0 || height <= 0 || max_level < 0 || win_w <= 2 || win_h <= 2 || win_w > 63 ||
         win_h > 63)
@@ -253,8 +259,10 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
         D.pad = pad;
         D.pitch = align_up((w + 2 * pad) * 4, 256);
         doffs[level] = total;
-        total += (size_t)D.pitch * (h + 2 * pad) + 256;
-        total = (total + 255) & ~(size_t)255;
+        if (!(flags & TBDK_PYR_NO_DERIVS)) {
+            total += (size_t)D.pitch * (h + 2 * pad) + 256;
+            total = (total + 255) & ~(size_t)255;
+        }
         nlev = level + 1;
         w = (w + 1) / 2;
         h = (h + 1) / 2;
@@ -264,6 +272,7 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
     hipError_t e = hipMalloc(&mem, total);
     if (e != hipSuccess) return map_err(e);
     // the derivative planes' BORDER_CONSTANT frame is zero once and never rewritten
+    // (levels only: every byte a reader can reach is rewritten by each build)
     e = hipMemset(mem, 0, total);
     if (e != hipSuccess) {
         (void)hipFree(mem);
@@ -274,9 +283,10 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
     pyr->win_w = win_w;
     pyr->win_h = win_h;
     pyr->depth = depth;
+    pyr->flags = flags;
     for (int level = 0; level < nlev; ++level) {
         pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
-        pyr->dv[level].data = static_cast<uint8_t*>(mem) + doffs[level];
+        pyr->dv[level].data = (flags & TBDK_PYR_NO_DERIVS) ? nullptr : static_cast<uint8_t*>(mem) + doffs[level];
     }
     return TBDK_OK;
 }
@@ -285,12 +295,17 @@ extern "C" {
 
 int tbdk_pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
 {
-    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, pyr);
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, 0, pyr);
+}
+
+int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+{
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, TBDK_PYR_NO_DERIVS, pyr);
 }
 
 int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
 {
-    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, pyr);
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, 0, pyr);
 }
 
 int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr)
@@ -312,10 +327,8 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     if (pyr->depth == TBDK_DEPTH_16F) {
         e = launch_pyr_build_f16(img, pitch, 0, *pyr, s);
     } else {
-        e = launch_pad_copy(img, pitch, pyr->lv[0], s);
-        for (int level = 1; e == hipSuccess && level < pyr->nlevels; ++level)
-            e = launch_pyr_down_padded(pyr->lv[level - 1], pyr->lv[level], s);
-        if (e == hipSuccess) e = launch_scharr_levels(*pyr, s);
+        e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse != 0, s);
+        if (e == hipSuccess && !(pyr->flags & TBDK_PYR_NO_DERIVS)) e = launch_scharr_levels(*pyr, s);
     }
     timing_end(ctx, rec, s);
     return map_err(e);
@@ -351,7 +364,7 @@ int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* ho
 
 int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16_t* host, int host_pitch)
 {
-    if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
+    if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels || !pyr->dv[level].data) return TBDK_EINVAL;
     const tbdk_level& D = pyr->dv[level];
     if (host_pitch < D.width * 4) return TBDK_EINVAL;
     const uint8_t* src = D.data + (size_t)D.pad * D.pitch + (size_t)D.pad * 4;

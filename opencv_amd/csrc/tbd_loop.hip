@@ -1,7 +1,7 @@
 // tbd_loop.hip — the per-stream tracking-by-detection loop (C ABI tbdk_tbd_*).
 //
 // Per frame (one HIP stream, one host thread per stream / GPU):
-//   1. pyramid (+ Scharr planes) of the new frame                       [HIP]
+//   1. pyramid of the new frame (levels only, one fused launch)          [HIP]
 //   2. sparse PyrLK of every live track's corners, prev -> new frame     [HIP, one launch,
 //      segmented layout: slot s owns points s*256 .. s*256+count[s]-1]
 //   3. tbd_fit_kernel, one wave per live track: ballot-compaction of the
@@ -330,7 +330,9 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     std::memset(t->pyr, 0, sizeof(t->pyr));
     int rc = TBDK_OK;
     for (int i = 0; i < 2 && rc == TBDK_OK; ++i)
-        rc = tbdk_pyr_create(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i]);
+        // levels only: PyrLK derives the window's Scharr values itself, so the
+        // build is one fused launch and writes no derivative planes
+        rc = tbdk_pyr_create_levels(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i]);
     if (rc != TBDK_OK) {
         release(t);
         return rc;

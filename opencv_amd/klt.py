@@ -96,13 +96,19 @@ class Pyramid:
     (Ix, Iy) planes."""
 
     def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21),
-                 dtype: torch.dtype = torch.uint8):
+                 dtype: torch.dtype = torch.uint8, derivs: bool = True):
+        """derivs=False (u8 only): levels without derivative planes
+        (tbdk_pyr_create_levels); PyrLK then derives the window's Scharr values
+        itself, with the same results."""
         if dtype not in (torch.uint8, torch.float16):
             raise _lib.TbdkError("Pyramid dtype must be torch.uint8 or torch.float16")
+        if not derivs and dtype != torch.uint8:
+            raise _lib.TbdkError("levels-only pyramids are u8")
         self.ctx = ctx
         self.dtype = dtype
         self.pyr = _lib.Pyr()
-        create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else ctx.lib.tbdk_pyr_create
+        create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else \
+            ctx.lib.tbdk_pyr_create if derivs else ctx.lib.tbdk_pyr_create_levels
         _lib.check(create(ctx.handle, int(width), int(height), int(max_level), int(win[0]), int(win[1]),
                           C.byref(self.pyr)), "tbdk_pyr_create")
         self.width, self.height = int(width), int(height)
@@ -161,12 +167,12 @@ class Pyramid:
 
 
 def build_pyramid(img: torch.Tensor, win=(21, 21), max_level: int = 3, ctx: Context | None = None,
-                  stream=None, dtype: torch.dtype | None = None) -> Pyramid:
-    """cv::buildOpticalFlowPyramid with derivatives; dtype torch.float16 (or a
-    float16 frame) selects the fp16 pixel path."""
+                  stream=None, dtype: torch.dtype | None = None, derivs: bool = True) -> Pyramid:
+    """cv::buildOpticalFlowPyramid (withDerivatives = derivs); dtype
+    torch.float16 (or a float16 frame) selects the fp16 pixel path."""
     ctx = ctx or Context.get(img.device.index or 0)
     dtype = dtype or (torch.float16 if img.dtype == torch.float16 else torch.uint8)
-    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype).build(img, stream)
+    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype, derivs).build(img, stream)
 
 
 def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torch.Tensor:

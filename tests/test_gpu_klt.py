@@ -77,6 +77,59 @@ def test_pyramid_bit_exact(gpu, shape, maxlev, win):
         assert np.array_equal(P.deriv(lvl), O.scharr(R.level(lvl))), f"deriv level {lvl}"
 
 
+@pytest.mark.parametrize("shape,maxlev,win", [((1080, 1920), 2, 21), ((1081, 1923), 2, 21), ((480, 640), 3, 21),
+                                             ((375, 1242), 3, 21), ((2160, 3840), 4, 21), ((137, 261), 2, 21),
+                                             ((61, 93), 4, 7), ((133, 70), 2, 21), ((66, 5000), 1, 21),
+                                             ((37, 29), 3, 15), ((300, 301), 5, 7)])
+def test_pyramid_levels_only_bit_exact(gpu, shape, maxlev, win):
+    """tbdk_pyr_create_levels: the fused build (padded level copy + two levels
+    below it per launch, LDS halos, reflect-101 mirrors written by the owners),
+    with the per-level fallback where a level is smaller than pad + 1; every
+    padded level bit-exact with the oracle's, padding included."""
+    K = klt()
+    img = np.random.default_rng(shape[1]).integers(0, 256, shape, dtype=np.uint8)
+    for _ in range(2):  # a rebuild rewrites every byte the first build wrote
+        P = K.build_pyramid(to_dev(img), (win, win), maxlev, ctx=gpu, derivs=False)
+        img = img[::-1].copy()
+    torch.cuda.synchronize()
+    assert not P.pyr.dv[0].data and P.pyr.flags == 1
+    R = O.Pyramid(img[::-1].copy(), (win, win), maxlev, pad=P.pyr.lv[0].pad)
+    assert P.nlevels == R.nlevels
+    for lvl in range(P.nlevels):
+        assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"level {lvl}"
+
+
+@pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])
+def test_lk_levels_only_equals_derivative_planes(gpu, win, maxlev):
+    """PyrLK on levels-only pyramids (the window's Scharr values derived in the
+    kernel, BORDER_CONSTANT zeros outside the level) and with ctx option
+    lk_scharr_fly on pyramids with planes: identical to the planes' results,
+    including windows over the frame edges and points outside it."""
+    K = klt()
+    fr, gt = K.synth_render(31 + win, 640, 480, 24, 0, 2, ctx=gpu)
+    rng = np.random.default_rng(win)
+    pts = np.concatenate([rng.uniform([-12, -12], [652, 492], (3000, 2)),
+                          np.array([[0, 0], [639, 479], [0.5, 240], [639.75, 10.25], [320, 0], [320, 479.5]])])
+    pts = pts.astype(np.float32)
+    lk = K.SparsePyrLKOpticalFlow((win, win), maxlev, 30)
+    out = {}
+    for mode in ("planes", "levels", "fly"):
+        d = mode != "levels"
+        Pa = K.build_pyramid(fr[0], (win, win), maxlev, ctx=gpu, derivs=d)
+        Pb = K.build_pyramid(fr[1], (win, win), maxlev, ctx=gpu, derivs=d)
+        gpu.set_option("lk_scharr_fly", 1 if mode == "fly" else 0)
+        try:
+            r = lk.calc(Pa, Pb, to_dev(pts), want_iters=True)
+            torch.cuda.synchronize()
+        finally:
+            gpu.set_option("lk_scharr_fly", 0)
+        out[mode] = [r.next_pts.cpu().numpy(), r.status.cpu().numpy(), r.err.cpu().numpy(), r.iters.cpu().numpy()]
+    for mode in ("levels", "fly"):
+        for a, b in zip(out["planes"], out[mode]):
+            assert np.array_equal(a, b), mode
+    assert out["planes"][1].mean() > 0.5
+
+
 @pytest.mark.parametrize("shape", [(1, 1), (3, 5), (480, 640), (1079, 1919), (375, 1242)])
 def test_pyr_down_plain_bit_exact(gpu, shape):
     K = klt()

@@ -25,7 +25,8 @@ import tbd_app_oracle as A  # noqa: E402
 import tbd_oracle as T  # noqa: E402
 from opencv_amd import _lib, tbd  # noqa: E402
 
-APP = os.path.join(ROOT, "opencv_amd", "bin", "tbdk_tbd_app")
+# TBDK_APP: another build of the CLI (tests/test_host_sanitizers.py runs a sanitized one)
+APP = os.environ.get("TBDK_APP") or os.path.join(ROOT, "opencv_amd", "bin", "tbdk_tbd_app")
 
 
 def write_gt_file(path, seed, nobj=24, nframes=60, start=0, w=1280, h=720, poses=False, history=None,

@@ -1,0 +1,32 @@
+"""tbdk_pyr_build timing: levels-only pyramids (one fused launch) vs pyramids
+with derivative planes (fused levels + the Scharr launch), 1080p / KITTI / 4K,
+HIP events over 200 builds each."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from opencv_amd import klt
+
+ctx = klt.Context.get(0)
+for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2), (1920, 1080, 3)):
+    fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
+    out = []
+    for derivs, fuse in ((False, 1), (False, 0), (True, 1)):
+        ctx.set_option("pyr_fuse", fuse)
+        P = klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=derivs)
+        for _ in range(20):
+            P.build(fr[0])
+        torch.cuda.synchronize()
+        ctx.timing_select(["pyr_build"])
+        ctx.timing_enable(True)
+        for i in range(200):
+            P.build(fr[i & 1])
+        torch.cuda.synchronize()
+        c, ms = ctx.timing_query("pyr_build")
+        ctx.timing_enable(False)
+        ctx.timing_select(None)
+        out.append(ms / c * 1000)
+    ctx.set_option("pyr_fuse", 1)
+    print(f"{W}x{H} maxLevel {ml}: levels only fused {out[0]:6.1f} us, per level {out[1]:6.1f} us; "
+          f"with Scharr planes {out[2]:6.1f} us")
