@@ -102,9 +102,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       eigenvalue strips as a fresh-start mismatch, forcing the re-walk
  *       rounds taken when a segment's fresh start differs from the
  *       reference's running box-filter sum (results equal).
- *   "pyr_fuse" (0/1, default 1): tbdk_pyr_build computes the level copy and
- *       two levels below it per launch (levels of at least pad + 1 pixels);
- *       0: one launch per level (results equal).
+ *   "pyr_fuse" (0/1, default 1): tbdk_pyr_build computes level 0's padded
+ *       copy and level 1 in one launch; 0: one launch per level (results
+ *       equal).
  *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;
@@ -180,10 +180,10 @@ int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr);
  * the CPU pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857). */
 int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream);
 /* A u8 pyramid without derivative planes (flags TBDK_PYR_NO_DERIVS, dv[i].data
- * NULL): levels only, built by tbdk_pyr_build in one fused launch for levels of
- * at least pad + 1 pixels each way (the level copy and two levels below it per
- * launch).  PyrLK on it derives the window's Scharr values in the kernel
- * (identical results); the TBD loop's pyramids are of this kind. */
+ * NULL): levels only; tbdk_pyr_build writes no Scharr planes (level 0's padded
+ * copy and level 1 in one launch, then one launch per level).  PyrLK on it
+ * derives the window's Scharr values in the kernel (identical results); the
+ * TBD loop's pyramids are of this kind. */
 int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h,
                            tbdk_pyr* pyr);
 

@@ -82,10 +82,11 @@ def test_pyramid_bit_exact(gpu, shape, maxlev, win):
                                              ((61, 93), 4, 7), ((133, 70), 2, 21), ((66, 5000), 1, 21),
                                              ((37, 29), 3, 15), ((300, 301), 5, 7)])
 def test_pyramid_levels_only_bit_exact(gpu, shape, maxlev, win):
-    """tbdk_pyr_create_levels: the fused build (padded level copy + two levels
-    below it per launch, LDS halos, reflect-101 mirrors written by the owners),
-    with the per-level fallback where a level is smaller than pad + 1; every
-    padded level bit-exact with the oracle's, padding included."""
+    """tbdk_pyr_create_levels: the fused build (the padded level-0 copy and
+    level 1, both straight from the frame with reflect-101 taps, in one launch;
+    then one pyrDown launch per level), tiny levels whose padding reflects more
+    than once included; every padded level bit-exact with the oracle's, padding
+    included."""
     K = klt()
     img = np.random.default_rng(shape[1]).integers(0, 256, shape, dtype=np.uint8)
     for _ in range(2):  # a rebuild rewrites every byte the first build wrote
