@@ -63,6 +63,10 @@ struct FbScratch {
     hipStream_t prep = nullptr;
     hipEvent_t fork = nullptr;
     hipEvent_t lev_ev[64] = {};
+    // the last tbdk_farneback call's stream and its completion: a call on
+    // another stream waits for it before reusing the scratch
+    hipStream_t last_stream = nullptr;
+    hipEvent_t done = nullptr;
 };
 
 namespace {
@@ -1193,6 +1197,7 @@ void fb_release(tbdk_ctx* ctx)
     if (ctx->fb->Rl) (void)hipFree(ctx->fb->Rl);
     if (ctx->fb->prep) (void)hipStreamDestroy(ctx->fb->prep);
     if (ctx->fb->fork) (void)hipEventDestroy(ctx->fb->fork);
+    if (ctx->fb->done) (void)hipEventDestroy(ctx->fb->done);
     for (hipEvent_t ev : ctx->fb->lev_ev)
         if (ev) (void)hipEventDestroy(ev);
     delete ctx->fb;
@@ -1278,6 +1283,12 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
     if (rc != TBDK_OK) return rc;
     FbScratch* f = ctx->fb;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    // every buffer of the scratch (R0 / R1 / Rl, T, I, the flow ping-pong) is
+    // still in use by the previous call until its stream reaches `done`
+    if (f->done && f->last_stream != s) {
+        const hipError_t w = hipStreamWaitEvent(s, f->done, 0);
+        if (w != hipSuccess) return map_status(w);
+    }
     const bool gauss = (p->flags & TBDK_OPTFLOW_FARNEBACK_GAUSSIAN) != 0;
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
@@ -1298,7 +1309,7 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
     }
     if (ahead) {
         if ((rc = fb_reserve_ahead(f, rtot, levels + 1)) != TBDK_OK) return rc;
-        e = hipEventRecord(f->fork, s);  // the previous call's readers of Rl, T, I are done
+        e = hipEventRecord(f->fork, s);  // the previous call's readers of Rl, T, I are done (any stream: see done)
         if (e == hipSuccess) e = hipStreamWaitEvent(f->prep, f->fork, 0);
     }
     auto prep_level = [&](int k, hipStream_t ps, float* R0, float* R1) {
@@ -1426,6 +1437,11 @@ int tbdk_farneback(tbdk_ctx* ctx, const uint8_t* prev, const uint8_t* next, int 
         ph = h;
         ppitch = pp;
     }
+    // the call's completion on s (its prep-stream work is joined into s by the
+    // level events before the last iterations)
+    if (e == hipSuccess && !f->done) e = hipEventCreateWithFlags(&f->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(f->done, s);
+    f->last_stream = s;
     return map_status(e);
 }
 
@@ -1443,7 +1459,12 @@ int tbdk_fb_level_image(tbdk_ctx* ctx, const uint8_t* img, int width, int height
     rc = fb_reserve(ctx, ctx->fb ? ctx->fb->cap_px : 0, (int64_t)height * tpitch);
     if (rc != TBDK_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    return map_status(launch_level_image(plan, img, width, height, pitch, ctx->fb->T, tpitch, dst, dst_width,
+    FbScratch* f = ctx->fb;  // T: ordered after the last tbdk_farneback call, as that call orders itself
+    if (f->done && f->last_stream != s) {
+        const hipError_t w = hipStreamWaitEvent(s, f->done, 0);
+        if (w != hipSuccess) return map_status(w);
+    }
+    return map_status(launch_level_image(plan, img, width, height, pitch, f->T, tpitch, dst, dst_width,
                                          dst_height, dst_pitch / 4, s));
 }
 

@@ -592,8 +592,9 @@ __global__ __launch_bounds__(256) void hog_window_kernel(HogWinArgs a)
 }
 
 // Batched window pass over 36-float blocks, one row of kHogWinTile windows per
-// workgroup: the blocks those windows share (their union: 20 x 11 at the
-// defaults instead of 16 x 55 block reads) and the detector are staged in LDS
+// workgroup: the blocks those windows share (their union: 20 x 11 for the
+// 48 x 96 detector, 22 x 15 for the 64 x 128 default, instead of 16 x 55 /
+// 16 x 105 block reads) and the detector are staged in LDS
 // once, coalesced; each wave then scores every fourth window exactly as
 // hog_window_kernel does (same products, sums and order), one lane per window
 // for the serial sums.
@@ -878,6 +879,26 @@ static hipError_t launch_grad(const uint8_t* img, int w, int h, int pitch, int c
 // dynamic LDS of the tiled block kernels: two workgroups per CU (the default
 // geometry takes 75 KB); above 64 KB the kernels opt in once per device
 constexpr size_t kHogTileLds = 80 * 1024;
+
+// the tiled window pass opts in to the whole LDS (the 64 x 128 detector's
+// tile takes ~76 KB: 22 x 15 blocks, the detector and 4 waves x 4 windows of
+// doubles); the limit leaves the kernel's static LDS its room
+constexpr size_t kHogWinTileLds = 160 * 1024 - 1024;
+
+static hipError_t win_lds_opt_in()
+{
+    static std::atomic<unsigned long long> opted{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (opted.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hog_window_tile_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHogWinTileLds);
+    if (e != hipSuccess) return e;
+    opted.fetch_or(bit, std::memory_order_acq_rel);
+    return hipSuccess;
+}
 
 static hipError_t tile_lds_opt_in()
 {
@@ -1362,7 +1383,7 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
         wtile.off_svm = wtile.rows * wtile.cols * 36;
         wtile.off_d = (wtile.off_svm + pl.wbx * pl.wby * 36 + 1) & ~1;
         wtile_lds = sizeof(float) * ((size_t)wtile.off_d + 2 * kHogWinTile * (size_t)(pl.wbx * pl.wby));
-        win_tiled = wtile_lds <= 64 * 1024;
+        win_tiled = wtile_lds <= kHogWinTileLds;
     }
     // every level's blocks get their own region of one buffer, so the window
     // pass runs once over all levels (small levels alone fill a fraction of the
@@ -1447,6 +1468,10 @@ int tbdk_hog_detect_multiscale(tbdk_ctx* ctx, const uint8_t* img, int width, int
             w.lv = S->lvtab, w.nlv = (int)ents.size();
             const int rec = timing_begin(ctx, "hog_window", s);
             if (win_tiled) {
+                e = wtile_lds > 64 * 1024 ? win_lds_opt_in() : hipSuccess;
+                if (e != hipSuccess) return map_status(e);
+                // "hog_window_tile": the tiled pass ran (tests count it; no event pair unless selected)
+                timing_end(ctx, timing_begin(ctx, "hog_window_tile", s), s);
                 hipLaunchKernelGGL(hog_window_tile_kernel, dim3(nwwg), dim3(256), wtile_lds, s, w, wtile);
             } else {
                 const size_t lds = sizeof(double) * 4 * kHogWinPerWg * (size_t)(pl.wbx * pl.wby);

@@ -538,6 +538,79 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
     }
 }
 
+// Partial selection (round 3): the greedy walk consumes the candidates in
+// descending key order and stops after max_corners accepted corners, typically
+// ~280 of ~700 candidates (1080p x 128 bench boxes: at most 312 of up to 2082).
+// Instead of sorting all of them, the 448 largest keys (plus the ties of the
+// 16-bit key prefix that reaches them) are found by a two-pass radix select on
+// the key's top 16 bits, moved to the front, and only they are sorted (512
+// keys); the others wait, unsorted, behind them.  Should the walk run out of
+// the sorted part before it is done, it takes the rest in descending order 64
+// at a time (wave-wide max selection); the walk's result does not depend on
+// how the candidates are batched, so the corners are the same.
+constexpr int kSelTarget = 448;
+constexpr int kSelRegs = 8;  // keys per thread held in registers while partitioning
+
+// wave 0: the bin where the running count from the top first reaches target,
+// and the count of keys in the bins above it (hist: 256 bins in LDS)
+__device__ __forceinline__ void radix_pick(const int* hist, int target, int lane, int* out_bin, int* out_above)
+{
+    int h[4], t = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        h[u] = hist[4 * lane + u];
+        t += h[u];
+    }
+    int suf = t;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_down(suf, d, 64);
+        suf += lane + d < 64 ? o : 0;
+    }
+    int above = suf - t;  // keys in the bins of the lanes above
+    if (above < target && suf >= target) {
+#pragma unroll
+        for (int u = 3; u >= 0; --u) {
+            if (above + h[u] >= target) {
+                *out_bin = 4 * lane + u;
+                *out_above = above;
+                break;
+            }
+            above += h[u];
+        }
+    }
+}
+
+// wave 0: the next (up to) 64 largest keys of an unsorted array (taken keys
+// are zeroed), lane l receiving the l-th; 0 when none is left
+__device__ uint64_t take_next64(uint64_t* rest, int nrest, int lane)
+{
+    uint64_t mine = 0ull;
+    for (int c = 0; c < 64; ++c) {
+        uint64_t best = 0ull;
+        int bi = -1;
+        for (int j = lane; j < nrest; j += 64) {
+            const uint64_t v = rest[j];
+            if (v > best) {
+                best = v;
+                bi = j;
+            }
+        }
+        uint64_t m = best;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t o = shfl_xor_u64(m, d);
+            m = o > m ? o : m;
+        }
+        if (m == 0ull) break;  // wave-uniform
+        if (bi >= 0 && best == m) rest[bi] = 0ull;  // keys are unique: one owner
+        if (lane == c) mine = m;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
+    return mine;
+}
+
 // LDS layout of the select kernel (one dynamic region):
 //   keys  : cap uint64 sort keys
 //   acc   : max_corners float2 accepted positions + 64 float2 (list mode)
@@ -642,9 +715,61 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
         if (tid == 0) a.counts[r] = -1;
         return;
     }
+    // ---- partial selection (see kSelTarget): the largest keys to the front
+    int S = total, nrest = 0;  // sorted part keys[0, S); the rest keys[kSelThreads, kSelThreads + nrest)
+    if (total > kSelThreads && total <= kSelRegs * kSelThreads && total + kSelThreads + 64 <= a.cap) {
+        __shared__ int hist[256];
+        __shared__ int s_pick[4];  // first-pass bin, keys above it; prefix, S
+        __shared__ int s_cnt[2];
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < total; i += kSelThreads) atomicAdd(&hist[(int)(keys[i] >> 56)], 1);
+        __syncthreads();
+        if (tid < 64) radix_pick(hist, kSelTarget, tid, &s_pick[0], &s_pick[1]);
+        __syncthreads();
+        const int b1 = s_pick[0], above1 = s_pick[1];
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < total; i += kSelThreads) {
+            const uint64_t k = keys[i];
+            if ((int)(k >> 56) == b1) atomicAdd(&hist[(int)(k >> 48) & 255], 1);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // second pass: the bin within b1 (the lane that holds it writes)
+            int b2 = -1, above2 = 0;
+            radix_pick(hist, kSelTarget - above1, tid, &b2, &above2);
+            if (b2 >= 0) {
+                s_pick[2] = (b1 << 8) | b2;
+                s_pick[3] = above1 + above2 + hist[b2];
+            }
+        }
+        if (tid == 0) s_cnt[0] = s_cnt[1] = 0;
+        __syncthreads();
+        const int sel = s_pick[3];
+        if (sel <= kSelThreads) {  // else: a wide tie of key prefixes, sort everything
+            const uint32_t t16 = (uint32_t)s_pick[2];
+            uint64_t kr[kSelRegs];
+#pragma unroll
+            for (int u = 0; u < kSelRegs; ++u) {
+                const int i = tid + u * kSelThreads;
+                kr[u] = i < total ? keys[i] : 0ull;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kSelRegs; ++u) {
+                if (tid + u * kSelThreads >= total) continue;
+                if ((uint32_t)(kr[u] >> 48) >= t16) keys[atomicAdd(&s_cnt[0], 1)] = kr[u];
+                else keys[kSelThreads + atomicAdd(&s_cnt[1], 1)] = kr[u];
+            }
+            __syncthreads();
+            S = sel;
+            nrest = total - sel;
+        }
+    }
     int np2 = kSelThreads;
-    while (np2 < total) np2 <<= 1;
-    for (int i = total + tid; i < np2; i += kSelThreads) keys[i] = 0ull;  // sorts last
+    while (np2 < S) np2 <<= 1;
+    for (int i = S + tid; i < np2; i += kSelThreads) keys[i] = 0ull;  // sorts last
     __syncthreads();
     GFTT_STAMP(1);
     switch (np2 / kSelThreads) {
@@ -663,11 +788,24 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     int n = 0;
     bool done = false;
     GFTT_TDECL;
-    for (int i0 = 0; i0 < total && !done; i0 += 64) {
+    int i0 = 0, rem = nrest;
+    while (!done) {
         GFTT_T(0);
-        const int i = i0 + lane;
-        const bool valid = i < total;
-        const uint32_t kk = valid ? (uint32_t)keys[i] : 0u;
+        // the sorted part 64 at a time, then (rarely) the rest in descending order
+        uint64_t key;
+        bool valid;
+        if (i0 < S) {
+            const int i = i0 + lane;
+            valid = i < S;
+            key = valid ? keys[i] : 0ull;
+            i0 += 64;
+        } else {
+            if (rem <= 0) break;  // wave-uniform
+            key = take_next64(keys + kSelThreads, nrest, lane);
+            valid = key != 0ull;
+            rem -= 64;
+        }
+        const uint32_t kk = (uint32_t)key;
         const int ix = (int)(kk & 0xFFFF), iy = (int)(kk >> 16);
         const float fx = (float)ix, fy = (float)iy;
         bool good = valid;
@@ -766,7 +904,7 @@ size_t gftt_select_smem(int cap, int max_corners, int img_bytes)
 // room for >= 4096 sort keys, else list mode with the largest key array
 void gftt_plan(GfttArgs& a, int max_area)
 {
-    const long lds = 160L * 1024 - 256;  // static LDS (counters) stays out of the dynamic budget
+    const long lds = 160L * 1024 - 2048;  // static LDS (counters, radix histogram) stays out of the dynamic budget
     const long fixed = (long)gftt_select_smem(0, a.max_corners, 0);
     long img = ((long)max_area + 15) & ~15L;
     long room = lds - fixed - img;

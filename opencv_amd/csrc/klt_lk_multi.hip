@@ -22,6 +22,8 @@
 //     active, J reloads when any point's integer origin moved), so every DPP and
 //     bpermute runs with all lanes on; a point that stopped keeps its values by
 //     selects.
+#include <type_traits>
+
 #include "lk_device.hpp"
 
 namespace tbdk {
@@ -153,6 +155,13 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 
 // waves per workgroup (tuning builds may change it; the kernel uses no LDS, so
 // one-wave workgroups let a finished wave's slot be refilled at once)
+// I x32 kept as packed row pairs and subtracted from the J pairs by one packed
+// op per row pair (1), or folded into each row's J rounding constant (0, one
+// VGPR per row; tuning builds)
+#ifndef TBDK_LK_IPACK
+#define TBDK_LK_IPACK 1
+#endif
+
 #ifndef TBDK_LK_MULTI_WAVES
 #define TBDK_LK_MULTI_WAVES 1
 #endif
@@ -248,11 +257,40 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         // started from ic and shifted right by 9 is diff = J x32 - I x32 itself
         // (2^9 * I is a multiple of the divisor: floor((X - 2^9 I) / 2^9) =
         // floor(X / 2^9) - I); Ix, Iy packed by row pairs as int16 x 2
+#if TBDK_LK_IPACK
+        uint32_t ipk[NP];  // I x32 of rows (2q, 2q+1) as int16 x 2
+#else
         int ic[WH];
+#endif
         uint32_t gxk[NP], gyk[NP];
         float A11, A12, A22;
         {
-            uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
+            int acc[3] = {0, 0, 0};
+            // one row pair of the setup: I x32 (-> ic), the interpolated Ix / Iy
+            // packed by row pairs (-> gxk, gyk) and the G sums, from the window
+            // rows' (I(x), I(x+1)), (Ix(x), Ix(x+1)), (Iy(x), Iy(x+1)) pairs
+            auto pair_step = [&](int q, uint32_t ip0, uint32_t ip1, uint32_t ip2, uint32_t dx0, uint32_t dx1,
+                                 uint32_t dx2, uint32_t dy0, uint32_t dy1, uint32_t dy2) {
+                const int r = 2 * q;
+                const bool two = r + 1 < WH;
+#if TBDK_LK_IPACK
+                const int i0 = bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9);
+                const int i1 = two ? bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) : 0;
+                ipk[q] = __builtin_amdgcn_perm((uint32_t)i1, (uint32_t)i0, 0x05040100u);
+#else
+                ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9) << 9);
+                if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) << 9);
+#endif
+                const int x0 = bilin_s<W_BITS1>(dx0, dx1, w0, w1, rnd14);
+                const int x1 = two ? bilin_s<W_BITS1>(dx1, dx2, w0, w1, rnd14) : 0;
+                const int y0 = bilin_s<W_BITS1>(dy0, dy1, w0, w1, rnd14);
+                const int y1 = two ? bilin_s<W_BITS1>(dy1, dy2, w0, w1, rnd14) : 0;
+                gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
+                gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
+                acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
+                acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
+                acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
+            };
             if constexpr (FLY) {
                 // calcSharrDeriv (lkpyramid.cpp:55-144) of the window, from the
                 // padded u8 level: one unaligned dword per row holds columns
@@ -262,7 +300,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 // hi - lo and (Iy(x), Iy(x+1)) = 3 (lo + hi) + 10 (t1(x), t1(x+1))
                 // directly as the pairs the bilinear sums take.  Integer and exact
                 // in 16 bits (|Ix|, |Iy| <= 4080); the level's reflect-101 frame is
-                // the reference's row / column reflection.
+                // the reference's row / column reflection.  The derivative rows are
+                // made as the row pairs consume them (a rolling window of three),
+                // so only the loaded dwords and the outputs are live at once.
                 const uint32_t ioff = act ? (uint32_t)((ipy - 1 + L.ipad) * L.ipitch + ipx + x - 1 + L.ipad) : 0u;
                 uint32_t u[WH + 3];
 #pragma unroll
@@ -272,30 +312,49 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 const bool edge = any_lane(act && (ipx < 0 || ipx + WW > L.w - 1 || ipy < 0 || ipy + WH > L.h - 1));
                 const uint32_t cm = ((unsigned)(ipx + x) < (unsigned)L.w ? 0x0000FFFFu : 0u) |
                                     ((unsigned)(ipx + x + 1) < (unsigned)L.w ? 0xFFFF0000u : 0u);
-#pragma unroll
-                for (int r = 0; r <= WH; ++r) {
+                auto drow = [&](auto mask, int r, uint32_t& ipo, uint32_t& dxo, uint32_t& dyo) {
                     const u16x2 al = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C010C00u));
                     const u16x2 ah = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C030C02u));
                     const u16x2 bl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C010C00u));
                     const u16x2 bh = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C030C02u));
                     const u16x2 cl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C010C00u));
                     const u16x2 ch = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C030C02u));
-                    ip[r] = __builtin_amdgcn_perm(0u, u[r + 1], 0x0C020C01u);  // (I(x), I(x+1))
+                    ipo = __builtin_amdgcn_perm(0u, u[r + 1], 0x0C020C01u);  // (I(x), I(x+1))
                     const u16x2 t0l = (al + cl) * (unsigned short)3 + bl * (unsigned short)10;
                     const u16x2 t0h = (ah + ch) * (unsigned short)3 + bh * (unsigned short)10;
                     const uint32_t t1l = as_u32(cl - al), t1h = as_u32(ch - ah);
                     const u16x2 mid = as_u16x2(__builtin_amdgcn_perm(t1h, t1l, 0x05040302u));  // (t1(x), t1(x+1))
                     uint32_t dx = as_u32(t0h - t0l);
                     uint32_t dy = as_u32((as_u16x2(t1l) + as_u16x2(t1h)) * (unsigned short)3 + mid * (unsigned short)10);
-                    if (edge) {
+                    if constexpr (decltype(mask)::value) {
                         const uint32_t m = (unsigned)(ipy + r) < (unsigned)L.h ? cm : 0u;
                         dx &= m;
                         dy &= m;
                     }
-                    dxp[r] = dx;
-                    dyp[r] = dy;
-                }
+                    dxo = dx;
+                    dyo = dy;
+                };
+                // the rows in pairs, each derivative row made as the pairs reach it
+                auto rows = [&](auto mask) {
+                    uint32_t ipa, dxa, dya, ipb = 0, dxb = 0, dyb = 0, ipc = 0, dxc = 0, dyc = 0;
+                    drow(mask, 0, ipa, dxa, dya);
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) {
+                        const int r = 2 * q;
+                        drow(mask, r + 1, ipb, dxb, dyb);
+                        if (r + 1 < WH) drow(mask, r + 2, ipc, dxc, dyc);
+                        pair_step(q, ipa, ipb, ipc, dxa, dxb, dxc, dya, dyb, dyc);
+                        ipa = ipc;
+                        dxa = dxc;
+                        dya = dyc;
+                    }
+                };
+                // (a wave-uniform choice between a masked and an unmasked copy of
+                // the rows needs 132 VGPRs against 102: the mask is three ops a row)
+                (void)edge;
+                rows(std::true_type{});
             } else {
+                uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
                 const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
                 const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4) : 0u;
 #pragma unroll
@@ -306,24 +365,20 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                     dxp[r] = __builtin_amdgcn_perm(d1, d0, 0x05040100u);  // (Ix(x), Ix(x+1))
                     dyp[r] = __builtin_amdgcn_perm(d1, d0, 0x07060302u);  // (Iy(x), Iy(x+1))
                 }
-            }
-            int acc[3] = {0, 0, 0};
 #pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                const int r = 2 * q;
-                const bool two = r + 1 < WH;
-                ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip[r], ip[r + 1], w0, w1, rnd9) << 9);
-                if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip[r + 1], ip[r + 2], w0, w1, rnd9) << 9);
-                const int x0 = bilin_s<W_BITS1>(dxp[r], dxp[r + 1], w0, w1, rnd14);
-                const int x1 = two ? bilin_s<W_BITS1>(dxp[r + 1], dxp[r + 2], w0, w1, rnd14) : 0;
-                const int y0 = bilin_s<W_BITS1>(dyp[r], dyp[r + 1], w0, w1, rnd14);
-                const int y1 = two ? bilin_s<W_BITS1>(dyp[r + 1], dyp[r + 2], w0, w1, rnd14) : 0;
-                gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
-                gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
-                acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
-                acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
-                acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
+                for (int q = 0; q < NP; ++q) {
+                    const int r = 2 * q;
+                    const int r2 = r + 2 <= WH ? r + 2 : WH;
+                    pair_step(q, ip[r], ip[r + 1], ip[r2], dxp[r], dxp[r + 1], dxp[r2], dyp[r], dyp[r + 1], dyp[r2]);
+                }
             }
+#if TBDK_LK_IPACK
+            // materialise the I pairs here: left to the compiler, their bilinear
+            // sums sink below the G reduction and the J loads, where the I
+            // rows they read are then still live (+22 VGPRs at the peak)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(ipk[q]));
+#endif
             if (k >= P) acc[0] = acc[1] = acc[2] = 0;
             float s[3];
             seg_sum_exact<3>(acc, e4, s4, s);
@@ -381,11 +436,22 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             for (int q = 0; q < NP; ++q) {
                 const int r = 2 * q;
                 // (diff_r, diff_r+1) as int16 x 2, |diff| <= 8160
+#if TBDK_LK_IPACK
+                // (J x32 of rows r, r+1) as int16 x 2, minus the I pair: one packed subtract
+                const uint32_t jv = r + 1 < WH ? pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9),
+                                                           bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9))
+                                               : pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9), 0);
+                const uint32_t d = as_u32(as_s16x2(jv) - as_s16x2(ipk[q]));
+#else
                 const uint32_t d = r + 1 < WH ? pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]),
                                                           bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]))
                                               : pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]), 0);
+#endif
                 b[0] = sdot2(d, gxk[q], b[0]);
                 b[1] = sdot2(d, gyk[q], b[1]);
+#ifdef TBDK_LK_NEWTON_SB
+                if (q % TBDK_LK_NEWTON_SB == TBDK_LK_NEWTON_SB - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
             }
             if (k >= P) b[0] = b[1] = 0;
             float fb[2];
@@ -428,10 +494,19 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #pragma unroll
                 for (int q = 0; q < NP; ++q) {
                     const int r = 2 * q;
+#if TBDK_LK_IPACK
+                    const int d0 = (bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] & 0xFFFFu);
+#else
                     const int d0 = bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]) >> 9;
+#endif
                     e += d0 < 0 ? -d0 : d0;
                     if (r + 1 < WH) {
+#if TBDK_LK_IPACK
+                        const int d1 =
+                            (bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] >> 16);
+#else
                         const int d1 = bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]) >> 9;
+#endif
                         e += d1 < 0 ? -d1 : d1;
                     }
                 }

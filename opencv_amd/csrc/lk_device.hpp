@@ -15,6 +15,8 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // packed 16-
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 __device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
 {

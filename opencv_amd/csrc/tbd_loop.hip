@@ -710,8 +710,19 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         auto ts0 = clk::now();
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
         // the one host wait of the frame, on the critical path: poll instead of
-        // a blocking synchronize (its wake-up latency is part of every frame)
+        // a blocking synchronize (its wake-up latency is part of every frame).
+        // The poll pauses between queries (the core's sibling thread keeps its
+        // issue slots) and gives up the core after kSpinUs: a fit that takes
+        // that long is not the per-frame case, and a blocking wait then costs
+        // nothing that matters.  One host core per loop while it spins
+        // (threading).
+        constexpr double kSpinUs = 2000.0;
         while ((e = hipEventQuery(t->fit_done)) == hipErrorNotReady) {
+            for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+            if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
+                e = hipEventSynchronize(t->fit_done);
+                break;
+            }
         }
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);

@@ -223,3 +223,31 @@ def test_4k_pair_bit_exact(gpu, flags, direct):
     got = _gpu_flow(gpu, fr[0], fr[1], flags=f)
     assert np.array_equal(got, ref), np.abs(got - ref).max()
     assert np.isfinite(ref).all() and np.abs(ref).max() > 0.5  # real motion, not a trivial field
+
+
+def test_calls_on_alternating_streams(gpu):
+    """Back-to-back calls on different streams share the context's scratch: a
+    call on another stream waits for the previous call's completion (the
+    prep-ahead fork orders only the caller's own stream), so every flow equals
+    the one computed alone."""
+    from opencv_amd import farneback as F
+
+    pairs = [_frames(900 + i, 640, 360, nobj=5) for i in range(4)]
+    fb = F.FarnebackOpticalFlow.create(ctx=gpu)
+    want = []
+    for a, b in pairs:
+        want.append(fb.calc(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()))
+        torch.cuda.synchronize()
+    want = [w.cpu().numpy() for w in want]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dev = [(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()) for a, b in pairs]
+    outs = [torch.empty((360, 640, 2), dtype=torch.float32, device="cuda") for _ in pairs]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, (a, b) in enumerate(dev):
+            st = streams[(i + rep) % 2]
+            with torch.cuda.stream(st):
+                fb.calc(a, b, outs[i], stream=st)
+        torch.cuda.synchronize()
+        for o, w in zip(outs, want):
+            assert np.array_equal(o.cpu().numpy(), w)

@@ -167,20 +167,33 @@ def test_detect_multiscale_level_streams_equal(gpu, lanes):
 @pytest.mark.parametrize("win", [(64, 128), (48, 96)])
 def test_window_pass_tiled_equals_per_window(gpu, win):
     """ctx option hog_window_tiled: the LDS-tiled window pass (rows of 16 windows,
-    ragged last tiles) and the per-window pass give the same rects and weights"""
+    ragged last tiles) and the per-window pass give the same rects and weights;
+    the tiled pass really runs for both detectors (the 64 x 128 default's tile
+    takes ~76 KB of LDS), counted through the "hog_window_tile" timing name"""
     hg = _hog(gpu, win)
     hg.setNumLevels(15)
     hg.setHitThreshold(-1.5)
     hg.setGroupThreshold(0)
     im = torch.from_numpy(_bgr(41, 700, 420, cn=3)).cuda()
-    ref = hg.detectMultiScale(im, confidences=True)
-    assert len(ref[0]) > 0
+
+    def run():
+        gpu.timing_select(["hog_window_tile"])
+        gpu.timing_enable(True)
+        try:
+            r = hg.detectMultiScale(im, confidences=True)
+            return r, gpu.timing_calls("hog_window_tile")
+        finally:
+            gpu.timing_enable(False)
+            gpu.timing_select(None)
+
+    ref, tiled = run()
+    assert len(ref[0]) > 0 and tiled > 0
     try:
         gpu.set_option("hog_window_tiled", 0)
-        got = hg.detectMultiScale(im, confidences=True)
+        got, tiled0 = run()
     finally:
         gpu.set_option("hog_window_tiled", 1)
-    assert got == ref
+    assert got == ref and tiled0 == 0
 
 
 def test_rejects_bad_arguments(gpu):
