@@ -142,8 +142,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       kernels read their host tables from, and the fit writes its results
  *       to, coherent pinned host memory directly instead of through copies
  *       (results equal).
- *   "timing_every" (>= 1, default 1): HIP events on every Nth launch of each
- *       kernel selected for timing (see tbdk_timing_calls). */
+ *   "timing_every" (>= 1, default 1): HIP events on a pseudo-random 1/N of the
+ *       launches of each kernel selected for timing: launch i (counted per
+ *       kernel name from tbdk_timing_enable) is timed iff splitmix64(i) % N == 0
+ *       (see tbdk_timing_calls). */
 
 /* device ordinal of the context */
 int tbdk_ctx_device(const tbdk_ctx* ctx);
@@ -159,7 +161,7 @@ int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double
  * "" = all).  Each timed launch costs two event records on the host. */
 int tbdk_timing_select(tbdk_ctx* ctx, const char* names);
 /* Selected launches of kernel `name` since tbdk_timing_enable, timed or not:
- * with the ctx option "timing_every" = N only every Nth of them records events
+ * with the ctx option "timing_every" = N only a 1/N sample of them records events
  * (tbdk_timing_query counts those), to keep the event records' host cost out
  * of a measured loop. */
 int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls);
@@ -260,7 +262,9 @@ typedef struct tbdk_gftt_params {
     int32_t max_corners;             /* > 0 */
     double quality_level;            /* > 0 */
     double min_distance;             /* >= 0 */
-    int32_t block_size;              /* 3 (the only supported value) */
+    int32_t block_size;              /* 1..63: cornerEigenValsVecs' box filter size */
+    int32_t use_harris;              /* 0: cornerMinEigenVal, 1: cornerHarris */
+    double harris_k;                 /* Harris k (cudaimgproc.hpp:604 default 0.04) */
 } tbdk_gftt_params;
 
 /* Replaces CornersDetector::detect (modules/cudaimgproc/src/gftt.cpp:98-213)
@@ -288,6 +292,15 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
  * scratch (one launch + one device copy on `stream`). */
 int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
                             int dst_pitch, void* stream);
+/* The corner response map of any blockSize (ksize 3, BORDER_REFLECT_101):
+ * cv::cuda::createMinEigenValCorner(CV_8UC1, blockSize, 3) (harris == 0) and
+ * cv::cuda::createHarrisCorner(CV_8UC1, blockSize, 3, k) (harris != 0)
+ * (cudaimgproc.hpp:548-566, corners.cpp:150-189), with the CPU
+ * cornerMinEigenVal / cornerHarris numerics (corner.cpp:52-152,237-326;
+ * Harris in the code paths an AVX x86-64 host runs).
+ * block_size 3 without Harris is tbdk_corner_min_eig_val. */
+int tbdk_corner_response(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
+                         int dst_pitch, int block_size, int harris, double harris_k, void* stream);
 int tbdk_gftt_reserve(tbdk_ctx* ctx, int max_rois, int64_t max_total_pixels);
 
 /* ---- KLT box propagation ----------------------------------------------------- */

@@ -245,17 +245,18 @@ private:
 };
 
 // cv::cuda::CornersDetector from createGoodFeaturesToTrackDetector(CV_8UC1,
-// maxCorners, qualityLevel, minDistance, blockSize=3, useHarris=false)
+// maxCorners, qualityLevel, minDistance, blockSize=3, useHarris=false, harrisK=0.04)
 // (cudaimgproc.hpp:582,603-604).  detect() runs on the whole image; detectRois()
 // is the batched per-box form the TBD loop uses (one launch set for all boxes).
 class CornersDetector {
 public:
     static std::unique_ptr<CornersDetector> create(Context& ctx, int maxCorners = 1000, double qualityLevel = 0.01,
                                                    double minDistance = 0.0, int blockSize = 3,
-                                                   bool useHarrisDetector = false, double /*harrisK*/ = 0.04)
+                                                   bool useHarrisDetector = false, double harrisK = 0.04)
     {
-        if (useHarrisDetector || blockSize != 3) throw Error(TBDK_EINVAL, "createGoodFeaturesToTrackDetector");
-        return std::unique_ptr<CornersDetector>(new CornersDetector(ctx, maxCorners, qualityLevel, minDistance));
+        if (blockSize < 1 || blockSize > 63) throw Error(TBDK_EINVAL, "createGoodFeaturesToTrackDetector");
+        return std::unique_ptr<CornersDetector>(
+            new CornersDetector(ctx, maxCorners, qualityLevel, minDistance, blockSize, useHarrisDetector, harrisK));
     }
 
     // corners: device, maxCorners float2; count: device int32 (corners found, -1 on
@@ -276,12 +277,14 @@ public:
     }
 
 private:
-    CornersDetector(Context& ctx, int maxc, double q, double md) : ctx_(&ctx)
+    CornersDetector(Context& ctx, int maxc, double q, double md, int block, bool harris, double k) : ctx_(&ctx)
     {
         p_.max_corners = maxc;
         p_.quality_level = q;
         p_.min_distance = md;
-        p_.block_size = 3;
+        p_.block_size = block;
+        p_.use_harris = harris ? 1 : 0;
+        p_.harris_k = k;
     }
     Context* ctx_;
     tbdk_gftt_params p_{};

@@ -80,6 +80,8 @@ class GfttParams(C.Structure):
         ("quality_level", C.c_double),
         ("min_distance", C.c_double),
         ("block_size", C.c_int32),
+        ("use_harris", C.c_int32),
+        ("harris_k", C.c_double),
     ]
 
 
@@ -183,6 +185,8 @@ SIGNATURES = {
     "tbdk_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "tbdk_corner_min_eig_val": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                           C.c_void_p]),
+    "tbdk_corner_response": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                       C.c_int, C.c_int, C.c_double, C.c_void_p]),
     "tbdk_ctx_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     "tbdk_timing_select": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbdk_timing_query": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),

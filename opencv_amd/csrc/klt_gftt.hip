@@ -548,6 +548,9 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
 // the sorted part before it is done, it takes the rest in descending order 64
 // at a time (wave-wide max selection); the walk's result does not depend on
 // how the candidates are batched, so the corners are the same.
+#ifndef TBDK_GFTT_PARTIAL
+#define TBDK_GFTT_PARTIAL 1  // 0: sort every candidate (A/B builds)
+#endif
 constexpr int kSelTarget = 448;
 constexpr int kSelRegs = 8;  // keys per thread held in registers while partitioning
 
@@ -717,7 +720,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     }
     // ---- partial selection (see kSelTarget): the largest keys to the front
     int S = total, nrest = 0;  // sorted part keys[0, S); the rest keys[kSelThreads, kSelThreads + nrest)
-    if (total > kSelThreads && total <= kSelRegs * kSelThreads && total + kSelThreads + 64 <= a.cap) {
+    if (TBDK_GFTT_PARTIAL && total > kSelThreads && total <= kSelRegs * kSelThreads && total + kSelThreads + 64 <= a.cap) {
         __shared__ int hist[256];
         __shared__ int s_pick[4];  // first-pass bin, keys above it; prefix, S
         __shared__ int s_cnt[2];
@@ -931,6 +934,11 @@ hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig)
         const hipError_t e = hipEventRecord(after_eig, s);
         if (e != hipSuccess) return e;
     }
+    return launch_gftt_select(a, s);
+}
+
+hipError_t launch_gftt_select(const GfttArgs& a, hipStream_t s)
+{
     const size_t smem = gftt_select_smem(a.cap, a.max_corners, a.img_bytes);
     // > 64 KiB of dynamic LDS must be opted into (160 KiB per CU on gfx950);
     // done once per device, for the whole LDS, off the per-frame path

@@ -1,5 +1,6 @@
 // runtime.hip — the C ABI of include/tbdk.h: contexts, pyramids, launches,
 // per-kernel HIP-event timing.  Host code, compiled by hipcc for gfx950.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +23,14 @@ static hipEvent_t take_event(tbdk_ctx* ctx)
     return e;
 }
 
+static uint64_t sample_hash(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
 int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
 {
     if (!ctx->timing) return -1;
@@ -35,7 +44,10 @@ int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
         ctx->timing_calls.emplace_back(name, 0);
         calls = &ctx->timing_calls.back().second;
     }
-    if ((*calls)++ % ctx->timing_every != 0) return -1;  // sampled: this launch is not timed
+    // sampled: launch i is timed iff splitmix64(i) % N == 0 -- a pseudo-random 1/N
+    // subset, so a per-frame pattern of differently sized launches (the TBD loop's
+    // four PyrLK call sites) cannot line up with the sampling period
+    if (sample_hash((uint64_t)(*calls)++) % (uint64_t)ctx->timing_every != 0) return -1;
     TimingRec r{name, take_event(ctx), take_event(ctx)};
     if (!r.begin || !r.end) return -1;
     (void)hipEventRecord(r.begin, s);
@@ -472,8 +484,10 @@ namespace tbdk {
 int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tbdk_gftt_params* p, GfttRoi* tab,
                  GfttPlan* plan)
 {
-    if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size != 3)
+    if (p->max_corners <= 0 || !(p->quality_level > 0) || p->min_distance < 0 || p->block_size < 1 ||
+        p->block_size > 63 || (p->use_harris != 0 && p->use_harris != 1) || !std::isfinite(p->harris_k))
         return TBDK_EINVAL;
+    if (gftt_generic(p) && nroi > 65535) return TBDK_EINVAL;  // the response launches' grid rows
     int64_t total = 0, ncblk = 0, words = 0;
     int max_area = 0;
     for (int i = 0; i < nroi; ++i) {
@@ -487,8 +501,11 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
         ncblk += strips;
         if (r.width >= 3 && r.height >= 3) words += strips * r.height;  // smaller ROIs have no interior
         max_area = std::max(max_area, r.width * r.height);
+        plan->max_w = std::max(plan->max_w, r.width);
+        plan->max_h = std::max(plan->max_h, r.height);
     }
     if (total > INT32_MAX || words > INT32_MAX) return TBDK_EINVAL;
+    if (gftt_generic(p) && total > INT32_MAX / 3) return TBDK_EINVAL;
     plan->nroi = nroi;
     plan->total = total;
     plan->ncblk = (int)ncblk;
@@ -497,14 +514,50 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
     return TBDK_OK;
 }
 
+static void gftt_resp_args(GfttRespArgs& ra, const GfttScratch& sc, const uint8_t* img, int pitch,
+                           const GfttRoi* d_rois, int nroi, int block, int harris, double hk)
+{
+    ra.img = img;
+    ra.pitch = pitch;
+    ra.rois = d_rois;
+    ra.nroi = nroi;
+    ra.cov = static_cast<float*>(sc.resp);
+    ra.rs = reinterpret_cast<double*>(static_cast<float*>(sc.resp) + 3 * (size_t)sc.cap_resp_px);
+    ra.eig = static_cast<float*>(sc.planes);
+    ra.blk_max = sc.blk;
+    ra.lmax = static_cast<uint64_t*>(sc.cand);
+    ra.block = block;
+    ra.harris = harris;
+    // cornerEigenValsVecs' scale for ksize 3 on 8-bit input (corner.cpp:248-255)
+    const double scale = 1.0 / ((double)(1 << 2) * block * 255.0);
+    ra.k = (float)(1.0 * scale);
+    ra.k2 = (float)(2.0 * scale);
+    ra.kf = (float)hk;
+    ra.hk = hk;
+}
+
 void gftt_scratch_free(GfttScratch& sc)
 {
-    for (void** p : {&sc.rois, reinterpret_cast<void**>(&sc.blk), &sc.planes, &sc.cand}) {
+    for (void** p : {&sc.rois, reinterpret_cast<void**>(&sc.blk), &sc.planes, &sc.cand, &sc.resp}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
     sc.cap_rois = 0;
     sc.cap_px = 0;
+    sc.cap_resp_px = 0;
+}
+
+int gftt_reserve_resp(GfttScratch& sc, int device, int64_t max_px)
+{
+    if (max_px <= sc.cap_resp_px) return TBDK_OK;
+    DeviceGuard g(device);
+    if (sc.resp) (void)hipFree(sc.resp);  // waits for the device: no launch still reads it
+    sc.resp = nullptr;
+    sc.cap_resp_px = 0;
+    const hipError_t e = hipMalloc(&sc.resp, (sizeof(float) * 3 + sizeof(double) * 3) * (size_t)std::max<int64_t>(max_px, 1));
+    if (e != hipSuccess) return map_err(e);
+    sc.cap_resp_px = max_px;
+    return TBDK_OK;
 }
 
 int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px)
@@ -555,7 +608,18 @@ int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, c
     a.counts = counts;
     a.eig_redo = ctx->opt_gftt_eig_redo;
     gftt_plan(a, plan.max_area);
-    hipError_t e = launch_gftt(a, s, after_eig);
+    hipError_t e;
+    if (!gftt_generic(p)) {
+        e = launch_gftt(a, s, after_eig);
+    } else {
+        rc = gftt_reserve_resp(sc, ctx->device, plan.total);
+        if (rc != TBDK_OK) return rc;
+        GfttRespArgs ra;
+        gftt_resp_args(ra, sc, img, pitch, d_rois, plan.nroi, p->block_size, p->use_harris, p->harris_k);
+        e = launch_gftt_resp(ra, plan.ncblk, plan.max_w, plan.max_h, plan.max_area, s);
+        if (e == hipSuccess && after_eig) e = hipEventRecord(after_eig, s);
+        if (e == hipSuccess) e = launch_gftt_select(a, s);
+    }
     timing_end(ctx, rec, s);
     return map_err(e);
 }
@@ -621,6 +685,39 @@ int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int he
     a.lmax = static_cast<uint64_t*>(ctx->gftt.cand);
     a.eig_redo = ctx->opt_gftt_eig_redo;
     e = launch_gftt_eig(a, s);
+    timing_end(ctx, rec, s);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)width * 4, (size_t)width * 4, height,
+                             hipMemcpyDeviceToDevice, s);
+    return map_err(e);
+}
+
+int tbdk_corner_response(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,
+                         int dst_pitch, int block_size, int harris, double harris_k, void* stream)
+{
+    if (!ctx || !img || !dst || width <= 0 || height <= 0 || pitch < width || dst_pitch < width * 4 ||
+        dst_pitch % 4 != 0 || block_size < 1 || block_size > 63 || !std::isfinite(harris_k))
+        return TBDK_EINVAL;
+    if (block_size == 3 && !harris)
+        return tbdk_corner_min_eig_val(ctx, img, width, height, pitch, dst, dst_pitch, stream);
+    tbdk_roi roi{0, 0, width, height};
+    tbdk_gftt_params p{1, 0.01, 0.0, block_size, harris ? 1 : 0, harris_k};
+    GfttPlan plan;
+    GfttRoi tab;
+    int rc = gftt_prepare(&roi, 1, width, height, &p, &tab, &plan);
+    if (rc != TBDK_OK) return rc;
+    rc = tbdk_gftt_reserve(ctx, 1, plan.total);
+    if (rc == TBDK_OK) rc = gftt_reserve_resp(ctx->gftt, ctx->device, plan.total);
+    if (rc != TBDK_OK) return rc;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemcpyAsync(ctx->gftt.rois, &tab, sizeof(GfttRoi), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return map_err(e);
+    int rec = timing_begin(ctx, "corner_response", s);
+    GfttRespArgs ra;
+    gftt_resp_args(ra, ctx->gftt, img, pitch, static_cast<const GfttRoi*>(ctx->gftt.rois), 1, block_size,
+                   harris ? 1 : 0, harris_k);
+    e = launch_gftt_resp(ra, plan.ncblk, plan.max_w, plan.max_h, plan.max_area, s);
     timing_end(ctx, rec, s);
     if (e == hipSuccess)
         e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)width * 4, (size_t)width * 4, height,

@@ -59,8 +59,10 @@ struct GfttScratch {
     int* blk = nullptr;      // per-strip eigenvalue maxima
     void* cand = nullptr;    // local-maximum words (uint64 per strip row)
     void* planes = nullptr;  // cap_px floats (eig)
+    void* resp = nullptr;    // blockSize != 3 / Harris: cov (3 floats) + row sums (3 doubles) per pixel
     int cap_rois = 0;
     int64_t cap_px = 0;
+    int64_t cap_resp_px = 0;
 };
 struct HogScratch;  // hog.hip
 
@@ -227,7 +229,7 @@ inline int64_t gftt_max_words(int64_t px) { return px / kGfttStrip + px / 3 + 1;
 size_t gftt_select_smem(int cap, int max_corners, int img_bytes);
 void gftt_plan(GfttArgs& a, int max_area);  // sets cap and img_bytes
 struct GfttPlan {
-    int nroi = 0, ncblk = 0, max_area = 0;
+    int nroi = 0, ncblk = 0, max_area = 0, max_w = 0, max_h = 0;
     int64_t total = 0;  // ROI pixels
     int64_t words = 0;  // local-maximum words
 };
@@ -244,4 +246,26 @@ int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, c
                 hipEvent_t after_eig = nullptr, int corner_stride = 0);  // 0: max_corners
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig = nullptr);
 hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s);  // eigenvalue planes only
+hipError_t launch_gftt_select(const GfttArgs& a, hipStream_t s);
+// blockSize != 3 or Harris (klt_gftt_resp.hip): the response plane, strip
+// maxima and local-maximum words in gftt_eig_kernel's layout
+struct GfttRespArgs {
+    const uint8_t* img;
+    int pitch;
+    const GfttRoi* rois;
+    int nroi;
+    float* cov;      // 3 floats per ROI pixel
+    double* rs;      // 3 doubles per ROI pixel
+    float* eig;      // response per ROI pixel
+    int* blk_max;
+    uint64_t* lmax;
+    int block;       // boxFilter size
+    int harris;      // 0: min eigenvalue, 1: Harris
+    float k, k2;     // Sobel taps x 1/(4*block*255)
+    float kf;        // (float)harris_k (the SIMD paths)
+    double hk;       // harris_k (the scalar path)
+};
+hipError_t launch_gftt_resp(const GfttRespArgs& a, int ncblk, int max_w, int max_h, int max_area, hipStream_t s);
+int gftt_reserve_resp(GfttScratch& sc, int device, int64_t max_px);
+inline bool gftt_generic(const tbdk_gftt_params* p) { return p->block_size != 3 || p->use_harris != 0; }
 }  // namespace tbdk

@@ -202,6 +202,23 @@ def corner_min_eigen_val(src: torch.Tensor, ctx: Context | None = None, stream=N
     return dst
 
 
+def corner_response(src: torch.Tensor, block_size: int = 3, harris: bool = False, k: float = 0.04,
+                    ctx: Context | None = None, stream=None) -> torch.Tensor:
+    """cv::cuda::createMinEigenValCorner(CV_8UC1, blockSize, 3) / createHarrisCorner(CV_8UC1,
+    blockSize, 3, k) ->compute (cudaimgproc.hpp:548-566): float32 (h, w) response map with
+    the CPU cornerMinEigenVal / cornerHarris numerics (corner.cpp:52-152,237-326)."""
+    if src.dtype != torch.uint8 or src.dim() != 2 or not src.is_cuda or src.stride(1) != 1:
+        raise _lib.TbdkError("corner_response expects a 2-D uint8 device tensor")
+    ctx = ctx or Context.get(src.device.index or 0)
+    h, w = src.shape
+    dst = torch.empty((h, w), dtype=torch.float32, device=src.device)
+    _lib.check(ctx.lib.tbdk_corner_response(ctx.handle, C.c_void_p(src.data_ptr()), w, h, src.stride(0),
+                                            C.c_void_p(dst.data_ptr()), dst.stride(0) * 4, int(block_size),
+                                            1 if harris else 0, float(k), _stream_ptr(stream)),
+               "tbdk_corner_response")
+    return dst
+
+
 # numpy mirror of tbdk_box_fit (include/tbdk.h)
 BOX_FIT_DTYPE = np.dtype([("m", "<f8", 6), ("cx", "<f8"), ("cy", "<f8"), ("npoints", "<i4"), ("valid", "<i4")])
 
@@ -391,14 +408,14 @@ class DensePyrLKOpticalFlow(SparsePyrLKOpticalFlow):
 
 class GoodFeaturesToTrackDetector:
     """cv::cuda::createGoodFeaturesToTrackDetector(CV_8UC1, maxCorners, qualityLevel,
-    minDistance, blockSize=3) (cudaimgproc.hpp:603-604) with the CPU
-    goodFeaturesToTrack semantics, applied to a batch of box ROIs of one image."""
+    minDistance, blockSize=3, useHarrisDetector=False, harrisK=0.04)
+    (cudaimgproc.hpp:603-604) with the CPU goodFeaturesToTrack semantics, applied
+    to a batch of box ROIs of one image."""
 
     def __init__(self, maxCorners: int = 1000, qualityLevel: float = 0.01, minDistance: float = 0.0,
-                 blockSize: int = 3, useHarrisDetector: bool = False, device: int = 0):
-        if useHarrisDetector:
-            raise _lib.TbdkError("Harris response is not implemented (min-eigenvalue only)")
-        self.prm = _lib.GfttParams(int(maxCorners), float(qualityLevel), float(minDistance), int(blockSize))
+                 blockSize: int = 3, useHarrisDetector: bool = False, harrisK: float = 0.04, device: int = 0):
+        self.prm = _lib.GfttParams(int(maxCorners), float(qualityLevel), float(minDistance), int(blockSize),
+                                   1 if useHarrisDetector else 0, float(harrisK))
         self.ctx = Context.get(device)
 
     def detect_rois(self, image: torch.Tensor, rois, stream=None):

@@ -94,6 +94,115 @@ void orc_min_eig(const uint8_t* img, int w, int h, int pitch, float* eig)
     free(dx); free(dy); free(rx); free(ry); free(cov); free(rs); free(sum);
 }
 
+/* cornerMinEigenVal / cornerHarris for any blockSize (ksize 3, u8 source,
+ * BORDER_REFLECT_101), restating cornerEigenValsVecs (corner.cpp:237-326):
+ *   scale = 1 / (4 * blockSize * 255); the ksize-3 Sobel rows as above
+ *   boxFilter(cov, blockSize, anchor blockSize/2, unnormalised, CV_64F sums):
+ *     RowSum (box_filter.simd.hpp:64-170, cn = 3): ksize 3 and 5 add the taps
+ *       left to right; other sizes run s = 0 + taps, then s += (S[i+k] - S[i])
+ *       along the bordered row
+ *     ColumnSum<double,float> (:175-273): SUM = 0 + the first ksize-1 rows,
+ *       then per row s = SUM + Sp; out = (float)s; SUM = s - Sm
+ *   calcMinEigenVal (:52-101): (a + c) - sqrt(t*t + b*b), a, c halved (all
+ *     three code paths round alike)
+ *   calcHarris (:104-152) over the continuous (flattened) map, index j: the
+ *     AVX lines (corner.avx.cpp:144-160: acbb - k*(ac*ac), k as float) for
+ *     j < N & ~7, one SSE2 block ((acbb) - (k*ac)*ac) if 4 more remain, the
+ *     scalar double expression for the rest: the code an AVX x86-64 host runs. */
+void orc_corner_response(const uint8_t* img, int w, int h, int pitch, int block, int harris, double hk, float* out)
+{
+    const double scale = 1.0 / ((double)(1 << 2) * block * 255.0);
+    const float k = (float)(1.0 * scale), k2 = (float)(2.0 * scale);
+    const size_t n = (size_t)w * h;
+    float* cov = (float*)malloc(sizeof(float) * 3 * (n ? n : 1));
+    for (int y = 0; y < h; ++y) {
+        const uint8_t* r0 = img + (size_t)orc_reflect101(y - 1, h) * pitch;
+        const uint8_t* r1 = img + (size_t)y * pitch;
+        const uint8_t* r2 = img + (size_t)orc_reflect101(y + 1, h) * pitch;
+        for (int x = 0; x < w; ++x) {
+            const int xl = orc_reflect101(x - 1, w), xr = orc_reflect101(x + 1, w);
+            float rx[3], ry[3];
+            const uint8_t* rr[3] = {r0, r1, r2};
+            for (int j = 0; j < 3; ++j) {
+                const float s0 = rr[j][xl], s1 = rr[j][x], s2 = rr[j][xr];
+                float t = -1.f * s0;
+                t = t + 0.f * s1;
+                t = t + 1.f * s2;
+                rx[j] = t;
+                float u = k * s0;
+                u = u + k2 * s1;
+                u = u + k * s2;
+                ry[j] = u;
+            }
+            const float dx = (rx[0] + rx[2]) * k + (rx[1] * k2 + 0.f);
+            const float dy = (ry[2] - ry[0]) + 0.f;
+            float* c = cov + 3 * ((size_t)y * w + x);
+            c[0] = dx * dx;
+            c[1] = dx * dy;
+            c[2] = dy * dy;
+        }
+    }
+    const int anc = block / 2;
+    double* rs = (double*)malloc(sizeof(double) * 3 * (n ? n : 1));
+    for (int y = 0; y < h; ++y) {
+        const float* c = cov + 3 * (size_t)y * w;
+        double* d = rs + 3 * (size_t)y * w;
+        for (int ch = 0; ch < 3; ++ch) {
+#define TAP(i) ((double)c[3 * orc_reflect101((i) - anc, w) + ch]) /* bordered-row element i */
+            if (block == 3 || block == 5) {
+                for (int x = 0; x < w; ++x) {
+                    double s = TAP(x) + TAP(x + 1);
+                    for (int t = 2; t < block; ++t) s = s + TAP(x + t);
+                    d[3 * x + ch] = s;
+                }
+            } else {
+                double s = 0;
+                for (int t = 0; t < block; ++t) s += TAP(t);
+                d[ch] = s;
+                for (int x = 0; x + 1 < w; ++x) {
+                    s += TAP(x + block) - TAP(x);
+                    d[3 * (x + 1) + ch] = s;
+                }
+            }
+#undef TAP
+        }
+    }
+    double* sum = (double*)malloc(sizeof(double) * 3 * (size_t)(w ? w : 1));
+    for (int i = 0; i < 3 * w; ++i) sum[i] = 0.0;
+    for (int r = 0; r < block - 1; ++r) {
+        const double* sp = rs + 3 * (size_t)orc_reflect101(r - anc, h) * w;
+        for (int i = 0; i < 3 * w; ++i) sum[i] += sp[i];
+    }
+    const size_t avx_end = n & ~(size_t)7, sse_end = avx_end + (n - avx_end >= 4 ? 4 : 0);
+    const float kf = (float)hk;
+    for (int y = 0; y < h; ++y) {
+        const double* sp = rs + 3 * (size_t)orc_reflect101(y - anc + block - 1, h) * w; /* entering */
+        const double* sm = rs + 3 * (size_t)orc_reflect101(y - anc, h) * w;             /* leaving */
+        for (int x = 0; x < w; ++x) {
+            float box[3];
+            for (int ch = 0; ch < 3; ++ch) {
+                const int i = 3 * x + ch;
+                const double s0 = sum[i] + sp[i];
+                box[ch] = (float)s0;
+                sum[i] = s0 - sm[i];
+            }
+            const size_t j = (size_t)y * w + x;
+            if (!harris) {
+                const float a = box[0] * 0.5f, b = box[1], c = box[2] * 0.5f;
+                const float t = a - c;
+                out[j] = (a + c) - sqrtf(b * b + t * t);
+            } else {
+                const float a = box[0], b = box[1], c = box[2];
+                const float acbb = a * c - b * b, ac = a + c;
+                if (j < avx_end) out[j] = acbb - kf * (ac * ac);
+                else if (j < sse_end) out[j] = acbb - (kf * ac) * ac;
+                else out[j] = (float)((double)acbb - hk * (double)ac * (double)ac);
+            }
+        }
+    }
+    free(cov); free(rs); free(sum);
+}
+
 typedef struct { float v; int idx; } orc_cand;
 
 static int orc_cand_cmp(const void* pa, const void* pb)
@@ -105,12 +214,15 @@ static int orc_cand_cmp(const void* pa, const void* pb)
     return (a->idx > b->idx) ? -1 : (a->idx < b->idx ? 1 : 0);  /* higher address first */
 }
 
-int orc_gftt(const uint8_t* img, int w, int h, int pitch, int maxCorners, double qualityLevel,
-             double minDistance, float* corners)
+/* goodFeaturesToTrack (featureselect.cpp:361-516) with blockSize and the
+ * Harris response (useHarrisDetector, harrisK) */
+int orc_gftt_ex(const uint8_t* img, int w, int h, int pitch, int maxCorners, double qualityLevel,
+                double minDistance, int block, int harris, double hk, float* corners)
 {
     if (w <= 0 || h <= 0) return 0;
     float* eig = (float*)malloc(sizeof(float) * (size_t)w * h);
-    orc_min_eig(img, w, h, pitch, eig);
+    if (block == 3 && !harris) orc_min_eig(img, w, h, pitch, eig);
+    else orc_corner_response(img, w, h, pitch, block, harris, hk, eig);
     double maxVal = 0;
     int first = 1;
     for (size_t i = 0; i < (size_t)w * h; ++i)
@@ -182,4 +294,10 @@ int orc_gftt(const uint8_t* img, int w, int h, int pitch, int maxCorners, double
     }
     free(eig); free(cand);
     return n;
+}
+
+int orc_gftt(const uint8_t* img, int w, int h, int pitch, int maxCorners, double qualityLevel,
+             double minDistance, float* corners)
+{
+    return orc_gftt_ex(img, w, h, pitch, maxCorners, qualityLevel, minDistance, 3, 0, 0.04, corners);
 }

@@ -102,6 +102,9 @@ int orc_gftt(const uint8_t* img, int w, int h, int pitch, int maxCorners, double
              double minDistance, float* corners);
 /* cornerMinEigenVal(blockSize=3, ksize=3, BORDER_REFLECT_101) -> eig (w x h float) */
 void orc_min_eig(const uint8_t* img, int w, int h, int pitch, float* eig);
+void orc_corner_response(const uint8_t* img, int w, int h, int pitch, int block, int harris, double hk, float* out);
+int orc_gftt_ex(const uint8_t* img, int w, int h, int pitch, int maxCorners, double qualityLevel,
+                double minDistance, int block, int harris, double hk, float* corners);
 #ifdef __cplusplus
 }
 #endif

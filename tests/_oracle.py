@@ -307,11 +307,39 @@ def min_eig(img: np.ndarray) -> np.ndarray:
     return out
 
 
-def gftt_rois(frame: np.ndarray, rois, max_corners=256, quality=0.01, min_distance=3.0):
+def gftt_ex(img: np.ndarray, max_corners=1000, quality=0.01, min_distance=0.0, block=3, harris=False,
+            k=0.04) -> np.ndarray:
+    """goodFeaturesToTrack with blockSize / useHarrisDetector / harrisK"""
+    lib = load()
+    lib.orc_gftt_ex.restype = C.c_int
+    lib.orc_gftt_ex.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                C.c_int, C.c_double, C.c_void_p]
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros((max(max_corners, 1), 2), dtype=np.float32)
+    n = lib.orc_gftt_ex(_ptr(img), w, h, img.strides[0], max_corners, quality, min_distance, block, int(harris), k,
+                        _ptr(out))
+    return out[:n]
+
+
+def corner_response(img: np.ndarray, block=3, harris=False, k=0.04) -> np.ndarray:
+    """cornerMinEigenVal / cornerHarris (ksize 3) of an isolated u8 image"""
+    lib = load()
+    lib.orc_corner_response.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                        C.c_void_p]
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), dtype=np.float32)
+    lib.orc_corner_response(_ptr(img), w, h, img.strides[0], block, int(harris), k, _ptr(out))
+    return out
+
+
+def gftt_rois(frame: np.ndarray, rois, max_corners=256, quality=0.01, min_distance=3.0, block=3, harris=False,
+              k=0.04):
     """Per-ROI goodFeaturesToTrack on isolated ROIs; corners in frame coordinates."""
     res = []
     for (x, y, w, h) in rois:
-        c = gftt(frame[y:y + h, x:x + w], max_corners, quality, min_distance)
+        c = gftt_ex(frame[y:y + h, x:x + w], max_corners, quality, min_distance, block, harris, k)
         res.append(c + np.float32([x, y]))
     return res
 

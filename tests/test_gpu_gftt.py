@@ -132,3 +132,50 @@ def test_gftt_large_candidate_sets(gpu, maxc, md):
     c, n = detect(gpu, img, rois, maxc, 0.001, md)
     assert (n > 0).all()
     check(img, rois, c, n, maxc, 0.001, md)
+
+
+MODES = [(5, False, 0.04), (7, False, 0.04), (4, False, 0.04), (2, False, 0.04), (1, False, 0.04),
+         (3, True, 0.04), (5, True, 0.06), (6, True, 0.04), (11, True, 0.04)]
+
+
+@pytest.mark.parametrize("block,harris,k", MODES)
+@pytest.mark.parametrize("shape", [(37, 61), (3, 3), (1, 7), (9, 1), (130, 121), (2, 2), (480, 640)])
+def test_corner_response_matches_oracle(gpu, shape, block, harris, k):
+    """cornerMinEigenVal / cornerHarris for blockSize != 3 and the Harris response
+    (klt_gftt_resp.hip) bit-exact with the oracle, including the calcHarris code
+    path split by flat index (AVX lines, one SSE2 block, scalar tail)"""
+    from opencv_amd import klt
+
+    h, w = shape
+    img = np.random.default_rng(h * 1000 + w + block).integers(0, 256, (h, w), dtype=np.uint8)
+    got = klt.corner_response(torch.from_numpy(img).cuda(), block, harris, k, ctx=gpu).cpu().numpy()
+    ref = O.corner_response(img, block, harris, k)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("block,harris,k", MODES)
+def test_gftt_block_harris_rois_match_oracle(gpu, block, harris, k):
+    """createGoodFeaturesToTrackDetector(blockSize, useHarrisDetector, harrisK)
+    over box ROIs: the corner lists equal the oracle's"""
+    from opencv_amd import klt
+
+    fr, gt = O.synth(20261015 + block, 640, 480, 32, 0, 1)
+    rois = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]] + [(0, 0, 3, 3), (5, 5, 2, 50), (600, 440, 40, 40)]
+    for maxc, q, md in ((256, 0.01, 3.0), (1000, 0.001, 0.0)):
+        det = klt.GoodFeaturesToTrackDetector(maxc, q, md, block, harris, k)
+        c, n = det.detect_rois(torch.from_numpy(np.ascontiguousarray(fr[0])).cuda(), rois)
+        torch.cuda.synchronize()
+        c, n = c.cpu().numpy(), n.cpu().numpy()
+        ref = O.gftt_rois(fr[0], rois, maxc, q, md, block, harris, k)
+        for i, r in enumerate(ref):
+            assert n[i] == len(r), f"roi {i}: count {n[i]} vs {len(r)}"
+            assert np.array_equal(c[i, :n[i]], r), f"roi {i}: corners differ"
+
+
+def test_gftt_params_rejected(gpu):
+    from opencv_amd import klt, _lib
+
+    img = torch.zeros((20, 20), dtype=torch.uint8, device="cuda")
+    for kw in ({"blockSize": 0}, {"blockSize": 64}, {"harrisK": float("nan")}):
+        with pytest.raises(_lib.TbdkError):
+            klt.GoodFeaturesToTrackDetector(10, 0.01, 0.0, **kw).detect_rois(img, [(0, 0, 20, 20)])
