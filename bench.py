@@ -521,6 +521,16 @@ def rank_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str, rank: int = 0):
+    """one line per bench leg on stderr (rank 0): a long run under a profiler
+    shows it is alive; stdout keeps the single JSON line"""
+    if rank == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_leg=None):
     """The bench contract, independent of what a step is: the rank's own
     sequence (seed + rank), W untimed warm-up steps, then EXACTLY K steps
@@ -529,7 +539,9 @@ def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_le
     baseline on rank 0 at N = 1 only.  Returns (line, per-step results)."""
     import torch.distributed as dist
 
+    progress("rendering the sequence", rank)
     measure.prepare(args.seed + rank)
+    progress("warm-up", rank)
     measure.warmup(args.warmup)
     if world > 1:
         dist.barrier()
@@ -553,6 +565,9 @@ def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_le
         "scaling": "weak",
         "vs_baseline": None,
     }
+    progress(f"timed region: {line['value']} frames/s", rank)
+    if cpu_leg is not None and rank == 0 and world == 1:
+        progress("cpu baseline")
     line["cpu_baseline"] = cpu_leg() if (cpu_leg is not None and rank == 0 and world == 1) else None
     return line, per_step
 
@@ -844,6 +859,7 @@ def main(argv=None):
     # look-ahead), a fresh loop, no timing events; reported, never `value`
     step_api = None
     if args.api != "step" and not args.no_step_api:
+        progress("step-API pass", rank)
         loop2 = m.new_loop(w0)
         el2 = timed_on_all_ranks(lambda: [loop2.step(frames[f], f, dets[f], stream) for f in range(w0, nframes)],
                                  world)
@@ -857,6 +873,7 @@ def main(argv=None):
     rest = [k for k in ("pyr_build", "lk_sparse", "gftt", "tbd_fit") if k not in timed or k == "lk_sparse"]
     kstats_aside = {}
     if rest:
+        progress("per-kernel event pass", rank)
         loop3 = m.new_loop(w0)
         ctx.timing_select(rest)
         ctx.timing_enable(True)
@@ -944,17 +961,23 @@ def main(argv=None):
                       "host_step_us": h_step / args.steps, "host_launch_us": h_launch / args.steps},
     })
     if args.repeats > 0:
+        progress("whole-sequence repeats", rank)
         line["sequence"] = sequence_repeats(m, world, args.repeats, 20)
     if not args.no_h2d:
+        progress("with-H2D variant", rank)
         line["with_h2d"] = with_h2d(m, world, 3, 20)
     del m.frames, frames, m.loop
     if not args.no_kitti:
+        progress("KITTI configs[3] leg", rank)
         line["kitti"] = kitti_leg(args, ctx, dev, world, rank)
     if rank == 0 and not args.no_farneback:
+        progress("Farneback secondary")
         line["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_f16:
+        progress("fp16 PyrLK secondary")
         line["lk_f16"] = lk_f16_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_hog:
+        progress("HOG secondary")
         line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -70,6 +70,10 @@ typedef struct tbdk_pyr {
                                         (tbdk_pyr_create_f16: fp16 levels, fp16 (Ix, Iy)
                                         derivative pairs) */
     int32_t flags;                   /* TBDK_PYR_NO_DERIVS: levels only */
+    int32_t cn;                      /* channels per pixel, interleaved (1; 2..4 from
+                                        tbdk_pyr_create_cn); level rows hold
+                                        (width + 2*pad)*cn bytes, derivative rows
+                                        (Ix_c, Iy_c) pairs for c = 0..cn-1 */
 } tbdk_pyr;
 
 #define TBDK_ABI_VERSION 2
@@ -189,6 +193,16 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
 int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h,
                            tbdk_pyr* pyr);
 
+/* Multi-channel frames (cv::cuda::SparsePyrLKOpticalFlow takes 1, 3 or 4
+ * channels, cudaoptflow/src/pyrlk.cpp:140-142,197-205; the CPU
+ * calcOpticalFlowPyrLK any count, lkpyramid.cpp:55-144,178-695): a pyramid of
+ * interleaved cn-channel u8 levels (cn = 1..4) with CV_16SC(2cn) derivative
+ * planes.  tbdk_pyr_build fills it from an interleaved frame (pitch >=
+ * width*cn); tbdk_lk_sparse on two such pyramids runs LKTrackerInvoker over
+ * winW*cn elements per window row (klt_cn.hip). */
+int tbdk_pyr_create_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_level, int win_w, int win_h,
+                       tbdk_pyr* pyr);
+
 /* The fp16 pixel path (no reference implementation: the
  * reference's CPU PyrLK takes 8-bit levels only, lkpyramid.cpp:1272-1276, and
  * its CUDA class reads CV_32F through textures, cudaoptflow/src/pyrlk.cpp:197-205).
@@ -206,11 +220,11 @@ int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* 
 /* Synchronous copy of level `level` to host memory (GpuMat::download
  * analogue; not for the hot path).  with_border != 0 copies the padded frame
  * ((height+2*pad) rows of (width+2*pad) pixels), else the interior; rows of
- * width * (1 or 2) bytes by depth (fp16 as raw bits). */
+ * width * cn * (1 or 2) bytes by depth (fp16 as raw bits). */
 int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
                       int with_border);
-/* Same for the derivative plane of `level` (interior, CV_16SC2 — fp16 pairs
- * as raw bits for TBDK_DEPTH_16F — host_pitch in bytes). */
+/* Same for the derivative plane of `level` (interior, CV_16SC(2cn) — fp16
+ * pairs as raw bits for TBDK_DEPTH_16F — host_pitch in bytes). */
 int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16_t* host, int host_pitch);
 
 /* Single-level cv::cuda::pyrDown replacement: dst = pyrDown(src),

@@ -54,6 +54,7 @@ class Pyr(C.Structure):
         ("storage", C.c_void_p),
         ("depth", C.c_int32),
         ("flags", C.c_int32),
+        ("cn", C.c_int32),
     ]
 
 
@@ -194,6 +195,8 @@ SIGNATURES = {
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_f16": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_levels": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_create_cn": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(Pyr)]),
     "tbdk_pyr_build_f16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
     "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),

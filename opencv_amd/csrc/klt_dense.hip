@@ -48,6 +48,7 @@ int tbdk_lk_dense(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, flo
                   uint8_t* status, int status_pitch, const tbdk_lk_params* p, void* stream)
 {
     if (!ctx || !prev || !next || !flow || !p || prev->nlevels <= 0) return TBDK_EINVAL;
+    if (prev->cn > 1 || next->cn > 1) return TBDK_EINVAL;  // the dense path takes one-channel pyramids
     // CV_Assert(winSize_[0] > 2 && winSize_[1] > 2) of PyrLKOpticalFlowBase::dense (pyrlk.cpp:243)
     if (p->win_w <= 2 || p->win_h <= 2) return TBDK_EINVAL;
     // the reference's dense() never reads the incoming flow, so useInitialFlow has

@@ -243,12 +243,12 @@ int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls)
 
 // both depths: u8 (1 B/px) levels + int16x2 derivatives, or fp16 (2 B/px) + fp16x2
 static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, int depth,
-                      int flags, tbdk_pyr* pyr)
+                      int flags, tbdk_pyr* pyr, int cn = 1)
 {
     if (!ctx || !pyr || width <= 0 || height <= 0 || max_level < 0 || win_w <= 2 || win_h <= 2 || win_w > 63 ||
-        win_h > 63)
+        win_h > 63 || cn < 1 || cn > 4)
         return TBDK_EINVAL;
-    const int bpp = depth == TBDK_DEPTH_16F ? 2 : 1;
+    const int bpp = (depth == TBDK_DEPTH_16F ? 2 : 1) * cn;
     DeviceGuard g(ctx->device);
     std::memset(pyr, 0, sizeof(*pyr));
     if (max_level >= TBDK_MAX_LEVELS) max_level = TBDK_MAX_LEVELS - 1;
@@ -269,7 +269,7 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
         D.width = w;
         D.height = h;
         D.pad = pad;
-        D.pitch = align_up((w + 2 * pad) * 4, 256);
+        D.pitch = align_up((w + 2 * pad) * 4 * cn, 256);
         doffs[level] = total;
         if (!(flags & TBDK_PYR_NO_DERIVS)) {
             total += (size_t)D.pitch * (h + 2 * pad) + 256;
@@ -296,6 +296,7 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
     pyr->win_h = win_h;
     pyr->depth = depth;
     pyr->flags = flags;
+    pyr->cn = cn;
     for (int level = 0; level < nlev; ++level) {
         pyr->lv[level].data = static_cast<uint8_t*>(mem) + offs[level];
         pyr->dv[level].data = (flags & TBDK_PYR_NO_DERIVS) ? nullptr : static_cast<uint8_t*>(mem) + doffs[level];
@@ -315,6 +316,12 @@ int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, 
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, TBDK_PYR_NO_DERIVS, pyr);
 }
 
+int tbdk_pyr_create_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_level, int win_w, int win_h,
+                       tbdk_pyr* pyr)
+{
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, 0, pyr, cn);
+}
+
 int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
 {
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, 0, pyr);
@@ -331,12 +338,15 @@ int tbdk_pyr_destroy(tbdk_ctx* ctx, tbdk_pyr* pyr)
 
 int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream)
 {
-    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pitch < pyr->lv[0].width) return TBDK_EINVAL;
+    const int cn = pyr && pyr->cn > 1 ? pyr->cn : 1;
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pitch < pyr->lv[0].width * cn) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     hipError_t e;
-    if (pyr->depth == TBDK_DEPTH_16F) {
+    if (cn > 1) {
+        e = launch_pyr_cn(img, pitch, *pyr, s);
+    } else if (pyr->depth == TBDK_DEPTH_16F) {
         e = launch_pyr_build_f16(img, pitch, 0, *pyr, s);
     } else {
         e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse != 0, s);
@@ -364,7 +374,7 @@ int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* ho
 {
     if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
     const tbdk_level& L = pyr->lv[level];
-    const int bpp = pyr->depth == TBDK_DEPTH_16F ? 2 : 1;
+    const int bpp = (pyr->depth == TBDK_DEPTH_16F ? 2 : 1) * (pyr->cn > 1 ? pyr->cn : 1);
     const int w = with_border ? L.width + 2 * L.pad : L.width;
     const int h = with_border ? L.height + 2 * L.pad : L.height;
     if (host_pitch < w * bpp) return TBDK_EINVAL;
@@ -378,10 +388,11 @@ int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16
 {
     if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels || !pyr->dv[level].data) return TBDK_EINVAL;
     const tbdk_level& D = pyr->dv[level];
-    if (host_pitch < D.width * 4) return TBDK_EINVAL;
-    const uint8_t* src = D.data + (size_t)D.pad * D.pitch + (size_t)D.pad * 4;
+    const int bpp = 4 * (pyr->cn > 1 ? pyr->cn : 1);
+    if (host_pitch < D.width * bpp) return TBDK_EINVAL;
+    const uint8_t* src = D.data + (size_t)D.pad * D.pitch + (size_t)D.pad * bpp;
     DeviceGuard g(ctx->device);
-    hipError_t e = hipMemcpy2D(host, host_pitch, src, D.pitch, (size_t)D.width * 4, D.height, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy2D(host, host_pitch, src, D.pitch, (size_t)D.width * bpp, D.height, hipMemcpyDeviceToHost);
     return map_err(e);
 }
 
@@ -419,6 +430,8 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     if (prev->depth != next->depth || (prev->depth != TBDK_DEPTH_8U && prev->depth != TBDK_DEPTH_16F))
         return TBDK_EINVAL;
     const bool f16 = prev->depth == TBDK_DEPTH_16F;
+    const int cn = prev->cn > 1 ? prev->cn : 1;
+    if (cn != (next->cn > 1 ? next->cn : 1) || (cn > 1 && f16)) return TBDK_EINVAL;
     const int pad_needed = p->win_w > p->win_h ? p->win_w + 2 : p->win_h + 2;
     int max_level = p->max_level;
     if (prev->nlevels - 1 < max_level) max_level = prev->nlevels - 1;
@@ -459,6 +472,14 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     // auto: several points per wave when the window has an instantiation, else the
     // one-point-per-wave strip kernel, else the generic LDS kernel (no derivative planes)
     if (p->impl < 0 || p->impl > 3) return TBDK_EINVAL;
+    if (cn > 1) {  // multi-channel frames: one kernel (klt_cn.hip), on the derivative planes
+        if (p->impl != 0 || !have_d || lk_cn_smem_bytes(p->win_w, p->win_h, cn) > 160 * 1024) return TBDK_EINVAL;
+        a.cn = cn;
+        int rec = timing_begin(ctx, "lk_sparse", s);
+        hipError_t e = launch_lk_cn(a, s);
+        timing_end(ctx, rec, s);
+        return map_err(e);
+    }
     if (f16) {  // the fp16 pixel path has one kernel (klt_f16.hip)
         if (p->impl != 0 || !have_d || !lk_f16_supported(p->win_w, p->win_h)) return TBDK_EINVAL;
         int rec = timing_begin(ctx, "lk_sparse", s);

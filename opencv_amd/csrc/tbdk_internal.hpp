@@ -136,6 +136,7 @@ struct LkArgs {
     const int32_t* seg_list;
     int seg_stride;
     int max_level, win_w, win_h, max_count, flags, n;
+    int cn;  // channels (klt_cn.hip; the one-channel kernels ignore it)
     double eps2;
     float min_eig;
     const float* prev_pts;
@@ -160,6 +161,10 @@ int lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const
                 uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
                 const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list = nullptr);
 int map_status(hipError_t e);
+// multi-channel u8 pyramids and PyrLK (klt_cn.hip)
+hipError_t launch_pyr_cn(const uint8_t* img, int pitch, const tbdk_pyr& pyr, hipStream_t s);
+hipError_t launch_lk_cn(const LkArgs& a, hipStream_t s);
+size_t lk_cn_smem_bytes(int win_w, int win_h, int cn);
 
 size_t lk_smem_bytes(int win_w, int win_h);
 hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);

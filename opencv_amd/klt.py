@@ -96,21 +96,29 @@ class Pyramid:
     (Ix, Iy) planes."""
 
     def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21),
-                 dtype: torch.dtype = torch.uint8, derivs: bool = True):
+                 dtype: torch.dtype = torch.uint8, derivs: bool = True, channels: int = 1):
         """derivs=False (u8 only): levels without derivative planes
         (tbdk_pyr_create_levels); PyrLK then derives the window's Scharr values
-        itself, with the same results."""
+        itself, with the same results.  channels 2..4 (u8 only): interleaved
+        multi-channel frames (tbdk_pyr_create_cn)."""
         if dtype not in (torch.uint8, torch.float16):
             raise _lib.TbdkError("Pyramid dtype must be torch.uint8 or torch.float16")
         if not derivs and dtype != torch.uint8:
             raise _lib.TbdkError("levels-only pyramids are u8")
+        if channels != 1 and (dtype != torch.uint8 or not derivs):
+            raise _lib.TbdkError("multi-channel pyramids are u8 with derivative planes")
         self.ctx = ctx
         self.dtype = dtype
+        self.channels = int(channels)
         self.pyr = _lib.Pyr()
-        create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else \
-            ctx.lib.tbdk_pyr_create if derivs else ctx.lib.tbdk_pyr_create_levels
-        _lib.check(create(ctx.handle, int(width), int(height), int(max_level), int(win[0]), int(win[1]),
-                          C.byref(self.pyr)), "tbdk_pyr_create")
+        if channels != 1:
+            _lib.check(ctx.lib.tbdk_pyr_create_cn(ctx.handle, int(width), int(height), int(channels), int(max_level),
+                                                  int(win[0]), int(win[1]), C.byref(self.pyr)), "tbdk_pyr_create_cn")
+        else:
+            create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else \
+                ctx.lib.tbdk_pyr_create if derivs else ctx.lib.tbdk_pyr_create_levels
+            _lib.check(create(ctx.handle, int(width), int(height), int(max_level), int(win[0]), int(win[1]),
+                              C.byref(self.pyr)), "tbdk_pyr_create")
         self.width, self.height = int(width), int(height)
 
     @property
@@ -118,7 +126,16 @@ class Pyramid:
         return int(self.pyr.nlevels)
 
     def build(self, img: torch.Tensor, stream=None) -> "Pyramid":
-        """From a 2-D uint8 frame (either depth) or, for an fp16 pyramid, a float16 frame."""
+        """From a 2-D uint8 frame (either depth) or, for an fp16 pyramid, a float16 frame;
+        a multi-channel pyramid from an (H, W, C) uint8 frame."""
+        if self.channels != 1:
+            if img.dim() != 3 or not img.is_cuda or img.dtype != torch.uint8 or \
+                    tuple(img.shape) != (self.height, self.width, self.channels) or img.stride(2) != 1 or \
+                    img.stride(1) != self.channels:
+                raise _lib.TbdkError("Pyramid.build expects an (H, W, C) uint8 device tensor of the pyramid's size")
+            _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
+                                                   C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
+            return self
         if img.dim() != 2 or not img.is_cuda or not (img.dtype == torch.uint8 or
                                                      (img.dtype == torch.float16 and self.dtype == torch.float16)):
             raise _lib.TbdkError("Pyramid.build expects a 2-D uint8 (or, fp16 pyramid, float16) device tensor")
@@ -140,7 +157,7 @@ class Pyramid:
         h = L.height + (2 * L.pad if with_border else 0)
         w = L.width + (2 * L.pad if with_border else 0)
         dt = np.float16 if self.dtype == torch.float16 else np.uint8
-        out = np.empty((h, w), dtype=dt)
+        out = np.empty((h, w) if self.channels == 1 else (h, w, self.channels), dtype=dt)
         _lib.check(self.ctx.lib.tbdk_pyr_download(self.ctx.handle, C.byref(self.pyr), int(i),
                                                   out.ctypes.data_as(C.c_void_p), out.strides[0],
                                                   int(bool(with_border))),
@@ -152,9 +169,10 @@ class Pyramid:
         (or float16 for an fp16 pyramid)."""
         import numpy as np
         L = self.pyr.dv[i]
-        out = np.empty((L.height, L.width, 2), dtype=np.float16 if self.dtype == torch.float16 else np.int16)
+        out = np.empty((L.height, L.width, 2 * self.channels),
+                       dtype=np.float16 if self.dtype == torch.float16 else np.int16)
         _lib.check(self.ctx.lib.tbdk_pyr_download_deriv(self.ctx.handle, C.byref(self.pyr), int(i),
-                                                        out.ctypes.data_as(C.c_void_p), L.width * 4),
+                                                        out.ctypes.data_as(C.c_void_p), out.strides[0]),
                    "tbdk_pyr_download_deriv")
         return out
 
@@ -169,10 +187,12 @@ class Pyramid:
 def build_pyramid(img: torch.Tensor, win=(21, 21), max_level: int = 3, ctx: Context | None = None,
                   stream=None, dtype: torch.dtype | None = None, derivs: bool = True) -> Pyramid:
     """cv::buildOpticalFlowPyramid (withDerivatives = derivs); dtype
-    torch.float16 (or a float16 frame) selects the fp16 pixel path."""
+    torch.float16 (or a float16 frame) selects the fp16 pixel path; an (H, W, C)
+    uint8 frame (C = 2..4, interleaved) a multi-channel pyramid."""
     ctx = ctx or Context.get(img.device.index or 0)
     dtype = dtype or (torch.float16 if img.dtype == torch.float16 else torch.uint8)
-    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype, derivs).build(img, stream)
+    cn = int(img.shape[2]) if img.dim() == 3 else 1
+    return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype, derivs, channels=cn).build(img, stream)
 
 
 def pyr_down(src: torch.Tensor, ctx: Context | None = None, stream=None) -> torch.Tensor:

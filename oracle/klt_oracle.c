@@ -53,54 +53,65 @@ static int orc_floor(float v)
 /* pyrDown_<FixPtCast<uchar,8>> (imgproc/src/pyramids.cpp:722-857): 5x5
  * [1 4 6 4 1]^2 in integers, (s + 128) >> 8, reflect-101 on the isolated
  * source plane, dst size given by the caller ((w+1)/2, (h+1)/2). */
-void orc_pyr_down(const uint8_t* src, int sw, int sh, int spitch,
-                  uint8_t* dst, int dw, int dh, int dpitch)
+void orc_pyr_down_cn(const uint8_t* src, int sw, int sh, int spitch, int cn,
+                     uint8_t* dst, int dw, int dh, int dpitch)
 {
-    static const int k[5] = {1, 4, 6, 4, 1};
-    int* row = (int*)malloc(sizeof(int) * 5 * (size_t)dw);
-    int* tab = (int*)malloc(sizeof(int) * 5 * (size_t)dw);
+    /* element x*cn + c of a row: taps of channel c at the reflected pixel columns
+     * (pyramids.cpp:746-790 builds tabL / tabR the same way per channel) */
+    const int dwn = dw * cn;
+    int* row = (int*)malloc(sizeof(int) * 5 * (size_t)dwn);
+    int* tab = (int*)malloc(sizeof(int) * 5 * (size_t)dwn);
     for (int x = 0; x < dw; ++x)
-        for (int i = 0; i < 5; ++i) tab[x * 5 + i] = orc_reflect101(2 * x + i - 2, sw);
+        for (int c = 0; c < cn; ++c)
+            for (int i = 0; i < 5; ++i) tab[(x * cn + c) * 5 + i] = orc_reflect101(2 * x + i - 2, sw) * cn + c;
     for (int y = 0; y < dh; ++y) {
         for (int j = 0; j < 5; ++j) {
             const uint8_t* s = src + (size_t)orc_reflect101(2 * y + j - 2, sh) * spitch;
-            int* r = row + j * dw;
-            for (int x = 0; x < dw; ++x) {
+            int* r = row + j * dwn;
+            for (int x = 0; x < dwn; ++x) {
                 const int* t = tab + x * 5;
                 r[x] = s[t[2]] * 6 + (s[t[1]] + s[t[3]]) * 4 + s[t[0]] + s[t[4]];
             }
         }
         uint8_t* d = dst + (size_t)y * dpitch;
-        for (int x = 0; x < dw; ++x) {
-            int v = row[2 * dw + x] * 6 + (row[dw + x] + row[3 * dw + x]) * 4 + row[x] + row[4 * dw + x];
+        for (int x = 0; x < dwn; ++x) {
+            int v = row[2 * dwn + x] * 6 + (row[dwn + x] + row[3 * dwn + x]) * 4 + row[x] + row[4 * dwn + x];
             d[x] = (uint8_t)((v + 128) >> 8);
         }
     }
-    (void)k;
     free(row);
     free(tab);
+}
+
+void orc_pyr_down(const uint8_t* src, int sw, int sh, int spitch,
+                  uint8_t* dst, int dw, int dh, int dpitch)
+{
+    orc_pyr_down_cn(src, sw, sh, spitch, 1, dst, dw, dh, dpitch);
 }
 
 /* copyMakeBorder(..., BORDER_REFLECT_101) of the interior into the border */
 static void orc_fill_border(orc_plane* p)
 {
+    const int cn = p->cn > 0 ? p->cn : 1;
     for (int y = -p->pad; y < p->h + p->pad; ++y) {
         int ry = orc_reflect101(y, p->h);
-        uint8_t* drow = p->data + (size_t)(y + p->pad) * p->pitch + p->pad;
-        const uint8_t* srow = p->data + (size_t)(ry + p->pad) * p->pitch + p->pad;
+        uint8_t* drow = p->data + (size_t)(y + p->pad) * p->pitch + (size_t)p->pad * cn;
+        const uint8_t* srow = p->data + (size_t)(ry + p->pad) * p->pitch + (size_t)p->pad * cn;
         for (int x = -p->pad; x < p->w + p->pad; ++x) {
             if (y >= 0 && y < p->h && x >= 0 && x < p->w) continue;
-            drow[x] = srow[orc_reflect101(x, p->w)];
+            const int rx = orc_reflect101(x, p->w);
+            for (int c = 0; c < cn; ++c) drow[x * cn + c] = srow[rx * cn + c];
         }
     }
 }
 
-static void orc_plane_alloc(orc_plane* p, int w, int h, int pad)
+static void orc_plane_alloc(orc_plane* p, int w, int h, int pad, int cn)
 {
     p->w = w;
     p->h = h;
     p->pad = pad;
-    p->pitch = w + 2 * pad;
+    p->cn = cn;
+    p->pitch = (w + 2 * pad) * cn;
     p->data = (uint8_t*)calloc((size_t)p->pitch * (h + 2 * pad), 1);
 }
 
@@ -109,20 +120,27 @@ static void orc_plane_alloc(orc_plane* p, int w, int h, int pad)
 int orc_build_pyramid(const uint8_t* img, int w, int h, int pitch,
                       int winW, int winH, int maxLevel, int pad, orc_pyr* pyr)
 {
+    return orc_build_pyramid_cn(img, w, h, pitch, 1, winW, winH, maxLevel, pad, pyr);
+}
+
+int orc_build_pyramid_cn(const uint8_t* img, int w, int h, int pitch, int cn,
+                         int winW, int winH, int maxLevel, int pad, orc_pyr* pyr)
+{
     if (maxLevel >= ORC_MAX_LEVELS) maxLevel = ORC_MAX_LEVELS - 1;
     memset(pyr, 0, sizeof(*pyr));
-    orc_plane_alloc(&pyr->lv[0], w, h, pad);
+    orc_plane_alloc(&pyr->lv[0], w, h, pad, cn);
     for (int y = 0; y < h; ++y)
-        memcpy(pyr->lv[0].data + (size_t)(y + pad) * pyr->lv[0].pitch + pad, img + (size_t)y * pitch, (size_t)w);
+        memcpy(pyr->lv[0].data + (size_t)(y + pad) * pyr->lv[0].pitch + (size_t)pad * cn, img + (size_t)y * pitch,
+               (size_t)w * cn);
     orc_fill_border(&pyr->lv[0]);
     int sw = w, sh = h;
     for (int level = 0; level <= maxLevel; ++level) {
         if (level != 0) {
             orc_plane* s = &pyr->lv[level - 1];
             orc_plane* d = &pyr->lv[level];
-            orc_plane_alloc(d, sw, sh, pad);
-            orc_pyr_down(s->data + (size_t)s->pad * s->pitch + s->pad, s->w, s->h, s->pitch,
-                         d->data + (size_t)d->pad * d->pitch + d->pad, d->w, d->h, d->pitch);
+            orc_plane_alloc(d, sw, sh, pad, cn);
+            orc_pyr_down_cn(s->data + (size_t)s->pad * s->pitch + (size_t)s->pad * cn, s->w, s->h, s->pitch, cn,
+                            d->data + (size_t)d->pad * d->pitch + (size_t)d->pad * cn, d->w, d->h, d->pitch);
             orc_fill_border(d);
         }
         pyr->nlevels = level + 1;
@@ -144,27 +162,37 @@ void orc_free_pyramid(orc_pyr* pyr)
 /* calcSharrDeriv (video/src/lkpyramid.cpp:55-144) */
 void orc_scharr(const uint8_t* src, int w, int h, int pitch, int16_t* dst, int dstride)
 {
-    int16_t* t0 = (int16_t*)malloc(sizeof(int16_t) * (size_t)(w + 2)) + 1;
-    int16_t* t1 = (int16_t*)malloc(sizeof(int16_t) * (size_t)(w + 2)) + 1;
+    orc_scharr_cn(src, w, h, pitch, 1, dst, dstride);
+}
+
+/* rows of colsn = w*cn elements, neighbours cn elements apart; the column
+ * border copies element x0 = cn / x1 = (w-2)*cn per channel (lkpyramid.cpp:111-116) */
+void orc_scharr_cn(const uint8_t* src, int w, int h, int pitch, int cn, int16_t* dst, int dstride)
+{
+    const int wn = w * cn;
+    int16_t* t0 = (int16_t*)malloc(sizeof(int16_t) * (size_t)(wn + 2 * cn)) + cn;
+    int16_t* t1 = (int16_t*)malloc(sizeof(int16_t) * (size_t)(wn + 2 * cn)) + cn;
     for (int y = 0; y < h; ++y) {
         const uint8_t* s0 = src + (size_t)(y > 0 ? y - 1 : (h > 1 ? 1 : 0)) * pitch;
         const uint8_t* s1 = src + (size_t)y * pitch;
         const uint8_t* s2 = src + (size_t)(y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0)) * pitch;
-        for (int x = 0; x < w; ++x) {
+        for (int x = 0; x < wn; ++x) {
             t0[x] = (int16_t)((s0[x] + s2[x]) * 3 + s1[x] * 10);
             t1[x] = (int16_t)(s2[x] - s0[x]);
         }
-        int x0 = w > 1 ? 1 : 0, x1 = w > 1 ? w - 2 : 0;
-        t0[-1] = t0[x0]; t0[w] = t0[x1];
-        t1[-1] = t1[x0]; t1[w] = t1[x1];
+        int x0 = (w > 1 ? 1 : 0) * cn, x1 = (w > 1 ? w - 2 : 0) * cn;
+        for (int k = 0; k < cn; ++k) {
+            t0[-cn + k] = t0[x0 + k]; t0[wn + k] = t0[x1 + k];
+            t1[-cn + k] = t1[x0 + k]; t1[wn + k] = t1[x1 + k];
+        }
         int16_t* d = dst + (size_t)y * dstride;
-        for (int x = 0; x < w; ++x) {
-            d[2 * x] = (int16_t)(t0[x + 1] - t0[x - 1]);
-            d[2 * x + 1] = (int16_t)((t1[x + 1] + t1[x - 1]) * 3 + t1[x] * 10);
+        for (int x = 0; x < wn; ++x) {
+            d[2 * x] = (int16_t)(t0[x + cn] - t0[x - cn]);
+            d[2 * x + 1] = (int16_t)((t1[x + cn] + t1[x - cn]) * 3 + t1[x] * 10);
         }
     }
-    free(t0 - 1);
-    free(t1 - 1);
+    free(t0 - cn);
+    free(t1 - cn);
 }
 
 /* --------------------------------------------------------------------- LK */
@@ -189,9 +217,9 @@ typedef struct orc_job {
     int begin, end;
 } orc_job;
 
-static const uint8_t* orc_px(const orc_plane* p, int x, int y)
+static const uint8_t* orc_px(const orc_plane* p, int x, int y, int cn)
 {
-    return p->data + (size_t)(y + p->pad) * p->pitch + (x + p->pad);
+    return p->data + (size_t)(y + p->pad) * p->pitch + (size_t)(x + p->pad) * cn;
 }
 
 /* LKTrackerInvoker::operator() for one point at one level
@@ -207,6 +235,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     const float FLT_SCALE = 1.f / (1 << 20);
     const int exact = prm->accum == ORC_ACCUM_EXACT;
     const int Icols = L->I->w, Irows = L->I->h, Jcols = L->J->w, Jrows = L->J->h;
+    const int cn = L->I->cn > 0 ? L->I->cn : 1, wcn = winW * cn; /* window row: winW*cn elements */
 
     float sc = (float)(1. / (1 << level));
     float prevx = jb->prevPts[2 * ptidx] * sc, prevy = jb->prevPts[2 * ptidx + 1] * sc;
@@ -248,25 +277,26 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     float t11 = 0, t12 = 0, t22 = 0;
     int64_t e11 = 0, e12 = 0, e22 = 0;
     const int dstep = L->dstride;
+    const int cn2 = 2 * cn;
     for (int y = 0; y < winH; ++y) {
-        const uint8_t* src = orc_px(L->I, ipx, ipy + y);
+        const uint8_t* src = orc_px(L->I, ipx, ipy + y, cn);
         const int stepI = L->I->pitch;
-        const int16_t* dsrc = L->dI + (size_t)(ipy + y + L->dpad) * dstep + 2 * (ipx + L->dpad);
-        int16_t* Iptr = Iwin + y * winW;
-        int16_t* dIptr = dIwin + 2 * y * winW;
-        for (int x = 0; x < winW; ++x) {
-            int ival = ORC_DESCALE(src[x] * iw00 + src[x + 1] * iw01 + src[x + stepI] * iw10 +
-                                   src[x + stepI + 1] * iw11, W_BITS1 - 5);
-            int ixval = ORC_DESCALE(dsrc[2 * x] * iw00 + dsrc[2 * x + 2] * iw01 + dsrc[2 * x + dstep] * iw10 +
-                                    dsrc[2 * x + dstep + 2] * iw11, W_BITS1);
-            int iyval = ORC_DESCALE(dsrc[2 * x + 1] * iw00 + dsrc[2 * x + 3] * iw01 + dsrc[2 * x + dstep + 1] * iw10 +
-                                    dsrc[2 * x + dstep + 3] * iw11, W_BITS1);
+        const int16_t* dsrc = L->dI + (size_t)(ipy + y + L->dpad) * dstep + (size_t)cn2 * (ipx + L->dpad);
+        int16_t* Iptr = Iwin + y * wcn;
+        int16_t* dIptr = dIwin + 2 * y * wcn;
+        for (int x = 0; x < wcn; ++x) {
+            int ival = ORC_DESCALE(src[x] * iw00 + src[x + cn] * iw01 + src[x + stepI] * iw10 +
+                                   src[x + stepI + cn] * iw11, W_BITS1 - 5);
+            int ixval = ORC_DESCALE(dsrc[2 * x] * iw00 + dsrc[2 * x + cn2] * iw01 + dsrc[2 * x + dstep] * iw10 +
+                                    dsrc[2 * x + dstep + cn2] * iw11, W_BITS1);
+            int iyval = ORC_DESCALE(dsrc[2 * x + 1] * iw00 + dsrc[2 * x + cn2 + 1] * iw01 +
+                                    dsrc[2 * x + dstep + 1] * iw10 + dsrc[2 * x + dstep + cn2 + 1] * iw11, W_BITS1);
             Iptr[x] = (int16_t)ival;
             dIptr[2 * x] = (int16_t)ixval;
             dIptr[2 * x + 1] = (int16_t)iyval;
         }
         if (exact) {
-            for (int x = 0; x < winW; ++x) {
+            for (int x = 0; x < wcn; ++x) {
                 int ix = dIptr[2 * x], iy = dIptr[2 * x + 1];
                 e11 += (int64_t)(ix * ix);
                 e12 += (int64_t)(ix * iy);
@@ -275,7 +305,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
         } else {
             /* SSE2 lanes: x in chunks of 4 (lkpyramid.cpp:279-316), scalar tail (:403-419) */
             int x = 0;
-            for (; x <= winW - 4; x += 4) {
+            for (; x <= wcn - 4; x += 4) {
                 for (int k = 0; k < 4; ++k) {
                     float fx = (float)dIptr[2 * (x + k)], fy = (float)dIptr[2 * (x + k) + 1];
                     q22[k] = q22[k] + fy * fy;
@@ -283,7 +313,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
                     q11[k] = q11[k] + fx * fx;
                 }
             }
-            for (; x < winW; ++x) {
+            for (; x < wcn; ++x) {
                 int ix = dIptr[2 * x], iy = dIptr[2 * x + 1];
                 t11 += (float)(ix * ix);
                 t12 += (float)(ix * iy);
@@ -339,22 +369,22 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
         int64_t eb1 = 0, eb2 = 0;
         const int stepJ = L->J->pitch;
         for (int y = 0; y < winH; ++y) {
-            const uint8_t* Jptr = orc_px(L->J, inx, iny + y);
-            const int16_t* Iptr = Iwin + y * winW;
-            const int16_t* dIptr = dIwin + 2 * y * winW;
-            int d[64];
-            for (int x = 0; x < winW; ++x)
-                d[x] = ORC_DESCALE(Jptr[x] * iw00 + Jptr[x + 1] * iw01 + Jptr[x + stepJ] * iw10 +
-                                   Jptr[x + stepJ + 1] * iw11, W_BITS1 - 5) - Iptr[x];
+            const uint8_t* Jptr = orc_px(L->J, inx, iny + y, cn);
+            const int16_t* Iptr = Iwin + y * wcn;
+            const int16_t* dIptr = dIwin + 2 * y * wcn;
+            int d[64 * 4];
+            for (int x = 0; x < wcn; ++x)
+                d[x] = ORC_DESCALE(Jptr[x] * iw00 + Jptr[x + cn] * iw01 + Jptr[x + stepJ] * iw10 +
+                                   Jptr[x + stepJ + cn] * iw11, W_BITS1 - 5) - Iptr[x];
             if (exact) {
-                for (int x = 0; x < winW; ++x) {
+                for (int x = 0; x < wcn; ++x) {
                     eb1 += (int64_t)(d[x] * dIptr[2 * x]);
                     eb2 += (int64_t)(d[x] * dIptr[2 * x + 1]);
                 }
             } else {
                 /* SSE2 lanes: chunks of 8, _mm_madd_epi16 pairs (x, x+4) (lkpyramid.cpp:507-534) */
                 int x = 0;
-                for (; x <= winW - 8; x += 8) {
+                for (; x <= wcn - 8; x += 8) {
                     const int* dd = d + x;
                     const int16_t* g = dIptr + 2 * x;
                     qb0[0] = qb0[0] + (float)(dd[0] * g[0] + dd[4] * g[8]);
@@ -366,7 +396,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
                     qb1[2] = qb1[2] + (float)(dd[3] * g[6] + dd[7] * g[14]);
                     qb1[3] = qb1[3] + (float)(dd[3] * g[7] + dd[7] * g[15]);
                 }
-                for (; x < winW; ++x) {
+                for (; x < wcn; ++x) {
                     tb1 += (float)(d[x] * dIptr[2 * x]);
                     tb2 += (float)(d[x] * dIptr[2 * x + 1]);
                 }
@@ -417,22 +447,23 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
         float errval = 0.f;
         const int stepJ = L->J->pitch;
         for (int y = 0; y < winH; ++y) {
-            const uint8_t* Jptr = orc_px(L->J, inx, iny + y);
-            const int16_t* Iptr = Iwin + y * winW;
-            for (int x = 0; x < winW; ++x) {
-                int diff = ORC_DESCALE(Jptr[x] * iw00 + Jptr[x + 1] * iw01 + Jptr[x + stepJ] * iw10 +
-                                       Jptr[x + stepJ + 1] * iw11, W_BITS1 - 5) - Iptr[x];
+            const uint8_t* Jptr = orc_px(L->J, inx, iny + y, cn);
+            const int16_t* Iptr = Iwin + y * wcn;
+            for (int x = 0; x < wcn; ++x) {
+                int diff = ORC_DESCALE(Jptr[x] * iw00 + Jptr[x + cn] * iw01 + Jptr[x + stepJ] * iw10 +
+                                       Jptr[x + stepJ + cn] * iw11, W_BITS1 - 5) - Iptr[x];
                 errval += fabsf((float)diff);
             }
         }
-        jb->err[ptidx] = errval * 1.f / (float)(32 * winW * winH);
+        jb->err[ptidx] = errval * 1.f / (float)(32 * winW * cn * winH);
     }
 }
 
 static void* orc_lk_worker(void* arg)
 {
     const orc_job* jb = (const orc_job*)arg;
-    int area = jb->prm->winW * jb->prm->winH;
+    const int cn = jb->lv->I->cn > 0 ? jb->lv->I->cn : 1;
+    int area = jb->prm->winW * jb->prm->winH * cn;
     int16_t* Iwin = (int16_t*)malloc(sizeof(int16_t) * (size_t)area * 3);
     for (int i = jb->begin; i < jb->end; ++i) orc_lk_point(jb, i, Iwin, Iwin + area);
     free(Iwin);
@@ -445,6 +476,7 @@ int orc_lk(const orc_pyr* prev, const orc_pyr* next,
 {
     if (npoints <= 0) return 0;
     if (prm->winW < 3 || prm->winH < 3 || prm->winW > 64 || prm->winH > 64) return -1;
+    if (prev->lv[0].cn > 4) return -1;
     int maxLevel = prm->maxLevel;
     if (prev->nlevels - 1 < maxLevel) maxLevel = prev->nlevels - 1;
     if (next->nlevels - 1 < maxLevel) maxLevel = next->nlevels - 1;
@@ -458,12 +490,13 @@ int orc_lk(const orc_pyr* prev, const orc_pyr* next,
     for (int level = maxLevel; level >= 0; --level) {
         const orc_plane* I = &prev->lv[level];
         const orc_plane* J = &next->lv[level];
-        if (I->w != J->w || I->h != J->h) return -2;
+        const int cn = I->cn > 0 ? I->cn : 1;
+        if (I->w != J->w || I->h != J->h || cn != (J->cn > 0 ? J->cn : 1)) return -2;
         int dpad = prm->winW > prm->winH ? prm->winW + 1 : prm->winH + 1;
-        int dstride = 2 * (I->w + 2 * dpad);
+        int dstride = 2 * cn * (I->w + 2 * dpad);
         int16_t* dI = (int16_t*)calloc((size_t)dstride * (I->h + 2 * dpad), sizeof(int16_t));
-        orc_scharr(I->data + (size_t)I->pad * I->pitch + I->pad, I->w, I->h, I->pitch,
-                   dI + (size_t)dpad * dstride + 2 * dpad, dstride);
+        orc_scharr_cn(I->data + (size_t)I->pad * I->pitch + (size_t)I->pad * cn, I->w, I->h, I->pitch, cn,
+                      dI + (size_t)dpad * dstride + 2 * cn * dpad, dstride);
         orc_level_ctx lctx = {I, J, dI, dpad, dstride};
         orc_job* jobs = (orc_job*)malloc(sizeof(orc_job) * (size_t)nth);
         pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nth);

@@ -30,6 +30,7 @@ extern "C" {
 typedef struct orc_plane {
     uint8_t* data;
     int w, h, pitch, pad;
+    int cn;          /* channels, interleaved (0 reads as 1) */
 } orc_plane;
 
 #define ORC_MAX_LEVELS 8
@@ -53,13 +54,20 @@ int  orc_reflect101(int p, int len);
 int  orc_build_pyramid(const uint8_t* img, int w, int h, int pitch,
                        int winW, int winH, int maxLevel, int pad, orc_pyr* pyr);
 void orc_free_pyramid(orc_pyr* pyr);
+/* the same for cn-channel interleaved u8 images (any cn; the CPU path's) */
+int  orc_build_pyramid_cn(const uint8_t* img, int w, int h, int pitch, int cn,
+                          int winW, int winH, int maxLevel, int pad, orc_pyr* pyr);
 
 /* pyrDown_<FixPtCast<uchar,8>> of one isolated plane (imgproc/src/pyramids.cpp:722-857) */
 void orc_pyr_down(const uint8_t* src, int sw, int sh, int spitch,
                   uint8_t* dst, int dw, int dh, int dpitch);
+void orc_pyr_down_cn(const uint8_t* src, int sw, int sh, int spitch, int cn,
+                     uint8_t* dst, int dw, int dh, int dpitch);
 
 /* calcSharrDeriv (lkpyramid.cpp:55-144): dst is (h x w x 2) int16, interleaved */
 void orc_scharr(const uint8_t* src, int w, int h, int pitch, int16_t* dst, int dstride);
+/* cn channels: dst (h x w x 2cn) int16, per pixel (Ix_c, Iy_c) for c = 0..cn-1 */
+void orc_scharr_cn(const uint8_t* src, int w, int h, int pitch, int cn, int16_t* dst, int dstride);
 
 typedef struct orc_lk_params {
     int winW, winH;

@@ -22,7 +22,8 @@ MAX_LEVELS = 8
 
 
 class Plane(C.Structure):
-    _fields_ = [("data", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("pitch", C.c_int), ("pad", C.c_int)]
+    _fields_ = [("data", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("pitch", C.c_int), ("pad", C.c_int),
+                ("cn", C.c_int)]
 
 
 class OPyr(C.Structure):
@@ -50,6 +51,10 @@ def load():
     lib.orc_build_pyramid.restype = C.c_int
     lib.orc_build_pyramid.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.POINTER(OPyr)]
+    lib.orc_build_pyramid_cn.restype = C.c_int
+    lib.orc_build_pyramid_cn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.POINTER(OPyr)]
+    lib.orc_scharr_cn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
     lib.orc_free_pyramid.argtypes = [C.POINTER(OPyr)]
     lib.orc_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.orc_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
@@ -74,19 +79,24 @@ class Pyramid:
     """Oracle pyramid (host memory), freed on GC."""
 
     def __init__(self, img: np.ndarray, win=(21, 21), max_level=3, pad=32):
+        """img: (H, W) u8, or (H, W, cn) interleaved channels"""
         lib = load()
         img = np.ascontiguousarray(img, dtype=np.uint8)
+        self.cn = 1 if img.ndim == 2 else img.shape[2]
         self.p = OPyr()
-        lib.orc_build_pyramid(_ptr(img), img.shape[1], img.shape[0], img.strides[0], win[0], win[1], max_level, pad,
-                              C.byref(self.p))
+        lib.orc_build_pyramid_cn(_ptr(img), img.shape[1], img.shape[0], img.strides[0], self.cn, win[0], win[1],
+                                 max_level, pad, C.byref(self.p))
         self.nlevels = self.p.nlevels
 
     def level(self, i: int, with_border=False) -> np.ndarray:
         L = self.p.lv[i]
+        cn = self.cn
         full = np.ctypeslib.as_array(C.cast(L.data, C.POINTER(C.c_uint8)), shape=(L.h + 2 * L.pad, L.pitch)).copy()
         if with_border:
-            return full[:, :L.w + 2 * L.pad]
-        return full[L.pad:L.pad + L.h, L.pad:L.pad + L.w]
+            out = full[:, :(L.w + 2 * L.pad) * cn]
+        else:
+            out = full[L.pad:L.pad + L.h, L.pad * cn:(L.pad + L.w) * cn]
+        return out if cn == 1 else out.reshape(out.shape[0], -1, cn)
 
     def __del__(self):
         if _lib is not None and getattr(self, "p", None) is not None:
@@ -104,11 +114,13 @@ def pyr_down(img: np.ndarray) -> np.ndarray:
 
 
 def scharr(img: np.ndarray) -> np.ndarray:
+    """calcSharrDeriv: (H, W, 2) int16 for (H, W) u8; (H, W, 2cn) for (H, W, cn)"""
     lib = load()
     img = np.ascontiguousarray(img, dtype=np.uint8)
-    h, w = img.shape
-    out = np.empty((h, w, 2), dtype=np.int16)
-    lib.orc_scharr(_ptr(img), w, h, img.strides[0], _ptr(out), 2 * w)
+    h, w = img.shape[:2]
+    cn = 1 if img.ndim == 2 else img.shape[2]
+    out = np.empty((h, w, 2 * cn), dtype=np.int16)
+    lib.orc_scharr_cn(_ptr(img), w, h, img.strides[0], cn, _ptr(out), 2 * cn * w)
     return out
 
 
@@ -382,6 +394,7 @@ def invert_affine(M) -> np.ndarray:
 # ---- dense Farneback (oracle/farneback_oracle.c) ----
 FARNEBACK_GAUSSIAN = 256
 OPTFLOW_USE_INITIAL_FLOW = 4
+OPTFLOW_LK_GET_MIN_EIGENVALS = 8
 
 
 def _fb_lib():
