@@ -33,6 +33,7 @@ extern "C" {
 /* pixel depths of a pyramid (cv::Mat depth codes: CV_8U = 0; 7 is OpenCV 4's CV_16F) */
 #define TBDK_DEPTH_8U 0
 #define TBDK_DEPTH_16F 7
+#define TBDK_DEPTH_32F 5
 
 /* flags, same values as the reference (video/include/opencv2/video/tracking.hpp:56-57) */
 #define TBDK_OPTFLOW_USE_INITIAL_FLOW 4
@@ -66,9 +67,10 @@ typedef struct tbdk_pyr {
     tbdk_level lv[TBDK_MAX_LEVELS];
     tbdk_level dv[TBDK_MAX_LEVELS];
     void* storage;                   /* owned by the library; free with tbdk_pyr_destroy */
-    int32_t depth;                   /* TBDK_DEPTH_8U (tbdk_pyr_create*) or TBDK_DEPTH_16F
+    int32_t depth;                   /* TBDK_DEPTH_8U (tbdk_pyr_create*), TBDK_DEPTH_16F
                                         (tbdk_pyr_create_f16: fp16 levels, fp16 (Ix, Iy)
-                                        derivative pairs) */
+                                        derivative pairs) or TBDK_DEPTH_32F
+                                        (tbdk_pyr_create_f32: fp32 levels and pairs) */
     int32_t flags;                   /* TBDK_PYR_NO_DERIVS: levels only */
     int32_t cn;                      /* channels per pixel, interleaved (1; 2..4 from
                                         tbdk_pyr_create_cn); level rows hold
@@ -217,6 +219,18 @@ int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level,
                         int win_w, int win_h, tbdk_pyr* pyr);
 int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream);
 
+/* The fp32 pixel path, for the 16U and 32F frames cv::cuda::SparsePyrLK-
+ * OpticalFlow takes (cudaoptflow/src/pyrlk.cpp:189-205; the CPU PyrLK has no
+ * such path): the fp16 path's algorithm with fp32 levels (4 B per pixel) and
+ * fp32 (Ix, Iy) derivative pairs (8 B per pixel), nothing rounded to fp16.
+ * tbdk_pyr_build fills it from a u8 frame, tbdk_pyr_build_u16 from a u16
+ * frame, tbdk_pyr_build_f32 from an fp32 frame (every conversion exact;
+ * pitches in bytes); tbdk_lk_sparse on two such pyramids (impl 0). */
+int tbdk_pyr_create_f32(tbdk_ctx* ctx, int width, int height, int max_level,
+                        int win_w, int win_h, tbdk_pyr* pyr);
+int tbdk_pyr_build_u16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream);
+int tbdk_pyr_build_f32(tbdk_ctx* ctx, const float* img, int pitch, tbdk_pyr* pyr, void* stream);
+
 /* Synchronous copy of level `level` to host memory (GpuMat::download
  * analogue; not for the hot path).  with_border != 0 copies the padded frame
  * ((height+2*pad) rows of (width+2*pad) pixels), else the interior; rows of
@@ -246,7 +260,8 @@ int tbdk_pyr_down_u8(tbdk_ctx* ctx, const uint8_t* src, int width, int height, i
  *                         status is 0 and the reference leaves it unset)
  *   iters               : n x i32 or NULL (Newton iterations over all levels)
  * All levels run in one launch.  prev and next must have the same depth; on
- * TBDK_DEPTH_16F pyramids the fp16 pixel path runs (impl must be 0). */
+ * TBDK_DEPTH_16F / TBDK_DEPTH_32F pyramids the fp16 / fp32 pixel path runs
+ * (impl must be 0). */
 int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
                    const float* prev_pts, float* next_pts, uint8_t* status, float* err,
                    int32_t* iters, int n, const tbdk_lk_params* params, void* stream);

@@ -194,6 +194,9 @@ SIGNATURES = {
     "tbdk_timing_calls": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64)]),
     "tbdk_pyr_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_f16": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_create_f32": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
+    "tbdk_pyr_build_u16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
+    "tbdk_pyr_build_f32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_create_levels": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Pyr)]),
     "tbdk_pyr_create_cn": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.POINTER(Pyr)]),

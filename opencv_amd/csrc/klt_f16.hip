@@ -17,6 +17,10 @@
 //     value an fma chain over the four fp16 taps; per window column the rows
 //     accumulated by fma in row order, the columns then summed left to right.
 // The restated order is oracle/klt16_oracle.c, which matches this bit for bit.
+// The fp32 pixel path (16U / 32F frames, the other depths
+// cv::cuda::SparsePyrLKOpticalFlow takes, cudaoptflow/src/pyrlk.cpp:189-205) is
+// the same code on fp32 storage (template F32): levels and derivative pairs are
+// kept in fp32 instead of being rounded to fp16.
 // Layout and work split follow klt_lk_multi.hip: lane = window column, P = 64 / WW
 // points per wave (lane 0 idle), all levels in one launch; the per-point column
 // sums go through LDS and are added by one lane per value in column order.
@@ -46,16 +50,6 @@ __device__ __forceinline__ int reflect101(int p, int len)
     return p;
 }
 
-// bilinear value of a packed (x, x+1) fp16 pair on rows r (p0) and r+1 (p1),
-// started from c: fma(w11, p1.hi, fma(w10, p1.lo, fma(w01, p0.hi, fma(w00, p0.lo, c))))
-__device__ __forceinline__ float bil16(uint32_t p0, uint32_t p1, float w00, float w01, float w10, float w11, float c)
-{
-    float t = __builtin_fmaf(w00, h_lo(p0), c);
-    t = __builtin_fmaf(w01, h_hi(p0), t);
-    t = __builtin_fmaf(w10, h_lo(p1), t);
-    return __builtin_fmaf(w11, h_hi(p1), t);
-}
-
 __device__ __forceinline__ void weights16(float a, float b, float& w00, float& w01, float& w10, float& w11)
 {
     w00 = (1.f - a) * (1.f - b);
@@ -65,6 +59,49 @@ __device__ __forceinline__ void weights16(float a, float b, float& w00, float& w
 }
 
 __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// storage of a pixel path: fp16 (2 B per value) or fp32 (4 B per value); a
+// "pair" is two consecutive values (I(x), I(x+1)) or a pixel's (Ix, Iy)
+template <bool F32>
+struct Pix {
+    typedef uint32_t pair_t;
+    static constexpr int B = 2;
+    __device__ static pair_t ld(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff)
+    {
+        return __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
+    }
+    __device__ static float lo(pair_t p) { return h_lo(p); }
+    __device__ static float hi(pair_t p) { return h_hi(p); }
+    __device__ static float at(const uint8_t* p) { return h_at(reinterpret_cast<const uint16_t*>(p)); }
+};
+template <>
+struct Pix<true> {
+    struct pair_t {
+        uint32_t x, y;
+    };
+    static constexpr int B = 4;
+    __device__ static pair_t ld(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff)
+    {
+        return pair_t{__builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0),
+                      __builtin_amdgcn_raw_buffer_load_b32(r, off + 4, soff, 0)};
+    }
+    __device__ static float lo(pair_t p) { return __builtin_bit_cast(float, p.x); }
+    __device__ static float hi(pair_t p) { return __builtin_bit_cast(float, p.y); }
+    __device__ static float at(const uint8_t* p) { return *reinterpret_cast<const float*>(p); }
+};
+
+// bilinear value of a pair on rows r (p0) and r+1 (p1), started from c:
+// fma(w11, p1.hi, fma(w10, p1.lo, fma(w01, p0.hi, fma(w00, p0.lo, c))))
+template <bool F32>
+__device__ __forceinline__ float bilp(typename Pix<F32>::pair_t p0, typename Pix<F32>::pair_t p1, float w00,
+                                      float w01, float w10, float w11, float c)
+{
+    typedef Pix<F32> P;
+    float t = __builtin_fmaf(w00, P::lo(p0), c);
+    t = __builtin_fmaf(w01, P::hi(p0), t);
+    t = __builtin_fmaf(w10, P::lo(p1), t);
+    return __builtin_fmaf(w11, P::hi(p1), t);
+}
 
 }  // namespace
 
@@ -157,6 +194,113 @@ __global__ void scharr_f16_levels_kernel(Scharr16Levels a)
     }
 }
 
+// ---- fp32 pyramid (the fp32 pixel path) ----------------------------------------
+
+// level 0: a u8 / u16 / fp32 frame (src_kind 0 / 1 / 2) converted exactly into the
+// padded fp32 level, reflect-101 frame; 4 values per thread
+__global__ void pad_copy_f32_kernel(const uint8_t* __restrict__ src, int spitch, int src_kind, int w, int h,
+                                    uint8_t* __restrict__ dst, int dpitch, int pad, int wp4)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y;
+    if (t >= wp4) return;
+    const uint8_t* srow = src + (size_t)reflect101(py - pad, h) * spitch;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int sx = reflect101(t * 4 + k - pad, w);
+        v[k] = src_kind == 2 ? reinterpret_cast<const float*>(srow)[sx]
+                             : src_kind == 1 ? (float)reinterpret_cast<const uint16_t*>(srow)[sx] : (float)srow[sx];
+    }
+    *reinterpret_cast<float4*>(dst + (size_t)py * dpitch + (size_t)t * 16) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__global__ void pyr_down_f32_kernel(const uint8_t* __restrict__ src, int spitch, int spad, uint8_t* __restrict__ dst,
+                                    int dpitch, int dpad, int dw, int dh, int wp4)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y;
+    if (t >= wp4) return;
+    const int ry = reflect101(py - dpad, dh);
+    const float* s0 = reinterpret_cast<const float*>(src + (size_t)(2 * ry - 2 + spad) * spitch) + spad;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rx = reflect101(t * 4 + k - dpad, dw);
+        float r[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float* q = reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(s0) +
+                                                            (size_t)j * spitch) + 2 * rx;
+            r[j] = q[0] * 6.f + (q[-1] + q[1]) * 4.f + q[-2] + q[2];
+        }
+        v[k] = (r[2] * 6.f + (r[1] + r[3]) * 4.f + r[0] + r[4]) * (1.f / 256.f);
+    }
+    *reinterpret_cast<float4*>(dst + (size_t)py * dpitch + (size_t)t * 16) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// calcSharrDeriv's formula in fp32 on every fp32 level, stored as fp32 (Ix, Iy)
+__global__ void scharr_f32_levels_kernel(Scharr16Levels a)
+{
+    const int lvl = blockIdx.z;
+    const int y = blockIdx.y;
+    const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int w = a.w[lvl], h = a.h[lvl];
+    if (y >= h || x0 >= w) return;
+    const int sp = a.spitch[lvl];
+    const float* r1 = reinterpret_cast<const float*>(a.src[lvl] + (size_t)(y + a.spad[lvl]) * sp) + a.spad[lvl] + x0;
+    const float* r0 = reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(r1) - sp);
+    const float* r2 = reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(r1) + sp);
+    float t0[6], t1[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int c = k - 1;
+        t0[k] = (r0[c] + r2[c]) * 3.f + r1[c] * 10.f;
+        t1[k] = r2[c] - r0[c];
+    }
+    float2* d = reinterpret_cast<float2*>(a.dst[lvl] + (size_t)(y + a.dpad[lvl]) * a.dpitch[lvl]) + a.dpad[lvl] + x0;
+    const int n = w - x0 < 4 ? w - x0 : 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float ix = t0[k + 2] - t0[k];
+        const float iy = (t1[k + 2] + t1[k]) * 3.f + t1[k + 1] * 10.f;
+        if (k < n) d[k] = make_float2(ix, iy);
+    }
+}
+
+hipError_t launch_pyr_build_f32(const uint8_t* img, int pitch, int src_kind, const tbdk_pyr& pyr, hipStream_t s)
+{
+    {
+        const tbdk_level& d = pyr.lv[0];
+        const int wp4 = (d.width + 2 * d.pad + 3) / 4, hp = d.height + 2 * d.pad;
+        hipLaunchKernelGGL(pad_copy_f32_kernel, dim3((wp4 + 255) / 256, hp), dim3(256), 0, s, img, pitch, src_kind,
+                           d.width, d.height, d.data, d.pitch, d.pad, wp4);
+    }
+    for (int l = 1; l < pyr.nlevels; ++l) {
+        const tbdk_level &sl = pyr.lv[l - 1], &dl = pyr.lv[l];
+        const int wp4 = (dl.width + 2 * dl.pad + 3) / 4, hp = dl.height + 2 * dl.pad;
+        hipLaunchKernelGGL(pyr_down_f32_kernel, dim3((wp4 + 255) / 256, hp), dim3(256), 0, s, sl.data, sl.pitch,
+                           sl.pad, dl.data, dl.pitch, dl.pad, dl.width, dl.height, wp4);
+    }
+    Scharr16Levels a;
+    int maxw = 0, maxh = 0;
+    for (int l = 0; l < pyr.nlevels; ++l) {
+        a.src[l] = pyr.lv[l].data;
+        a.dst[l] = pyr.dv[l].data;
+        a.w[l] = pyr.lv[l].width;
+        a.h[l] = pyr.lv[l].height;
+        a.spitch[l] = pyr.lv[l].pitch;
+        a.spad[l] = pyr.lv[l].pad;
+        a.dpitch[l] = pyr.dv[l].pitch;
+        a.dpad[l] = pyr.dv[l].pad;
+        maxw = a.w[l] > maxw ? a.w[l] : maxw;
+        maxh = a.h[l] > maxh ? a.h[l] : maxh;
+    }
+    hipLaunchKernelGGL(scharr_f32_levels_kernel, dim3(((maxw + 3) / 4 + 255) / 256, maxh, pyr.nlevels), dim3(256), 0,
+                       s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s)
 {
     {
@@ -192,9 +336,12 @@ hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, cons
 
 // ---- sparse LK on fp16 levels ------------------------------------------------
 
-template <int WW, int WH>
+template <int WW, int WH, bool F32>
 __global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
 {
+    typedef Pix<F32> PX;
+    typedef typename PX::pair_t pair_t;
+    constexpr int VB = PX::B, DB = 2 * PX::B;  // bytes per value / per derivative pair
     constexpr int P = 64 / WW;  // points per wave
     __shared__ float red[3][64];
     const int lane = threadIdx.x;
@@ -290,41 +437,41 @@ __global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
         nextx -= halfx;
         nexty -= halfy;
         int pinx = (int)floorf(nextx), piny = (int)floorf(nexty);
-        uint32_t jp[WH + 1];
+        pair_t jp[WH + 1];
 
         float iv[WH], gx[WH], gy[WH];
         float A11, A12, A22;
         {
-            const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + (ipx + x + L.ipad) * 2) : 0u;
-            const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * 4) : 0u;
-            uint32_t ip[WH + 1], d0[WH + 1], d1[WH + 1];
+            const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + (ipx + x + L.ipad) * VB) : 0u;
+            const uint32_t doff = act ? (uint32_t)((ipy + L.dpad) * L.dpitch + (ipx + x + L.dpad) * DB) : 0u;
+            pair_t ip[WH + 1], d0[WH + 1], d1[WH + 1];
 #pragma unroll
             for (int r = 0; r <= WH; ++r) {
-                ip[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);  // (I(x), I(x+1))
-                d0[r] = __builtin_amdgcn_raw_buffer_load_b32(rD, doff, r * L.dpitch, 0);      // (Ix, Iy)(x)
-                d1[r] = __builtin_amdgcn_raw_buffer_load_b32(rD, doff + 4, r * L.dpitch, 0);  // (Ix, Iy)(x+1)
+                ip[r] = PX::ld(rI, ioff, r * L.ipitch);         // (I(x), I(x+1))
+                d0[r] = PX::ld(rD, doff, r * L.dpitch);         // (Ix, Iy)(x)
+                d1[r] = PX::ld(rD, doff + DB, r * L.dpitch);    // (Ix, Iy)(x+1)
             }
             float a11 = 0.f, a12 = 0.f, a22 = 0.f;
 #pragma unroll
             for (int r = 0; r < WH; ++r) {
-                iv[r] = bil16(ip[r], ip[r + 1], w00, w01, w10, w11, 0.f);
-                float t = __builtin_fmaf(w00, h_lo(d0[r]), 0.f);
-                t = __builtin_fmaf(w01, h_lo(d1[r]), t);
-                t = __builtin_fmaf(w10, h_lo(d0[r + 1]), t);
-                gx[r] = __builtin_fmaf(w11, h_lo(d1[r + 1]), t);
-                t = __builtin_fmaf(w00, h_hi(d0[r]), 0.f);
-                t = __builtin_fmaf(w01, h_hi(d1[r]), t);
-                t = __builtin_fmaf(w10, h_hi(d0[r + 1]), t);
-                gy[r] = __builtin_fmaf(w11, h_hi(d1[r + 1]), t);
+                iv[r] = bilp<F32>(ip[r], ip[r + 1], w00, w01, w10, w11, 0.f);
+                float t = __builtin_fmaf(w00, PX::lo(d0[r]), 0.f);
+                t = __builtin_fmaf(w01, PX::lo(d1[r]), t);
+                t = __builtin_fmaf(w10, PX::lo(d0[r + 1]), t);
+                gx[r] = __builtin_fmaf(w11, PX::lo(d1[r + 1]), t);
+                t = __builtin_fmaf(w00, PX::hi(d0[r]), 0.f);
+                t = __builtin_fmaf(w01, PX::hi(d1[r]), t);
+                t = __builtin_fmaf(w10, PX::hi(d0[r + 1]), t);
+                gy[r] = __builtin_fmaf(w11, PX::hi(d1[r + 1]), t);
                 a11 = __builtin_fmaf(gx[r], gx[r], a11);
                 a12 = __builtin_fmaf(gx[r], gy[r], a12);
                 a22 = __builtin_fmaf(gy[r], gy[r], a22);
             }
             {
                 const bool jin = act && !(pinx < -WW || pinx >= L.w || piny < -WH || piny >= L.h);
-                const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + (pinx + x + L.jpad) * 2) : 0u;
+                const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + (pinx + x + L.jpad) * VB) : 0u;
 #pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = __builtin_amdgcn_raw_buffer_load_b32(rJ, joff, r * L.jpitch, 0);
+                for (int r = 0; r <= WH; ++r) jp[r] = PX::ld(rJ, joff, r * L.jpitch);
             }
             if (k >= P) a11 = a12 = a22 = 0.f;
             colsum3(a11, a12, a22, A11, A12, A22);
@@ -353,9 +500,9 @@ __global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
             nit += act ? 1 : 0;
             const bool moved = act && (inx != pinx || iny != piny);
             if (any_lane(moved)) {
-                const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + (inx + x + L.jpad) * 2) : 0u;
+                const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + (inx + x + L.jpad) * VB) : 0u;
 #pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = __builtin_amdgcn_raw_buffer_load_b32(rJ, joff, r * L.jpitch, 0);
+                for (int r = 0; r <= WH; ++r) jp[r] = PX::ld(rJ, joff, r * L.jpitch);
                 pinx = inx;
                 piny = iny;
             }
@@ -363,7 +510,7 @@ __global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
             float b1 = 0.f, b2 = 0.f;
 #pragma unroll
             for (int r = 0; r < WH; ++r) {
-                const float d = bil16(jp[r], jp[r + 1], w00, w01, w10, w11, -iv[r]);  // J - I at the window pixel
+                const float d = bilp<F32>(jp[r], jp[r + 1], w00, w01, w10, w11, -iv[r]);  // J - I at the window pixel
                 b1 = __builtin_fmaf(d, gx[r], b1);
                 b2 = __builtin_fmaf(d, gy[r], b2);
             }
@@ -401,12 +548,12 @@ __global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
             }
             if (any_lane(want)) {
                 weights16(npx - inx, npy - iny, w00, w01, w10, w11);
-                const uint32_t joff = want ? (uint32_t)((iny + L.jpad) * L.jpitch + (inx + x + L.jpad) * 2) : 0u;
+                const uint32_t joff = want ? (uint32_t)((iny + L.jpad) * L.jpitch + (inx + x + L.jpad) * VB) : 0u;
 #pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = __builtin_amdgcn_raw_buffer_load_b32(rJ, joff, r * L.jpitch, 0);
+                for (int r = 0; r <= WH; ++r) jp[r] = PX::ld(rJ, joff, r * L.jpitch);
                 float e = 0.f;
 #pragma unroll
-                for (int r = 0; r < WH; ++r) e += fabsf(bil16(jp[r], jp[r + 1], w00, w01, w10, w11, -iv[r]));
+                for (int r = 0; r < WH; ++r) e += fabsf(bilp<F32>(jp[r], jp[r + 1], w00, w01, w10, w11, -iv[r]));
                 if (k >= P) e = 0.f;
                 float es, unused;
                 colsum2(e, 0.f, es, unused);
@@ -439,15 +586,16 @@ bool lk_f16_supported(int win_w, int win_h)
     }
 }
 
-hipError_t launch_lk_f16(const LkArgs& a, hipStream_t s)
+hipError_t launch_lk_f16(const LkArgs& a, bool f32, hipStream_t s)
 {
     if (!lk_f16_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
     const int per_wg = 64 / a.win_w;
     const dim3 grid((a.n + per_wg - 1) / per_wg), block(64);
     switch (a.win_w) {
-#define TBDK_CASE(W)                                                     \
-    case W:                                                              \
-        hipLaunchKernelGGL((lk_f16_kernel<W, W>), grid, block, 0, s, a); \
+#define TBDK_CASE(W)                                                                  \
+    case W:                                                                           \
+        if (f32) hipLaunchKernelGGL((lk_f16_kernel<W, W, true>), grid, block, 0, s, a); \
+        else hipLaunchKernelGGL((lk_f16_kernel<W, W, false>), grid, block, 0, s, a);   \
         break;
         TBDK_F16_WINDOWS(TBDK_CASE)
 #undef TBDK_CASE

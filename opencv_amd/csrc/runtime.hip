@@ -248,7 +248,8 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
     if (!ctx || !pyr || width <= 0 || height <= 0 || max_level < 0 || win_w <= 2 || win_h <= 2 || win_w > 63 ||
         win_h > 63 || cn < 1 || cn > 4)
         return TBDK_EINVAL;
-    const int bpp = (depth == TBDK_DEPTH_16F ? 2 : 1) * cn;
+    const int bpp = (depth == TBDK_DEPTH_32F ? 4 : depth == TBDK_DEPTH_16F ? 2 : 1) * cn;
+    const int dbpp = (depth == TBDK_DEPTH_32F ? 8 : 4) * cn;  // derivative pair bytes per pixel
     DeviceGuard g(ctx->device);
     std::memset(pyr, 0, sizeof(*pyr));
     if (max_level >= TBDK_MAX_LEVELS) max_level = TBDK_MAX_LEVELS - 1;
@@ -269,7 +270,7 @@ static int pyr_create(tbdk_ctx* ctx, int width, int height, int max_level, int w
         D.width = w;
         D.height = h;
         D.pad = pad;
-        D.pitch = align_up((w + 2 * pad) * 4 * cn, 256);
+        D.pitch = align_up((w + 2 * pad) * dbpp, 256);
         doffs[level] = total;
         if (!(flags & TBDK_PYR_NO_DERIVS)) {
             total += (size_t)D.pitch * (h + 2 * pad) + 256;
@@ -322,6 +323,11 @@ int tbdk_pyr_create_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_lev
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_8U, 0, pyr, cn);
 }
 
+int tbdk_pyr_create_f32(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
+{
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_32F, 0, pyr);
+}
+
 int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
 {
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, 0, pyr);
@@ -348,6 +354,8 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
         e = launch_pyr_cn(img, pitch, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_16F) {
         e = launch_pyr_build_f16(img, pitch, 0, *pyr, s);
+    } else if (pyr->depth == TBDK_DEPTH_32F) {
+        e = launch_pyr_build_f32(img, pitch, 0, *pyr, s);
     } else {
         e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse != 0, s);
         if (e == hipSuccess && !(pyr->flags & TBDK_PYR_NO_DERIVS)) e = launch_scharr_levels(*pyr, s);
@@ -369,12 +377,36 @@ int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* 
     return map_err(e);
 }
 
+static int pyr_build_f32_from(tbdk_ctx* ctx, const void* img, int pitch, int bytes_per_px, int kind, tbdk_pyr* pyr,
+                              void* stream)
+{
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pyr->depth != TBDK_DEPTH_32F ||
+        pitch < bytes_per_px * pyr->lv[0].width || pitch % bytes_per_px != 0)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "pyr_build", s);
+    hipError_t e = launch_pyr_build_f32(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk_pyr_build_u16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream)
+{
+    return pyr_build_f32_from(ctx, img, pitch, 2, 1, pyr, stream);
+}
+
+int tbdk_pyr_build_f32(tbdk_ctx* ctx, const float* img, int pitch, tbdk_pyr* pyr, void* stream)
+{
+    return pyr_build_f32_from(ctx, img, pitch, 4, 2, pyr, stream);
+}
+
 int tbdk_pyr_download(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, uint8_t* host, int host_pitch,
                       int with_border)
 {
     if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels) return TBDK_EINVAL;
     const tbdk_level& L = pyr->lv[level];
-    const int bpp = (pyr->depth == TBDK_DEPTH_16F ? 2 : 1) * (pyr->cn > 1 ? pyr->cn : 1);
+    const int bpp = (pyr->depth == TBDK_DEPTH_32F ? 4 : pyr->depth == TBDK_DEPTH_16F ? 2 : 1) * (pyr->cn > 1 ? pyr->cn : 1);
     const int w = with_border ? L.width + 2 * L.pad : L.width;
     const int h = with_border ? L.height + 2 * L.pad : L.height;
     if (host_pitch < w * bpp) return TBDK_EINVAL;
@@ -388,7 +420,7 @@ int tbdk_pyr_download_deriv(tbdk_ctx* ctx, const tbdk_pyr* pyr, int level, int16
 {
     if (!ctx || !pyr || !host || level < 0 || level >= pyr->nlevels || !pyr->dv[level].data) return TBDK_EINVAL;
     const tbdk_level& D = pyr->dv[level];
-    const int bpp = 4 * (pyr->cn > 1 ? pyr->cn : 1);
+    const int bpp = (pyr->depth == TBDK_DEPTH_32F ? 8 : 4) * (pyr->cn > 1 ? pyr->cn : 1);
     if (host_pitch < D.width * bpp) return TBDK_EINVAL;
     const uint8_t* src = D.data + (size_t)D.pad * D.pitch + (size_t)D.pad * bpp;
     DeviceGuard g(ctx->device);
@@ -427,9 +459,11 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     if (!prev_pts || !next_pts || !status) return TBDK_EINVAL;
     if (p->win_w <= 2 || p->win_h <= 2 || p->win_w > 63 || p->win_h > 63 || p->max_level < 0) return TBDK_EINVAL;
     if (prev->nlevels <= 0 || next->nlevels <= 0) return TBDK_EINVAL;
-    if (prev->depth != next->depth || (prev->depth != TBDK_DEPTH_8U && prev->depth != TBDK_DEPTH_16F))
+    if (prev->depth != next->depth ||
+        (prev->depth != TBDK_DEPTH_8U && prev->depth != TBDK_DEPTH_16F && prev->depth != TBDK_DEPTH_32F))
         return TBDK_EINVAL;
-    const bool f16 = prev->depth == TBDK_DEPTH_16F;
+    const bool f32 = prev->depth == TBDK_DEPTH_32F;
+    const bool f16 = prev->depth == TBDK_DEPTH_16F || f32;  // the float pixel paths
     const int cn = prev->cn > 1 ? prev->cn : 1;
     if (cn != (next->cn > 1 ? next->cn : 1) || (cn > 1 && f16)) return TBDK_EINVAL;
     const int pad_needed = p->win_w > p->win_h ? p->win_w + 2 : p->win_h + 2;
@@ -483,7 +517,7 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     if (f16) {  // the fp16 pixel path has one kernel (klt_f16.hip)
         if (p->impl != 0 || !have_d || !lk_f16_supported(p->win_w, p->win_h)) return TBDK_EINVAL;
         int rec = timing_begin(ctx, "lk_sparse", s);
-        hipError_t e = launch_lk_f16(a, s);
+        hipError_t e = launch_lk_f16(a, f32, s);
         timing_end(ctx, rec, s);
         return map_err(e);
     }

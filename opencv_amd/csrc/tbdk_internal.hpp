@@ -118,6 +118,8 @@ hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr,
 // the fp16 pyramid (klt_f16.hip): level 0 from a u8 (img_f16 = 0) or fp16 frame,
 // the fp16 pyrDown levels and the fp16 derivative pairs
 hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s);
+// fp32 pixel path: src_kind 0 u8, 1 u16, 2 fp32 frame
+hipError_t launch_pyr_build_f32(const uint8_t* img, int pitch, int src_kind, const tbdk_pyr& pyr, hipStream_t s);
 
 // ---- kernels (klt_lk.hip) ----
 struct LkLevel {
@@ -178,7 +180,7 @@ bool lk_multi_supported(int win_w, int win_h);
 hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s);
 // the fp16 pixel path (klt_f16.hip)
 bool lk_f16_supported(int win_w, int win_h);
-hipError_t launch_lk_f16(const LkArgs& a, hipStream_t s);
+hipError_t launch_lk_f16(const LkArgs& a, bool f32, hipStream_t s);  // fp16 or (f32) fp32 pixel path
 
 // ---- box propagation (box_fit.hip) ----
 hipError_t launch_box_propagate(const float* prev, const float* next, const uint8_t* status, const int32_t* offsets,

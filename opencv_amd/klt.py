@@ -93,7 +93,8 @@ DEPTH_8U, DEPTH_16F = 0, 7  # TBDK_DEPTH_* (cv::Mat depth codes; 7 = OpenCV 4's 
 class Pyramid:
     """A padded pyramid in device memory (tbdk_pyr): u8 levels with int16 Scharr
     planes, or (dtype=torch.float16) the fp16 pixel path's fp16 levels with fp16
-    (Ix, Iy) planes."""
+    (Ix, Iy) planes, or (dtype=torch.float32) the fp32 pixel path (16U / 32F
+    frames) with fp32 levels and planes."""
 
     def __init__(self, ctx: Context, width: int, height: int, max_level: int = 3, win=(21, 21),
                  dtype: torch.dtype = torch.uint8, derivs: bool = True, channels: int = 1):
@@ -101,8 +102,8 @@ class Pyramid:
         (tbdk_pyr_create_levels); PyrLK then derives the window's Scharr values
         itself, with the same results.  channels 2..4 (u8 only): interleaved
         multi-channel frames (tbdk_pyr_create_cn)."""
-        if dtype not in (torch.uint8, torch.float16):
-            raise _lib.TbdkError("Pyramid dtype must be torch.uint8 or torch.float16")
+        if dtype not in (torch.uint8, torch.float16, torch.float32):
+            raise _lib.TbdkError("Pyramid dtype must be torch.uint8, torch.float16 or torch.float32")
         if not derivs and dtype != torch.uint8:
             raise _lib.TbdkError("levels-only pyramids are u8")
         if channels != 1 and (dtype != torch.uint8 or not derivs):
@@ -116,6 +117,7 @@ class Pyramid:
                                                   int(win[0]), int(win[1]), C.byref(self.pyr)), "tbdk_pyr_create_cn")
         else:
             create = ctx.lib.tbdk_pyr_create_f16 if dtype == torch.float16 else \
+                ctx.lib.tbdk_pyr_create_f32 if dtype == torch.float32 else \
                 ctx.lib.tbdk_pyr_create if derivs else ctx.lib.tbdk_pyr_create_levels
             _lib.check(create(ctx.handle, int(width), int(height), int(max_level), int(win[0]), int(win[1]),
                               C.byref(self.pyr)), "tbdk_pyr_create")
@@ -135,6 +137,14 @@ class Pyramid:
                 raise _lib.TbdkError("Pyramid.build expects an (H, W, C) uint8 device tensor of the pyramid's size")
             _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
                                                    C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
+            return self
+        if self.dtype == torch.float32 and img.dim() == 2 and img.is_cuda and img.stride(1) == 1 and \
+                img.dtype in (torch.uint16, torch.float32):
+            if img.shape[0] != self.height or img.shape[1] != self.width:
+                raise _lib.TbdkError("image size does not match the pyramid")
+            fn = self.ctx.lib.tbdk_pyr_build_u16 if img.dtype == torch.uint16 else self.ctx.lib.tbdk_pyr_build_f32
+            _lib.check(fn(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)) * img.element_size(),
+                          C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build (fp32 path)")
             return self
         if img.dim() != 2 or not img.is_cuda or not (img.dtype == torch.uint8 or
                                                      (img.dtype == torch.float16 and self.dtype == torch.float16)):
@@ -156,7 +166,7 @@ class Pyramid:
         L = self.pyr.lv[i]
         h = L.height + (2 * L.pad if with_border else 0)
         w = L.width + (2 * L.pad if with_border else 0)
-        dt = np.float16 if self.dtype == torch.float16 else np.uint8
+        dt = {torch.float16: np.float16, torch.float32: np.float32}.get(self.dtype, np.uint8)
         out = np.empty((h, w) if self.channels == 1 else (h, w, self.channels), dtype=dt)
         _lib.check(self.ctx.lib.tbdk_pyr_download(self.ctx.handle, C.byref(self.pyr), int(i),
                                                   out.ctypes.data_as(C.c_void_p), out.strides[0],
@@ -170,7 +180,7 @@ class Pyramid:
         import numpy as np
         L = self.pyr.dv[i]
         out = np.empty((L.height, L.width, 2 * self.channels),
-                       dtype=np.float16 if self.dtype == torch.float16 else np.int16)
+                       dtype={torch.float16: np.float16, torch.float32: np.float32}.get(self.dtype, np.int16))
         _lib.check(self.ctx.lib.tbdk_pyr_download_deriv(self.ctx.handle, C.byref(self.pyr), int(i),
                                                         out.ctypes.data_as(C.c_void_p), out.strides[0]),
                    "tbdk_pyr_download_deriv")
@@ -187,10 +197,12 @@ class Pyramid:
 def build_pyramid(img: torch.Tensor, win=(21, 21), max_level: int = 3, ctx: Context | None = None,
                   stream=None, dtype: torch.dtype | None = None, derivs: bool = True) -> Pyramid:
     """cv::buildOpticalFlowPyramid (withDerivatives = derivs); dtype
-    torch.float16 (or a float16 frame) selects the fp16 pixel path; an (H, W, C)
-    uint8 frame (C = 2..4, interleaved) a multi-channel pyramid."""
+    torch.float16 (or a float16 frame) selects the fp16 pixel path, torch.float32
+    (or a uint16 / float32 frame) the fp32 pixel path; an (H, W, C) uint8 frame
+    (C = 2..4, interleaved) a multi-channel pyramid."""
     ctx = ctx or Context.get(img.device.index or 0)
-    dtype = dtype or (torch.float16 if img.dtype == torch.float16 else torch.uint8)
+    dtype = dtype or (torch.float16 if img.dtype == torch.float16 else
+                      torch.float32 if img.dtype in (torch.uint16, torch.float32) else torch.uint8)
     cn = int(img.shape[2]) if img.dim() == 3 else 1
     return Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, dtype, derivs, channels=cn).build(img, stream)
 

@@ -1,5 +1,8 @@
-/* klt16_oracle.c — CPU restatement of the fp16 pixel path of sparse PyrLK
- * (TEST INFRASTRUCTURE ONLY; loaded by tests/ and bench.py's cpu_baseline).
+/* klt16_oracle.c — CPU restatement of the fp16 and fp32 pixel paths of sparse
+ * PyrLK (TEST INFRASTRUCTURE ONLY; loaded by tests/ and bench.py's cpu_baseline).
+ * The fp32 path (16U and 32F frames, the other depths cv::cuda::SparsePyrLK-
+ * OpticalFlow takes, cudaoptflow/src/pyrlk.cpp:189-205) is the same algorithm
+ * with fp32 levels and derivative pairs (no rounding to fp16).
  *
  * The reference has no fp16/fp32 CPU PyrLK (calcSharrDeriv and LKTrackerInvoker
  * take 8-bit levels, video/src/lkpyramid.cpp:57,1272-1276), so this file is the
@@ -99,10 +102,50 @@ void orc16_scharr(const uint16_t* src, int w, int h, int pitch, uint16_t* dst)
     }
 }
 
+/* one pyrDown level of the fp32 pixel path (the same order, no rounding) */
+void orc32_pyr_down(const float* src, int sw, int sh, int spitch, float* dst, int dw, int dh, int dpitch)
+{
+    for (int y = 0; y < dh; ++y)
+        for (int x = 0; x < dw; ++x) {
+            float r[5];
+            for (int j = 0; j < 5; ++j) {
+                const float* row = src + (size_t)orc_reflect101(2 * y + j - 2, sh) * spitch;
+                float s0 = row[orc_reflect101(2 * x - 2, sw)];
+                float s1 = row[orc_reflect101(2 * x - 1, sw)];
+                float s2 = row[orc_reflect101(2 * x, sw)];
+                float s3 = row[orc_reflect101(2 * x + 1, sw)];
+                float s4 = row[orc_reflect101(2 * x + 2, sw)];
+                r[j] = s2 * 6.f + (s1 + s3) * 4.f + s0 + s4;
+            }
+            dst[(size_t)y * dpitch + x] = (r[2] * 6.f + (r[1] + r[3]) * 4.f + r[0] + r[4]) * (1.f / 256.f);
+        }
+}
+
+/* calcSharrDeriv's formula on an fp32 level: dst (h x w x 2) fp32 (Ix, Iy) */
+void orc32_scharr(const float* src, int w, int h, int pitch, float* dst)
+{
+    for (int y = 0; y < h; ++y) {
+        const float* r0 = src + (size_t)orc_reflect101(y - 1, h) * pitch;
+        const float* r1 = src + (size_t)y * pitch;
+        const float* r2 = src + (size_t)orc_reflect101(y + 1, h) * pitch;
+        for (int x = 0; x < w; ++x) {
+            float t0[3], t1[3];
+            for (int k = 0; k < 3; ++k) {
+                const int c = orc_reflect101(x + k - 1, w);
+                t0[k] = (r0[c] + r2[c]) * 3.f + r1[c] * 10.f;
+                t1[k] = r2[c] - r0[c];
+            }
+            dst[((size_t)y * w + x) * 2] = t0[2] - t0[0];
+            dst[((size_t)y * w + x) * 2 + 1] = (t1[2] + t1[0]) * 3.f + t1[1] * 10.f;
+        }
+    }
+}
+
 typedef struct orc16_level {
-    const uint16_t* px; /* h x w fp16 */
-    const uint16_t* d;  /* h x w x 2 fp16 (Ix, Iy), or NULL for a J-only level */
+    const void* px;     /* h x w fp16 (or fp32 with f32) */
+    const void* d;      /* h x w x 2 fp16 / fp32 (Ix, Iy), or NULL for a J-only level */
     int w, h;
+    int f32;            /* the fp32 pixel path: the same algorithm on fp32 levels */
 } orc16_level;
 
 typedef struct orc16_pyr {
@@ -112,13 +155,15 @@ typedef struct orc16_pyr {
 
 static inline float px16(const orc16_level* L, int x, int y)
 {
-    return orc16_h2f(L->px[(size_t)orc_reflect101(y, L->h) * L->w + orc_reflect101(x, L->w)]);
+    const size_t k = (size_t)orc_reflect101(y, L->h) * L->w + orc_reflect101(x, L->w);
+    return L->f32 ? ((const float*)L->px)[k] : orc16_h2f(((const uint16_t*)L->px)[k]);
 }
 
 static inline float dv16(const orc16_level* L, int x, int y, int c)
 {
     if (x < 0 || y < 0 || x >= L->w || y >= L->h) return 0.f; /* BORDER_CONSTANT 0 frame */
-    return orc16_h2f(L->d[((size_t)y * L->w + x) * 2 + c]);
+    const size_t k = ((size_t)y * L->w + x) * 2 + c;
+    return L->f32 ? ((const float*)L->d)[k] : orc16_h2f(((const uint16_t*)L->d)[k]);
 }
 
 static inline void weights16(float a, float b, float* w)
@@ -323,7 +368,9 @@ int orc16_lk(const orc16_pyr* prev, const orc16_pyr* next, const float* prevPts,
     if (prev->nlevels - 1 < maxLevel) maxLevel = prev->nlevels - 1;
     if (next->nlevels - 1 < maxLevel) maxLevel = next->nlevels - 1;
     for (int l = 0; l <= maxLevel; ++l)
-        if (prev->lv[l].w != next->lv[l].w || prev->lv[l].h != next->lv[l].h || !prev->lv[l].d) return -2;
+        if (prev->lv[l].w != next->lv[l].w || prev->lv[l].h != next->lv[l].h || !prev->lv[l].d ||
+            prev->lv[l].f32 != next->lv[l].f32)
+            return -2;
     const double eps = prm->epsilon < 0. ? 0. : (prm->epsilon > 10. ? 10. : prm->epsilon);
     int nth = prm->nthreads > 0 ? prm->nthreads : 1;
     if (nth > npoints) nth = npoints;

@@ -145,7 +145,7 @@ def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, 
 # ---- the fp16 pixel path (oracle/klt16_oracle.c) ------------------------------
 
 class Level16(C.Structure):
-    _fields_ = [("px", C.c_void_p), ("d", C.c_void_p), ("w", C.c_int), ("h", C.c_int)]
+    _fields_ = [("px", C.c_void_p), ("d", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("f32", C.c_int)]
 
 
 class OPyr16(C.Structure):
@@ -157,6 +157,8 @@ def _lib16():
     if not getattr(lib, "_f16_ready", False):
         lib.orc16_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
         lib.orc16_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.orc32_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        lib.orc32_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         lib.orc16_lk.restype = C.c_int
         lib.orc16_lk.argtypes = [C.POINTER(OPyr16), C.POINTER(OPyr16), C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_int, C.POINTER(LkParams), C.c_void_p]
@@ -184,25 +186,49 @@ def scharr16(img: np.ndarray) -> np.ndarray:
     return out
 
 
+def pyr_down32(img: np.ndarray) -> np.ndarray:
+    """the fp32 pixel path's pyrDown (pyr_down16's order, no rounding)."""
+    lib = _lib16()
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w = img.shape
+    out = np.empty(((h + 1) // 2, (w + 1) // 2), dtype=np.float32)
+    lib.orc32_pyr_down(_ptr(img), w, h, w, _ptr(out), out.shape[1], out.shape[0], out.shape[1])
+    return out
+
+
+def scharr32(img: np.ndarray) -> np.ndarray:
+    """calcSharrDeriv's formula in fp32 on an fp32 level: (H, W, 2) float32 (Ix, Iy)."""
+    lib = _lib16()
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w = img.shape
+    out = np.empty((h, w, 2), dtype=np.float32)
+    lib.orc32_scharr(_ptr(img), w, h, w, _ptr(out))
+    return out
+
+
 class Pyramid16:
     """fp16 oracle pyramid: levels (float16) and their fp16 derivative planes;
-    the level rule of cv::buildOpticalFlowPyramid (lkpyramid.cpp:782-787)."""
+    the level rule of cv::buildOpticalFlowPyramid (lkpyramid.cpp:782-787).
+    f32=True: the fp32 pixel path (float32 levels and derivative pairs; a
+    uint8 / uint16 / float32 frame converts exactly)."""
 
-    def __init__(self, img: np.ndarray, win=(21, 21), max_level=3):
-        l0 = np.ascontiguousarray(img.astype(np.float16) if img.dtype != np.float16 else img)
+    def __init__(self, img: np.ndarray, win=(21, 21), max_level=3, f32: bool = False):
+        dt = np.float32 if f32 else np.float16
+        l0 = np.ascontiguousarray(img.astype(dt) if img.dtype != dt else img)
+        down, sch = (pyr_down32, scharr32) if f32 else (pyr_down16, scharr16)
         self.levels = [l0]
         w, h = l0.shape[1], l0.shape[0]
         for _ in range(max_level):
             w, h = (w + 1) // 2, (h + 1) // 2
             if w <= win[0] or h <= win[1]:
                 break
-            self.levels.append(pyr_down16(self.levels[-1]))
-        self.derivs = [scharr16(L) for L in self.levels]
+            self.levels.append(down(self.levels[-1]))
+        self.derivs = [sch(L) for L in self.levels]
         self.nlevels = len(self.levels)
         self.p = OPyr16()
         self.p.nlevels = self.nlevels
         for i, (L, D) in enumerate(zip(self.levels, self.derivs)):
-            self.p.lv[i] = Level16(L.ctypes.data, D.ctypes.data, L.shape[1], L.shape[0])
+            self.p.lv[i] = Level16(L.ctypes.data, D.ctypes.data, L.shape[1], L.shape[0], int(f32))
 
 
 def lk16(prev: Pyramid16, nxt: Pyramid16, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01,

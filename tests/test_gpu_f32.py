@@ -1,0 +1,101 @@
+"""GPU parity of the fp32 pixel path (16U and 32F frames, the other depths
+cv::cuda::SparsePyrLKOpticalFlow takes, cudaoptflow/src/pyrlk.cpp:189-205;
+the CPU PyrLK has no such path).  The checker is oracle/klt16_oracle.c in its
+fp32 mode (the fp16 path's algorithm with nothing rounded to fp16): fp32
+levels, their reflect-101 frames and fp32 derivative pairs bit-exact from u8,
+u16 and fp32 frames; sparse LK bit-exact (points, status, error, iterations)."""
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+from test_gpu_f16 import box_points, edge_points, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(kind, w, h, seed=7):
+    frames, gt = O.synth(seed, w, h, 8, 0, 2)
+    if kind == "u8":
+        return frames[0], frames[1], gt
+    if kind == "u16":
+        rng = np.random.default_rng(seed)
+        return [(f.astype(np.uint16) * 257 + rng.integers(0, 257, f.shape)).astype(np.uint16) for f in frames[:2]] + [gt]
+    rng = np.random.default_rng(seed + 1)
+    return [(f.astype(np.float32) / 255.0 + rng.normal(0, 1e-3, f.shape)).astype(np.float32) for f in frames[:2]] + [gt]
+
+
+def _dev_pyr(ctx, img, win, max_level):
+    from opencv_amd import klt
+
+    return klt.Pyramid(ctx, img.shape[1], img.shape[0], max_level, win, torch.float32).build(to_dev(img))
+
+
+@pytest.mark.parametrize("kind", ["u8", "u16", "f32"])
+@pytest.mark.parametrize("shape", [(480, 640), (217, 333), (97, 131)])
+def test_f32_pyramid_bit_exact(gpu, kind, shape):
+    h, w = shape
+    a, _, _ = _frames(kind, w, h)
+    P = _dev_pyr(gpu, a, (21, 21), 3)
+    R = O.Pyramid16(a, (21, 21), 3, f32=True)
+    assert P.nlevels == R.nlevels
+    for i in range(P.nlevels):
+        got = P.level(i)
+        assert got.dtype == np.float32
+        assert np.array_equal(got.view(np.uint32), R.levels[i].view(np.uint32)), f"level {i}"
+        assert np.array_equal(P.deriv(i).view(np.uint32), R.derivs[i].view(np.uint32)), f"deriv {i}"
+        full = P.level(i, with_border=True)
+        pad = P.pyr.lv[i].pad
+        ref = R.levels[i]
+        hh, ww = ref.shape
+        ry = [O.load().orc_reflect101(y - pad, hh) for y in range(hh + 2 * pad)]
+        rx = [O.load().orc_reflect101(x - pad, ww) for x in range(ww + 2 * pad)]
+        assert np.array_equal(full.view(np.uint32), ref[np.ix_(ry, rx)].view(np.uint32)), f"border {i}"
+
+
+@pytest.mark.parametrize("kind", ["u8", "u16", "f32"])
+@pytest.mark.parametrize("win,maxlev", [(21, 3), (7, 0), (15, 2), (31, 1)])
+def test_f32_lk_bit_exact(gpu, kind, win, maxlev):
+    from opencv_amd import klt
+
+    a, b, gt = _frames(kind, 640, 480, seed=win)
+    pts = np.concatenate([box_points(gt[0], 32, seed=win), edge_points(640, 480)])
+    Pa, Pb = _dev_pyr(gpu, a, (win, win), maxlev), _dev_pyr(gpu, b, (win, win), maxlev)
+    lk = klt.SparsePyrLKOpticalFlow((win, win), maxlev, 30)
+    r = lk.calc(Pa, Pb, to_dev(pts), want_iters=True)
+    torch.cuda.synchronize()
+    Ra, Rb = O.Pyramid16(a, (win, win), maxlev, f32=True), O.Pyramid16(b, (win, win), maxlev, f32=True)
+    nx, st, er, it = O.lk16(Ra, Rb, pts, (win, win), maxlev)
+    g_st = r.status.cpu().numpy()
+    assert np.array_equal(g_st, st)
+    ok = st == 1
+    assert np.array_equal(r.next_pts.cpu().numpy()[ok].view(np.uint32), nx[ok].view(np.uint32))
+    assert np.array_equal(r.err.cpu().numpy()[ok].view(np.uint32), er[ok].view(np.uint32))
+    assert np.array_equal(r.iters.cpu().numpy(), it)
+
+
+def test_f32_lk_flags_and_frames_from_torch(gpu):
+    """initial flow / min-eigenvalue output; calc() on uint16 / float32 frames
+    builds fp32 pyramids itself"""
+    from opencv_amd import klt
+
+    a, b, gt = _frames("u16", 320, 240, seed=3)
+    pts = box_points(gt[0], 24, seed=3)
+    init = pts + np.float32([1.5, -0.75])
+    lk = klt.SparsePyrLKOpticalFlow((21, 21), 3, 30, True)
+    r = lk.calc(to_dev(a.view(np.int16)).view(torch.uint16), to_dev(b.view(np.int16)).view(torch.uint16),
+                to_dev(pts), to_dev(init))
+    torch.cuda.synchronize()
+    nx, st, er, _ = O.lk16(O.Pyramid16(a, (21, 21), 3, f32=True), O.Pyramid16(b, (21, 21), 3, f32=True), pts,
+                           flags=O.OPTFLOW_USE_INITIAL_FLOW, init=init)
+    ok = st == 1
+    assert np.array_equal(r.status.cpu().numpy(), st)
+    assert np.array_equal(r.next_pts.cpu().numpy()[ok].view(np.uint32), nx[ok].view(np.uint32))
+    lk2 = klt.SparsePyrLKOpticalFlow((21, 21), 3, 30, getMinEigenVals=True)
+    af, bf, _ = _frames("f32", 320, 240, seed=3)
+    r2 = lk2.calc(to_dev(af), to_dev(bf), to_dev(pts))
+    torch.cuda.synchronize()
+    nx2, st2, er2, _ = O.lk16(O.Pyramid16(af, (21, 21), 3, f32=True), O.Pyramid16(bf, (21, 21), 3, f32=True), pts,
+                              flags=O.OPTFLOW_LK_GET_MIN_EIGENVALS)
+    assert np.array_equal(r2.status.cpu().numpy(), st2)
+    assert np.array_equal(r2.err.cpu().numpy().view(np.uint32), er2.view(np.uint32))

@@ -276,3 +276,32 @@ def test_f16_lk_recovers_translation_and_tracks_u8_path():
     nt, stt, _, _ = O.lk16(O.Pyramid16(img), O.Pyramid16(shifted), g)
     assert (stt == 1).all()
     assert np.abs(nt - (g + np.float32([2, -1]))).max() < 0.02
+
+
+def test_f32_path_definitions_and_tracking():
+    """the fp32 pixel path (16U / 32F frames): pyrDown in the fp16 path's order
+    without rounding, the Scharr formula in fp32; on u8-valued frames it tracks
+    as the 8-bit and fp16 paths do (a sanity bound), and a 16U frame (x257)
+    tracks the same motion"""
+    frames, gt = O.synth(20261016, 320, 240, 12, 0, 2)
+    a = frames[0].astype(np.float32)
+    d = O.pyr_down32(a)
+    ref = O.pyr_down16(frames[0].astype(np.float16)).astype(np.float32)
+    assert np.abs(d - ref).max() <= np.abs(ref).max() * 2 ** -10  # fp16 rounding is the only difference
+    y, x = 7, 9
+    c = O.scharr32(a)
+    t0 = [(a[y - 1, x + k] + a[y + 1, x + k]) * np.float32(3) + a[y, x + k] * np.float32(10) for k in (-1, 0, 1)]
+    assert c[y, x, 0] == np.float32(t0[2] - t0[0])
+    rng = np.random.default_rng(1)
+    pts = np.concatenate([np.stack([rng.uniform(x, x + bw, 24), rng.uniform(y, y + bh, 24)], 1)
+                          for v, x, y, bw, bh in gt[0] if v]).astype(np.float32)
+    nx, st, _, _ = O.lk(O.Pyramid(frames[0]), O.Pyramid(frames[1]), pts, accum=O.ACCUM_EXACT)
+    nx32, st32, _, _ = O.lk16(O.Pyramid16(frames[0], f32=True), O.Pyramid16(frames[1], f32=True), pts)
+    both = (st == 1) & (st32 == 1)
+    assert both.mean() > 0.9 and (st == st32).mean() > 0.99
+    assert (np.abs(nx - nx32)[both].max(1) <= 1e-2).mean() >= 0.99
+    u16 = [f.astype(np.uint16) * 257 for f in frames[:2]]
+    nxu, stu, _, _ = O.lk16(O.Pyramid16(u16[0], f32=True), O.Pyramid16(u16[1], f32=True), pts)
+    bothu = (stu == 1) & (st32 == 1)
+    assert bothu.mean() > 0.9
+    assert (np.abs(nxu - nx32)[bothu].max(1) <= 1e-2).mean() >= 0.99
