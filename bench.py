@@ -825,10 +825,14 @@ def main(argv=None):
     ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
 
     m = TbdMeasure(args, ctx, dev)
+    # the CPU baseline (rank 0, N = 1) runs after every GPU leg: 20 s of all-core
+    # host load between the timed region and the secondary GPU legs left those
+    # legs measuring a cooled-down device (whole-sequence repeats ~9 % below
+    # the timed region right after it)
+    line, ms = run_contract(args, world, rank, m, torch.cuda.synchronize, "cuda", cpu_leg=None)
     nb = 60  # frames handed to the CPU baseline (it stops at its time budget)
-    cpu_leg = None if args.no_cpu_baseline else \
-        (lambda: cpu_baseline_line(m.frames[:nb].cpu().numpy(), m.gtn[:nb], args, restore_affinity=full_affinity))
-    line, ms = run_contract(args, world, rank, m, torch.cuda.synchronize, "cuda", cpu_leg=cpu_leg)
+    cpu_in = (m.frames[:nb].cpu().numpy(), m.gtn[:nb]) if (rank == 0 and world == 1 and
+                                                          not args.no_cpu_baseline) else None
     stream, cfg, frames, dets = m.stream, m.cfg, m.frames, m.dets
     timed = m.timed_kernels
     lk_pts = lk_it = klt_pts = ntr = redet = early = 0
@@ -979,6 +983,9 @@ def main(argv=None):
     if rank == 0 and not args.no_hog:
         progress("HOG secondary")
         line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+    if cpu_in is not None:
+        progress("cpu baseline")
+        line["cpu_baseline"] = cpu_baseline_line(cpu_in[0], cpu_in[1], args, restore_affinity=full_affinity)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
