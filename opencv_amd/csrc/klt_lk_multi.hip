@@ -159,7 +159,10 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 // op per row pair (1), or folded into each row's J rounding constant (0, one
 // VGPR per row; tuning builds)
 #ifndef TBDK_LK_IPACK
-#define TBDK_LK_IPACK 1
+#define TBDK_LK_IPACK 1  // derivative-plane instance (94 VGPRs -> 5 waves per SIMD)
+#endif
+#ifndef TBDK_LK_IPACK_FLY
+#define TBDK_LK_IPACK_FLY 0  // Scharr-on-the-fly instance: 4 waves per SIMD either way, one op fewer per row pair
 #endif
 
 #ifndef TBDK_LK_MULTI_WAVES
@@ -181,6 +184,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 {
     constexpr int P = 64 / WW;         // points per wave
     constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
+    constexpr bool IPACK = FLY ? TBDK_LK_IPACK_FLY != 0 : TBDK_LK_IPACK != 0;
     const int lane = threadIdx.x & 63;
     // point k of the wave owns lanes [1 + k*WW, 1 + (k+1)*WW); lane 0 (and any
     // lane past the last point) is idle with k == P and contributes 0
@@ -257,11 +261,8 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         // started from ic and shifted right by 9 is diff = J x32 - I x32 itself
         // (2^9 * I is a multiple of the divisor: floor((X - 2^9 I) / 2^9) =
         // floor(X / 2^9) - I); Ix, Iy packed by row pairs as int16 x 2
-#if TBDK_LK_IPACK
-        uint32_t ipk[NP];  // I x32 of rows (2q, 2q+1) as int16 x 2
-#else
-        int ic[WH];
-#endif
+        uint32_t ipk[IPACK ? NP : 1];  // I x32 of rows (2q, 2q+1) as int16 x 2
+        int ic[IPACK ? 1 : WH];
         uint32_t gxk[NP], gyk[NP];
         float A11, A12, A22;
         {
@@ -273,14 +274,14 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                                  uint32_t dx2, uint32_t dy0, uint32_t dy1, uint32_t dy2) {
                 const int r = 2 * q;
                 const bool two = r + 1 < WH;
-#if TBDK_LK_IPACK
-                const int i0 = bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9);
-                const int i1 = two ? bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) : 0;
-                ipk[q] = __builtin_amdgcn_perm((uint32_t)i1, (uint32_t)i0, 0x05040100u);
-#else
-                ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9) << 9);
-                if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) << 9);
-#endif
+                if constexpr (IPACK) {
+                    const int i0 = bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9);
+                    const int i1 = two ? bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) : 0;
+                    ipk[q] = __builtin_amdgcn_perm((uint32_t)i1, (uint32_t)i0, 0x05040100u);
+                } else {
+                    ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9) << 9);
+                    if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) << 9);
+                }
                 const int x0 = bilin_s<W_BITS1>(dx0, dx1, w0, w1, rnd14);
                 const int x1 = two ? bilin_s<W_BITS1>(dx1, dx2, w0, w1, rnd14) : 0;
                 const int y0 = bilin_s<W_BITS1>(dy0, dy1, w0, w1, rnd14);
@@ -372,13 +373,13 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                     pair_step(q, ip[r], ip[r + 1], ip[r2], dxp[r], dxp[r + 1], dxp[r2], dyp[r], dyp[r + 1], dyp[r2]);
                 }
             }
-#if TBDK_LK_IPACK
-            // materialise the I pairs here: left to the compiler, their bilinear
-            // sums sink below the G reduction and the J loads, where the I
-            // rows they read are then still live (+22 VGPRs at the peak)
+            if constexpr (IPACK) {
+                // materialise the I pairs here: left to the compiler, their bilinear
+                // sums sink below the G reduction and the J loads, where the I
+                // rows they read are then still live (+22 VGPRs at the peak)
 #pragma unroll
-            for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(ipk[q]));
-#endif
+                for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(ipk[q]));
+            }
             if (k >= P) acc[0] = acc[1] = acc[2] = 0;
             float s[3];
             seg_sum_exact<3>(acc, e4, s4, s);
@@ -436,17 +437,18 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             for (int q = 0; q < NP; ++q) {
                 const int r = 2 * q;
                 // (diff_r, diff_r+1) as int16 x 2, |diff| <= 8160
-#if TBDK_LK_IPACK
-                // (J x32 of rows r, r+1) as int16 x 2, minus the I pair: one packed subtract
-                const uint32_t jv = r + 1 < WH ? pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9),
-                                                           bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9))
-                                               : pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9), 0);
-                const uint32_t d = as_u32(as_s16x2(jv) - as_s16x2(ipk[q]));
-#else
-                const uint32_t d = r + 1 < WH ? pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]),
-                                                          bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]))
-                                              : pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]), 0);
-#endif
+                uint32_t d;
+                if constexpr (IPACK) {
+                    // (J x32 of rows r, r+1) as int16 x 2, minus the I pair: one packed subtract
+                    const uint32_t jv = r + 1 < WH ? pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9),
+                                                               bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9))
+                                                   : pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9), 0);
+                    d = as_u32(as_s16x2(jv) - as_s16x2(ipk[q]));
+                } else {
+                    d = r + 1 < WH ? pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]),
+                                               bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]))
+                                   : pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]), 0);
+                }
                 b[0] = sdot2(d, gxk[q], b[0]);
                 b[1] = sdot2(d, gyk[q], b[1]);
 #ifdef TBDK_LK_NEWTON_SB
@@ -494,19 +496,18 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #pragma unroll
                 for (int q = 0; q < NP; ++q) {
                     const int r = 2 * q;
-#if TBDK_LK_IPACK
-                    const int d0 = (bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] & 0xFFFFu);
-#else
-                    const int d0 = bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]) >> 9;
-#endif
+                    int d0;
+                    if constexpr (IPACK)
+                        d0 = (bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] & 0xFFFFu);
+                    else
+                        d0 = bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]) >> 9;
                     e += d0 < 0 ? -d0 : d0;
                     if (r + 1 < WH) {
-#if TBDK_LK_IPACK
-                        const int d1 =
-                            (bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] >> 16);
-#else
-                        const int d1 = bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]) >> 9;
-#endif
+                        int d1;
+                        if constexpr (IPACK)
+                            d1 = (bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] >> 16);
+                        else
+                            d1 = bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]) >> 9;
                         e += d1 < 0 ? -d1 : d1;
                     }
                 }
