@@ -59,6 +59,19 @@ def pyr_bytes(w: int, h: int, nlevels: int) -> int:
     return sum(sizes[i] + sizes[i + 1] for i in range(nlevels - 1))
 
 
+def pyr_build_bytes(w: int, h: int, nlevels: int, pad: int = 32) -> int:
+    """The bytes a levels-only build must move (the loop's pyramids): the frame
+    read once, every padded level written (reflect-101 frame included), and each
+    level from 2 on reading its interior predecessor (level 1 is made from the
+    frame itself).  B_pyr above leaves out the padded level-0 copy."""
+    sizes, padded = [], []
+    for _ in range(nlevels):
+        sizes.append(w * h)
+        padded.append((w + 2 * pad) * (h + 2 * pad))
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return sizes[0] + sum(padded) + sum(sizes[1:nlevels - 1])
+
+
 def max_over_ranks(value: float, world: int, device=None) -> float:
     """Max of a per-rank wall time over all ranks (the contract's job time).
     Collective only when world > 1; the tensor lives on `device` (cuda for
@@ -81,8 +94,11 @@ def replica_throughput(steps: int, world: int, max_elapsed: float) -> float:
 
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/rNN_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes,
-    see tools/profile_round.sh).  None when no summary covers the kernel."""
+    (profiles/rNN_pmc.json, separate --pmc passes, see tools/profile_round.sh):
+    FETCH_SIZE + WRITE_SIZE as counted.  The guide's x2 applies to wide (16 B
+    per lane) streaming reads; these kernels load 4 B per lane (or less), and the
+    pyramid's counts match its known read / write sets without it.
+    None when no summary covers the kernel."""
     d = os.path.join(ROOT, "profiles")
     try:
         files = sorted(f for f in os.listdir(d) if f.endswith("_pmc.json"))
@@ -92,7 +108,7 @@ def pmc_traffic(kernel_substr: str):
         k = json.load(open(os.path.join(d, f)))["kernels"]
         for name, v in k.items():
             if kernel_substr in name and v.get("fetch_bytes") is not None and v.get("write_bytes") is not None:
-                return v["fetch_bytes"] + v["write_bytes"], f
+                return v["fetch_size_kib"] * 1024 + v["write_bytes"], f
     return None, None
 
 
@@ -772,6 +788,8 @@ def main(argv=None):
                     help="ctx option tbd_early_gftt (A/B runs; 0 off, 1 new tracks, 2 + re-detection boxes)")
     ap.add_argument("--no-spec-lookahead", action="store_true", help="ctx option tbd_spec_lookahead = 0 (A/B runs)")
     ap.add_argument("--no-zero-copy", action="store_true", help="ctx option tbd_zero_copy = 0 (A/B runs)")
+    ap.add_argument("--pyr-derivs", action="store_true",
+                    help="ctx option tbd_pyr_derivs = 1: loop pyramids with Scharr planes (A/B runs)")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="HIP events on every Nth launch of the timed kernels in the timed region")
     ap.add_argument("--kstats", default="lk_sparse",
@@ -823,6 +841,7 @@ def main(argv=None):
     ctx.set_option("tbd_early_gftt", args.early_gftt)
     ctx.set_option("tbd_spec_lookahead", 0 if args.no_spec_lookahead else 1)
     ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
+    ctx.set_option("tbd_pyr_derivs", 1 if args.pyr_derivs else 0)
 
     m = TbdMeasure(args, ctx, dev)
     # the CPU baseline (rank 0, N = 1) runs after every GPU leg: 20 s of all-core
@@ -915,17 +934,21 @@ def main(argv=None):
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}
     pb = pyr_bytes(args.width, args.height, nlev)
+    pbb = pyr_build_bytes(args.width, args.height, nlev)
     pyr = kstats.get("pyr_build", kstats_aside.get("pyr_build", nolaunch))
-    pyr_gbs = pb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
+    pyr_gbs = pbb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     cnt = pmc_bytes(PYR_KERNELS)
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb, "kernel": "pyr_build",
-                "traffic": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,
-                "traffic_raw": (cnt["fetch_raw"] + cnt["write"]) if cnt else None,
+                "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pbb, "b_pyr_survey": pb,
+                "kernel": "pyr_build",
+                "traffic": (cnt["fetch_raw"] + cnt["write"]) if cnt else None,
+                "traffic_fetch_x2": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,
+                "traffic_over_algorithmic": round((cnt["fetch_raw"] + cnt["write"]) / pbb, 3) if cnt else None,
                 "traffic_kernels": cnt["kernels"] if cnt else None, "traffic_source": cnt["source"] if cnt else None,
-                "note": "achieved = SURVEY §8d algorithmic bytes (new frame read, levels 1.. written and re-read) / "
-                        "the build's HIP-event time; traffic = counter bytes per build (FETCH_SIZE x2 and raw, "
-                        "+ WRITE_SIZE), which include the Scharr planes the algorithmic count leaves out"}
+                "note": "achieved = the levels-only build's algorithmic bytes (frame read once, every padded level "
+                        "written, levels >= 2 reading their predecessor; bytes_per_launch) / the build's HIP-event "
+                        "time (both launches); b_pyr_survey = SURVEY §8d's B_pyr (no level-0 copy); traffic = "
+                        "FETCH_SIZE + WRITE_SIZE per build from the committed PMC summary (4-byte loads: no x2)"}
     # north_star's "HBM-read roofline on pyramid+PyrLK": SURVEY §8d bytes B_pyr + B_lk + N*21,
     # with B_lk at its upper bound (2 full pyramids), over the two stages' summed time
     w_, h_, lv_bytes = args.width, args.height, 0
@@ -934,9 +957,9 @@ def main(argv=None):
         w_, h_ = (w_ + 1) // 2, (h_ + 1) // 2
     b_lk = 2 * lv_bytes + 21 * (lk_pts / max(1, args.steps))
     t_pl = ((pyr["avg_us"] or 0.0) + (lk["avg_us"] or 0.0)) * 1e-6
-    hbm_pl = (pb + b_lk) / t_pl / 1e9 if t_pl > 0 else 0.0
+    hbm_pl = (pbb + b_lk) / t_pl / 1e9 if t_pl > 0 else 0.0
     roof_pl = {"bound": "hbm", "achieved": round(hbm_pl, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-               "frac": round(hbm_pl / PEAK_HBM_GBS, 4), "bytes_per_frame": pb + b_lk,
+               "frac": round(hbm_pl / PEAK_HBM_GBS, 4), "bytes_per_frame": pbb + b_lk,
                "kernels": "pyr_build + lk_sparse",
                "note": "B_lk taken at its SURVEY §8d upper bound (2 full pyramids); PyrLK is compute-bound "
                        "(~360 flop/B vs ridge ~20), so this fraction is structurally small (DESIGN.md §3)"}

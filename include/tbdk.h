@@ -148,6 +148,9 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       kernels read their host tables from, and the fit writes its results
  *       to, coherent pinned host memory directly instead of through copies
  *       (results equal).
+ *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
+ *       pyramids carry Scharr derivative planes and PyrLK reads them instead of
+ *       deriving the window's values (results equal; A/B runs).
  *   "timing_every" (>= 1, default 1): HIP events on a pseudo-random 1/N of the
  *       launches of each kernel selected for timing: launch i (counted per
  *       kernel name from tbdk_timing_enable) is timed iff splitmix64(i) % N == 0
@@ -362,6 +365,7 @@ int tbdk_box_propagate(tbdk_ctx* ctx, const float* prev_pts, const float* next_p
  *  core/include/opencv2/core/base.hpp BORDER_*) */
 #define TBDK_INTER_NEAREST 0
 #define TBDK_INTER_LINEAR 1
+#define TBDK_INTER_CUBIC 2            /* remapBicubic, BicubicTab_i (imgwarp.cpp:152-268, 860-958) */
 #define TBDK_INTER_AREA 3            /* treated as INTER_LINEAR, as cv::warpAffine does */
 #define TBDK_WARP_INVERSE_MAP 16
 #define TBDK_BORDER_CONSTANT 0
@@ -379,7 +383,7 @@ int tbdk_box_propagate(tbdk_ctx* ctx, const float* prev_pts, const float* next_p
  *   src, dst : device u8 images (row pitch in bytes); dst must not alias src
  *   M        : HOST 2x3 row-major double matrix (dst <- src unless
  *              TBDK_WARP_INVERSE_MAP, then dst -> src, as in the reference)
- *   flags    : TBDK_INTER_NEAREST / LINEAR / AREA | TBDK_WARP_INVERSE_MAP
+ *   flags    : TBDK_INTER_NEAREST / LINEAR / CUBIC / AREA | TBDK_WARP_INVERSE_MAP
  *   border   : TBDK_BORDER_*; border_value used by BORDER_CONSTANT */
 int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int src_height, int src_pitch,
                         uint8_t* dst, int dst_width, int dst_height, int dst_pitch, const double* M,

@@ -76,12 +76,21 @@ private:
 // gives the fp16 pixel path's pyramid (tbdk_pyr_create_f16).
 class Pyramid {
 public:
-    Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}, int depth = TBDK_DEPTH_8U)
+    // depth TBDK_DEPTH_8U (cn 1..4 channels, interleaved), TBDK_DEPTH_16F or TBDK_DEPTH_32F (one channel)
+    Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}, int depth = TBDK_DEPTH_8U,
+            int cn = 1)
         : ctx_(&ctx)
     {
+        if (cn != 1 && depth != TBDK_DEPTH_8U) throw Error(TBDK_EINVAL, "Pyramid: multi-channel pyramids are 8U");
         if (depth == TBDK_DEPTH_16F)
             check(tbdk_pyr_create_f16(ctx.get(), width, height, max_level, win.width, win.height, &p_),
                   "tbdk_pyr_create_f16");
+        else if (depth == TBDK_DEPTH_32F)
+            check(tbdk_pyr_create_f32(ctx.get(), width, height, max_level, win.width, win.height, &p_),
+                  "tbdk_pyr_create_f32");
+        else if (cn != 1)
+            check(tbdk_pyr_create_cn(ctx.get(), width, height, cn, max_level, win.width, win.height, &p_),
+                  "tbdk_pyr_create_cn");
         else
             check(tbdk_pyr_create(ctx.get(), width, height, max_level, win.width, win.height, &p_), "tbdk_pyr_create");
     }
@@ -99,7 +108,19 @@ public:
         if (width != p_.lv[0].width || height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build_f16");
         check(tbdk_pyr_build_f16(ctx_->get(), data, pitch, &p_, stream), "tbdk_pyr_build_f16");
     }
+    // 16U / 32F frames (pitch in bytes) into an fp32 pyramid (the CUDA class's other depths)
+    void build_u16(const uint16_t* data, int width, int height, int pitch, void* stream = nullptr)
+    {
+        if (width != p_.lv[0].width || height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build_u16");
+        check(tbdk_pyr_build_u16(ctx_->get(), data, pitch, &p_, stream), "tbdk_pyr_build_u16");
+    }
+    void build_f32(const float* data, int width, int height, int pitch, void* stream = nullptr)
+    {
+        if (width != p_.lv[0].width || height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build_f32");
+        check(tbdk_pyr_build_f32(ctx_->get(), data, pitch, &p_, stream), "tbdk_pyr_build_f32");
+    }
     int depth() const { return p_.depth; }
+    int channels() const { return p_.cn > 1 ? p_.cn : 1; }
     const tbdk_pyr& get() const { return p_; }
     int levels() const { return p_.nlevels; }
 
@@ -289,6 +310,17 @@ private:
     Context* ctx_;
     tbdk_gftt_params p_{};
 };
+
+// cv::cuda::createMinEigenValCorner(CV_8UC1, blockSize, 3)->compute (harris false) and
+// cv::cuda::createHarrisCorner(CV_8UC1, blockSize, 3, k)->compute (harris true)
+// (cudaimgproc.hpp:548-566): dst is a device float plane (dst_pitch bytes)
+inline void cornerResponse(Context& ctx, const GpuImage& src, float* dst, int dst_pitch, int blockSize = 3,
+                           bool harris = false, double k = 0.04, void* stream = nullptr)
+{
+    check(tbdk_corner_response(ctx.get(), src.data, src.width, src.height, src.pitch, dst, dst_pitch, blockSize,
+                               harris ? 1 : 0, k, stream),
+          "tbdk_corner_response");
+}
 
 // cv::cuda::pyrDown (cudawarping.hpp:201): dst must be ((w+1)/2, (h+1)/2)
 inline void pyrDown(Context& ctx, const GpuImage& src, GpuImage& dst, void* stream = nullptr)

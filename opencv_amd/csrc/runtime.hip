@@ -180,6 +180,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_hog_block_tiled = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_pyr_derivs") == 0) {
+        ctx->opt_tbd_pyr_derivs = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "pyr_fuse") == 0) {
         ctx->opt_pyr_fuse = value != 0;
         return TBDK_OK;
@@ -805,7 +809,8 @@ int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int sr
         return TBDK_EINVAL;
     int inter = flags & 7;
     if (inter == TBDK_INTER_AREA) inter = TBDK_INTER_LINEAR;
-    if ((inter != TBDK_INTER_NEAREST && inter != TBDK_INTER_LINEAR) || (flags & ~(7 | TBDK_WARP_INVERSE_MAP)))
+    if ((inter != TBDK_INTER_NEAREST && inter != TBDK_INTER_LINEAR && inter != TBDK_INTER_CUBIC) ||
+        (flags & ~(7 | TBDK_WARP_INVERSE_MAP)))
         return TBDK_EINVAL;
     if (border < TBDK_BORDER_CONSTANT || border > TBDK_BORDER_TRANSPARENT) return TBDK_EINVAL;
     // dst == src: the reference clones src (imgwarp.cpp:2595-2596); here aliasing is an error

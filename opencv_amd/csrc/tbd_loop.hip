@@ -331,8 +331,11 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     int rc = TBDK_OK;
     for (int i = 0; i < 2 && rc == TBDK_OK; ++i)
         // levels only: PyrLK derives the window's Scharr values itself, so the
-        // build is one fused launch and writes no derivative planes
-        rc = tbdk_pyr_create_levels(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i]);
+        // build writes no derivative planes (ctx option tbd_pyr_derivs = 1: with
+        // the planes, for A/B runs; same results)
+        rc = ctx->opt_tbd_pyr_derivs
+                 ? tbdk_pyr_create(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i])
+                 : tbdk_pyr_create_levels(ctx, cfg->width, cfg->height, cfg->max_level, cfg->win, cfg->win, &t->pyr[i]);
     if (rc != TBDK_OK) {
         release(t);
         return rc;

@@ -1,7 +1,11 @@
-// warp.hip — cv::warpAffine for u8 gray images (INTER_NEAREST / INTER_LINEAR,
-// every border mode) on gfx950, bit-exact with the CPU implementation's
-// fixed-point path (imgproc/src/imgwarp.cpp:2155-2290 map generation,
-// remapBilinear :649-866 / remapNearest :330-440; see oracle/warp_oracle.c).
+// warp.hip — cv::warpAffine for u8 gray images (INTER_NEAREST / INTER_LINEAR /
+// INTER_CUBIC, every border mode) on gfx950, bit-exact with the CPU
+// implementation's fixed-point path (imgproc/src/imgwarp.cpp:2155-2290 map
+// generation, remapBilinear :649-866 / remapNearest :330-440 / remapBicubic
+// :860-958; see oracle/warp_oracle.c).  INTER_CUBIC derives each pixel's 16
+// BicubicTab_i weights in the kernel (interpolateCubic in float, the products
+// rounded to short, initInterTab2D's sum correction, :152-160, 213-268)
+// instead of reading a table: the same integers, no device globals.
 //
 // One thread per 4 destination pixels of a row: the per-row term
 // (M1*y + M2)*1024 is formed once per thread in double exactly as the
@@ -45,6 +49,53 @@ __device__ __forceinline__ int border_interp(int p, int len, int border)
         return p;
     }
     return -1;
+}
+
+// interpolateCubic (imgwarp.cpp:152-160)
+__device__ __forceinline__ void cubic_coeffs(float x, float* c)
+{
+    const float A = -0.75f;
+    c[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    c[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    c[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+// BicubicTab_i[ay*32 + ax] (initInterTab2D, imgwarp.cpp:213-268)
+__device__ __forceinline__ void bicubic_tab(int ay, int ax, int* w)
+{
+    const float scale = 1.f / 32;
+    float cy[4], cx[4];
+    cubic_coeffs(ay * scale, cy);
+    cubic_coeffs(ax * scale, cx);
+    int isum = 0;
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+            int iv = __float2int_rn(cy[k1] * cx[k2] * 32768);  // saturate_cast<short>(float)
+            iv = iv < -32768 ? -32768 : (iv > 32767 ? 32767 : iv);
+            w[k1 * 4 + k2] = iv;
+            isum += iv;
+        }
+    if (isum != 32768) {  // the correction searches taps (2..3, 2..3), as the reference does
+        const int diff = isum - 32768;
+        int M = 10, m = 10;
+#pragma unroll
+        for (int k1 = 2; k1 < 4; ++k1)
+#pragma unroll
+            for (int k2 = 2; k2 < 4; ++k2) {
+                const int t = k1 * 4 + k2;
+                if (w[t] < w[m]) m = t;
+                else if (w[t] > w[M]) M = t;
+            }
+        // w[] is indexed by runtime values here: keep it in registers via selects
+#pragma unroll
+        for (int t = 10; t < 16; ++t) {
+            if (diff < 0 && t == M) w[t] -= diff;
+            if (diff >= 0 && t == m) w[t] -= diff;
+        }
+    }
 }
 
 struct WarpArgs {
@@ -94,6 +145,50 @@ __global__ __launch_bounds__(256) void warp_affine_kernel(WarpArgs a)
         const int X = wrap_add(X0, ad) >> 5, Y = wrap_add(Y0, bd) >> 5;
         const int sx = sat16(X >> 5), sy = sat16(Y >> 5);
         const int ax = X & 31, ay = Y & 31;
+        if (INTER == 2) {  // remapBicubic (imgwarp.cpp:860-958)
+            int w[16];
+            bicubic_tab(ay, ax, w);
+            const int bx = sx - 1, by = sy - 1;
+            int sum;
+            if ((unsigned)bx < (unsigned)(a.sw - 3 > 0 ? a.sw - 3 : 0) &&
+                (unsigned)by < (unsigned)(a.sh - 3 > 0 ? a.sh - 3 : 0)) {
+                const uint8_t* S = a.src + (size_t)by * a.spitch + bx;
+                sum = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r, S += a.spitch)
+                    sum += S[0] * w[4 * r] + S[1] * w[4 * r + 1] + S[2] * w[4 * r + 2] + S[3] * w[4 * r + 3];
+            } else {
+                if (a.border == TBDK_BORDER_TRANSPARENT &&
+                    ((unsigned)(bx + 1) >= (unsigned)a.sw || (unsigned)(by + 1) >= (unsigned)a.sh)) {
+                    keep[k] = true;
+                    continue;
+                }
+                const int b1 = a.border != TBDK_BORDER_TRANSPARENT ? a.border : TBDK_BORDER_REFLECT_101;
+                if (b1 == TBDK_BORDER_CONSTANT && (bx >= a.sw || bx + 4 <= 0 || by >= a.sh || by + 4 <= 0)) {
+                    out[k] = cval;
+                    continue;
+                }
+                int xs[4], ys[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    xs[q] = border_interp(bx + q, a.sw, b1);
+                    ys[q] = border_interp(by + q, a.sh, b1);
+                }
+                const int cv = cval;
+                sum = cv * 32768;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (ys[r] < 0) continue;
+                    const uint8_t* S = a.src + (size_t)ys[r] * a.spitch;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (xs[q] >= 0) sum += (S[xs[q]] - cv) * w[4 * r + q];
+                }
+            }
+            const int r = (sum + (1 << 14)) >> 15;  // FixedPtCast<int, uchar, 15>
+            out[k] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+            continue;
+        }
         // BilinearTab_i (imgwarp.cpp:211-268): 15-bit weights, exact for INTER_LINEAR
         const int w0 = (32 - ay) * (32 - ax) * 32, w1 = (32 - ay) * ax * 32;
         const int w2 = ay * (32 - ax) * 32, w3 = ay * ax * 32;
@@ -183,6 +278,7 @@ hipError_t launch_warp_affine(const uint8_t* src, int sw, int sh, int spitch, ui
     a.cval = cval;
     const dim3 grid((dw + 4 * 256 - 1) / (4 * 256), dh), block(256);
     if (inter == 0) hipLaunchKernelGGL(warp_affine_kernel<0>, grid, block, 0, s, a);
+    else if (inter == 2) hipLaunchKernelGGL(warp_affine_kernel<2>, grid, block, 0, s, a);
     else hipLaunchKernelGGL(warp_affine_kernel<1>, grid, block, 0, s, a);
     return hipGetLastError();
 }

@@ -279,7 +279,7 @@ def box_propagate(prev_pts: torch.Tensor, next_pts: torch.Tensor, status, offset
 
 
 # interpolation flags / border modes (reference values, imgproc.hpp / core/base.hpp)
-INTER_NEAREST, INTER_LINEAR, INTER_AREA, WARP_INVERSE_MAP = 0, 1, 3, 16
+INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA, WARP_INVERSE_MAP = 0, 1, 2, 3, 16
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = range(6)
 
 

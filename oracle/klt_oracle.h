@@ -134,6 +134,7 @@ int orc_border_interpolate(int p, int len, int border);
 void orc_invert_affine(const double* M, double* out);
 /* cv::warpAffine of a CV_8UC1 image; flags = INTER_NEAREST(0) / INTER_LINEAR(1) /
  * INTER_AREA(3, as LINEAR) | WARP_INVERSE_MAP(16); returns -1 for other modes */
+void orc_bicubic_tab(int ay, int ax, short* w);
 int orc_warp_affine_u8(const uint8_t* src, int sw, int sh, int spitch, uint8_t* dst, int dw, int dh, int dpitch,
                        const double* M, int flags, int border, int bval);
 #ifdef __cplusplus

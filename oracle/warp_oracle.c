@@ -11,6 +11,10 @@
  *   remapBilinear<FixedPtCast<int,uchar,15>> with BilinearTab_i (15-bit
  *     weights (32-a)(32-b)*32 ..., exact for INTER_LINEAR)            :649-866, 211-268
  *   remapNearest                                                    :330-440
+ *   INTER_CUBIC: the same map (5-bit table index); remapBicubic<FixedPtCast<int,
+ *     uchar,15>> (:860-958) with BicubicTab_i built as initInterTab2D does
+ *     (:152-160 interpolateCubic in float, A = -0.75; :213-268 products
+ *     rounded to short, the sum corrected to 2^15 on the central 2x2)
  *   borderInterpolate (core/src/copy.cpp) for REFLECT/REFLECT_101/WRAP,
  *     clip() for REPLICATE, cval for CONSTANT, skip for TRANSPARENT.
  * saturate_cast<int>(double) is cvRound (SSE2 cvtsd2si: round half to even,
@@ -56,6 +60,45 @@ int orc_border_interpolate(int p, int len, int border)
 
 static int clipi(int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; }
 
+/* interpolateCubic (imgwarp.cpp:152-160), float */
+static void cubic_coeffs(float x, float* c)
+{
+    const float A = -0.75f;
+    c[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    c[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    c[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+/* BicubicTab_i[ay*32 + ax] (initInterTab2D, imgwarp.cpp:213-268) */
+void orc_bicubic_tab(int ay, int ax, short* w)
+{
+    const float scale = 1.f / 32;
+    float cy[4], cx[4];
+    cubic_coeffs(ay * scale, cy);
+    cubic_coeffs(ax * scale, cx);
+    int isum = 0;
+    for (int k1 = 0; k1 < 4; ++k1)
+        for (int k2 = 0; k2 < 4; ++k2) {
+            const float v = cy[k1] * cx[k2];
+            int iv = (int)nearbyintf(v * 32768); /* saturate_cast<short>(float): cvRound, then clamp */
+            iv = iv < -32768 ? -32768 : (iv > 32767 ? 32767 : iv);
+            w[k1 * 4 + k2] = (short)iv;
+            isum += iv;
+        }
+    if (isum != 32768) {
+        const int diff = isum - 32768;
+        int Mk1 = 2, Mk2 = 2, mk1 = 2, mk2 = 2;
+        for (int k1 = 2; k1 < 4; ++k1)
+            for (int k2 = 2; k2 < 4; ++k2) {
+                if (w[k1 * 4 + k2] < w[mk1 * 4 + mk2]) mk1 = k1, mk2 = k2;
+                else if (w[k1 * 4 + k2] > w[Mk1 * 4 + Mk2]) Mk1 = k1, Mk2 = k2;
+            }
+        if (diff < 0) w[Mk1 * 4 + Mk2] = (short)(w[Mk1 * 4 + Mk2] - diff);
+        else w[mk1 * 4 + mk2] = (short)(w[mk1 * 4 + mk2] - diff);
+    }
+}
+
 void orc_invert_affine(const double* M, double* out)
 {
     double m[6];
@@ -79,7 +122,7 @@ int orc_warp_affine_u8(const uint8_t* src, int sw, int sh, int spitch, uint8_t* 
 {
     int inter = flags & 7;
     if (inter == 3) inter = 1; /* INTER_AREA -> INTER_LINEAR (:2600-2601) */
-    if (inter != 0 && inter != 1) return -1;
+    if (inter != 0 && inter != 1 && inter != 2) return -1;
     double M[6];
     if (flags & ORC_WARP_INVERSE_MAP) {
         for (int i = 0; i < 6; ++i) M[i] = M0[i];
@@ -112,6 +155,43 @@ int orc_warp_affine_u8(const uint8_t* src, int sw, int sh, int spitch, uint8_t* 
             const int X = wrap_add(X0, ad) >> 5, Y = wrap_add(Y0, bd) >> 5;
             const int sx = sat16(X >> 5), sy = sat16(Y >> 5);
             const int ax = X & 31, ay = Y & 31;
+            if (inter == 2) { /* remapBicubic (imgwarp.cpp:860-958) */
+                short w[16];
+                orc_bicubic_tab(ay, ax, w);
+                const int bx = sx - 1, by = sy - 1;
+                int sum;
+                if ((unsigned)bx < (unsigned)(sw - 3 > 0 ? sw - 3 : 0) && (unsigned)by < (unsigned)(sh - 3 > 0 ? sh - 3 : 0)) {
+                    const uint8_t* S = src + (size_t)by * spitch + bx;
+                    sum = 0;
+                    for (int r = 0; r < 4; ++r, S += spitch)
+                        sum += S[0] * w[4 * r] + S[1] * w[4 * r + 1] + S[2] * w[4 * r + 2] + S[3] * w[4 * r + 3];
+                } else {
+                    if (border == ORC_BORDER_TRANSPARENT &&
+                        ((unsigned)(bx + 1) >= (unsigned)sw || (unsigned)(by + 1) >= (unsigned)sh))
+                        continue;
+                    const int b1 = border != ORC_BORDER_TRANSPARENT ? border : ORC_BORDER_REFLECT_101;
+                    if (b1 == ORC_BORDER_CONSTANT && (bx >= sw || bx + 4 <= 0 || by >= sh || by + 4 <= 0)) {
+                        D[x] = cval;
+                        continue;
+                    }
+                    int xs[4], ys[4];
+                    for (int i = 0; i < 4; ++i) {
+                        xs[i] = orc_border_interpolate(bx + i, sw, b1);
+                        ys[i] = orc_border_interpolate(by + i, sh, b1);
+                    }
+                    const int cv = cval;
+                    sum = cv * 32768;
+                    for (int i = 0; i < 4; ++i) {
+                        if (ys[i] < 0) continue;
+                        const uint8_t* S = src + (size_t)ys[i] * spitch;
+                        for (int j = 0; j < 4; ++j)
+                            if (xs[j] >= 0) sum += (S[xs[j]] - cv) * w[4 * i + j];
+                    }
+                }
+                const int r = (sum + (1 << 14)) >> 15; /* FixedPtCast<int, uchar, 15> */
+                D[x] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+                continue;
+            }
             /* BilinearTab_i[ay*32+ax] = {(32-ay)(32-ax), (32-ay)ax, ay(32-ax), ay*ax} * 32 */
             const int w0 = (32 - ay) * (32 - ax) * 32, w1 = (32 - ay) * ax * 32;
             const int w2 = ay * (32 - ax) * 32, w3 = ay * ax * 32;

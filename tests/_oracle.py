@@ -384,7 +384,7 @@ def gftt_rois(frame: np.ndarray, rois, max_corners=256, quality=0.01, min_distan
 
 # border modes / flags (reference values: core/base.hpp, imgproc.hpp)
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = range(6)
-INTER_NEAREST, INTER_LINEAR, INTER_AREA = 0, 1, 3
+INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA = 0, 1, 2, 3
 WARP_INVERSE_MAP = 16
 
 

@@ -19,7 +19,7 @@ def run(gpu, src, M, dsize, flags, border, bval, init=None):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("inter", [O.INTER_NEAREST, O.INTER_LINEAR, O.INTER_AREA])
+@pytest.mark.parametrize("inter", [O.INTER_NEAREST, O.INTER_LINEAR, O.INTER_CUBIC, O.INTER_AREA])
 @pytest.mark.parametrize("border", [O.BORDER_CONSTANT, O.BORDER_REPLICATE, O.BORDER_REFLECT, O.BORDER_WRAP,
                                     O.BORDER_REFLECT_101, O.BORDER_TRANSPARENT])
 @pytest.mark.parametrize("inverse", [False, True])
@@ -46,13 +46,14 @@ def test_warp_1080p_box_propagation(gpu):
     src = fr[0]
     a = np.deg2rad(0.8)
     M = np.array([[1.01 * np.cos(a), -1.01 * np.sin(a), 2.5], [1.01 * np.sin(a), 1.01 * np.cos(a), -1.75]])
-    for flags in (O.INTER_LINEAR, O.INTER_NEAREST | O.WARP_INVERSE_MAP):
+    for flags in (O.INTER_LINEAR, O.INTER_NEAREST | O.WARP_INVERSE_MAP, O.INTER_CUBIC):
         got = run(gpu, src, M, (1920, 1080), flags, O.BORDER_REFLECT_101, 0)
         assert np.array_equal(got, O.warp_affine(src, M, (1920, 1080), flags, O.BORDER_REFLECT_101, 0))
     for M in (np.zeros((2, 3)), np.array([[1e6, 0, 0], [0, 1e-7, 5e9]]), np.array([[0, 1, 0], [1, 0, 0]])):
         small = src[:64, :96].copy()
-        got = run(gpu, small, M, (70, 50), O.INTER_LINEAR, O.BORDER_CONSTANT, 3)
-        assert np.array_equal(got, O.warp_affine(small, M, (70, 50), O.INTER_LINEAR, O.BORDER_CONSTANT, 3))
+        for inter in (O.INTER_LINEAR, O.INTER_CUBIC):
+            got = run(gpu, small, M, (70, 50), inter, O.BORDER_CONSTANT, 3)
+            assert np.array_equal(got, O.warp_affine(small, M, (70, 50), inter, O.BORDER_CONSTANT, 3))
 
 
 def test_warp_rejects_bad_arguments(gpu):
@@ -60,7 +61,7 @@ def test_warp_rejects_bad_arguments(gpu):
 
     s = torch.zeros((10, 10), dtype=torch.uint8, device="cuda")
     with pytest.raises(_lib.TbdkError):
-        klt.warp_affine(s, np.eye(2, 3), (10, 10), flags=2, ctx=gpu)  # INTER_CUBIC unsupported
+        klt.warp_affine(s, np.eye(2, 3), (10, 10), flags=4, ctx=gpu)  # INTER_LANCZOS4 unsupported
     with pytest.raises(_lib.TbdkError):
         klt.warp_affine(s, np.eye(2, 3), (10, 10), borderMode=7, ctx=gpu)
     with pytest.raises(_lib.TbdkError):

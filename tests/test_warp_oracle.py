@@ -78,8 +78,57 @@ def ref_test_maps(M, dsize, inter, inverse):
     return mx, fa
 
 
+def cubic_coeffs(x):
+    """interpolateCubic of the reference test (test_imgwarp_strict.cpp:379-387), float32"""
+    f = np.float32
+    x = f(x)
+    A = f(-0.75)
+    c0 = ((A * (x + f(1)) - f(5) * A) * (x + f(1)) + f(8) * A) * (x + f(1)) - f(4) * A
+    c1 = ((A + f(2)) * x - (A + f(3))) * x * x + f(1)
+    c2 = ((A + f(2)) * (f(1) - x) - (A + f(3))) * (f(1) - x) * (f(1) - x) + f(1)
+    return [c0, c1, c2, f(1) - c0 - c1 - c2]
+
+
+def ref_test_remap_cubic(src, mx, fa, border, bval):
+    """remap_generic with ksize 4, ofs 1 (test_imgwarp_strict.cpp:928-1017)"""
+    sh, sw = src.shape
+    dh, dw = fa.shape
+    out = np.zeros((dh, dw), np.float64)
+    s = src.astype(np.float32)
+    f = np.float32
+    for dy in range(dh):
+        for dx in range(dw):
+            isx, isy = int(mx[dy, dx, 0]) - 1, int(mx[dy, dx, 1]) - 1
+            w = cubic_coeffs((fa[dy, dx] & 31) / f(32))
+            wy = cubic_coeffs(((fa[dy, dx] >> 5) & 31) / f(32))
+            if 0 <= isx < sw - 3 and 0 <= isy < sh - 3:
+                ix = []
+                for y in range(4):
+                    acc = f(0)
+                    for i in range(4):
+                        acc = f(acc + w[i] * s[isy + y, isx + i])
+                    ix.append(acc)
+            else:
+                ax = [border_interp_c(isx + k, sw, border) for k in range(4)]
+                ay = [border_interp_c(isy + k, sh, border) for k in range(4)]
+                ix = []
+                for i in range(4):
+                    acc = f(0)
+                    for j in range(4):
+                        v = s[ay[i], ax[j]] if (ay[i] >= 0 and ax[j] >= 0) else f(bval)
+                        acc = f(acc + f(v * w[j]))
+                    ix.append(acc)
+            acc = f(0)
+            for i in range(4):
+                acc = f(acc + f(wy[i] * ix[i]))
+            out[dy, dx] = acc
+    return out
+
+
 def ref_test_remap(src, mx, fa, inter, border, bval):
     """remap_nearest / remap_generic (float weights, ksize 2) of the reference test."""
+    if inter == O.INTER_CUBIC:
+        return ref_test_remap_cubic(src, mx, fa, border, bval)
     sh, sw = src.shape
     dh, dw = fa.shape
     out = np.zeros((dh, dw), np.float64)
@@ -125,6 +174,11 @@ CASES = [
     (6, (37, 29), (41, 33), 12.0, 1.6, O.INTER_NEAREST, False, O.BORDER_CONSTANT),
     (7, (31, 27), (35, 35), -150.0, 0.9, O.INTER_NEAREST, True, O.BORDER_REFLECT_101),
     (8, (26, 38), (32, 32), 95.0, 1.4, O.INTER_NEAREST, False, O.BORDER_WRAP),
+    (9, (37, 29), (41, 33), 30.0, 1.3, O.INTER_CUBIC, False, O.BORDER_CONSTANT),
+    (10, (40, 31), (40, 31), -115.0, 0.7, O.INTER_CUBIC, True, O.BORDER_REPLICATE),
+    (11, (23, 45), (30, 30), 170.0, 1.9, O.INTER_CUBIC, False, O.BORDER_REFLECT),
+    (12, (33, 33), (29, 35), 64.0, 0.45, O.INTER_CUBIC, False, O.BORDER_WRAP),
+    (13, (50, 20), (44, 26), -33.0, 1.1, O.INTER_CUBIC, True, O.BORDER_REFLECT_101),
 ]
 
 
@@ -139,7 +193,9 @@ def test_warp_oracle_matches_reference_validator(seed, ssz, dsz, angle, scale, i
     got = O.warp_affine(src, M, dsz, flags, border, bval)
     mx, fa = ref_test_maps(M, dsz, inter, inverse)
     ref = ref_test_remap(src, mx, fa, inter, border, bval)
-    diff = np.abs(got.astype(np.float64) - ref)
+    # validate_results (:247-266) ignores reference values outside [0, 255] (cubic overshoot)
+    inside = (ref >= 0.0) & (ref <= 255.0)
+    diff = np.abs(got.astype(np.float64) - ref) * inside
     assert diff.max() <= 1.0, diff.max()
     if inter == O.INTER_NEAREST:
         assert diff.max() == 0
@@ -169,4 +225,34 @@ def test_warp_transparent_keeps_destination():
     M = rotation_matrix(10, 10, 45, 1.5)
     init = np.full((30, 30), 99, np.uint8)
     out = O.warp_affine(src, M, (30, 30), O.INTER_LINEAR, O.BORDER_TRANSPARENT, 0, dst=init)
+    assert (out == 99).any() and (out != 99).any()
+
+
+def test_bicubic_table_sums_and_known_answers():
+    """BicubicTab_i: every entry's 16 weights sum to 2^15 (initInterTab2D's
+    correction, imgwarp.cpp:251-264); integer shifts and the identity warp
+    reproduce the source with INTER_CUBIC"""
+    import ctypes as C
+
+    lib = O.load()
+    lib.orc_bicubic_tab.argtypes = [C.c_int, C.c_int, C.c_void_p]
+    for ay in range(32):
+        for ax in range(32):
+            w = np.zeros(16, np.int16)
+            lib.orc_bicubic_tab(ay, ax, w.ctypes.data_as(C.c_void_p))
+            assert int(w.astype(np.int64).sum()) == 32768
+            if ax == 0 and ay == 0:
+                # 1.0 * 2^15 saturates to 32767 and the sum correction searches
+                # taps (2..3, 2..3), so the missing unit lands on tap (2, 2)
+                assert w[5] == 32767 and w[10] == 1 and (np.delete(w, [5, 10]) == 0).all()
+    rng = np.random.default_rng(21)
+    src = rng.integers(0, 256, (24, 40), dtype=np.uint8)
+    ident = np.array([[1, 0, 0], [0, 1, 0]], np.float64)
+    assert np.array_equal(O.warp_affine(src, ident, (40, 24), O.INTER_CUBIC, O.BORDER_REFLECT_101), src)
+    T = np.array([[1, 0, 3], [0, 1, -2]], np.float64)
+    out = O.warp_affine(src, T, (40, 24), O.INTER_CUBIC, O.BORDER_CONSTANT, 7)
+    assert np.array_equal(out[0:22, 3:40], src[2:24, 0:37])
+    init = np.full((30, 30), 99, np.uint8)
+    out = O.warp_affine(src, rotation_matrix(10, 10, 45, 1.5), (30, 30), O.INTER_CUBIC, O.BORDER_TRANSPARENT, 0,
+                        dst=init)
     assert (out == 99).any() and (out != 99).any()
