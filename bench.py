@@ -917,7 +917,7 @@ def main(argv=None):
     else:
         flops_per_launch, achieved = 0.0, 0.0
     # the auto choice is lk_multi_kernel (several points per wave) for the odd square windows it covers
-    traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}>")
+    traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true>")  # the loop's FLY instance
     if traffic is None:
         traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",

@@ -698,7 +698,10 @@ __device__ __forceinline__ void fb_lds_barrier()
     __builtin_amdgcn_s_barrier();
 }
 
-constexpr int kFbRB = 4;        // output rows per batch of fb_iter (4 or 8)
+#ifndef TBDK_FB_RB
+#define TBDK_FB_RB 4
+#endif
+constexpr int kFbRB = TBDK_FB_RB;  // output rows per batch of fb_iter (4 or 8)
 constexpr int kFbThreads = 256; // two threads per strip column
 
 // M of NR rows t0 + half, t0 + half + 2, ... (relative to the segment's first
@@ -754,7 +757,8 @@ __device__ __forceinline__ void fb_rows(const FbIterArgs& a, const FbRsrc& rs, f
 // fixed-order function of the pixel's neighbourhood, independent of the
 // strip/segment split.
 template <int M, bool GAUSS>
-__global__ __launch_bounds__(kFbThreads, (M <= 6 ? (GAUSS ? 2 : 3) : (GAUSS ? 1 : 2))) void fb_iter_kernel(FbIterArgs a)
+__global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1)
+                                                       : (M <= 6 ? (GAUSS ? 2 : 3) : (GAUSS ? 1 : 2)))) void fb_iter_kernel(FbIterArgs a)
 {
     constexpr int K = 2 * M + 1;
     constexpr int OW = fb_ow(M);
