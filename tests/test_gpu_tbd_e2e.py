@@ -100,3 +100,12 @@ def test_tbd_loop_equals_oracle_pipeline_kitti(gpu, k):
     """BASELINE configs[3]: the KITTI-shaped 1242x375 sequences s..s+7, 128 objects (one per GPU in the bench)."""
     s = run_pair(gpu, 1242, 375, 128, 12, SEED + k)
     assert s["preds"] > 0
+
+
+def test_tbd_loop_equals_oracle_pipeline_1080p_long(gpu):
+    """configs[2] over 64 frames (13 re-detection frames, 5 % of the detections
+    dropped at random): tracks born, coasting, deleted and re-created many times
+    over, still frame-by-frame equal to the oracle pipeline"""
+    s = run_pair(gpu, 1920, 1080, 128, 64, SEED + 7, 0.05)
+    assert s["preds"] > 63 * 100
+    assert s["refreshed"] > 13 * 100
