@@ -997,6 +997,10 @@ def main(argv=None):
     if not args.no_kitti:
         progress("KITTI configs[3] leg", rank)
         line["kitti"] = kitti_leg(args, ctx, dev, world, rank)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before any leg imports _oracle: every CPU baseline of the line runs the
+        # -O3 -march=native build (native_oracle() is a no-op once _oracle is loaded)
+        native_oracle()
     if rank == 0 and not args.no_farneback:
         progress("Farneback secondary")
         line["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
