@@ -270,8 +270,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             // one row pair of the setup: I x32 (-> ic), the interpolated Ix / Iy
             // packed by row pairs (-> gxk, gyk) and the G sums, from the window
             // rows' (I(x), I(x+1)), (Ix(x), Ix(x+1)), (Iy(x), Iy(x+1)) pairs
+            // dw0/dw1: the weights of the derivative rows r (top) and r+1 (bottom) of
+            // the pair's first row, dw2/dw3 those of rows r+1 and r+2 of its second
+            // (w0, w1 unless the level frame's zero rule masks a row or a column)
             auto pair_step = [&](int q, uint32_t ip0, uint32_t ip1, uint32_t ip2, uint32_t dx0, uint32_t dx1,
-                                 uint32_t dx2, uint32_t dy0, uint32_t dy1, uint32_t dy2) {
+                                 uint32_t dx2, uint32_t dy0, uint32_t dy1, uint32_t dy2, uint32_t dw0, uint32_t dw1,
+                                 uint32_t dw2, uint32_t dw3) {
                 const int r = 2 * q;
                 const bool two = r + 1 < WH;
                 if constexpr (IPACK) {
@@ -282,10 +286,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                     ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9) << 9);
                     if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) << 9);
                 }
-                const int x0 = bilin_s<W_BITS1>(dx0, dx1, w0, w1, rnd14);
-                const int x1 = two ? bilin_s<W_BITS1>(dx1, dx2, w0, w1, rnd14) : 0;
-                const int y0 = bilin_s<W_BITS1>(dy0, dy1, w0, w1, rnd14);
-                const int y1 = two ? bilin_s<W_BITS1>(dy1, dy2, w0, w1, rnd14) : 0;
+                const int x0 = bilin_s<W_BITS1>(dx0, dx1, dw0, dw1, rnd14);
+                const int x1 = two ? bilin_s<W_BITS1>(dx1, dx2, dw2, dw3, rnd14) : 0;
+                const int y0 = bilin_s<W_BITS1>(dy0, dy1, dw0, dw1, rnd14);
+                const int y1 = two ? bilin_s<W_BITS1>(dy1, dy2, dw2, dw3, rnd14) : 0;
                 gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
                 gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
                 acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
@@ -295,65 +299,84 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             if constexpr (FLY) {
                 // calcSharrDeriv (lkpyramid.cpp:55-144) of the window, from the
                 // padded u8 level: one unaligned dword per row holds columns
-                // x-1 .. x+2, rows -1 .. WH; unpacked as int16 pairs (x-1, x) and
-                // (x+1, x+2), the vertical pass t0 = 3(a+c) + 10b, t1 = c - a runs
-                // on both pairs, and the horizontal pass gives (Ix(x), Ix(x+1)) =
-                // hi - lo and (Iy(x), Iy(x+1)) = 3 (lo + hi) + 10 (t1(x), t1(x+1))
-                // directly as the pairs the bilinear sums take.  Integer and exact
-                // in 16 bits (|Ix|, |Iy| <= 4080); the level's reflect-101 frame is
-                // the reference's row / column reflection.  The derivative rows are
-                // made as the row pairs consume them (a rolling window of three),
-                // so only the loaded dwords and the outputs are live at once.
+                // x-1 .. x+2, rows -1 .. WH+1.  The reference's vertical-then-
+                // horizontal integer passes are linear, so they are evaluated in the
+                // other order, each source row's horizontal terms shared by the
+                // three derivative rows that read it: per row j the u16 pairs
+                // lo = (x-1, x), hi = (x+1, x+2), mid = (x, x+1) (mid is also the I
+                // pair), hd = hi - lo and sm = 3 (lo + hi) + 10 mid; then for
+                // derivative row r (source rows r, r+1, r+2)
+                //   (Ix(x), Ix(x+1)) = 3 (hd_r + hd_r+2) + 10 hd_r+1,
+                //   (Iy(x), Iy(x+1)) = sm_r+2 - sm_r,
+                // the same integers as t0 = 3(a+c) + 10b, t1 = c - a then
+                // t0(x+1) - t0(x-1), 3 (t1(x-1) + t1(x+1)) + 10 t1(x) (|Ix|, |Iy|
+                // <= 4080: exact modulo 2^16).  The level's reflect-101 frame is the
+                // reference's row / column reflection.
                 const uint32_t ioff = act ? (uint32_t)((ipy - 1 + L.ipad) * L.ipitch + ipx + x - 1 + L.ipad) : 0u;
                 uint32_t u[WH + 3];
 #pragma unroll
                 for (int r = 0; r < WH + 3; ++r) u[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);
-                // outside the level the derivative planes hold BORDER_CONSTANT 0
-                // (lkpyramid.cpp:1357): masked only in waves with a window at an edge
-                const bool edge = any_lane(act && (ipx < 0 || ipx + WW > L.w - 1 || ipy < 0 || ipy + WH > L.h - 1));
+                // Outside the level the derivative planes hold BORDER_CONSTANT 0
+                // (lkpyramid.cpp:1357).  A zero derivative contributes nothing to the
+                // bilinear sums, so the rule is applied to the derivative weights:
+                // the column halves (x, x+1) outside [0, w) by cm, derivative rows
+                // outside [0, h) by the per-lane row bits vm (three ops a row, for
+                // all waves: a wave-uniform masked / unmasked split needs more
+                // VGPRs than it saves)
                 const uint32_t cm = ((unsigned)(ipx + x) < (unsigned)L.w ? 0x0000FFFFu : 0u) |
                                     ((unsigned)(ipx + x + 1) < (unsigned)L.w ? 0xFFFF0000u : 0u);
-                auto drow = [&](auto mask, int r, uint32_t& ipo, uint32_t& dxo, uint32_t& dyo) {
-                    const u16x2 al = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C010C00u));
-                    const u16x2 ah = as_u16x2(__builtin_amdgcn_perm(0u, u[r], 0x0C030C02u));
-                    const u16x2 bl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C010C00u));
-                    const u16x2 bh = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 1], 0x0C030C02u));
-                    const u16x2 cl = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C010C00u));
-                    const u16x2 ch = as_u16x2(__builtin_amdgcn_perm(0u, u[r + 2], 0x0C030C02u));
-                    ipo = __builtin_amdgcn_perm(0u, u[r + 1], 0x0C020C01u);  // (I(x), I(x+1))
-                    const u16x2 t0l = (al + cl) * (unsigned short)3 + bl * (unsigned short)10;
-                    const u16x2 t0h = (ah + ch) * (unsigned short)3 + bh * (unsigned short)10;
-                    const uint32_t t1l = as_u32(cl - al), t1h = as_u32(ch - ah);
-                    const u16x2 mid = as_u16x2(__builtin_amdgcn_perm(t1h, t1l, 0x05040302u));  // (t1(x), t1(x+1))
-                    uint32_t dx = as_u32(t0h - t0l);
-                    uint32_t dy = as_u32((as_u16x2(t1l) + as_u16x2(t1h)) * (unsigned short)3 + mid * (unsigned short)10);
-                    if constexpr (decltype(mask)::value) {
-                        const uint32_t m = (unsigned)(ipy + r) < (unsigned)L.h ? cm : 0u;
-                        dx &= m;
-                        dy &= m;
-                    }
-                    dxo = dx;
-                    dyo = dy;
+                const int rlo = min(max(-ipy, 0), 32), rhi = min(max(L.h - ipy, 0), 32);
+                const uint32_t vm = (uint32_t)(((1ull << rhi) - 1ull) & ~((1ull << rlo) - 1ull));
+                const uint32_t wd0 = w0 & cm, wd1 = w1 & cm;
+                auto rowbit = [&](int r) { return (uint32_t)((int)(vm << (31 - r)) >> 31); };  // row r valid: ~0
+                auto src = [&](int j, uint32_t& mid, uint32_t& hd, uint32_t& sm) {
+                    const u16x2 lo = as_u16x2(__builtin_amdgcn_perm(0u, u[j], 0x0C010C00u));
+                    const u16x2 hi = as_u16x2(__builtin_amdgcn_perm(0u, u[j], 0x0C030C02u));
+                    mid = __builtin_amdgcn_perm(0u, u[j], 0x0C020C01u);
+                    hd = as_u32(hi - lo);
+                    sm = as_u32((lo + hi) * (unsigned short)3 + as_u16x2(mid) * (unsigned short)10);
                 };
-                // the rows in pairs, each derivative row made as the pairs reach it
-                auto rows = [&](auto mask) {
-                    uint32_t ipa, dxa, dya, ipb = 0, dxb = 0, dyb = 0, ipc = 0, dxc = 0, dyc = 0;
-                    drow(mask, 0, ipa, dxa, dya);
+                // derivative row r from the source rows' terms (a, b, c = rows r, r+1, r+2)
+                auto drow = [&](uint32_t hda, uint32_t hdb, uint32_t hdc, uint32_t sma, uint32_t smc, uint32_t& dx,
+                                uint32_t& dy) {
+                    dx = as_u32((as_u16x2(hda) + as_u16x2(hdc)) * (unsigned short)3 + as_u16x2(hdb) * (unsigned short)10);
+                    dy = as_u32(as_u16x2(smc) - as_u16x2(sma));
+                };
+                // rolling window over the source rows: (m, h, s) of rows j-2, j-1, j
+                uint32_t m0, h0, s0, m1, h1, s1, m2, h2, s2;
+                src(0, m0, h0, s0);
+                src(1, m1, h1, s1);
+                src(2, m2, h2, s2);
+                uint32_t dxa, dya;
+                drow(h0, h1, h2, s0, s2, dxa, dya);  // derivative row 0
+                uint32_t ipa = m1;                   // I row 0
+                uint32_t ra = rowbit(0);
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) {
-                        const int r = 2 * q;
-                        drow(mask, r + 1, ipb, dxb, dyb);
-                        if (r + 1 < WH) drow(mask, r + 2, ipc, dxc, dyc);
-                        pair_step(q, ipa, ipb, ipc, dxa, dxb, dxc, dya, dyb, dyc);
-                        ipa = ipc;
-                        dxa = dxc;
-                        dya = dyc;
+                for (int q = 0; q < NP; ++q) {
+                    const int r = 2 * q;
+                    // rows r+1 (source r+3) and r+2 (source r+4)
+                    m0 = m1; h0 = h1; s0 = s1;
+                    m1 = m2; h1 = h2; s1 = s2;
+                    src(r + 3, m2, h2, s2);
+                    uint32_t dxb, dyb, dxc = 0, dyc = 0, ipc = 0;
+                    drow(h0, h1, h2, s0, s2, dxb, dyb);
+                    const uint32_t ipb = m1;
+                    const uint32_t rb = rowbit(r + 1);
+                    uint32_t rc = 0;
+                    if (r + 1 < WH) {
+                        m0 = m1; h0 = h1; s0 = s1;
+                        m1 = m2; h1 = h2; s1 = s2;
+                        src(r + 4, m2, h2, s2);
+                        drow(h0, h1, h2, s0, s2, dxc, dyc);
+                        ipc = m1;
+                        rc = rowbit(r + 2);
                     }
-                };
-                // (a wave-uniform choice between a masked and an unmasked copy of
-                // the rows needs 132 VGPRs against 102: the mask is three ops a row)
-                (void)edge;
-                rows(std::true_type{});
+                    pair_step(q, ipa, ipb, ipc, dxa, dxb, dxc, dya, dyb, dyc, wd0 & ra, wd1 & rb, wd0 & rb, wd1 & rc);
+                    ipa = ipc;
+                    dxa = dxc;
+                    dya = dyc;
+                    ra = rc;
+                }
             } else {
                 uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
                 const uint32_t ioff = act ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
@@ -370,7 +393,8 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 for (int q = 0; q < NP; ++q) {
                     const int r = 2 * q;
                     const int r2 = r + 2 <= WH ? r + 2 : WH;
-                    pair_step(q, ip[r], ip[r + 1], ip[r2], dxp[r], dxp[r + 1], dxp[r2], dyp[r], dyp[r + 1], dyp[r2]);
+                    pair_step(q, ip[r], ip[r + 1], ip[r2], dxp[r], dxp[r + 1], dxp[r2], dyp[r], dyp[r + 1], dyp[r2],
+                              w0, w1, w0, w1);
                 }
             }
             if constexpr (IPACK) {
