@@ -136,17 +136,19 @@ __device__ __forceinline__ int bilin_c(uint32_t p0, uint32_t p1, uint32_t w0, ui
     return sdot2(p0, w0, t);
 }
 
-// (t0 >> 9, t1 >> 9) as int16 x 2 in two instructions: t0 >> 9, then the SDWA
-// form of the second shift writes only the high word (WORD_1) of the result,
-// keeping the low word
-__device__ __forceinline__ uint32_t pack_diff(int t0, int t1)
+// (t0 >> SH, t1 >> SH) as int16 x 2 in two instructions: t0 >> SH, then the
+// SDWA form of the second shift writes only the high word (WORD_1) of the
+// result, keeping the low word
+template <int SH>
+__device__ __forceinline__ uint32_t pack_shr(int t0, int t1)
 {
-    uint32_t d = (uint32_t)(t0 >> 9);
-    asm("v_ashrrev_i32_sdwa %0, 9, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+    uint32_t d = (uint32_t)(t0 >> SH);
+    asm("v_ashrrev_i32_sdwa %0, %2, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         : "+v"(d)
-        : "v"(t1));
+        : "v"(t1), "i"(SH));
     return d;
 }
+__device__ __forceinline__ uint32_t pack_diff(int t0, int t1) { return pack_shr<9>(t0, t1); }
 
 __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
@@ -158,11 +160,17 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 // I x32 kept as packed row pairs and subtracted from the J pairs by one packed
 // op per row pair (1), or folded into each row's J rounding constant (0, one
 // VGPR per row; tuning builds)
+// How I enters the Newton step's b sums (tuning builds may change it):
+//   0: folded into each row's J rounding constant (one VGPR per row)
+//   1: I pairs packed by rows, one v_pk_sub per row pair and step
+//   2: b = sum(Jd * g) - sum(I * g): the second sum (per lane, per level) is
+//      made once in the level setup, so the step needs no I at all; the final
+//      error recomputes the I rows from the level
 #ifndef TBDK_LK_IPACK
 #define TBDK_LK_IPACK 1  // derivative-plane instance (94 VGPRs -> 5 waves per SIMD)
 #endif
 #ifndef TBDK_LK_IPACK_FLY
-#define TBDK_LK_IPACK_FLY 0  // Scharr-on-the-fly instance: 4 waves per SIMD either way, one op fewer per row pair
+#define TBDK_LK_IPACK_FLY 0  // Scharr-on-the-fly instance
 #endif
 
 #ifndef TBDK_LK_MULTI_WAVES
@@ -184,7 +192,8 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 {
     constexpr int P = 64 / WW;         // points per wave
     constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
-    constexpr bool IPACK = FLY ? TBDK_LK_IPACK_FLY != 0 : TBDK_LK_IPACK != 0;
+    constexpr int IM = FLY ? TBDK_LK_IPACK_FLY : TBDK_LK_IPACK;
+    constexpr bool IPACK = IM == 1, ILIN = IM == 2;
     const int lane = threadIdx.x & 63;
     // point k of the wave owns lanes [1 + k*WW, 1 + (k+1)*WW); lane 0 (and any
     // lane past the last point) is idle with k == P and contributes 0
@@ -262,7 +271,8 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         // (2^9 * I is a multiple of the divisor: floor((X - 2^9 I) / 2^9) =
         // floor(X / 2^9) - I); Ix, Iy packed by row pairs as int16 x 2
         uint32_t ipk[IPACK ? NP : 1];  // I x32 of rows (2q, 2q+1) as int16 x 2
-        int ic[IPACK ? 1 : WH];
+        int ic[IM == 0 ? WH : 1];
+        int cgx = 0, cgy = 0;  // ILIN: this lane's sum(I x32 * Ix), sum(I x32 * Iy)
         uint32_t gxk[NP], gyk[NP];
         float A11, A12, A22;
         {
@@ -278,20 +288,27 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                                  uint32_t dw2, uint32_t dw3) {
                 const int r = 2 * q;
                 const bool two = r + 1 < WH;
-                if constexpr (IPACK) {
-                    const int i0 = bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9);
-                    const int i1 = two ? bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) : 0;
-                    ipk[q] = __builtin_amdgcn_perm((uint32_t)i1, (uint32_t)i0, 0x05040100u);
+                uint32_t ipq = 0;
+                if constexpr (IPACK || ILIN) {
+                    const int i0 = bilin_s<0>(ip0, ip1, w0, w1, rnd9);
+                    const int i1 = two ? bilin_s<0>(ip1, ip2, w0, w1, rnd9) : 0;
+                    ipq = pack_shr<W_BITS1 - 5>(i0, i1);
+                    if constexpr (IPACK) ipk[q] = ipq;
                 } else {
                     ic[r] = rnd9 - (bilin_s<W_BITS1 - 5>(ip0, ip1, w0, w1, rnd9) << 9);
                     if (two) ic[r + 1] = rnd9 - (bilin_s<W_BITS1 - 5>(ip1, ip2, w0, w1, rnd9) << 9);
                 }
-                const int x0 = bilin_s<W_BITS1>(dx0, dx1, dw0, dw1, rnd14);
-                const int x1 = two ? bilin_s<W_BITS1>(dx1, dx2, dw2, dw3, rnd14) : 0;
-                const int y0 = bilin_s<W_BITS1>(dy0, dy1, dw0, dw1, rnd14);
-                const int y1 = two ? bilin_s<W_BITS1>(dy1, dy2, dw2, dw3, rnd14) : 0;
-                gxk[q] = __builtin_amdgcn_perm((uint32_t)x1, (uint32_t)x0, 0x05040100u);
-                gyk[q] = __builtin_amdgcn_perm((uint32_t)y1, (uint32_t)y0, 0x05040100u);
+                // interpolated Ix / Iy of rows r, r+1, shifted and packed (pack_shr)
+                const int x0 = bilin_s<0>(dx0, dx1, dw0, dw1, rnd14);
+                const int x1 = two ? bilin_s<0>(dx1, dx2, dw2, dw3, rnd14) : 0;
+                const int y0 = bilin_s<0>(dy0, dy1, dw0, dw1, rnd14);
+                const int y1 = two ? bilin_s<0>(dy1, dy2, dw2, dw3, rnd14) : 0;
+                gxk[q] = pack_shr<W_BITS1>(x0, x1);
+                gyk[q] = pack_shr<W_BITS1>(y0, y1);
+                if constexpr (ILIN) {
+                    cgx = sdot2(ipq, gxk[q], cgx);
+                    cgy = sdot2(ipq, gyk[q], cgy);
+                }
                 acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
                 acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
                 acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
@@ -462,7 +479,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 const int r = 2 * q;
                 // (diff_r, diff_r+1) as int16 x 2, |diff| <= 8160
                 uint32_t d;
-                if constexpr (IPACK) {
+                if constexpr (ILIN) {
+                    // (J x32 of rows r, r+1) as int16 x 2; I enters through cgx / cgy
+                    d = r + 1 < WH ? pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9),
+                                               bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9))
+                                   : pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9), 0);
+                } else if constexpr (IPACK) {
                     // (J x32 of rows r, r+1) as int16 x 2, minus the I pair: one packed subtract
                     const uint32_t jv = r + 1 < WH ? pack_diff(bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9),
                                                                bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9))
@@ -478,6 +500,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #ifdef TBDK_LK_NEWTON_SB
                 if (q % TBDK_LK_NEWTON_SB == TBDK_LK_NEWTON_SB - 1) __builtin_amdgcn_sched_barrier(0);
 #endif
+            }
+            if constexpr (ILIN) {
+                // sum((Jd - I) g) = sum(Jd g) - sum(I g): the same lane partial
+                // (modulo 2^32 on the way, exact at the end)
+                b[0] -= cgx;
+                b[1] -= cgy;
             }
             if (k >= P) b[0] = b[1] = 0;
             float fb[2];
@@ -512,6 +540,24 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 want = false;
             }
             if (any_lane(want)) {
+                // ILIN: the I rows again (the level-0 window at prev, its weights),
+                // packed by row pairs before the J rows are loaded (with both row
+                // sets live at once this block set the kernel's register peak)
+                uint32_t ipr[ILIN ? NP : 1];
+                if constexpr (ILIN) {
+                    uint32_t iw0, iw1, ir[WH + 1];
+                    bilinear_weights(prevx - ipx, prevy - ipy, iw0, iw1);
+                    const uint32_t ioff = want ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
+#pragma unroll
+                    for (int r = 0; r <= WH; ++r) ir[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) {
+                        const int r = 2 * q;
+                        ipr[q] = pack_shr<W_BITS1 - 5>(bilin_s<0>(ir[r], ir[r + 1], iw0, iw1, rnd9),
+                                                        r + 1 < WH ? bilin_s<0>(ir[r + 1], ir[r + 2], iw0, iw1, rnd9) : 0);
+                        asm volatile("" : "+v"(ipr[q]));
+                    }
+                }
                 bilinear_weights(npx - inx, npy - iny, w0, w1);
                 const uint32_t joff = want ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
 #pragma unroll
@@ -521,14 +567,18 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 for (int q = 0; q < NP; ++q) {
                     const int r = 2 * q;
                     int d0;
-                    if constexpr (IPACK)
+                    if constexpr (ILIN)
+                        d0 = (bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipr[q] & 0xFFFFu);
+                    else if constexpr (IPACK)
                         d0 = (bilin_s<0>(jp[r], jp[r + 1], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] & 0xFFFFu);
                     else
                         d0 = bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]) >> 9;
                     e += d0 < 0 ? -d0 : d0;
                     if (r + 1 < WH) {
                         int d1;
-                        if constexpr (IPACK)
+                        if constexpr (ILIN)
+                            d1 = (bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipr[q] >> 16);
+                        else if constexpr (IPACK)
                             d1 = (bilin_s<0>(jp[r + 1], jp[r + 2], w0, w1, rnd9) >> 9) - (int)(int16_t)(ipk[q] >> 16);
                         else
                             d1 = bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]) >> 9;
