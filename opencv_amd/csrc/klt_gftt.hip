@@ -65,13 +65,15 @@ __device__ __forceinline__ int roi_of_cblock(const GfttRoi* rois, int nroi, int 
 }
 
 // DPP wave shifts (GFX9): lane i receives lane i-1 (shr) / lane i+1 (shl)
+// (the lane without a source reads 0 by bound_ctrl, so no old value has to be
+// materialised first)
 __device__ __forceinline__ float from_left(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float from_right(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
 // Sobel rows of one image row at columns (x-1, x, x+1) in the reference's
@@ -118,7 +120,7 @@ constexpr int kEigPref = 8;   // pixel rows in flight per wave
 struct EigLane {
     __amdgpu_buffer_rsrc_t rs;
     int x, H, hm2, pitch;
-    bool at_left, at_right, out_lane;
+    bool mir, out_lane;  // mir: a lane outside the ROI holding its reflect-101 column
     float k, k2;
 };
 
@@ -127,13 +129,17 @@ __device__ __forceinline__ float eig_ld(const EigLane& g, int row)
     return (float)__builtin_amdgcn_raw_buffer_load_b8(g.rs, g.x, row * g.pitch, 0);
 }
 
-// Sobel row terms of the pixel row whose own value is v (neighbours by DPP)
+// Sobel row terms of the pixel row whose own value is v (neighbours by DPP).
+// Every lane holds the pixel of its column's reflect-101 image (lanes left or
+// right of the ROI: the mirrored column), so the neighbours of an in-ROI lane
+// are the reference's reflected pixels as they are; a mirrored lane sees its
+// column's neighbours in the opposite order and swaps them, and then holds that
+// column's Sobel terms and covariances exactly — the box filter's reflect-101
+// of the cov image (cov(-1) = cov(1)) with no per-channel fix-up.
 __device__ __forceinline__ SobelRow eig_srow(const EigLane& g, float v)
 {
     const float l = from_left(v), rr = from_right(v);
-    const float l2 = g.at_left ? rr : l, r2 = g.at_right ? l : rr;
-    const bool one = g.at_left && g.at_right;
-    return sobel_row(one ? v : l2, v, one ? v : r2, g.k, g.k2);
+    return sobel_row(g.mir ? rr : l, v, g.mir ? l : rr, g.k, g.k2);
 }
 
 // the three cov channels of one row and their boxFilter row sums ((l + c) + r in double)
@@ -145,9 +151,7 @@ __device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p,
     const float cv[3] = {dx * dx, dx * dy, dy * dy};
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-        float l = from_left(cv[ch]), rr = from_right(cv[ch]);
-        if (g.at_left) l = g.at_right ? cv[ch] : rr;
-        if (g.at_right) rr = g.at_left ? cv[ch] : l;
+        const float l = from_left(cv[ch]), rr = from_right(cv[ch]);
         out[ch] = (double)l + (double)cv[ch] + (double)rr;
     }
 }
@@ -260,9 +264,24 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     const int strip = blockIdx.x - R.cblk;
     const int xc = strip * kGfttStrip - kGfttHalo + lane;  // this lane's ROI column
     g.out_lane = lane >= kGfttHalo && lane < kGfttHalo + kGfttStrip && xc < R.w;
-    g.x = xc < 0 ? 0 : (xc >= R.w ? R.w - 1 : xc);  // halo lanes outside: any in-ROI column
-    g.at_left = g.x == 0;
-    g.at_right = g.x == R.w - 1;
+    // the lane's column of the reflect-101 image (borderInterpolate, REFLECT_101);
+    // only columns -2 .. w+1 are read by an output (its cov at -1 .. w), lanes
+    // farther out take any in-ROI column
+    {
+        const int w = R.w;
+        int xm = xc < -2 || xc > w + 1 ? min(max(xc, 0), w - 1) : xc;
+        if (w == 1) {
+            xm = 0;
+        } else {
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {  // two reflections reach [0, w) from -2 .. w+1 for w >= 2
+                if (xm < 0) xm = -xm;
+                if (xm >= w) xm = 2 * (w - 1) - xm;
+            }
+        }
+        g.x = xm;
+        g.mir = xc < 0 || xc >= w;
+    }
     const double scale = 1.0 / ((double)(1 << 2) * 3 * 255.0);
     g.k = (float)(1.0 * scale);
     g.k2 = (float)(2.0 * scale);
