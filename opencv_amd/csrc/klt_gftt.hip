@@ -25,6 +25,7 @@
 #include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <type_traits>
 
 #include "tbdk_internal.hpp"
 
@@ -461,6 +462,87 @@ __device__ __forceinline__ void sort_keys(uint64_t* keys, int np2, int tid)
     __syncthreads();
 }
 
+// Sort of exactly kSelThreads (512) keys, descending (the partial selection's
+// usual case): each wave sorts its 64 keys in registers (a 21-stage bitonic
+// network over the wave's lanes, no barrier), then every key's final place is
+// its rank: its index in its own run plus, for each of the other seven sorted
+// runs, the count of keys ahead of it there (branchless binary searches, the
+// seven runs' reads in flight together; >= for runs of lower wave index and >
+// for higher ones, so the equal padding keys get distinct places).  Same result
+// as the 45-stage bitonic sort over the workgroup with its six LDS stages.
+// lane ^ J of a 32-bit value without the LDS unit where DPP reaches it:
+// quad_perm for 1 and 2, a row shift each way and a select for 4 and 8,
+// ds_swizzle (no address VGPR) for 16, ds_bpermute for 32
+template <int J>
+__device__ __forceinline__ int xor_lane(int v, int lane)
+{
+    if constexpr (J == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);
+    else if constexpr (J == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);
+    else if constexpr (J == 4 || J == 8) {
+        const int up = __builtin_amdgcn_mov_dpp(v, 0x100 | J, 0xF, 0xF, true);  // row_shl: lane + J
+        const int dn = __builtin_amdgcn_mov_dpp(v, 0x110 | J, 0xF, 0xF, true);  // row_shr: lane - J
+        return (lane & J) ? dn : up;
+    } else if constexpr (J == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
+    else return __shfl_xor(v, J);
+}
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane_u64(uint64_t v, int lane)
+{
+    const int lo = xor_lane<J>((int)(uint32_t)v, lane), hi = xor_lane<J>((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ void sort_keys_512(uint64_t* keys, int tid)
+{
+    static_assert(kSelThreads == 512, "eight runs of 64");
+    const int lane = tid & 63, w = tid >> 6;
+    uint64_t x = keys[tid];
+    auto stage = [&](auto jc, int k) {
+        constexpr int j = decltype(jc)::value;
+        const uint64_t y = xor_lane_u64<j>(x, lane);
+        const bool desc = (lane & k) == 0 || k == 64;
+        const bool take_max = ((lane & j) == 0) == desc;
+        x = take_max ? (x > y ? x : y) : (x < y ? x : y);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    using I32 = std::integral_constant<int, 32>;
+    stage(I1{}, 2);
+    stage(I2{}, 4), stage(I1{}, 4);
+    stage(I4{}, 8), stage(I2{}, 8), stage(I1{}, 8);
+    stage(I8{}, 16), stage(I4{}, 16), stage(I2{}, 16), stage(I1{}, 16);
+    stage(I16{}, 32), stage(I8{}, 32), stage(I4{}, 32), stage(I2{}, 32), stage(I1{}, 32);
+    stage(I32{}, 64), stage(I16{}, 64), stage(I8{}, 64), stage(I4{}, 64), stage(I2{}, 64), stage(I1{}, 64);
+    keys[tid] = x;  // the wave's own run (no other wave reads or writes it yet)
+    __syncthreads();
+    int rank = lane;
+    int pos[8];
+    bool all[8];  // the whole run is ahead (a count of 64, which the 6-step search cannot reach)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint64_t c = keys[r * 64 + 63];
+        all[r] = r < w ? c >= x : c > x;
+        pos[r] = 0;
+    }
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint64_t c = keys[r * 64 + pos[r] + st - 1];
+            const bool ahead = r < w ? c >= x : c > x;
+            pos[r] += ahead ? st : 0;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) rank += r != w ? (all[r] ? 64 : pos[r]) : 0;
+    __syncthreads();
+    keys[rank] = x;
+    __syncthreads();
+}
+
 // Bitonic sort of np2 keys in LDS only (every stage a compare-exchange pass
 // over LDS pairs): the path for ROIs with more than 4 * kSelThreads candidates.
 // Slower than sort_keys, but it keeps the kernel's register footprint at that
@@ -489,20 +571,27 @@ __device__ __forceinline__ void sort_keys_lds(uint64_t* keys, int np2, int tid)
 // corner (the candidate is rejected), 1..64 = a candidate of this step in lane
 // v-1 (recorded in inb when it precedes this lane).  RAD is the window radius;
 // all window rows are read before any is examined (one LDS round trip).
+// Candidates sit on integer pixels, so "closer than min_distance" is the same
+// set of window offsets for every candidate ((float)(dx*dx + dy*dy) < md2,
+// featureselect.cpp:466-481 with integer dx, dy): one uniform byte mask per
+// window row.  Byte values 1..64 never have the top bit that 255 has, so the
+// rejection test is one mask over the row; only this step's candidates inside
+// the mask are visited one by one.
 template <int RAD>
 __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, int ix, int iy, float fx, float fy,
                                             int lane, double md2, bool& good, unsigned long long& inb)
 {
     constexpr int NR = 2 * RAD + 1;
     constexpr bool THREE = NR + 7 > 16;  // the shifted window can need a third word
+    constexpr uint64_t kHi = 0x8080808080808080ull, kLo7 = 0x7F7F7F7F7F7F7F7Full;
     const int x0 = ix - RAD;
-    uint64_t cv_lo = 0, cv_hi = 0;  // window bytes whose column lies inside the ROI
+    uint64_t cv_lo = 0, cv_hi = 0;  // 0xFF for window bytes whose column lies inside the ROI
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
         const int xx = x0 + t;
-        const uint64_t bit = (xx >= 0 && xx < rw) ? 0x80ull : 0ull;
-        if (t < 8) cv_lo |= bit << (8 * t);
-        else cv_hi |= bit << (8 * (t - 8));
+        const uint64_t b = (xx >= 0 && xx < rw) ? 0xFFull : 0ull;
+        if (t < 8) cv_lo |= b << (8 * t);
+        else cv_hi |= b << (8 * (t - 8));
     }
     uint64_t w0[NR], w1[NR], w2[NR];
     int sh[NR];
@@ -518,10 +607,20 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
         w2[d] = THREE ? wp[2] : 0ull;
         sh[d] = base - al;  // in [-RAD, 7]
     }
+    uint64_t rej = 0;
 #pragma unroll
     for (int d = 0; d < NR; ++d) {
         const int yy = iy - RAD + d;
         if (yy < 0 || yy >= rh) continue;
+        // uniform: the offsets of this row closer than min_distance
+        uint64_t close_lo = 0, close_hi = 0;
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            const float ddx = (float)(t - RAD), ddy = (float)(d - RAD);
+            const uint64_t b = ((double)(ddx * ddx + ddy * ddy) < md2 && !(d == RAD && t == RAD)) ? 0xFFull : 0ull;
+            if (t < 8) close_lo |= b << (8 * t);
+            else close_hi |= b << (8 * (t - 8));
+        }
         uint64_t lo, hi;
         if (sh[d] >= 0) {
             const int b8 = 8 * sh[d];
@@ -532,9 +631,12 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
             lo = w0[d] << b8;
             hi = (w1[d] << b8) | (w0[d] >> (64 - b8));
         }
-        uint64_t nz_lo = (((lo & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | lo) & cv_lo;
-        uint64_t nz_hi = (((hi & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | hi) & cv_hi;
-        if (d == RAD) nz_lo &= ~(0x80ull << (8 * RAD));  // not the candidate itself
+        lo &= cv_lo & close_lo;
+        hi &= cv_hi & close_hi;
+        rej |= (lo | hi) & kHi;  // an accepted corner (255) closer than min_distance
+        // this step's candidates (1..64) in the mask: nonzero bytes without the top bit
+        uint64_t nz_lo = (((lo & kLo7) + kLo7) | lo) & ~lo & kHi;
+        uint64_t nz_hi = (((hi & kLo7) + kLo7) | hi) & ~hi & kHi;
         while (nz_lo | nz_hi) {
             int t;
             uint64_t src;
@@ -549,12 +651,12 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
                 t += 8;
             }
             const int v = (int)((src >> (8 * (t & 7))) & 0xFF);
-            const float ddx = fx - (float)(x0 + t), ddy = fy - (float)yy;
-            if (!((double)(ddx * ddx + ddy * ddy) < md2)) continue;
-            if (v == 255) good = false;                      // accepted earlier
-            else if (v - 1 < lane) inb |= 1ull << (v - 1);  // earlier in this step
+            if (v - 1 < lane) inb |= 1ull << (v - 1);  // earlier in this step
         }
     }
+    if (rej) good = false;
+    (void)fx;
+    (void)fy;
 }
 
 // Partial selection (round 3): the greedy walk consumes the candidates in
@@ -795,7 +897,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     __syncthreads();
     GFTT_STAMP(1);
     switch (np2 / kSelThreads) {
-    case 1: sort_keys<1>(keys, np2, tid); break;
+    case 1: sort_keys_512(keys, tid); break;
     case 2: sort_keys<2>(keys, np2, tid); break;
     case 4: sort_keys<4>(keys, np2, tid); break;
     default: sort_keys_lds(keys, np2, tid); break;
