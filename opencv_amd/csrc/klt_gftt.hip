@@ -165,7 +165,7 @@ __device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p,
 // into lm.  S0 = the SUM the walk started from; Scap = the SUM before row
 // ycap (the next segment's fresh-start row); S = the SUM after the last row.
 __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, uint64_t* __restrict__ lm,
-                                            int w, int y0, int y1, int ys, int ye, int ycap, bool fresh,
+                                            int w, int ep, int y0, int y1, int ys, int ye, int ycap, bool fresh,
                                             double (&S)[3], double (&S0)[3], double (&Scap)[3], int& best)
 {
     const int H = g.H;
@@ -229,7 +229,7 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
                 const float t = aa - cc;
                 const float e = (aa + cc) - sqrtf(bb * bb + t * t);
                 if (y >= y0 && y < y1 && g.out_lane) {
-                    E[(size_t)y * w] = e;
+                    E[(size_t)y * ep] = e;
                     const int kk = fkey(e);
                     best = kk > best ? kk : best;
                 }
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         return s_bad;
     };
     if (live) {
-        eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
+        eig_segment(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
         if (ycap >= 0) {
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         __syncthreads();  // s_cap is rewritten below
         if (wv >= bad && live) {
             best = INT_MIN;
-            eig_segment(g, E, has_lm ? lm : nullptr, R.w, y0, y1, ys, ye, ycap, false, S, S0, Scap, best);
+            eig_segment(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S, S0, Scap, best);
             if (ycap >= 0) {
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -788,7 +788,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                 const int st = wi / R.h, y = wi - st * R.h;
                 if (y < 1 || y > R.h - 2) continue;
                 uint64_t word = a.lmax[R.moff + wi];
-                const float* Er = Ep + (size_t)y * R.w + st * kGfttStrip - kGfttHalo;
+                const float* Er = Ep + (size_t)y * gftt_epitch(R.w) + st * kGfttStrip - kGfttHalo;
                 while (word) {  // up to 8 value loads in flight per round
                     int xs[8];
                     float vs[8];
@@ -811,10 +811,10 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                 }
             }
         } else {
-            const int iw = R.w - 2, n = iw * (R.h - 2);
+            const int iw = R.w - 2, n = iw * (R.h - 2), ep = gftt_epitch(R.w);
             for (int p = tid; p < n; p += kSelThreads) {
                 const int y = p / iw + 1, x = p - (y - 1) * iw + 1;
-                const float* Ec = Ep + (size_t)y * R.w + x;
+                const float* Ec = Ep + (size_t)y * ep + x;
                 const float v = Ec[0] > thr ? Ec[0] : 0.f;
                 if (v == 0.f) continue;
                 float m = v;
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                 for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
                     for (int dx = -1; dx <= 1; ++dx) {
-                        const float q0 = Ec[dy * R.w + dx];
+                        const float q0 = Ec[dy * ep + dx];
                         const float q = q0 > thr ? q0 : 0.f;
                         m = q > m ? q : m;
                     }

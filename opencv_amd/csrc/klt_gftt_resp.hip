@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64) void gftt_resp_colsum_kernel(GfttRespArgs a)
             else if (j < sse_end) e = acbb - (a.kf * ac) * ac;
             else e = (float)((double)acbb - a.hk * (double)ac * (double)ac);
         }
-        E[(size_t)y * W] = e;
+        E[(size_t)y * gftt_epitch(W)] = e;
     }
 }
 
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64) void gftt_resp_lmax_kernel(GfttRespArgs a)
     int best = INT_MIN;
     float e1 = 0.f, e2 = 0.f;
     for (int y = 0; y < H; ++y) {
-        const float e = E[(size_t)y * R.w];
+        const float e = E[(size_t)y * gftt_epitch(R.w)];
         if (out_lane) best = rfkey(e) > best ? rfkey(e) : best;
         const int yc = y - 1;
         if (has_lm && yc >= 1 && yc <= H - 2) {  // uniform

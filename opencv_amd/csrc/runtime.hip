@@ -556,7 +556,7 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
             return TBDK_EINVAL;
         tab[i] = GfttRoi{r.x, r.y, r.width, r.height, (int)total, (int)words, (int)ncblk};
         const int64_t strips = (r.width + kGfttStrip - 1) / kGfttStrip;
-        total += (int64_t)r.width * r.height;
+        total += (int64_t)gftt_epitch(r.width) * r.height;
         ncblk += strips;
         if (r.width >= 3 && r.height >= 3) words += strips * r.height;  // smaller ROIs have no interior
         max_area = std::max(max_area, r.width * r.height);
@@ -746,7 +746,7 @@ int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int he
     e = launch_gftt_eig(a, s);
     timing_end(ctx, rec, s);
     if (e == hipSuccess)
-        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)width * 4, (size_t)width * 4, height,
+        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)gftt_epitch(width) * 4, (size_t)width * 4, height,
                              hipMemcpyDeviceToDevice, s);
     return map_err(e);
 }
@@ -779,7 +779,7 @@ int tbdk_corner_response(tbdk_ctx* ctx, const uint8_t* img, int width, int heigh
     e = launch_gftt_resp(ra, plan.ncblk, plan.max_w, plan.max_h, plan.max_area, s);
     timing_end(ctx, rec, s);
     if (e == hipSuccess)
-        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)width * 4, (size_t)width * 4, height,
+        e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, ctx->gftt.planes, (size_t)gftt_epitch(width) * 4, (size_t)width * 4, height,
                              hipMemcpyDeviceToDevice, s);
     return map_err(e);
 }

@@ -203,14 +203,19 @@ namespace tbdk {
 // ---- GFTT over ROIs (klt_gftt.hip) ----
 struct GfttRoi {
     int x, y, w, h;
-    int off;   // first pixel of this ROI in the eigenvalue plane
+    int off;   // first value of this ROI in the eigenvalue plane (rows gftt_epitch(w) floats apart)
     int moff;  // first local-maximum word of this ROI (one uint64 per strip row)
     int cblk;  // first kGfttStrip-column strip of this ROI in the flat per-strip grid
 };
-// output columns per wave of the eigenvalue walk: lanes 3..60 (3 halo lanes per
-// side: eigenvalues are exact in lanes 2..61, the 3x3 local-maximum test in 3..60)
-constexpr int kGfttStrip = 58;
-constexpr int kGfttHalo = 3;
+// output columns per wave of the eigenvalue walk: lanes 4..59 (4 halo lanes per
+// side: eigenvalues are exact in lanes 2..61, the 3x3 local-maximum test in 3..60).
+// 56 columns = 224 bytes of eigenvalues, a whole number of 32-byte sectors, and
+// eigenvalue rows gftt_epitch(w) floats apart from 32-byte aligned ROI offsets:
+// every strip row is written as whole sectors (58 columns of a tight plane wrote
+// ~1.7x the plane's bytes in partial sectors)
+constexpr int kGfttStrip = 56;
+constexpr int kGfttHalo = 4;
+__host__ __device__ constexpr int gftt_epitch(int w) { return (w + 7) & ~7; }
 struct GfttArgs {
     const uint8_t* img;
     int pitch;

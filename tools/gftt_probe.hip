@@ -61,7 +61,7 @@ int main()
         rois.push_back(tbdk::GfttRoi{b[0], b[1], b[2], b[3], total, words, ncblk});
         if (b[2] >= 3 && b[3] >= 3) words += (b[2] + tbdk::kGfttStrip - 1) / tbdk::kGfttStrip * b[3];
         ncblk += (b[2] + tbdk::kGfttStrip - 1) / tbdk::kGfttStrip;
-        total += b[2] * b[3];
+        total += tbdk::gftt_epitch(b[2]) * b[3];
         max_area = std::max(max_area, b[2] * b[3]);
         max_w = std::max(max_w, b[2]);
     }
