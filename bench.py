@@ -788,6 +788,8 @@ def main(argv=None):
                     help="ctx option tbd_early_gftt (A/B runs; 0 off, 1 new tracks, 2 + re-detection boxes)")
     ap.add_argument("--no-spec-lookahead", action="store_true", help="ctx option tbd_spec_lookahead = 0 (A/B runs)")
     ap.add_argument("--no-zero-copy", action="store_true", help="ctx option tbd_zero_copy = 0 (A/B runs)")
+    ap.add_argument("--ctx-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra tbdk_ctx_set_option before the legs (A/B runs), repeatable")
     ap.add_argument("--pyr-derivs", action="store_true",
                     help="ctx option tbd_pyr_derivs = 1: loop pyramids with Scharr planes (A/B runs)")
     ap.add_argument("--timing-every", type=int, default=5,
@@ -842,6 +844,9 @@ def main(argv=None):
     ctx.set_option("tbd_spec_lookahead", 0 if args.no_spec_lookahead else 1)
     ctx.set_option("tbd_zero_copy", 0 if args.no_zero_copy else 1)
     ctx.set_option("tbd_pyr_derivs", 1 if args.pyr_derivs else 0)
+    for kv in args.ctx_option:
+        name, _, val = kv.partition("=")
+        ctx.set_option(name, int(val))
 
     m = TbdMeasure(args, ctx, dev)
     # the CPU baseline (rank 0, N = 1) runs after every GPU leg: 20 s of all-core

@@ -148,6 +148,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       kernels read their host tables from, and the fit writes its results
  *       to, coherent pinned host memory directly instead of through copies
  *       (results equal).
+ *   "tbd_fit_flag" (0/1, default 1; taken by tbdk_tbd_create, with zero copy):
+ *       the fit kernel's last wave publishes the frame's results by a
+ *       system-scope flag in pinned memory that the host polls, instead of an
+ *       event recorded behind the fit (whose marker held the next frame's
+ *       pyramid back; results equal).
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
  *       pyramids carry Scharr derivative planes and PyrLK reads them instead of
  *       deriving the window's values (results equal; A/B runs).

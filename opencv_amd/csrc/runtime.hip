@@ -162,6 +162,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_zero_copy = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_fit_flag") == 0) {
+        ctx->opt_tbd_fit_flag = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "fb_prep_ahead") == 0) {
         ctx->opt_fb_prep_ahead = value != 0;
         return TBDK_OK;

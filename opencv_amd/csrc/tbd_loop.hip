@@ -67,7 +67,8 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
                                                      const uint8_t* __restrict__ slot_status,
                                                      const int32_t* __restrict__ slot_iters,
                                                      int32_t* __restrict__ slot_counts, FitOut* __restrict__ out,
-                                                     int min_fit)
+                                                     int min_fit, unsigned* __restrict__ fit_cnt, int32_t* flag,
+                                                     int tag)
 {
     __shared__ float2 sa[kSlotPts], sb[kSlotPts];
     const int e = blockIdx.x;
@@ -113,6 +114,16 @@ __global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict_
             o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
         }
         out[e] = o;
+        if (flag) {
+            // publish: every wave releases its result (pinned host memory) at
+            // system scope before counting itself; the last one resets the count
+            // for the next launch (stream-ordered) and raises the frame's tag
+            const unsigned prev = __hip_atomic_fetch_add(fit_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (prev + 1u == (unsigned)nents) {
+                *fit_cnt = 0u;
+                __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 
@@ -208,6 +219,14 @@ struct tbdk_tbd {
     // mappings of the coherent pinned buffers; no copy is issued (d_pre, d_fit,
     // d_tab, d_la, d_spec, d_etab are those mappings, not device allocations)
     bool zc = false;
+    // fit completion by flag (zero copy, option tbd_fit_flag): the fit's last
+    // wave stores the frame's tag to h_flag (through its mapping d_flag) at
+    // system scope; d_fitcnt counts the finished waves
+    bool fit_flag = false;
+    int32_t* h_flag = nullptr;
+    int32_t* d_flag = nullptr;
+    unsigned* d_fitcnt = nullptr;
+    int fit_tag = 0;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
     hipEvent_t early_done = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
@@ -264,7 +283,7 @@ int release(tbdk_tbd* t)
         if (t->freed[k]) (void)hipEventDestroy(t->freed[k]);
     }
     if (t->up_s) (void)hipStreamDestroy(t->up_s);
-    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts};
+    void* dev[] = {t->slot_pts, t->slot_next, t->slot_status, t->slot_iters, t->slot_counts, t->d_fitcnt};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (!t->zc) {
@@ -272,7 +291,7 @@ int release(tbdk_tbd* t)
         for (void* p : staged)
             if (p) (void)hipFree(p);
     }
-    void* host[] = {t->h_pre, t->h_fit, t->h_tab, t->h_la, t->h_etab[0], t->h_spec};
+    void* host[] = {t->h_pre, t->h_fit, t->h_tab, t->h_la, t->h_etab[0], t->h_spec, t->h_flag};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -377,6 +396,13 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
+    t->fit_flag = t->zc && ctx->opt_tbd_fit_flag != 0;
+    if (t->fit_flag) {
+        hm(reinterpret_cast<void**>(&t->h_flag), 64);
+        sm(reinterpret_cast<void**>(&t->d_flag), t->h_flag, 64);
+        dm(reinterpret_cast<void**>(&t->d_fitcnt), 64);
+        if (e == hipSuccess) __atomic_store_n(t->h_flag, 0, __ATOMIC_RELEASE);
+    }
     if (t->h_pre && t->d_pre) {
         t->h_ents = static_cast<FitEntry*>(t->h_pre);
         t->h_lists = reinterpret_cast<int32_t*>(t->h_ents + S);
@@ -699,12 +725,15 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             e = hipStreamWaitEvent(s, t->la_done, 0);
             if (e != hipSuccess) return map_status(e);
         }
+        const bool by_flag = t->fit_flag && nents > 0;
+        const int tag = by_flag ? ++t->fit_tag : 0;
         int rec = timing_begin(t->ctx, "tbd_fit", s);
         hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
-                           t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points);
+                           t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points,
+                           by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag);
         timing_end(t->ctx, rec, s);
         if (!t->zc) e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipEventRecord(t->fit_done, s);
+        if (e == hipSuccess && !by_flag) e = hipEventRecord(t->fit_done, s);
         if (e != hipSuccess) return map_status(e);
         if (next) {  // runs on the device while this step waits for the fit and tracks
             rc = enqueue_next_pyr();
@@ -720,11 +749,25 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         // nothing that matters.  One host core per loop while it spins
         // (threading).
         constexpr double kSpinUs = 2000.0;
-        while ((e = hipEventQuery(t->fit_done)) == hipErrorNotReady) {
-            for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
-            if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
-                e = hipEventSynchronize(t->fit_done);
-                break;
+        if (by_flag) {
+            // the fit's flag; past kSpinUs the stream is synchronized (it holds
+            // the fit, then the next pyramid) and the flag read once more
+            e = hipSuccess;
+            while (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) != tag) {
+                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+                if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
+                    e = hipStreamSynchronize(s);
+                    if (e == hipSuccess && __atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) != tag) e = hipErrorUnknown;
+                    break;
+                }
+            }
+        } else {
+            while ((e = hipEventQuery(t->fit_done)) == hipErrorNotReady) {
+                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+                if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
+                    e = hipEventSynchronize(t->fit_done);
+                    break;
+                }
             }
         }
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();

@@ -236,6 +236,27 @@ def test_tbd_zero_copy_matches_copies(gpu):
     assert res[0] == res[1]
 
 
+def test_tbd_fit_flag_matches_event(gpu):
+    """Fit completion published by the fit kernel's system-scope flag (default)
+    and by an event behind the fit give the same frames."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 32, 12
+    frames, gt = klt.synth_render(9, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
+    res = []
+    try:
+        for fl in (1, 0):
+            gpu.set_option("tbd_fit_flag", fl)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            res.append(([_mkey(m) for m in ms], loop.tracks()))
+    finally:
+        gpu.set_option("tbd_fit_flag", 1)
+    assert res[0] == res[1]
+
+
 def test_tbd_run_host_matches_run(gpu):
     """tbdk_tbd_run_host (frames uploaded from pinned host memory through the
     three-frame device ring) gives the same frames as tbdk_tbd_run on the same
