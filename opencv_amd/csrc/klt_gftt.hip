@@ -187,66 +187,91 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) S0[ch] = S[ch];
     float e1 = 0.f, e2 = 0.f;  // eigenvalues of rows y - 1, y - 2
-    float nxt[kEigPref];
+    // E and lm through buffer stores: a lane that must not write gets an offset
+    // past the buffer, which the hardware drops, so the steady rows below stay
+    // one straight-line block (no exec-mask branches between rows)
+    const __amdgpu_buffer_rsrc_t rE =
+        __builtin_amdgcn_make_buffer_rsrc(E - g.x, (short)0, ep * H * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc(lm, (short)0, lm ? H * 8 : 0, 0x00020000);
+    constexpr uint32_t kDrop = 0x80000000u;
+    const uint32_t eoff = g.out_lane ? (uint32_t)g.x * 4u : kDrop;
+    // one walked row y (cur = pixel row y + 2); the flags are compile-time true
+    // in the steady rows
+    auto row = [&](auto steady, int y, float cur, bool has_next, bool store, bool lmx) {
+        constexpr bool ST = decltype(steady)::value;
+        double in[3];
+        SobelRow wc = wb;
+        if (ST || has_next) {  // entering cov row y + 1 (image rows y, y+1, y+2)
+            wc = eig_srow(g, cur);
+            eig_rowsums(g, wa, wb, wc, in);
+        } else {  // rs(refl(H)) == rs(H - 2) == rs(y - 1)
 #pragma unroll
-    for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(ys + 2 + j, H));
-    for (int yb = ys; yb < ye; yb += kEigPref) {
-        float cur[kEigPref];
+            for (int ch = 0; ch < 3; ++ch) in[ch] = qa[ch];
+        }
+        float box[3];
 #pragma unroll
-        for (int j = 0; j < kEigPref; ++j) cur[j] = nxt[j];
+        for (int ch = 0; ch < 3; ++ch) {
+            const double t = S[ch] + in[ch];
+            box[ch] = (float)t;
+            S[ch] = t - qa[ch];
+            qa[ch] = qb[ch];
+            qb[ch] = in[ch];
+        }
+        wa = wb;
+        wb = wc;
+        const float aa = box[0] * 0.5f, bb = box[1], cc = box[2] * 0.5f;
+        const float t = aa - cc;
+        const float e = (aa + cc) - sqrtf(bb * bb + t * t);
+        if (ST || store) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), rE, eoff == kDrop ? kDrop : eoff + (uint32_t)(y * ep * 4), 0, 0);
+            const int kk = fkey(e);
+            best = (g.out_lane && kk > best) ? kk : best;
+        }
+        if (ST || lmx) {  // row y - 1's 3x3 neighbourhood is now complete
+            float m = fmaxf(e2, e);
+            m = fmaxf(m, fmaxf(from_left(e2), from_right(e2)));
+            m = fmaxf(m, fmaxf(from_left(e1), from_right(e1)));
+            m = fmaxf(m, fmaxf(from_left(e), from_right(e)));
+            const uint64_t bal = __ballot(x_in && e1 >= m);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 bv = {(unsigned)bal, (unsigned)(bal >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(bv, rL, lane == 0 ? (uint32_t)((y - 1) * 8) : kDrop, 0, 0);
+        }
+        e2 = e1;
+        e1 = e;
+    };
+    // any row, flags at run time (the capture of Scap before row ycap included)
+    auto generic = [&](int y) {
+        if (y == ycap) {
 #pragma unroll
-        for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(yb + kEigPref + 2 + j, H));  // in flight
-        const int nb = ye - yb < kEigPref ? ye - yb : kEigPref;  // uniform
+            for (int ch = 0; ch < 3; ++ch) Scap[ch] = S[ch];
+        }
+        const int yc = y - 1;
+        row(std::false_type{}, y, y + 1 < H ? pix_fwd(y + 2) : 0.f, y + 1 < H, y >= y0 && y < y1,
+            yc >= y0 && yc < y1 && yc >= 1 && yc <= H - 2);
+    };
+    // steady rows [sa, sb): own rows with a complete 3x3 row above, a next row,
+    // and not the capture row; the rest of [ys, ye) by generic rows
+    const int sa = max(max(y0 + 1, 2), ys);
+    int sb = min(min(y1, H - 1), ye);
+    if (ycap >= 0) sb = min(sb, ycap);
+    int y = ys;
+    if (sb - sa >= kEigPref) {
+        for (; y < sa; ++y) generic(y);
+        float nxt[kEigPref];
 #pragma unroll
-        for (int j = 0; j < kEigPref; ++j) {
-            if (j < nb) {
-                const int y = yb + j;
-                if (y == ycap) {
+        for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(y + 2 + j);
+        for (; y + kEigPref <= sb; y += kEigPref) {
+            float cur[kEigPref];
 #pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) Scap[ch] = S[ch];
-                }
-                double in[3];
-                SobelRow wc = wb;
-                if (y + 1 < H) {  // entering cov row y + 1 (image rows y, y+1, y+2)
-                    wc = eig_srow(g, cur[j]);
-                    eig_rowsums(g, wa, wb, wc, in);
-                } else {  // rs(refl(H)) == rs(H - 2) == rs(y - 1)
+            for (int j = 0; j < kEigPref; ++j) cur[j] = nxt[j];
 #pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) in[ch] = qa[ch];
-                }
-                float box[3];
+            for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(y + kEigPref + 2 + j, H));  // in flight
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    const double t = S[ch] + in[ch];
-                    box[ch] = (float)t;
-                    S[ch] = t - qa[ch];
-                    qa[ch] = qb[ch];
-                    qb[ch] = in[ch];
-                }
-                wa = wb;
-                wb = wc;
-                const float aa = box[0] * 0.5f, bb = box[1], cc = box[2] * 0.5f;
-                const float t = aa - cc;
-                const float e = (aa + cc) - sqrtf(bb * bb + t * t);
-                if (y >= y0 && y < y1 && g.out_lane) {
-                    E[(size_t)y * ep] = e;
-                    const int kk = fkey(e);
-                    best = kk > best ? kk : best;
-                }
-                const int yc = y - 1;  // row whose 3x3 neighbourhood is now complete
-                if (yc >= y0 && yc < y1 && yc >= 1 && yc <= H - 2) {  // uniform
-                    float m = fmaxf(e2, e);
-                    m = fmaxf(m, fmaxf(from_left(e2), from_right(e2)));
-                    m = fmaxf(m, fmaxf(from_left(e1), from_right(e1)));
-                    m = fmaxf(m, fmaxf(from_left(e), from_right(e)));
-                    const unsigned long long bal = __ballot(x_in && e1 >= m);
-                    if (lane == 0 && lm) lm[yc] = bal;
-                }
-                e2 = e1;
-                e1 = e;
-            }
+            for (int j = 0; j < kEigPref; ++j) row(std::true_type{}, y + j, cur[j], true, true, true);
         }
     }
+    for (; y < ye; ++y) generic(y);
 }
 
 __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
