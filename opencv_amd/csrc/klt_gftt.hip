@@ -117,6 +117,9 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
 #endif
 constexpr int kEigWaves = TBDK_GFTT_EIG_WAVES;  // row segments (waves) per strip
 constexpr int kEigPref = 8;   // pixel rows in flight per wave
+#ifndef GFTT_ESTAMP  // eigenvalue-walk phase hooks for tools/ probes (no-ops in the library build)
+#define GFTT_ESTAMP(i)
+#endif
 
 struct EigLane {
     __amdgpu_buffer_rsrc_t rs;
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         __syncthreads();
         return s_bad;
     };
+    GFTT_ESTAMP(0);
     if (live) {
         eig_segment(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
         if (ycap >= 0) {
@@ -353,6 +357,7 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         }
     }
     int bad = first_mismatch(0);
+    GFTT_ESTAMP(1);
     // Cold: segment `bad` is walked again from its predecessor's final SUM (the
     // reference's value: the predecessor's own start was verified), and the
     // segments after it concurrently from their fresh starts plus the drift
@@ -389,6 +394,7 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     }
     if (lane == 0) s_best[wv] = best;
     __syncthreads();
+    GFTT_ESTAMP(2);
     if (threadIdx.x == 0) {
         int m = s_best[0];
 #pragma unroll

@@ -11,6 +11,11 @@ __device__ unsigned long long* g_stamps;
     do {                                                                                \
         if (threadIdx.x == 0) g_stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+__device__ unsigned long long* g_estamps;
+#define GFTT_ESTAMP(i)                                                                     \
+    do {                                                                                   \
+        if (threadIdx.x == 0) g_estamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 __device__ unsigned long long* g_tacc;
 #define GFTT_TDECL                      \
     unsigned long long tacc_[6] = {0}; \
@@ -85,6 +90,9 @@ int main()
     CK(hipMalloc(&dcorners, sizeof(float2) * 256 * nroi));
     CK(hipMalloc(&dst, 8 * 4 * nroi));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst)));
+    unsigned long long* dest;
+    CK(hipMalloc(&dest, 8 * 4 * (size_t)ncblk));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_estamps), &dest, sizeof(dest)));
     unsigned long long* dtacc;
     CK(hipMalloc(&dtacc, 8 * 8 * nroi));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_tacc), &dtacc, sizeof(dtacc)));
@@ -128,6 +136,24 @@ int main()
             pm[k] = std::max(pm[k], d);
         }
     printf("nroi %d total px %d max_area %d: gftt %.1f us/launch\n", nroi, total, max_area, ms * 1000 / reps);
+    {  // eigenvalue walk: per-workgroup spans of the last launch
+        std::vector<unsigned long long> es(4 * (size_t)ncblk);
+        CK(hipMemcpy(es.data(), dest, 8 * 4 * (size_t)ncblk, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double walk = 0, wmax = 0, rest = 0;
+        for (int b = 0; b < ncblk; ++b) {
+            t0 = std::min(t0, es[4 * b]);
+            t1 = std::max(t1, es[4 * b + 2]);
+            const double w = (double)(es[4 * b + 1] - es[4 * b]);
+            walk += w / ncblk;
+            wmax = std::max(wmax, w);
+            rest += (double)(es[4 * b + 2] - es[4 * b + 1]) / ncblk;
+        }
+        unsigned long long late = 0;
+        for (int b = 0; b < ncblk; ++b) late = std::max(late, es[4 * b] - t0);
+        printf("eig: %d workgroups, span %llu ticks (last start +%llu), walk mean %.0f max %.0f, after-walk mean %.0f\n",
+               ncblk, t1 - t0, late, walk, wmax, rest);
+    }
     printf("select phases (s_memtime ticks) mean/max: load %.0f/%.0f sort %.0f/%.0f walk %.0f/%.0f\n", ph[0], pm[0],
            ph[1], pm[1], ph[2], pm[2]);
     long sa = 0;
