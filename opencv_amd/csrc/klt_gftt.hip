@@ -117,6 +117,9 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
 #endif
 constexpr int kEigWaves = TBDK_GFTT_EIG_WAVES;  // row segments (waves) per strip
 constexpr int kEigPref = 8;   // pixel rows in flight per wave
+#ifndef TBDK_GFTT_WALK_PRIO
+#define TBDK_GFTT_WALK_PRIO 3  // s_setprio of gftt_select's walking wave
+#endif
 #ifndef GFTT_ESTAMP  // eigenvalue-walk phase hooks for tools/ probes (no-ops in the library build)
 #define GFTT_ESTAMP(i)
 #endif
@@ -935,6 +938,10 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     }
     GFTT_STAMP(2);
     if (tid >= 64) return;
+    // the walk is one wave's serial chain on the frame's critical path: ahead of
+    // the throughput-bound PyrLK waves sharing its SIMD for instruction issue
+    // (+0.6 % frames/s in three alternating loop runs out of three)
+    __builtin_amdgcn_s_setprio(TBDK_GFTT_WALK_PRIO);
 
     // ---- greedy walk in sorted order (featureselect.cpp:421-503), 64 candidates per step
     const int lane = tid;
