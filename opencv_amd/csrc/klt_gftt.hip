@@ -807,21 +807,32 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     // value > thr and it is >= all 8 neighbours (any larger neighbour exceeds
     // thr too), i.e. its local-maximum bit from the eigenvalue walk is set.
     // thr <= 0 (no positive eigenvalue in the ROI): the literal test.
+    // this thread's first local-maximum word is loaded together with the strip
+    // maxima (the threshold needs all of them; the word needs none): one global
+    // round trip fewer before the value loads
+    const int nstrip = (R.w + kGfttStrip - 1) / kGfttStrip;
+    const int nw = R.w >= 3 && R.h >= 3 ? nstrip * R.h : 0;
+    const uint64_t word0 = tid < nw ? a.lmax[R.moff + tid] : 0ull;
     int mk = INT_MIN;
-    for (int b = R.cblk, e = R.cblk + (R.w + kGfttStrip - 1) / kGfttStrip; b < e; ++b)
-        mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
+    {
+        int b = R.cblk;
+        const int e = R.cblk + nstrip;
+        for (; b + 4 <= e; b += 4) {  // four maxima in flight
+            const int m0 = a.blk_max[b], m1 = a.blk_max[b + 1], m2 = a.blk_max[b + 2], m3 = a.blk_max[b + 3];
+            mk = max(max(mk, max(m0, m1)), max(m2, m3));
+        }
+        for (; b < e; ++b) mk = a.blk_max[b] > mk ? a.blk_max[b] : mk;
+    }
     const float thr = (float)((double)fkey_inv(mk) * a.quality);
     if (tid == 0) s_total = 0;
     __syncthreads();
     const float* Ep = a.eig + R.off;
     if (R.w >= 3 && R.h >= 3) {
         if (thr > 0.f) {
-            const int nstrip = (R.w + kGfttStrip - 1) / kGfttStrip;
-            const int nw = nstrip * R.h;
             for (int wi = tid; wi < nw; wi += kSelThreads) {
                 const int st = wi / R.h, y = wi - st * R.h;
                 if (y < 1 || y > R.h - 2) continue;
-                uint64_t word = a.lmax[R.moff + wi];
+                uint64_t word = wi == tid ? word0 : a.lmax[R.moff + wi];
                 const float* Er = Ep + (size_t)y * gftt_epitch(R.w) + st * kGfttStrip - kGfttHalo;
                 while (word) {  // up to 8 value loads in flight per round
                     int xs[8];
@@ -868,6 +879,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
         }
     }
     __syncthreads();
+    GFTT_STAMP(4);
     const int total = s_total;
     if (total > a.cap) {  // candidate buffer overflow: report, never silently truncate
         if (tid == 0) a.counts[r] = -1;
@@ -925,6 +937,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
             nrest = total - sel;
         }
     }
+    GFTT_STAMP(5);
     int np2 = kSelThreads;
     while (np2 < S) np2 <<= 1;
     for (int i = S + tid; i < np2; i += kSelThreads) keys[i] = 0ull;  // sorts last

@@ -9,7 +9,7 @@
 __device__ unsigned long long* g_stamps;
 #define GFTT_STAMP(i)                                                                   \
     do {                                                                                \
-        if (threadIdx.x == 0) g_stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0) g_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 __device__ unsigned long long* g_estamps;
 #define GFTT_ESTAMP(i)                                                                     \
@@ -88,7 +88,7 @@ int main()
     CK(hipMalloc(&dcounts, 4 * nroi));
     CK(hipMalloc(&dcand, 8 * (size_t)std::max(words, 1)));
     CK(hipMalloc(&dcorners, sizeof(float2) * 256 * nroi));
-    CK(hipMalloc(&dst, 8 * 4 * nroi));
+    CK(hipMalloc(&dst, 8 * 8 * nroi));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst)));
     unsigned long long* dest;
     CK(hipMalloc(&dest, 8 * 4 * (size_t)ncblk));
@@ -124,14 +124,14 @@ int main()
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    std::vector<unsigned long long> st(4 * nroi);
+    std::vector<unsigned long long> st(8 * nroi);
     std::vector<int> cnt(nroi);
-    CK(hipMemcpy(st.data(), dst, 8 * 4 * nroi, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(st.data(), dst, 8 * 8 * nroi, hipMemcpyDeviceToHost));
     CK(hipMemcpy(cnt.data(), dcounts, 4 * nroi, hipMemcpyDeviceToHost));
     double ph[3] = {0, 0, 0}, pm[3] = {0, 0, 0};
     for (int r = 0; r < nroi; ++r)
         for (int k = 0; k < 3; ++k) {
-            double d = (double)(st[4 * r + k + 1] - st[4 * r + k]);
+            double d = (double)(st[8 * r + k + 1] - st[8 * r + k]);
             ph[k] += d / nroi;
             pm[k] = std::max(pm[k], d);
         }
@@ -156,6 +156,14 @@ int main()
     }
     printf("select phases (s_memtime ticks) mean/max: load %.0f/%.0f sort %.0f/%.0f walk %.0f/%.0f\n", ph[0], pm[0],
            ph[1], pm[1], ph[2], pm[2]);
+    {
+        double g = 0, ps = 0;
+        for (int r = 0; r < nroi; ++r) {
+            g += (double)(st[8 * r + 4] - st[8 * r]) / nroi;
+            ps += (double)(st[8 * r + 5] - st[8 * r + 4]) / nroi;
+        }
+        printf("  load = gather %.0f + partial selection %.0f + padding %.0f\n", g, ps, ph[0] - g - ps);
+    }
     long sa = 0;
     for (int r = 0; r < nroi; ++r) sa += cnt[r];
     std::vector<unsigned long long> ta(8 * nroi);
