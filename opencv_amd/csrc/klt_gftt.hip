@@ -619,6 +619,55 @@ __device__ __forceinline__ void window_test(const uint8_t* img, int rw, int rh, 
     constexpr bool THREE = NR + 7 > 16;  // the shifted window can need a third word
     constexpr uint64_t kHi = 0x8080808080808080ull, kLo7 = 0x7F7F7F7F7F7F7F7Full;
     const int x0 = ix - RAD;
+    if constexpr (RAD <= 2) {
+        // windows of <= 5 bytes: one dword-aligned 8-byte read per row holds the
+        // row's window after a shift of < 4 bytes, so each row is one 64-bit
+        // word (the general path below shifts a 16-byte pair)
+        uint64_t cv = 0;
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            const int xx = x0 + t;
+            cv |= ((xx >= 0 && xx < rw) ? 0xFFull : 0ull) << (8 * t);
+        }
+        uint64_t wv[NR];
+        int sh[NR];
+#pragma unroll
+        for (int d = 0; d < NR; ++d) {
+            const int yy = iy - RAD + d;
+            const int yc = yy < 0 ? 0 : (yy >= rh ? rh - 1 : yy);
+            const int base = yc * rw + x0;  // may be < 0 (first row, x0 < 0) or past the row: masked
+            const int al = base > 0 ? (base & ~3) : 0;
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + al);
+            wv[d] = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);
+            sh[d] = base - al;  // in [-RAD, 3]
+        }
+        uint64_t rej = 0;
+#pragma unroll
+        for (int d = 0; d < NR; ++d) {
+            const int yy = iy - RAD + d;
+            if (yy < 0 || yy >= rh) continue;
+            uint64_t close = 0;
+#pragma unroll
+            for (int t = 0; t < NR; ++t) {
+                const float ddx = (float)(t - RAD), ddy = (float)(d - RAD);
+                close |= (((double)(ddx * ddx + ddy * ddy) < md2 && !(d == RAD && t == RAD)) ? 0xFFull : 0ull)
+                         << (8 * t);
+            }
+            const uint64_t v = (sh[d] >= 0 ? wv[d] >> (8 * sh[d]) : wv[d] << (-8 * sh[d])) & cv & close;
+            rej |= v & kHi;
+            uint64_t nz = (((v & kLo7) + kLo7) | v) & ~v & kHi;
+            while (nz) {
+                const int t = __builtin_ctzll(nz) >> 3;
+                nz &= nz - 1ull;
+                const int c = (int)((v >> (8 * t)) & 0xFF);
+                if (c - 1 < lane) inb |= 1ull << (c - 1);  // earlier in this step
+            }
+        }
+        if (rej) good = false;
+        (void)fx;
+        (void)fy;
+        return;
+    }
     uint64_t cv_lo = 0, cv_hi = 0;  // 0xFF for window bytes whose column lies inside the ROI
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
