@@ -58,6 +58,37 @@ __global__ void pyr_down_padded_kernel(const uint8_t* __restrict__ src, int spit
     const int ry = reflect101(py - dpad, dh);
     const uint8_t* s0 = src + (size_t)(2 * ry - 2 + spad) * spitch + spad;
     uint32_t v = 0;
+    const int x0 = t * 4 - dpad;
+    if (x0 >= 0 && x0 + 3 < dw && ((spitch | spad) & 3) == 0) {
+        // four consecutive in-level pixels: source columns 2x0-2 .. 2x0+8 of each
+        // of the 5 rows (inside the source's frame) as dword loads
+        const int c0 = 2 * x0 - 2 + spad, base = c0 & ~3, o = c0 - base;  // o in {0, 2}
+        const uint8_t* r0 = src + (size_t)(2 * ry - 2 + spad) * spitch + base;
+        int h[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(r0 + (size_t)j * spitch);
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, o), a1 = __builtin_amdgcn_alignbyte(w2, w1, o),
+                           a2 = __builtin_amdgcn_alignbyte(w3, w2, o);
+            int px[11];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                px[k] = (int)((a0 >> (8 * k)) & 255u);
+                px[4 + k] = (int)((a1 >> (8 * k)) & 255u);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) px[8 + k] = (int)((a2 >> (8 * k)) & 255u);
+            const int kj = j == 2 ? 6 : (j == 1 || j == 3) ? 4 : 1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                h[k] += kj * (px[2 * k + 2] * 6 + (px[2 * k + 1] + px[2 * k + 3]) * 4 + px[2 * k] + px[2 * k + 4]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)((h[k] + 128) >> 8) << (8 * k);
+        *reinterpret_cast<uint32_t*>(dst + (size_t)py * dpitch + t * 4) = v;
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int rx = reflect101(t * 4 + k - dpad, dw);
@@ -159,7 +190,8 @@ struct PyrRolesArgs {
     uint8_t* d1;         // the level below (padded)
     int p1, pad1, w1, h1;
     int nA;              // blocks of role A (role B: the rest)
-    int wa4, wb4;        // 4-pixel items per padded row of roles A and B
+    int wa4, wb4;        // items per padded row of roles A (4 or 16 bytes) and B (4 pixels)
+    int a16;             // role A copies 16 bytes per thread (source, copy and pitches 16-byte aligned, pad % 16 == 0)
 };
 
 __device__ __forceinline__ int pyr5(int a, int b, int c, int d, int e) { return c * 6 + (b + d) * 4 + a + e; }
@@ -190,6 +222,23 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
         const int py = item / a.wa4, t = item - py * a.wa4;
         if (py >= a.sh + 2 * a.cpad) return;
         const uint8_t* srow = a.src + (size_t)reflect101(py - a.cpad, a.sh) * a.spitch;
+        if (a.a16) {  // 16 bytes per thread: one dwordx4 load and store in the frame's interior
+            const int x0 = 16 * t - a.cpad;
+            uint4 v;
+            if (x0 >= 0 && x0 + 15 < a.sw) {
+                v = *reinterpret_cast<const uint4*>(srow + x0);
+            } else {
+                uint32_t q[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    q[d] = 0;
+                    for (int k = 0; k < 4; ++k) q[d] |= (uint32_t)srow[reflect101(x0 + 4 * d + k, a.sw)] << (8 * k);
+                }
+                v = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+            *reinterpret_cast<uint4*>(a.copy + (size_t)py * a.cpitch + 16 * t) = v;
+            return;
+        }
         const int x0 = 4 * t - a.cpad;
         uint32_t v;
         if (a.vec && (x0 & 3) == 0 && x0 >= 0 && x0 + 3 < a.sw) {
@@ -267,7 +316,9 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
     a.w1 = D1.width;
     a.h1 = D1.height;
     auto blocks = [](long items) { return (int)((items + kRoleThreads - 1) / kRoleThreads); };
-    a.wa4 = (S.width + 2 * S.pad + 3) / 4;
+    a.a16 = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)spitch | reinterpret_cast<uintptr_t>(S.data) |
+              (uintptr_t)S.pitch | (uintptr_t)S.pad) & 15) == 0 && S.pitch >= ((S.width + 2 * S.pad + 15) & ~15);
+    a.wa4 = a.a16 ? (S.width + 2 * S.pad + 15) / 16 : (S.width + 2 * S.pad + 3) / 4;
     a.wb4 = (D1.width + 2 * D1.pad + 3) / 4;
     a.nA = blocks((long)a.wa4 * (S.height + 2 * S.pad));
     const int nB = blocks((long)a.wb4 * (D1.height + 2 * D1.pad));
