@@ -58,68 +58,80 @@ struct FitOut {
     int iters;      // Newton iterations of those corners over all levels (flop accounting)
 };
 
-// One wave per live track.  Fit terms follow getRTMatrix's non-full-affine
-// branch (float products summed in double), accumulated wave-parallel in a
-// fixed order (box_fit.hpp: wave_fit_similarity).
-__global__ __launch_bounds__(64) void tbd_fit_kernel(const FitEntry* __restrict__ ents, int nents,
-                                                     float2* __restrict__ slot_pts,
-                                                     const float2* __restrict__ slot_next,
-                                                     const uint8_t* __restrict__ slot_status,
-                                                     const int32_t* __restrict__ slot_iters,
-                                                     int32_t* __restrict__ slot_counts, FitOut* __restrict__ out,
-                                                     int min_fit, unsigned* __restrict__ fit_cnt, int32_t* flag,
-                                                     int tag)
+// One wave per live track, kFitWaves tracks per workgroup.  Fit terms follow
+// getRTMatrix's non-full-affine branch (float products summed in double),
+// accumulated wave-parallel in a fixed order (box_fit.hpp: wave_fit_similarity).
+constexpr int kFitWaves = 8;
+__global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry* __restrict__ ents, int nents,
+                                                                 float2* __restrict__ slot_pts,
+                                                                 const float2* __restrict__ slot_next,
+                                                                 const uint8_t* __restrict__ slot_status,
+                                                                 const int32_t* __restrict__ slot_iters,
+                                                                 int32_t* __restrict__ slot_counts,
+                                                                 FitOut* __restrict__ out, int min_fit,
+                                                                 unsigned* __restrict__ fit_cnt, int32_t* flag, int tag)
 {
-    __shared__ float2 sa[kSlotPts], sb[kSlotPts];
-    const int e = blockIdx.x;
-    if (e >= nents) return;
-    const int lane = threadIdx.x;
-    const FitEntry E = ents[e];
-    const int row = E.src >= 0 ? E.src : E.slot;  // where the tracked set and its PyrLK results are
-    const int c0 = slot_counts[row];
-    const int cnt = c0 < 0 ? 0 : c0;  // -1: GFTT candidate overflow, no corners
-    const size_t base = (size_t)E.slot * kSlotPts, rb = (size_t)row * kSlotPts;
-    int m = 0, it = 0;
-    for (int j0 = 0; j0 < kSlotPts; j0 += 64) {
-        const int j = j0 + lane;
-        const bool ok = j < cnt && slot_status[rb + j];
-        it += j < cnt ? slot_iters[rb + j] : 0;
-        const unsigned long long bal = __ballot(ok);
-        if (ok) {
-            const int pos = m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-            sa[pos] = slot_pts[rb + j];
-            sb[pos] = slot_next[rb + j];
+    __shared__ float2 s_a[kFitWaves][kSlotPts], s_b[kFitWaves][kSlotPts];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int e = blockIdx.x * kFitWaves + wv;
+    if (e < nents) {
+        float2* sa = s_a[wv];
+        float2* sb = s_b[wv];
+        const FitEntry E = ents[e];
+        const int row = E.src >= 0 ? E.src : E.slot;  // where the tracked set and its PyrLK results are
+        const int c0 = slot_counts[row];
+        const int cnt = c0 < 0 ? 0 : c0;  // -1: GFTT candidate overflow, no corners
+        const size_t base = (size_t)E.slot * kSlotPts, rb = (size_t)row * kSlotPts;
+        int m = 0, it = 0;
+        for (int j0 = 0; j0 < kSlotPts; j0 += 64) {
+            const int j = j0 + lane;
+            const bool ok = j < cnt && slot_status[rb + j];
+            it += j < cnt ? slot_iters[rb + j] : 0;
+            const unsigned long long bal = __ballot(ok);
+            if (ok) {
+                const int pos = m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                sa[pos] = slot_pts[rb + j];
+                sb[pos] = slot_next[rb + j];
+            }
+            m += __popcll(bal);
         }
-        m += __popcll(bal);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's compacted lists (its own LDS)
+        __builtin_amdgcn_wave_barrier();
+        for (int j = lane; j < m; j += 64) slot_pts[base + j] = sb[j];
+        for (int off = 32; off >= 1; off >>= 1) it += __shfl_xor(it, off, 64);
+        const SimilarityFit f = wave_fit_similarity(sa, sb, m, lane);
+        if (lane == 0) {
+            slot_counts[E.slot] = m;
+            FitOut o;
+            o.n = m;
+            o.npts = cnt;
+            o.iters = it;
+            o.valid = 0;
+            o.cx = o.cy = 0.0;
+            o.scale = 0.0;
+            if (m >= min_fit && m > 0 && f.ok) {
+                const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
+                o.cx = f.p * cx0 - f.q * cy0 + f.tx;
+                o.cy = f.q * cx0 + f.p * cy0 + f.ty;
+                o.scale = sqrt(f.p * f.p + f.q * f.q);
+                o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
+            }
+            out[e] = o;
+        }
     }
-    __syncthreads();
-    for (int j = lane; j < m; j += 64) slot_pts[base + j] = sb[j];
-    for (int off = 32; off >= 1; off >>= 1) it += __shfl_xor(it, off, 64);
-    const SimilarityFit f = wave_fit_similarity(sa, sb, m, lane);
-    if (lane == 0) {
-        slot_counts[E.slot] = m;
-        FitOut o;
-        o.n = m;
-        o.npts = cnt;
-        o.iters = it;
-        o.valid = 0;
-        o.cx = o.cy = 0.0;
-        o.scale = 0.0;
-        if (m >= min_fit && m > 0 && f.ok) {
-            const double cx0 = E.x + E.w / 2, cy0 = E.y + E.h / 2;
-            o.cx = f.p * cx0 - f.q * cy0 + f.tx;
-            o.cy = f.q * cx0 + f.p * cy0 + f.ty;
-            o.scale = sqrt(f.p * f.p + f.q * f.q);
-            o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
-        }
-        out[e] = o;
-        if (flag) {
-            // publish: every wave releases its result (pinned host memory) at
-            // system scope before counting itself; the last one resets the count
-            // for the next launch (stream-ordered) and raises the frame's tag
-            const unsigned prev = __hip_atomic_fetch_add(fit_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (prev + 1u == (unsigned)nents) {
+    if (flag) {
+        // publish: after the workgroup's barrier one thread releases the
+        // workgroup's results (pinned host memory) at system scope and counts
+        // them (one release per workgroup, not per wave); the last workgroup
+        // resets the count for the next launch (stream-ordered) and raises the
+        // frame's tag
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int first = blockIdx.x * kFitWaves;
+            const unsigned nin = (unsigned)(nents - first < kFitWaves ? nents - first : kFitWaves);
+            const unsigned prev = __hip_atomic_fetch_add(fit_cnt, nin, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (prev + nin == (unsigned)nents) {
                 *fit_cnt = 0u;
                 __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -728,7 +740,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         const bool by_flag = t->fit_flag && nents > 0;
         const int tag = by_flag ? ++t->fit_tag : 0;
         int rec = timing_begin(t->ctx, "tbd_fit", s);
-        hipLaunchKernelGGL(tbd_fit_kernel, dim3(nents), dim3(64), 0, s, t->d_ents, nents, t->slot_pts, t->slot_next,
+        hipLaunchKernelGGL(tbd_fit_kernel, dim3((nents + kFitWaves - 1) / kFitWaves), dim3(64 * kFitWaves), 0, s,
+                           t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points,
                            by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag);
         timing_end(t->ctx, rec, s);
