@@ -148,6 +148,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       kernels read their host tables from, and the fit writes its results
  *       to, coherent pinned host memory directly instead of through copies
  *       (results equal).
+ *   "tbd_early_la" (0/1/2, default 1): with a look-ahead frame, the TBD loop
+ *       tracks this step's early GFTT rows into the next frame right after the
+ *       fit (1: on re-detection frames, where no speculative PyrLK runs; 2:
+ *       every frame); the next step's refreshed-set PyrLK skips them (results
+ *       equal).
  *   "tbd_fit_flag" (0/1, default 1; taken by tbdk_tbd_create, with zero copy):
  *       the fit kernel's last wave publishes the frame's results by a
  *       system-scope flag in pinned memory that the host polls, instead of an

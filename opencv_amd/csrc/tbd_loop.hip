@@ -187,6 +187,13 @@ struct tbdk_tbd {
     // frame): [slots] pinned / device, membership
     int32_t* h_spec = nullptr;
     int32_t* d_spec = nullptr;
+    // look-ahead PyrLK of this step's early GFTT rows (option tbd_early_la): the
+    // rows it tracked into the next frame (ers_row), which the next step's
+    // refreshed-set PyrLK then skips; their staged list
+    std::vector<char> ers_row;
+    std::vector<int> ers_list;
+    int32_t* h_ers = nullptr;
+    int32_t* d_ers = nullptr;
     std::vector<int> spec_list;
     std::vector<char> spec_member;
     const uint8_t* la_frame = nullptr;
@@ -299,11 +306,11 @@ int release(tbdk_tbd* t)
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (!t->zc) {
-        void* staged[] = {t->d_pre, t->d_fit, t->d_tab, t->d_la, t->d_etab, t->d_spec};
+        void* staged[] = {t->d_pre, t->d_fit, t->d_tab, t->d_la, t->d_etab, t->d_spec, t->d_ers};
         for (void* p : staged)
             if (p) (void)hipFree(p);
     }
-    void* host[] = {t->h_pre, t->h_fit, t->h_tab, t->h_la, t->h_etab[0], t->h_spec, t->h_flag};
+    void* host[] = {t->h_pre, t->h_fit, t->h_tab, t->h_la, t->h_etab[0], t->h_spec, t->h_flag, t->h_ers};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete t->tracker;
@@ -400,6 +407,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     hm(reinterpret_cast<void**>(&t->h_tab), sizeof(GfttRoi) * S);
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
+    hm(reinterpret_cast<void**>(&t->h_ers), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
     if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
     sm(&t->d_pre, t->h_pre, pre_bytes);
@@ -407,6 +415,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     sm(reinterpret_cast<void**>(&t->d_tab), t->h_tab, sizeof(GfttRoi) * S);
     sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
+    sm(reinterpret_cast<void**>(&t->d_ers), t->h_ers, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
     t->fit_flag = t->zc && ctx->opt_tbd_fit_flag != 0;
     if (t->fit_flag) {
@@ -424,6 +433,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->refreshed.assign((size_t)S, 0);
     t->la_member.assign((size_t)S, 0);
     t->spec_member.assign((size_t)S, 0);
+    t->ers_row.assign((size_t)4 * S, 0);
     t->b_list.assign((size_t)S, 0);
     t->src_row.assign((size_t)S, -1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->pyr_ready, hipEventDisableTiming);
@@ -686,7 +696,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             const tbd::Rect& b = tr.bboxes.back();
             const int src = t->src_row[(size_t)slot];
             t->h_ents[nents++] = FitEntry{slot, b.x, b.y, b.width, b.height, src};
-            if (src >= 0) t->b_list[nB++] = src;  // refreshed: tracked from its GFTT row
+            if (src >= 0) {  // refreshed: tracked from its GFTT row (unless the look-ahead did)
+                if (!(la_lk && t->ers_row[(size_t)src])) t->b_list[nB++] = src;
+            }
             else if (!(la_lk && t->la_member[(size_t)slot])) t->h_lists[nA++] = slot;
         }
         // refreshed sets after the unchanged ones (a separate scratch list: with
@@ -706,6 +718,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     for (int sl : t->la_list) t->la_member[(size_t)sl] = 0;
     t->la_list.clear();
+    for (int r : t->ers_list) t->ers_row[(size_t)r] = 0;
+    t->ers_list.clear();
     for (int sl : t->src_list) t->src_row[(size_t)sl] = -1;  // the fit compacts them into their slots
     t->src_list.clear();
 
@@ -839,6 +853,36 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 }
                 t->la_lk = true;
             }
+        }
+        // ---- look-ahead PyrLK of this step's early GFTT rows (option
+        // tbd_early_la; 1: re-detection frames, where the speculative PyrLK above
+        // does not run and the device would idle through the host tracker step,
+        // 2: every frame).  Each early row is the corner set a track refreshed in
+        // this step's ROI will be tracked from in the next step (new tracks, the
+        // re-detection guesses the tracker confirms), so the next step's PyrLK
+        // of the refreshed sets skips the rows tracked here: the same points, the
+        // same pyramids (this frame's and the look-ahead), the same results.
+        const int ela = t->ctx->opt_tbd_early_la;
+        const int ne = (int)t->erois.size();
+        if (next && early_launched && ne > 0 && (ela >= 2 || (ela == 1 && frame_id % c.redetect_every == 0))) {
+            for (int q = 0; q < ne; ++q) t->h_ers[q] = erow0 + q;
+            hipStream_t ls = t->la_s;
+            e = hipStreamWaitEvent(ls, t->la_ready, 0);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ls, t->early_done, 0);
+            if (e == hipSuccess && !t->zc)
+                e = hipMemcpyAsync(t->d_ers, t->h_ers, sizeof(int32_t) * ne, hipMemcpyHostToDevice, ls);
+            if (e != hipSuccess) return map_status(e);
+            rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
+                             reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                             ne * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_ers);
+            if (rc != TBDK_OK) return rc;
+            e = hipEventRecord(t->la_done, ls);
+            if (e != hipSuccess) return map_status(e);
+            for (int q = 0; q < ne; ++q) {
+                t->ers_row[(size_t)(erow0 + q)] = 1;
+                t->ers_list.push_back(erow0 + q);
+            }
+            t->la_lk = true;
         }
     } else {
         if (next) {

@@ -179,7 +179,9 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     post-tracker GFTT computes, so do the early GFTTs of the guessed
     re-detection boxes (option value 2) where the tracker confirms the guess,
     and the speculative look-ahead PyrLK (launched
-    before the tracker step) equals the post-tracker one: same per-frame
+    before the tracker step) and the look-ahead PyrLK of the early rows (option
+    tbd_early_la, re-detection frames or every frame) equal the post-tracker
+    ones: same per-frame
     metrics, predictions and tracks with the options on and off, under the
     reference's bounds quirk (most new tracks served early, speculated sets
     deleted by the tracker) and with re-detection frames mixed in."""
@@ -191,9 +193,11 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
     res = {}
     try:
-        for early, spec in ((2, 1), (2, 0), (1, 1), (1, 0), (0, 1), (0, 0)):
+        for early, spec, ela in ((2, 1, 1), (2, 1, 0), (2, 1, 2), (2, 0, 1), (1, 1, 1), (1, 1, 2), (1, 0, 1),
+                                 (0, 1, 1), (0, 0, 0)):
             gpu.set_option("tbd_early_gftt", early)
             gpu.set_option("tbd_spec_lookahead", spec)
+            gpu.set_option("tbd_early_la", ela)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms, preds = [], []
             if api == "run":
@@ -203,16 +207,18 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
                     nxt = frames[f + 1] if api == "ahead" and f + 1 < F else None
                     ms.append(loop.step(frames[f], f, dets[f], next_frame=nxt))
                     preds.append(loop.predictions())
-            res[early, spec] = ([_mkey(m) for m in ms], preds, loop.tracks(), sum(m.early_gftt for m in ms))
+            res[early, spec, ela] = ([_mkey(m) for m in ms], preds, loop.tracks(), sum(m.early_gftt for m in ms))
     finally:
         gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
-    for key in ((2, 1), (2, 0), (1, 1), (1, 0), (0, 1)):
-        assert res[key][0] == res[0, 0][0], key
-        assert res[key][1] == res[0, 0][1], key
-        assert res[key][2] == res[0, 0][2], key
-    assert res[1, 1][3] > 2 * F and res[0, 0][3] == 0  # the early path was taken (and off means off)
-    assert res[2, 1][3] > res[1, 1][3] + F  # re-detection guesses confirmed
+        gpu.set_option("tbd_early_la", 1)
+    base = res[0, 0, 0]
+    for key, r in res.items():
+        assert r[0] == base[0], key
+        assert r[1] == base[1], key
+        assert r[2] == base[2], key
+    assert res[1, 1, 1][3] > 2 * F and base[3] == 0  # the early path was taken (and off means off)
+    assert res[2, 1, 1][3] > res[1, 1, 1][3] + F  # re-detection guesses confirmed
 
 
 def test_tbd_zero_copy_matches_copies(gpu):
