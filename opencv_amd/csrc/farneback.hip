@@ -622,46 +622,59 @@ __device__ __forceinline__ void fb_finish(const FbIterArgs& a, int x, int y, con
 __device__ __forceinline__ int fb_slot(int l) { return l + (l >> 2); }
 constexpr int kFbSlots = kFbStrip + kFbStrip / 4;
 
-// horizontal window + 2x2 solve of one batch row: thread task -> (row r, 4
-// consecutive output columns starting at strip offset o0)
+// horizontal window + 2x2 solve of one batch row: thread task -> (row r, TK
+// consecutive output columns starting at strip offset o0).  Box sums restart at
+// every strip offset divisible by 4 (image columns divisible by 4) and slide
+// from there, whatever TK is, so the sums do not depend on the task split.
+#ifndef TBDK_FB_TK
+#define TBDK_FB_TK 2  // output columns per horizontal task (2: twice the threads in the solve phase)
+#endif
+constexpr int kFbTK = TBDK_FB_TK;
+static_assert(kFbTK == 2 || kFbTK == 4, "tasks of 2 or 4 columns");
 template <int M, bool GAUSS>
 __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
                                               int y, int ox0)
 {
-    constexpr int NW = 4 + 2 * M;
+    constexpr int TK = kFbTK;
     constexpr int OW = fb_ow(M);
-    float out[5][4];
+    float out[5][TK];
+    const int g0 = o0 & ~3, sk = o0 - g0;  // the box sums' group start, slides to o0 (0 or 2)
 #pragma unroll
     for (int ch = 0; ch < 5; ++ch) {
         const float* row = vb[r][ch];
         if (GAUSS) {
             // optflowgf.cpp:548-553: sum = v[x]*k0; sum += k[i]*(v[x-i] + v[x+i])
+            constexpr int NW = TK + 2 * M;
             float win[NW];
 #pragma unroll
             for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(o0 + i, kFbStrip - 1))];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < TK; ++k) {
                 float s = win[k + M] * a.gk[0];
 #pragma unroll
                 for (int i = 1; i <= M; ++i) s += a.gk[i] * (win[k + M - i] + win[k + M + i]);
                 out[ch][k] = s;
             }
         } else {
-            // window of output o0 (image column divisible by 4) summed from the
-            // left, the next three slid: out[k] = (out[k-1] + v[k+2m]) - v[k-1]
+            // window of group start g0 summed from the left, then slid:
+            // out(c) = (out(c-1) + v[c+2m]) - v[c-1]
+            constexpr int NW = 4 + 2 * M;
             float win[NW];
 #pragma unroll
-            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(g0 + i, kFbStrip - 1))];
             float sacc = win[0];
 #pragma unroll
             for (int i = 1; i <= 2 * M; ++i) sacc += win[i];
-            out[ch][0] = sacc;
+            float v[4];
+            v[0] = sacc;
 #pragma unroll
-            for (int k = 1; k < 4; ++k) out[ch][k] = (out[ch][k - 1] + win[k + 2 * M]) - win[k - 1];
+            for (int k = 1; k < 4; ++k) v[k] = (v[k - 1] + win[k + 2 * M]) - win[k - 1];
+#pragma unroll
+            for (int k = 0; k < TK; ++k) out[ch][k] = TK == 4 ? v[k] : (sk ? v[2 + k] : v[k]);
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < TK; ++k) {
         const int o = o0 + k, x = ox0 + o;
         if (o >= OW || x >= a.w) break;
         double g11, g12, g22, h1, h2;
@@ -762,7 +775,7 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
 {
     constexpr int K = 2 * M + 1;
     constexpr int OW = fb_ow(M);
-    constexpr int NQ = (OW + 3) / 4;      // 4-column horizontal tasks per row
+    constexpr int NQ = (OW + kFbTK - 1) / kFbTK;  // horizontal tasks per row
     constexpr int RR = kFbRB + 2 * M;     // M ring rows
     constexpr int VC = 4;                 // centres per thread in the vertical pass
     __shared__ float mr[5 * RR * kFbStrip];
@@ -835,9 +848,9 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
         if (more) fb_rows_b<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A, B);
         fb_lds_barrier();
         const int nb = min(kFbRB, nrows - s0);
-        if (tid < nb * NQ) {
-            const int r = tid / NQ, q = tid - r * NQ;
-            if (ox0 + 4 * q < a.w) fb_horizontal<M, GAUSS>(a, vb, r, 4 * q, y0 + s0 + r, ox0);
+        for (int task = tid; task < nb * NQ; task += kFbThreads) {
+            const int r = task / NQ, q = task - r * NQ;
+            if (ox0 + kFbTK * q < a.w) fb_horizontal<M, GAUSS>(a, vb, r, kFbTK * q, y0 + s0 + r, ox0);
         }
         // the next batch's M rows overwrite ring rows the vertical pass read,
         // and its vertical pass vb rows this horizontal pass reads: both are
