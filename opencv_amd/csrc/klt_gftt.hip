@@ -7,15 +7,17 @@
 // evaluation order documented in oracle/gftt_oracle.c; built with
 // -ffp-contract=off so every expression rounds exactly as written.
 //
-// Three launches, all ROIs of a frame batched in each:
-//   1. gftt_eig   : one wave per 60-column strip of a ROI: Sobel 3x3
-//                   (reflect-101 inside the ROI) -> cov = (Dx^2, DxDy, Dy^2) ->
-//                   the boxFilter's row sums in double (neighbour columns by
-//                   DPP wave shifts) -> the reference's running ColumnSum walked
-//                   top to bottom -> min eigenvalue; per-strip max
-//   2. gftt_nms   : one thread per ROI pixel: threshold-to-zero at max*q,
-//                   3x3 dilate-equality, candidates to per-block slots
-//   3. gftt_select: one 512-thread workgroup per ROI: gather, sort by
+// Two launches, all ROIs of a frame batched in each:
+//   1. gftt_eig   : one workgroup per 56-column strip of a ROI, its waves
+//                   walking row segments: Sobel 3x3 (reflect-101 inside the
+//                   ROI) -> cov = (Dx^2, DxDy, Dy^2) -> the boxFilter's row
+//                   sums in double (neighbour columns by DPP wave shifts) ->
+//                   the reference's running ColumnSum walked top to bottom ->
+//                   min eigenvalue; per-strip max and the rows' 3x3
+//                   local-maximum ballots (the threshold-independent half of
+//                   the reference's threshold + dilate test)
+//   2. gftt_select: one 512-thread workgroup per ROI: candidates (local
+//                   maxima above max*q), sort by
 //                   (value desc, address desc) — the reference's deterministic
 //                   tie-break (featureselect.cpp:56-64) — then the greedy
 //                   min-distance walk (:421-503) by one wave, 64 candidates per
@@ -93,11 +95,11 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
     return SobelRow{t, u};
 }
 
-// Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 58-column strip of
-// a ROI per workgroup.  Lane L holds ROI column x0 - 3 + L (lanes 3..60 produce
-// output, three halo lanes per side); each lane loads only its own pixel of a
-// row and gets its neighbours by DPP wave shifts, reflect-101 at the ROI edges
-// turning the missing neighbour into the other one.
+// Fused Sobel -> cov -> boxFilter -> min eigenvalue for one 56-column strip of
+// a ROI per workgroup.  Lane L holds ROI column x0 - 4 + L (lanes 4..59 produce
+// output, four halo lanes per side); each lane loads only its own pixel of a
+// row and gets its neighbours by DPP wave shifts; lanes outside the ROI hold
+// their reflect-101 column (see eig_srow).
 //
 // The box filter is the reference's running ColumnSum (box_filter.simd.hpp:
 // 176-273), per channel: SUM = (0 + rs(-1)) + rs(0); per row y:
@@ -334,8 +336,8 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     const int ycap = y1 < H ? y1 - 1 : -1;  // the next segment starts fresh at y1 - 1
     int best = INT_MIN;
     double S[3], S0[3], Scap[3];
-    // lanes whose box sums reach an output: the eigenvalues of lanes 2..61 (the
-    // local-maximum test of lanes 3..60 reads their neighbours) inside the ROI;
+    // lanes whose box sums reach an output: the eigenvalues of lanes 3..60 (the
+    // local-maximum test of output lanes 4..59 reads their neighbours) inside the ROI;
     // the outer halo lanes and clamped columns carry sums nothing reads
     const bool need = lane >= kGfttHalo - 1 && lane <= kGfttHalo + kGfttStrip && xc >= 0 && xc < R.w;
     // segment `from` on: the first whose start may differ from the reference's SUM

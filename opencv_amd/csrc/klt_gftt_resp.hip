@@ -16,7 +16,7 @@
 //   3. gftt_resp_colsum : ColumnSum<double,float> (:175-273) walked down each
 //                         column by one thread, then calcMinEigenVal or
 //                         calcHarris (:52-152) at the flat index of the pixel
-//   4. gftt_resp_lmax   : per 58-column strip, the maximum key and the 3x3
+//   4. gftt_resp_lmax   : per 56-column strip, the maximum key and the 3x3
 //                         local-maximum ballots in gftt_eig_kernel's layout, so
 //                         gftt_select_kernel runs unchanged on the result.
 // These ROIs are rare (the TBD loop and the sample use blockSize 3, min
