@@ -540,6 +540,45 @@ def rank_env():
 _T0 = time.perf_counter()
 
 
+def hbm_copy_peak(dev, nbytes: int = 1 << 31, reps: int = 20) -> dict:
+    """an HBM roofline also against a measured stream-copy peak.
+    A device-to-device copy of a 2 GiB buffer (far beyond the L2s and the
+    256 MB Infinity Cache), read + write bytes / HIP-event time, best of
+    `reps` copies after warm-up."""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    src.fill_(1)
+    dst = torch.empty_like(src)
+    for _ in range(3):
+        dst.copy_(src)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    ok = bool(torch.equal(dst[:: 1 << 20], src[:: 1 << 20]))
+    del src, dst
+    gbs = 2 * nbytes / (best / 1000.0) / 1e9
+    return {"value": round(gbs, 1), "unit": "GB/s", "bytes": 2 * nbytes, "copies": reps, "checked": ok,
+            "frac_of_spec": round(gbs / PEAK_HBM_GBS, 4),
+            "note": "torch device-to-device copy of a 2 GiB buffer: read + write bytes / fastest HIP-event time"}
+
+
+def add_copy_peak_fracs(obj, peak_gbs: float):
+    """Every HBM-bound roofline object in the line gets its fraction of the
+    measured copy peak beside the spec-peak fraction."""
+    if isinstance(obj, dict):
+        if obj.get("bound") == "hbm" and isinstance(obj.get("achieved"), (int, float)):
+            obj["copy_peak"] = peak_gbs
+            obj["frac_copy_peak"] = round(obj["achieved"] / peak_gbs, 4)
+        for v in obj.values():
+            add_copy_peak_fracs(v, peak_gbs)
+
+
 def progress(msg: str, rank: int = 0):
     """one line per bench leg on stderr (rank 0): a long run under a profiler
     shows it is alive; stdout keeps the single JSON line"""
@@ -811,6 +850,7 @@ def main(argv=None):
     ap.add_argument("--fb-pairs", type=int, default=10)
     ap.add_argument("--no-f16", action="store_true", help="skip the secondary fp16 pixel path measurement")
     ap.add_argument("--f16-pairs", type=int, default=10)
+    ap.add_argument("--no-copy-peak", action="store_true", help="skip the measured HBM stream-copy peak")
     ap.add_argument("--no-hog", action="store_true", help="skip the secondary HOG detector measurement")
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
@@ -818,6 +858,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
     if args.no_secondary:
         args.no_step_api = args.no_h2d = args.no_kitti = args.no_farneback = args.no_f16 = args.no_hog = True
+        args.no_copy_peak = True
         args.repeats = 0
 
     world, rank, local = rank_env()
@@ -1019,6 +1060,10 @@ def main(argv=None):
     if rank == 0 and not args.no_hog:
         progress("HOG secondary")
         line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+    if rank == 0 and not args.no_copy_peak:
+        progress("HBM copy peak")
+        line["hbm_copy_peak"] = hbm_copy_peak(dev)
+        add_copy_peak_fracs(line, line["hbm_copy_peak"]["value"])
     if cpu_in is not None:
         progress("cpu baseline")
         line["cpu_baseline"] = cpu_baseline_line(cpu_in[0], cpu_in[1], args, restore_affinity=full_affinity)

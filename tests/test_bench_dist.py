@@ -140,3 +140,19 @@ def test_host_topology_helpers():
     assert 1 <= n <= info["affinity_cpus"]
     r = bench.pin_rank(0)  # no KFD topology here: nothing pinned, nothing changed
     assert isinstance(r, dict) and "pinned" in r
+
+
+def test_copy_peak_fractions_on_hbm_rooflines_only():
+    """hbm_copy_peak's value lands beside every HBM roofline (nested ones too),
+    never on a VALU one."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    line = {"roofline": {"bound": "valu", "achieved": 20.0},
+            "roofline_pyramid": {"bound": "hbm", "achieved": 400.0},
+            "farneback": {"roofline": {"bound": "hbm", "achieved": 2000.0}}}
+    bench.add_copy_peak_fracs(line, 5000.0)
+    assert "frac_copy_peak" not in line["roofline"]
+    assert line["roofline_pyramid"]["frac_copy_peak"] == 0.08
+    assert line["farneback"]["roofline"]["frac_copy_peak"] == 0.4
+    assert line["farneback"]["roofline"]["copy_peak"] == 5000.0
