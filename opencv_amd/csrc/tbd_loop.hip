@@ -746,7 +746,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                              nB * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + nA);
             if (rc != TBDK_OK) return rc;
         }
-        hipError_t e;
+        hipError_t e = hipSuccess;  // zero-copy without a look-ahead wait sets it nowhere below
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
             e = hipStreamWaitEvent(s, t->la_done, 0);
             if (e != hipSuccess) return map_status(e);
