@@ -512,6 +512,13 @@ struct FbIterArgs {
 
 __device__ __forceinline__ float fb_border(int i) { return i < 2 ? 0.14f : 0.4472f; }
 
+// 1: each batch's 2x2 solves run at the top of the next batch, beside its M
+// rows' finish (whose bilinear R1 terms are selected, not branched around);
+// 0: the solve right after the horizontal sums (tuning builds)
+#ifndef TBDK_FB_DEFER
+#define TBDK_FB_DEFER 1
+#endif
+
 // FarnebackUpdateMatrices at pixel (x, y) (optflowgf.cpp:235-309), in three
 // phases so a strip can keep two rows of loads in flight: A = the pixel's flow
 // and R0 (7 loads), B = the four R1 neighbours of x + flow (20 loads, their
@@ -580,6 +587,23 @@ __device__ __forceinline__ void fb_finish(const FbIterArgs& a, int x, int y, con
     const float dx = A.dx, dy = A.dy;
     const float R00 = A.r0[0], R01 = A.r0[1], R02 = A.r0[2], R03 = A.r0[3], R04 = A.r0[4];
     float r2, r3, r4, r5, r6;
+#if TBDK_FB_DEFER
+    // the R1 terms evaluated for every pixel and selected by B.in (same
+    // values as the branch), so the finish of interior rows is one basic
+    // block the deferred solve can interleave with
+    {
+        const float fx = B.fx, fy = B.fy;
+        const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+        float r[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) r[c] = a00 * B.q[c][0] + a01 * B.q[c][1] + a10 * B.q[c][2] + a11 * B.q[c][3];
+        r2 = B.in ? r[0] : 0.f;
+        r3 = B.in ? r[1] : 0.f;
+        r4 = B.in ? (R02 + r[2]) * 0.5f : R02;
+        r5 = B.in ? (R03 + r[3]) * 0.5f : R03;
+        r6 = B.in ? (R04 + r[4]) * 0.25f : R04 * 0.5f;
+    }
+#else
     if (B.in) {
         const float fx = B.fx, fy = B.fy;
         const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
@@ -597,6 +621,7 @@ __device__ __forceinline__ void fb_finish(const FbIterArgs& a, int x, int y, con
         r5 = R03;
         r6 = R04 * 0.5f;
     }
+#endif
     r2 = (R00 - r2) * 0.5f;
     r3 = (R01 - r3) * 0.5f;
     r2 += r4 * dy + r6 * dx;
@@ -632,12 +657,10 @@ constexpr int kFbSlots = kFbStrip + kFbStrip / 4;
 constexpr int kFbTK = TBDK_FB_TK;
 static_assert(kFbTK == 2 || kFbTK == 4, "tasks of 2 or 4 columns");
 template <int M, bool GAUSS>
-__device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
-                                              int y, int ox0)
+__device__ __forceinline__ void fb_hsums(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
+                                         float (&out)[5][kFbTK])
 {
     constexpr int TK = kFbTK;
-    constexpr int OW = fb_ow(M);
-    float out[5][TK];
     const int g0 = o0 & ~3, sk = o0 - g0;  // the box sums' group start, slides to o0 (0 or 2)
 #pragma unroll
     for (int ch = 0; ch < 5; ++ch) {
@@ -673,10 +696,19 @@ __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (
             for (int k = 0; k < TK; ++k) out[ch][k] = TK == 4 ? v[k] : (sk ? v[2 + k] : v[k]);
         }
     }
+}
+
+// the 2x2 solve (optflowgf.cpp:190-200) of a horizontal task's TK outputs and
+// their stores; `ok` false: nothing stored
+template <int M, bool GAUSS>
+__device__ __forceinline__ void fb_solve(const FbIterArgs& a, const float (&out)[5][kFbTK], int o0, int y, int ox0,
+                                         bool ok)
+{
+    constexpr int TK = kFbTK;
+    constexpr int OW = fb_ow(M);
+    float rx[TK], ry[TK];
 #pragma unroll
     for (int k = 0; k < TK; ++k) {
-        const int o = o0 + k, x = ox0 + o;
-        if (o >= OW || x >= a.w) break;
         double g11, g12, g22, h1, h2;
         if (GAUSS) {
             g11 = out[0][k];
@@ -692,16 +724,30 @@ __device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (
             h2 = out[4][k] * a.scale;
         }
         const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
-        const float fx = (float)((g11 * h2 - g12 * h1) * idet);
-        const float fy = (float)((g22 * h1 - g12 * h2) * idet);
+        rx[k] = (float)((g11 * h2 - g12 * h1) * idet);
+        ry[k] = (float)((g22 * h1 - g12 * h2) * idet);
+    }
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+        const int o = o0 + k, x = ox0 + o;
+        if (!ok || o >= OW || x >= a.w) break;
         if (a.out_il) {
-            *reinterpret_cast<float2*>(a.fout + (size_t)y * a.out_pitch + 2 * x) = make_float2(fx, fy);
+            *reinterpret_cast<float2*>(a.fout + (size_t)y * a.out_pitch + 2 * x) = make_float2(rx[k], ry[k]);
         } else {
             const size_t off = (size_t)y * a.pitch + x;
-            a.fout[off] = fx;
-            a.fout[off + a.fplane] = fy;
+            a.fout[off] = rx[k];
+            a.fout[off + a.fplane] = ry[k];
         }
     }
+}
+
+template <int M, bool GAUSS>
+__device__ __forceinline__ void fb_horizontal(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
+                                              int y, int ox0)
+{
+    float out[5][kFbTK];
+    fb_hsums<M, GAUSS>(a, vb, r, o0, out);
+    fb_solve<M, GAUSS>(a, out, o0, y, ox0, true);
 }
 
 // workgroup barrier that waits only for LDS traffic
@@ -805,8 +851,20 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
     FbRowB B[NR];
     fb_rows_a<NR>(a, rs, x, ybase, 2 * M, half, A);
     fb_rows_b<NR>(a, rs, x, ybase, 2 * M, half, A, B);
+#if TBDK_FB_DEFER
+    // the solve of batch s0's horizontal task runs at the top of the next
+    // iteration, in one basic block with the next M rows' finish (independent
+    // work the scheduler interleaves with the double-precision chain)
+    static_assert(kFbRB * ((OW + kFbTK - 1) / kFbTK) <= kFbThreads, "one horizontal task per thread and batch (TBDK_FB_RB=8 builds: TBDK_FB_DEFER=0)");
+    float pend[5][kFbTK];
+    int pend_o0 = 0, pend_y = 0;
+    bool pend_ok = false;
+#endif
     for (int s0 = 0; s0 < nrows; s0 += kFbRB) {
         fb_rows_finish<NR>(a, mr, RR, x, col, ybase, 2 * M + s0, half, A, B);
+#if TBDK_FB_DEFER
+        fb_solve<M, GAUSS>(a, pend, pend_o0, pend_y, ox0, pend_ok);
+#endif
         const bool more = s0 + kFbRB < nrows;
         if (more) fb_rows_a<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A);
         fb_lds_barrier();
@@ -848,15 +906,29 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
         if (more) fb_rows_b<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A, B);
         fb_lds_barrier();
         const int nb = min(kFbRB, nrows - s0);
+#if TBDK_FB_DEFER
+        {
+            const bool in = tid < nb * NQ;
+            const int r = in ? tid / NQ : 0, q = in ? tid - r * NQ : 0;
+            pend_ok = in && ox0 + kFbTK * q < a.w;
+            pend_o0 = kFbTK * q;
+            pend_y = y0 + s0 + r;
+            fb_hsums<M, GAUSS>(a, vb, r, pend_o0, pend);
+        }
+#else
         for (int task = tid; task < nb * NQ; task += kFbThreads) {
             const int r = task / NQ, q = task - r * NQ;
             if (ox0 + kFbTK * q < a.w) fb_horizontal<M, GAUSS>(a, vb, r, kFbTK * q, y0 + s0 + r, ox0);
         }
+#endif
         // the next batch's M rows overwrite ring rows the vertical pass read,
         // and its vertical pass vb rows this horizontal pass reads: both are
         // ordered by the two barriers above (this pass ends before the next
         // batch's first barrier)
     }
+#if TBDK_FB_DEFER
+    fb_solve<M, GAUSS>(a, pend, pend_o0, pend_y, ox0, pend_ok);
+#endif
 }
 
 template <int M>
