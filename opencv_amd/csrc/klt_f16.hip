@@ -336,8 +336,14 @@ hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, cons
 
 // ---- sparse LK on fp16 levels ------------------------------------------------
 
+// fp16 instances up to the 21x21 window: at most 128 VGPRs, so 4 waves per
+// SIMD (the compiler's own choice was 129, i.e. 3); the fp32 instances keep
+// the compiler's allocation (capping them spills)
+#ifndef TBDK_LK16_MINW
+#define TBDK_LK16_MINW 4
+#endif
 template <int WW, int WH, bool F32>
-__global__ __launch_bounds__(64) void lk_f16_kernel(LkArgs a)
+__global__ __launch_bounds__(64, (!F32 && WW <= 21) ? TBDK_LK16_MINW : 1) void lk_f16_kernel(LkArgs a)
 {
     typedef Pix<F32> PX;
     typedef typename PX::pair_t pair_t;
