@@ -140,31 +140,88 @@ def host_cores():
     return n, {"affinity_cpus": len(aff), "cgroup_cpu_quota": quota}
 
 
-def gpu_numa_cpus(local_rank: int):
-    """(numa node, cpus) of the host CPUs local to the local_rank-th visible GPU,
-    read from sysfs (KFD topology nodes, in HIP device order, and the GPU's PCI
-    device) without touching the GPU; None when the topology does not say."""
-    root = "/sys/class/kfd/kfd/topology/nodes"
-    try:
-        gpus = []
-        for n in sorted(os.listdir(root), key=int):
-            props = {}
-            for line in open(os.path.join(root, n, "properties")):
-                kv = line.split()
-                if len(kv) == 2:
+def _gpu_bdfs_kfd(sysroot: str):
+    """PCI addresses of the GPUs in HIP device order from the KFD topology
+    (nodes with SIMDs, in node order, location_id = bus << 8 | dev << 3 | fn);
+    None when a GPU node carries no location_id."""
+    root = os.path.join(sysroot, "class/kfd/kfd/topology/nodes")
+    out = []
+    for n in sorted(os.listdir(root), key=int):
+        props = {}
+        for line in open(os.path.join(root, n, "properties")):
+            kv = line.split()
+            if len(kv) == 2:
+                try:
                     props[kv[0]] = int(kv[1])
-            if props.get("simd_count", 0) > 0 and "location_id" in props:
-                gpus.append((props.get("domain", 0), props["location_id"]))
+                except ValueError:
+                    pass
+        if props.get("simd_count", 0) > 0:
+            if "location_id" not in props:
+                return None
+            dom, loc = props.get("domain", 0), props["location_id"]
+            out.append(f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}")
+    return out or None
+
+
+def _gpu_bdfs_drm(sysroot: str):
+    """Fallback: the AMD display-class PCI devices behind /sys/class/drm/card*,
+    in PCI address order (the order KFD enumerates them on a node)."""
+    root = os.path.join(sysroot, "class/drm")
+    bdfs = set()
+    for c in os.listdir(root):
+        if not c.startswith("card") or "-" in c:
+            continue
+        dev = os.path.join(root, c, "device")
+        try:
+            if open(os.path.join(dev, "vendor")).read().strip() != "0x1002":
+                continue
+            if not open(os.path.join(dev, "class")).read().strip().startswith("0x03"):
+                continue
+            bdfs.add(os.path.basename(os.path.realpath(dev)))
+        except OSError:
+            continue
+    return sorted(bdfs) or None
+
+
+def gpu_numa_cpus(local_rank: int, sysroot: str = "/sys"):
+    """(numa node, cpus, source) of the host CPUs local to the local_rank-th
+    visible GPU, from sysfs only (no GPU call, so it can run before HIP starts):
+    the GPU's PCI address from the KFD topology, else from the DRM cards; its
+    CPUs from the PCI device's local_cpulist, else its NUMA node's cpulist.
+    None when sysfs does not say."""
+    bdfs, src = None, None
+    for fn, name in ((_gpu_bdfs_kfd, "kfd"), (_gpu_bdfs_drm, "drm")):
+        try:
+            bdfs = fn(sysroot)
+        except (OSError, ValueError):
+            bdfs = None
+        if bdfs:
+            src = name
+            break
+    if not bdfs:
+        return None
+    try:
         vis = os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
         if vis:
-            gpus = [gpus[int(i)] for i in vis.split(",")]
-        dom, loc = gpus[local_rank]
-        bdf = f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}"
-        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+            bdfs = [bdfs[int(i)] for i in vis.split(",")]
+        bdf = bdfs[local_rank]
+        dev = os.path.join(sysroot, "bus/pci/devices", bdf)
+        node = -1
+        try:
+            node = int(open(os.path.join(dev, "numa_node")).read())
+        except (OSError, ValueError):
+            pass
+        try:
+            cpus = parse_cpulist(open(os.path.join(dev, "local_cpulist")).read())
+            if cpus:
+                return node, cpus, f"{src}:{bdf}:local_cpulist"
+        except (OSError, ValueError):
+            pass
         if node < 0:
             return None
-        return node, parse_cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read())
-    except (OSError, ValueError, IndexError, KeyError):
+        cpus = parse_cpulist(open(os.path.join(sysroot, f"devices/system/node/node{node}/cpulist")).read())
+        return (node, cpus, f"{src}:{bdf}:numa_node") if cpus else None
+    except (OSError, ValueError, IndexError):
         return None
 
 
@@ -175,13 +232,24 @@ def pin_rank(local_rank: int):
     Returns what was done, for the JSON line."""
     got = gpu_numa_cpus(local_rank)
     if got is None:
-        return {"pinned": False, "reason": "no NUMA information for the GPU"}
-    node, cpus = got
+        return {"pinned": False, "reason": "no NUMA / local_cpulist information for the GPU in sysfs"}
+    node, cpus, src = got
     allowed = sorted(set(cpus) & os.sched_getaffinity(0))
     if not allowed:
-        return {"pinned": False, "numa_node": node, "reason": "NUMA-local CPUs outside the affinity mask"}
+        return {"pinned": False, "numa_node": node, "source": src,
+                "reason": "GPU-local CPUs outside the affinity mask"}
+    if set(allowed) == os.sched_getaffinity(0):
+        return {"pinned": False, "numa_node": node, "source": src, "cpus": len(allowed),
+                "reason": "the affinity mask is already GPU-local"}
+    # every thread the process has so far (none is a HIP thread yet: pinning
+    # precedes the first GPU call), so later threads inherit the mask
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), allowed)
+        except OSError:
+            pass
     os.sched_setaffinity(0, allowed)
-    return {"pinned": True, "numa_node": node, "cpus": len(allowed)}
+    return {"pinned": True, "numa_node": node, "source": src, "cpus": len(allowed)}
 
 
 # ---- CPU baseline -----------------------------------------------------------------------------
@@ -540,32 +608,47 @@ def rank_env():
 _T0 = time.perf_counter()
 
 
-def hbm_copy_peak(dev, nbytes: int = 1 << 31, reps: int = 20) -> dict:
+def hbm_copy_peak(dev, ctx=None, nbytes: int = 1 << 31, reps: int = 20) -> dict:
     """an HBM roofline also against a measured stream-copy peak.
-    A device-to-device copy of a 2 GiB buffer (far beyond the L2s and the
-    256 MB Infinity Cache), read + write bytes / HIP-event time, best of
-    `reps` copies after warm-up."""
+    libtbdk's hand-written copy kernel (tbdk_hbm_copy: global_load_dwordx4 /
+    global_store_dwordx4, four 16-byte loads in flight per lane) over a 2 GiB
+    buffer (far beyond the L2s and the 256 MB Infinity Cache), read + write bytes
+    / HIP-event time (events on the launch stream), best of `reps` copies after
+    warm-up; the torch copy_ figure beside it."""
     import torch
+    from opencv_amd import klt
+
+    ctx = ctx or klt.Context.get(dev)
     src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    src.fill_(1)
+    src.copy_(torch.arange(nbytes // 4, dtype=torch.int32, device=dev).view(torch.uint8))
     dst = torch.empty_like(src)
-    for _ in range(3):
-        dst.copy_(src)
-    best = None
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        dst.copy_(src)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
-        best = ms if best is None else min(best, ms)
-    ok = bool(torch.equal(dst[:: 1 << 20], src[:: 1 << 20]))
+    stream = torch.cuda.current_stream()
+
+    def best_of(fn):
+        for _ in range(3):
+            fn()
+        best = None
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best
+
+    t_torch = best_of(lambda: dst.copy_(src))
+    dst.zero_()
+    t_k = best_of(lambda: klt.hbm_copy(dst, src, ctx=ctx, stream=stream))
+    ok = bool(torch.equal(dst, src))
     del src, dst
-    gbs = 2 * nbytes / (best / 1000.0) / 1e9
+    gbs = 2 * nbytes / (t_k / 1000.0) / 1e9
     return {"value": round(gbs, 1), "unit": "GB/s", "bytes": 2 * nbytes, "copies": reps, "checked": ok,
             "frac_of_spec": round(gbs / PEAK_HBM_GBS, 4),
-            "note": "torch device-to-device copy of a 2 GiB buffer: read + write bytes / fastest HIP-event time"}
+            "torch_copy_gbs": round(2 * nbytes / (t_torch / 1000.0) / 1e9, 1),
+            "note": "tbdk_hbm_copy (hand-written 16 B/lane stream copy) of a 2 GiB buffer: read + write bytes / "
+                    "fastest HIP-event time; torch_copy_gbs: torch copy_ of the same buffers"}
 
 
 def add_copy_peak_fracs(obj, peak_gbs: float):
@@ -972,6 +1055,7 @@ def main(argv=None):
         achieved = flops_per_launch / (lk["avg_us"] * 1e-6) / 1e12
     else:
         flops_per_launch, achieved = 0.0, 0.0
+    lk_every = kstats_aside.get("lk_sparse", {}).get("avg_us")
     # the auto choice is lk_multi_kernel (several points per wave) for the odd square windows it covers
     traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true>")  # the loop's FLY instance
     if traffic is None:
@@ -982,10 +1066,15 @@ def main(argv=None):
                 "note": "PyrLK is VALU (int16 dot2 + fp32) bound, no MFMA (no contraction on this path); peak = "
                         "fp32 vector rate; algorithmic flops per SURVEY.md §8(d) with the measured iteration "
                         f"count; launch duration = HIP events on a pseudo-random 1/{args.timing_every} of the "
-                        "launches of the timed region (avg_us_every_launch: every launch, in a separate pass); "
-                        "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch (committed PMC summary)",
+                        "launches of the timed region (avg_us_every_launch / frac_every_launch: every launch, in a "
+                        "separate pass over the same frames); traffic = raw FETCH_SIZE + WRITE_SIZE per launch "
+                        "(committed PMC summary, no x2: the kernel's global loads are 4 B per lane, the guide's x2 "
+                        "is for 16 B/lane streaming reads)",
+                "access_width": "global_load_dword (4 B/lane, u8 rows as unaligned dwords); stores 8 B/lane",
                 "avg_us_sampled": lk["avg_us"],
-                "avg_us_every_launch": kstats_aside.get("lk_sparse", {}).get("avg_us"),
+                "avg_us_every_launch": lk_every,
+                "frac_every_launch": (round(flops_per_launch / (lk_every * 1e-6) / 1e12 / PEAK_F32_TFLOPS, 4)
+                                      if lk_every else None),
                 "flops_per_launch": flops_per_launch,
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}
@@ -1062,7 +1151,7 @@ def main(argv=None):
         line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_copy_peak:
         progress("HBM copy peak")
-        line["hbm_copy_peak"] = hbm_copy_peak(dev)
+        line["hbm_copy_peak"] = hbm_copy_peak(dev, ctx)
         add_copy_peak_fracs(line, line["hbm_copy_peak"]["value"])
     if cpu_in is not None:
         progress("cpu baseline")

@@ -763,6 +763,15 @@ int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int n
                       int t0, int nframes, uint8_t* out, int pitch, int32_t* gt_boxes,
                       void* stream);
 
+/* ---- measurement ---------------------------------------------------------- */
+
+/* Copies `bytes` (a multiple of 16; dst and src 16-byte aligned, not
+ * overlapping) device to device with a hand-written 16-byte-per-lane stream
+ * copy (global_load_dwordx4 / global_store_dwordx4), asynchronously on
+ * `stream`; timed as kernel "hbm_copy".  bench.py's measured HBM copy peak
+ * (SURVEY.md §8(d)); no reference counterpart. */
+int tbdk_hbm_copy(tbdk_ctx* ctx, void* dst, const void* src, int64_t bytes, void* stream);
+
 /* Library version string */
 const char* tbdk_version(void);
 /* TBDK_ABI_VERSION of the library (struct layouts of this header) */

@@ -268,6 +268,7 @@ SIGNATURES = {
                                           C.POINTER(ScenarioMetrics)]),
     "tbdk_tbd_tracks": (C.c_int, [C.c_void_p, C.POINTER(TrackInfo), C.c_int, C.POINTER(C.c_int)]),
     "tbdk_tbd_predictions": (C.c_int, [C.c_void_p, C.POINTER(Prediction), C.c_int, C.POINTER(C.c_int)]),
+    "tbdk_hbm_copy": (C.c_int, [_P, _P, _P, C.c_int64, _P]),
     "tbdk_synth_render": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "tbdk_lk_dense": (C.c_int, [_P, C.POINTER(Pyr), C.POINTER(Pyr), _P, C.c_int, _P, C.c_int, C.POINTER(LkParams),

@@ -258,11 +258,16 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
         const int y = reflect101(py - a.pad1, a.h1);
         const int x0 = reflect101(4 * t - a.pad1, a.w1);
         uint32_t v = 0;
-        // fast path: four consecutive in-image pixels whose taps need no reflection
+        // fast path: four consecutive in-image pixels whose taps need no reflection.
+        // x0 even (the pads are multiples of 16) puts the taps' first byte c0 at
+        // offset 2 of an aligned dword, so the four aligned dwords read per row end
+        // with the dword holding byte c0 + 10 < sw: no byte past the row's last
+        // in-image dword is touched (a frame ending at its allocation's last byte
+        // with sw % 4 == 0 is safe; sw % 4 != 0 needs a dword pitch, a.vec).
         const bool fast = a.vec && 2 * y - 2 >= 0 && 2 * y + 2 < a.sh && 4 * t - a.pad1 == x0 && 2 * x0 - 2 >= 0 &&
-                          2 * x0 + 8 < a.sw && x0 + 3 < a.w1;
+                          2 * x0 + 8 < a.sw && x0 + 3 < a.w1 && (x0 & 1) == 0;
         if (fast) {
-            const int c0 = 2 * x0 - 2, base = c0 & ~3, o = c0 - base;  // o in {0, 2}
+            const int c0 = 2 * x0 - 2, base = c0 & ~3, o = 2;  // c0 - base
             int h[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < 5; ++j) {

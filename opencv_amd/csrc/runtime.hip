@@ -844,6 +844,21 @@ int tbdk_warp_affine_u8(tbdk_ctx* ctx, const uint8_t* src, int src_width, int sr
     return map_err(e);
 }
 
+int tbdk_hbm_copy(tbdk_ctx* ctx, void* dst, const void* src, int64_t bytes, void* stream)
+{
+    if (!ctx || !dst || !src || bytes < 0 || (bytes & 15) != 0 ||
+        ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0)
+        return TBDK_EINVAL;
+    const char *d = static_cast<const char*>(dst), *sp = static_cast<const char*>(src);
+    if (d < sp + bytes && sp < d + bytes && bytes > 0) return TBDK_EINVAL;  // overlapping
+    DeviceGuard g(ctx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rec = timing_begin(ctx, "hbm_copy", s);
+    hipError_t e = launch_hbm_copy(src, dst, (size_t)bytes / 16, s);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
 int tbdk_synth_render(tbdk_ctx* ctx, uint32_t seed, int width, int height, int nobj, int t0, int nframes,
                       uint8_t* out, int pitch, int32_t* gt_boxes, void* stream)
 {

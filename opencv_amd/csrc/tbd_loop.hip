@@ -24,6 +24,8 @@
 // same corners), every other refreshed set runs the post-tracker GFTT.  On
 // re-detection frames the early GFTT also runs on the box each existing track
 // will get if the tracker assigns it the detection overlapping it most.
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -119,13 +121,15 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
             }
             out[e] = o;
         }
+        // every wave that wrote a FitOut releases it at system scope itself: the
+        // workgroup barrier below orders waves only at workgroup scope, and thread
+        // 0's release waits only for its own wave's stores
+        if (flag) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (flag) {
-        // publish: after the workgroup's barrier one thread releases the
-        // workgroup's results (pinned host memory) at system scope and counts
-        // them (one release per workgroup, not per wave); the last workgroup
-        // resets the count for the next launch (stream-ordered) and raises the
-        // frame's tag
+        // publish: after the workgroup's barrier one thread counts the
+        // workgroup's results at system scope; the last workgroup resets the
+        // count for the next launch (stream-ordered) and raises the frame's tag
         __syncthreads();
         if (threadIdx.x == 0) {
             const int first = blockIdx.x * kFitWaves;
@@ -775,14 +779,23 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         // that long is not the per-frame case, and a blocking wait then costs
         // nothing that matters.  One host core per loop while it spins
         // (threading).
-        constexpr double kSpinUs = 2000.0;
+        // Past kYieldUs (several times a frame's fit wait) each poll gives the
+        // core away once (sched_yield), so ranks sharing a host's cores (8 GPUs,
+        // a CPU share each) do not starve each other's tracker threads.
+        constexpr double kSpinUs = 2000.0, kYieldUs = 300.0;
+        auto pause_or_yield = [&](double us) {
+            if (us > kYieldUs) sched_yield();
+            else
+                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+        };
         if (by_flag) {
             // the fit's flag; past kSpinUs the stream is synchronized (it holds
             // the fit, then the next pyramid) and the flag read once more
             e = hipSuccess;
             while (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) != tag) {
-                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
-                if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
+                const double us = std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
+                pause_or_yield(us);
+                if (us > kSpinUs) {
                     e = hipStreamSynchronize(s);
                     if (e == hipSuccess && __atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) != tag) e = hipErrorUnknown;
                     break;
@@ -790,8 +803,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             }
         } else {
             while ((e = hipEventQuery(t->fit_done)) == hipErrorNotReady) {
-                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
-                if (std::chrono::duration<double, std::micro>(clk::now() - ts0).count() > kSpinUs) {
+                const double us = std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
+                pause_or_yield(us);
+                if (us > kSpinUs) {
                     e = hipEventSynchronize(t->fit_done);
                     break;
                 }
@@ -886,6 +900,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
     } else {
         if (next) {
+            // the next pyramid is rebuilt over the previous frame's, which the
+            // previous step's look-ahead PyrLK (on la_s) may still be reading
+            if (had_la_lk) {
+                hipError_t e = hipStreamWaitEvent(s, t->la_done, 0);
+                if (e != hipSuccess) return map_status(e);
+            }
             rc = enqueue_next_pyr();
             if (rc != TBDK_OK) return rc;
         }

@@ -196,6 +196,7 @@ hipError_t launch_warp_affine(const uint8_t* src, int sw, int sh, int spitch, ui
 
 // ---- synthetic renderer (synth.hip) ----
 struct SynPoseDev;  // == syn_pose
+hipError_t launch_hbm_copy(const void* src, void* dst, size_t n16, hipStream_t s);
 hipError_t launch_synth(const void* poses_dev, int nobj, uint32_t bgseed, int W, int H, int nframes,
                         uint8_t* out, int pitch, hipStream_t s);
 

@@ -475,6 +475,20 @@ class GoodFeaturesToTrackDetector:
         return c[0, :k]
 
 
+def hbm_copy(dst: torch.Tensor, src: torch.Tensor, ctx: Context | None = None, stream=None):
+    """dst <- src (contiguous device tensors of equal byte size, a multiple of
+    16) through libtbdk's 16-byte-per-lane stream-copy kernel (tbdk_hbm_copy;
+    bench.py's HBM copy peak)."""
+    nbytes = src.numel() * src.element_size()
+    if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()) or \
+            dst.numel() * dst.element_size() != nbytes:
+        raise ValueError("hbm_copy: contiguous device tensors of equal byte size")
+    ctx = ctx or Context.get(src.device.index)
+    _lib.check(ctx.lib.tbdk_hbm_copy(ctx.handle, C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), nbytes,
+                                     _stream_ptr(stream)), "tbdk_hbm_copy")
+    return dst
+
+
 def synth_render(seed: int, width: int, height: int, nobj: int, t0: int, nframes: int, device: int = 0,
                  ctx: Context | None = None, stream=None):
     """Render frames [t0, t0+nframes) of the synthetic sequence into HBM.

@@ -211,11 +211,35 @@ typedef struct orc_job {
     uint8_t* status;
     float* err;
     int32_t* iters;
+    float* gate;         /* optional: per point, the smallest relative margin of any gate evaluated */
     const orc_lk_params* prm;
     int level, maxLevel, maxCount;
     double eps2;
     int begin, end;
 } orc_job;
+
+/* Diagnostics for the tolerance clause of SURVEY.md §8(c) ("any status
+ * disagreement must lie within 1e-3 (relative) of the minEig/bounds
+ * thresholds"): how close a gate's operand came to its threshold, relative to
+ * the threshold.  The bounds gates floor(x) < -win / floor(x) >= cols are
+ * x < -win / x >= cols on the float coordinate. */
+static void orc_gate_note(const orc_job* jb, int ptidx, float m)
+{
+    if (jb->gate && m < jb->gate[ptidx]) jb->gate[ptidx] = m;
+}
+
+static void orc_gate_bounds(const orc_job* jb, int ptidx, float x, float y, int winW, int winH, int cols, int rows)
+{
+    if (!jb->gate) return;
+    float m = fabsf(x + (float)winW) / (float)winW;
+    float t = fabsf(x - (float)cols) / (float)cols;
+    if (t < m) m = t;
+    t = fabsf(y + (float)winH) / (float)winH;
+    if (t < m) m = t;
+    t = fabsf(y - (float)rows) / (float)rows;
+    if (t < m) m = t;
+    orc_gate_note(jb, ptidx, m);
+}
 
 static const uint8_t* orc_px(const orc_plane* p, int x, int y, int cn)
 {
@@ -258,6 +282,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     prevx -= halfx;
     prevy -= halfy;
     int ipx = orc_floor(prevx), ipy = orc_floor(prevy);
+    orc_gate_bounds(jb, ptidx, prevx, prevy, winW, winH, Icols, Irows);
     if (ipx < -winW || ipx >= Icols || ipy < -winH || ipy >= Irows) {
         if (level == 0) {
             jb->status[ptidx] = 0;
@@ -340,6 +365,8 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
                    (float)(2 * winW * winH);
     if (jb->err && (prm->flags & ORC_OPTFLOW_LK_GET_MIN_EIGENVALS) != 0) jb->err[ptidx] = minEig;
+    if (prm->minEigThreshold > 0) orc_gate_note(jb, ptidx, fabsf(minEig - prm->minEigThreshold) / prm->minEigThreshold);
+    orc_gate_note(jb, ptidx, fabsf(D - FLT_EPSILON) / FLT_EPSILON);
     if (minEig < prm->minEigThreshold || D < FLT_EPSILON) {
         if (level == 0) jb->status[ptidx] = 0;
         return;
@@ -352,6 +379,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     int nit = 0;
     for (int j = 0; j < jb->maxCount; ++j) {
         int inx = orc_floor(nextx), iny = orc_floor(nexty);
+        orc_gate_bounds(jb, ptidx, nextx, nexty, winW, winH, Jcols, Jrows);
         if (inx < -winW || inx >= Jcols || iny < -winH || iny >= Jrows) {
             if (level == 0) jb->status[ptidx] = 0;
             break;
@@ -435,6 +463,7 @@ static void orc_lk_point(const orc_job* jb, int ptidx, int16_t* Iwin, int16_t* d
     if (jb->status[ptidx] && jb->err && level == 0 && (prm->flags & ORC_OPTFLOW_LK_GET_MIN_EIGENVALS) == 0) {
         float npx = jb->nextPts[2 * ptidx] - halfx, npy = jb->nextPts[2 * ptidx + 1] - halfy;
         int inx = orc_floor(npx), iny = orc_floor(npy);
+        orc_gate_bounds(jb, ptidx, npx, npy, winW, winH, Jcols, Jrows);
         if (inx < -winW || inx >= Jcols || iny < -winH || iny >= Jrows) {
             jb->status[ptidx] = 0;
             return;
@@ -474,6 +503,13 @@ int orc_lk(const orc_pyr* prev, const orc_pyr* next,
            const float* prevPts, float* nextPts, uint8_t* status, float* err,
            int npoints, const orc_lk_params* prm, int32_t* iters)
 {
+    return orc_lk_gate(prev, next, prevPts, nextPts, status, err, npoints, prm, iters, NULL);
+}
+
+int orc_lk_gate(const orc_pyr* prev, const orc_pyr* next,
+                const float* prevPts, float* nextPts, uint8_t* status, float* err,
+                int npoints, const orc_lk_params* prm, int32_t* iters, float* gate)
+{
     if (npoints <= 0) return 0;
     if (prm->winW < 3 || prm->winH < 3 || prm->winW > 64 || prm->winH > 64) return -1;
     if (prev->lv[0].cn > 4) return -1;
@@ -484,6 +520,8 @@ int orc_lk(const orc_pyr* prev, const orc_pyr* next,
     double eps = prm->epsilon < 0. ? 0. : (prm->epsilon > 10. ? 10. : prm->epsilon);
     for (int i = 0; i < npoints; ++i) status[i] = 1;
     if (iters) memset(iters, 0, sizeof(int32_t) * (size_t)npoints);
+    if (gate)
+        for (int i = 0; i < npoints; ++i) gate[i] = FLT_MAX;
     int nth = prm->nthreads > 0 ? prm->nthreads : 1;
     if (nth > npoints) nth = npoints;
 
@@ -508,6 +546,7 @@ int orc_lk(const orc_pyr* prev, const orc_pyr* next,
             jb->status = status;
             jb->err = err;
             jb->iters = iters;
+            jb->gate = gate;
             jb->prm = prm;
             jb->level = level;
             jb->maxLevel = maxLevel;
@@ -549,6 +588,7 @@ int orc_synth_frames(uint32_t seed, int W, int H, int nobj, int t0, int nframes,
                 if (!g[0]) g[1] = g[2] = g[3] = g[4] = 0;
             }
         }
+        if (!out) continue; /* ground truth only */
         uint8_t* img = out + (size_t)f * pitch * H;
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) img[(size_t)y * pitch + x] = (uint8_t)syn_background(x, y, bgseed);

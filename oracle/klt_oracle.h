@@ -86,8 +86,15 @@ typedef struct orc_lk_params {
 int  orc_lk(const orc_pyr* prev, const orc_pyr* next,
             const float* prevPts, float* nextPts, uint8_t* status, float* err,
             int npoints, const orc_lk_params* prm, int32_t* iters);
+/* the same, and per point (gate, optional) the smallest relative margin of
+ * any minEig / determinant / bounds gate it evaluated at any level:
+ * |v - thr| / |thr| (test diagnostics for SURVEY.md §8(c)) */
+int  orc_lk_gate(const orc_pyr* prev, const orc_pyr* next,
+                 const float* prevPts, float* nextPts, uint8_t* status, float* err,
+                 int npoints, const orc_lk_params* prm, int32_t* iters, float* gate);
 
-/* synthetic sequence (opencv_amd/csrc/synth_spec.h) rendered on the CPU */
+/* synthetic sequence (opencv_amd/csrc/synth_spec.h) rendered on the CPU
+ * (out NULL: the ground-truth boxes only) */
 int  orc_synth_frames(uint32_t seed, int W, int H, int nobj, int t0, int nframes,
                       uint8_t* out, int pitch, int32_t* gt_boxes /* nframes*nobj*5 or NULL */);
 

@@ -60,10 +60,14 @@ class KltTbdLoop:
     def __init__(self, width, height, win=21, max_level=2, lk_iters=30, lk_epsilon=0.01, min_eig=1e-4,
                  max_corners=256, quality=0.01, min_distance=3.0, redetect_every=5, min_points=32,
                  min_fit_points=4, bounds=(0, 1280, 0, 720), max_tracks=1024, accum=None, nthreads=16,
-                 tracker=None, gftt_pool=None, **tracker_args):
+                 tracker=None, gftt_pool=None, shadow_accum=None, **tracker_args):
         """tracker: an object with tbd_oracle.Tracker's step / tracks / metric lists
         (default: tbd_oracle.Tracker); gftt_pool: an executor running the ROIs'
-        goodFeaturesToTrack calls concurrently (default: one after another)."""
+        goodFeaturesToTrack calls concurrently (default: one after another);
+        shadow_accum: also run every frame's PyrLK call on the same inputs in this
+        accumulation order (it drives nothing) and keep both calls' outputs and
+        gate margins in self.shadow (SURVEY.md §8(c)'s per-call tolerance along
+        the loop's own trajectory)."""
         self.W, self.H = width, height
         self.win, self.ml, self.iters, self.eps, self.min_eig = win, max_level, lk_iters, lk_epsilon, min_eig
         self.max_corners, self.quality, self.min_distance = max_corners, quality, min_distance
@@ -80,6 +84,8 @@ class KltTbdLoop:
         heapq.heapify(self.free)
         self.preds = {}
         self.metrics = {}
+        self.shadow_accum = shadow_accum
+        self.shadow = None
 
     def _klt(self, P):
         """Steps 2-3 for every slotted track, in the tracker's order."""
@@ -87,8 +93,14 @@ class KltTbdLoop:
         counts = [len(self.sets.get(i, ())) for i in ids]
         pts = np.concatenate([self.sets[i] for i in ids if len(self.sets.get(i, ()))]) if sum(counts) else \
             np.zeros((0, 2), np.float32)
+        gate = np.empty(len(pts), np.float32) if self.shadow_accum is not None else None
         nxt, st, _, _ = O.lk(self.prev, P, pts, (self.win, self.win), self.ml, self.iters, self.eps, 0,
-                             self.min_eig, self.accum, self.nthreads, want_err=False)
+                             self.min_eig, self.accum, self.nthreads, want_err=False, gate=gate)
+        if self.shadow_accum is not None:
+            sgate = np.empty(len(pts), np.float32)
+            snxt, sst, _, _ = O.lk(self.prev, P, pts, (self.win, self.win), self.ml, self.iters, self.eps, 0,
+                                   self.min_eig, self.shadow_accum, self.nthreads, want_err=False, gate=sgate)
+            self.shadow = dict(nxt=nxt, st=st, gate=gate, s_nxt=snxt, s_st=sst, s_gate=sgate)
         preds, off, tracked = {}, 0, 0
         boxes = {t.id: t.bboxes[-1] for t in self.tracker.tracks}
         for i, n in zip(ids, counts):
@@ -112,6 +124,7 @@ class KltTbdLoop:
         """dets: tbd_oracle.Detection list of this frame."""
         P = O.Pyramid(frame, (self.win, self.win), self.ml)
         preds, lk_points, tracked = {}, 0, 0
+        self.shadow = None
         if self.prev is not None and self.tracker.tracks:
             preds, lk_points, tracked = self._klt(P)
         before = {t.id for t in self.tracker.tracks}

@@ -61,6 +61,9 @@ def load():
     lib.orc_lk.restype = C.c_int
     lib.orc_lk.argtypes = [C.POINTER(OPyr), C.POINTER(OPyr), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                            C.POINTER(LkParams), C.c_void_p]
+    lib.orc_lk_gate.restype = C.c_int
+    lib.orc_lk_gate.argtypes = [C.POINTER(OPyr), C.POINTER(OPyr), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.c_int, C.POINTER(LkParams), C.c_void_p, C.c_void_p]
     lib.orc_synth_frames.restype = C.c_int
     lib.orc_synth_frames.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                      C.c_void_p]
@@ -125,9 +128,13 @@ def scharr(img: np.ndarray) -> np.ndarray:
 
 
 def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01, flags=0,
-       min_eig=1e-4, accum=ACCUM_SSE2, nthreads=8, init: np.ndarray | None = None, want_err: bool = True):
+       min_eig=1e-4, accum=ACCUM_SSE2, nthreads=8, init: np.ndarray | None = None, want_err: bool = True,
+       gate: np.ndarray | None = None):
     """calcOpticalFlowPyrLK; want_err=False passes err = noArray(), which also
-    skips the level-0 error pass and its bounds check (lkpyramid.cpp:654-693)."""
+    skips the level-0 error pass and its bounds check (lkpyramid.cpp:654-693).
+    gate: optional float32 (n,) out, per point the smallest relative margin
+    |v - thr| / |thr| of any minEig / determinant / bounds gate evaluated
+    (orc_lk_gate; SURVEY.md §8(c)'s threshold clause)."""
     lib = load()
     pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 2)
     n = pts.shape[0]
@@ -137,8 +144,13 @@ def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, 
     iters = np.zeros(n, dtype=np.int32)
     prm = LkParams(win[0], win[1], max_level, max_count, eps, flags, min_eig, accum, nthreads)
     if n:
-        lib.orc_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status),
-                   _ptr(err) if want_err else None, n, C.byref(prm), _ptr(iters))
+        if gate is not None:
+            assert gate.dtype == np.float32 and gate.flags.c_contiguous and gate.shape == (n,)
+            lib.orc_lk_gate(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status),
+                            _ptr(err) if want_err else None, n, C.byref(prm), _ptr(iters), _ptr(gate))
+        else:
+            lib.orc_lk(C.byref(prev.p), C.byref(nxt.p), _ptr(pts), _ptr(nxt_pts), _ptr(status),
+                       _ptr(err) if want_err else None, n, C.byref(prm), _ptr(iters))
     return nxt_pts, status, err, iters
 
 
@@ -256,6 +268,15 @@ def synth(seed: int, W: int, H: int, nobj: int, t0: int, nframes: int):
     rc = lib.orc_synth_frames(seed, W, H, nobj, t0, nframes, _ptr(out), W, _ptr(gt))
     assert rc == 0
     return out, gt[:, :nobj]
+
+
+def synth_gt(seed: int, W: int, H: int, nobj: int, t0: int, nframes: int):
+    """the sequence's ground-truth boxes (nframes, nobj, 5) without rendering frames"""
+    lib = load()
+    gt = np.zeros((nframes, max(nobj, 1), 5), dtype=np.int32)
+    rc = lib.orc_synth_frames(seed, W, H, nobj, t0, nframes, None, W, _ptr(gt))
+    assert rc == 0
+    return gt[:, :nobj]
 
 
 def read_png_gray(path: str) -> np.ndarray:

@@ -156,3 +156,61 @@ def test_copy_peak_fractions_on_hbm_rooflines_only():
     assert line["roofline_pyramid"]["frac_copy_peak"] == 0.08
     assert line["farneback"]["roofline"]["frac_copy_peak"] == 0.4
     assert line["farneback"]["roofline"]["copy_peak"] == 5000.0
+
+
+def _fake_sysfs(root, kfd_location=True):
+    """Two GPUs on PCI 0000:c1:00.0 (NUMA node 1, CPUs 16-31) and
+    0000:05:00.0 (node 0, CPUs 0-15 by local_cpulist) plus a CPU KFD node; KFD
+    lists them in the order c1, 05 (not PCI order)."""
+    import pathlib
+
+    r = pathlib.Path(root)
+    gpus = [("0000:c1:00.0", 0xC100, 1, None), ("0000:05:00.0", 0x0500, 0, "0-15")]
+    kfd = r / "class/kfd/kfd/topology/nodes"
+    (kfd / "0").mkdir(parents=True)
+    (kfd / "0/properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for i, (bdf, loc, node, local) in enumerate(gpus, 1):
+        (kfd / str(i)).mkdir()
+        (kfd / f"{i}/properties").write_text(
+            f"simd_count 1024\ndomain 0\n" + (f"location_id {loc}\n" if kfd_location else "") + "gfx_target_version 90500\n")
+        d = r / "bus/pci/devices" / bdf
+        d.mkdir(parents=True)
+        (d / "numa_node").write_text(f"{node}\n")
+        (d / "vendor").write_text("0x1002\n")
+        (d / "class").write_text("0x038000\n")
+        if local:
+            (d / "local_cpulist").write_text(local + "\n")
+        card = r / f"class/drm/card{i - 1}"
+        card.mkdir(parents=True)
+        (card / "device").symlink_to(d)
+        (r / f"class/drm/card{i - 1}-DP-1").mkdir()
+    nd = r / "devices/system/node"
+    (nd / "node0").mkdir(parents=True)
+    (nd / "node0/cpulist").write_text("0-15,64-79\n")
+    (nd / "node1").mkdir()
+    (nd / "node1/cpulist").write_text("16-31\n")
+
+
+def test_gpu_numa_cpus_fake_sysfs(tmp_path, monkeypatch):
+    """bench.gpu_numa_cpus over a fake sysfs tree: the KFD order with
+    location_id; without it the DRM cards in PCI order; the PCI device's
+    local_cpulist before its NUMA node's cpulist; ROCR_VISIBLE_DEVICES
+    remapping; nothing when sysfs has neither"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    a = tmp_path / "a"
+    _fake_sysfs(a)
+    assert bench.gpu_numa_cpus(0, str(a)) == (1, list(range(16, 32)), "kfd:0000:c1:00.0:numa_node")
+    assert bench.gpu_numa_cpus(1, str(a)) == (0, list(range(16)), "kfd:0000:05:00.0:local_cpulist")
+    assert bench.gpu_numa_cpus(2, str(a)) is None
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    assert bench.gpu_numa_cpus(0, str(a))[2] == "kfd:0000:05:00.0:local_cpulist"
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    b = tmp_path / "b"
+    _fake_sysfs(b, kfd_location=False)
+    assert bench.gpu_numa_cpus(0, str(b)) == (0, list(range(16)), "drm:0000:05:00.0:local_cpulist")
+    assert bench.gpu_numa_cpus(1, str(b)) == (1, list(range(16, 32)), "drm:0000:c1:00.0:numa_node")
+    assert bench.gpu_numa_cpus(0, str(tmp_path / "empty")) is None

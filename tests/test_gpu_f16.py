@@ -10,7 +10,11 @@ one fixed operation order).  Bars:
     min-eigenvalue output, points outside the image);
   * the fp16 path against the 8-bit path on the same frames (different
     arithmetic): >= 99 % of points tracked by both within 1e-2 px, status
-    agreement >= 99.5 % — at 640x480 and at BASELINE configs[4]'s 4K size.
+    agreement >= 99.5 % — at 640x480 and at BASELINE configs[4]'s 4K size;
+  * BASELINE configs[4] itself (3840x2160, 512 objects x 256 points, the
+    bench's lk_f16 leg): both fp16 pyramids bit-exact, and the GPU's LK over
+    all 131k points bit-exact vs the oracle on a seeded 8192-point sample
+    (every point's result depends only on its own inputs).
 """
 import ctypes as C
 
@@ -177,6 +181,29 @@ def test_f16_vs_u8_path_4k(gpu):
     """BASELINE configs[4] shape: 3840x2160, 512 objects x 256 points, 3 levels"""
     n, d = compare_with_u8_path(gpu, 3840, 2160, 512, 256, 2)
     assert n > 100000
+
+
+def test_f16_4k_bit_exact_sample(gpu):
+    """configs[4]: 4K, 512 objects x 256 points (131,072), 3 levels (max_level 2 as the
+    bench's lk_f16 leg); pyramids whole, LK on a seeded 8192-point sample"""
+    W, H, nobj = 3840, 2160, 512
+    frames, gt = K().synth_render(20261015, W, H, nobj, 0, 2, ctx=gpu)
+    pts = box_points(gt[0].numpy(), 256)
+    assert len(pts) == nobj * 256
+    P0 = K().build_pyramid(frames[0], (21, 21), 2, ctx=gpu, dtype=torch.float16)
+    P1 = K().build_pyramid(frames[1], (21, 21), 2, ctx=gpu, dtype=torch.float16)
+    got = run_gpu_lk(gpu, P0, P1, pts, (21, 21), 2)
+    f = frames.cpu().numpy()
+    R0, R1 = O.Pyramid16(f[0], (21, 21), 2), O.Pyramid16(f[1], (21, 21), 2)
+    for P, R in ((P0, R0), (P1, R1)):
+        assert P.nlevels == R.nlevels == 3
+        for i in range(3):
+            assert np.array_equal(P.level(i).view(np.uint16), R.levels[i].view(np.uint16)), f"level {i}"
+            assert np.array_equal(P.deriv(i).view(np.uint16), R.derivs[i].view(np.uint16)), f"deriv {i}"
+    idx = np.sort(np.random.default_rng(4).choice(len(pts), 8192, replace=False))
+    ref = O.lk16(R0, R1, pts[idx], (21, 21), 2, nthreads=16)
+    assert_same(tuple(a[idx] for a in got), ref, "4K sample")
+    assert got[1].mean() > 0.9
 
 
 def test_f16_argument_checks(gpu):

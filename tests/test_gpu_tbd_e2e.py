@@ -21,9 +21,29 @@ and tbdk_tbd_run's per-frame metrics equal the frame-by-frame ones.
 Configurations: BASELINE configs[2] (1920x1080, 128 objects, the reference's
 hard-coded 1280x720 bounds filter) and configs[3] (KITTI 1242x375, its 8
 sequences seeds s..s+7).  16 / 12 frames cover three / two re-detection
-frames (0, 5, 10, 15)."""
+frames (0, 5, 10, 15).
+
+configs[2] at its full length (500 frames, seed 20261015) is compared twice
+(test_tbd_loop_full_sequence_and_reference_order), with the two oracle
+pipelines running in CPU worker processes beside the GPU loop
+(tests/_loop_worker.py):
+  * the exact-order pipeline: every frame equal as above (bit-exact);
+  * the reference's SSE2 accumulation order (video/src/lkpyramid.cpp:278-316,
+    422-440, 507-534, 619-633), as an independent loop driving itself: per
+    frame TP/FN/FP/GT and every track's predPosition (the cvRound-ed Rect of
+    tbd.cpp:288-304) against the GPU's.  Stated tolerance: predPosition equal
+    on >= 99.5 % of track-frames, TP/FN/FP equal on >= 99 % of frames
+    (measured, profiles/r04_loop_divergence_cpu.json: 1 track-frame of
+    64,000 differs, at frame 478; every frame's metrics and boxes equal);
+  * every PyrLK call of the exact-order loop re-run in SSE2 order on the same
+    inputs: >= 99.5 % within 1e-2 px, status agreement
+    >= 99.5 %, every status disagreement within 1e-3 (relative) of a
+    minEig / bounds threshold."""
+import json
 import os
+import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -32,6 +52,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import tbd_loop_oracle as L  # noqa: E402
+import _loop_compare as LC  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -109,3 +130,97 @@ def test_tbd_loop_equals_oracle_pipeline_1080p_long(gpu):
     s = run_pair(gpu, 1920, 1080, 128, 64, SEED + 7, 0.05)
     assert s["preds"] > 63 * 100
     assert s["refreshed"] > 13 * 100
+
+
+def _host_cores():
+    """CPUs this process may use (affinity, capped by a cgroup v2 quota: the GPU
+    box grants each GPU a share of a larger host)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def test_tbd_loop_full_sequence_and_reference_order(gpu, tmp_path):
+    """configs[2] at full length: 1920x1080 x 128 objects x 500 frames (seed
+    20261015, 100 re-detection frames), the GPU loop against the exact-order
+    oracle pipeline every frame, and against the reference's SSE2 order within
+    the stated loop-level and per-call tolerances (module docstring)"""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 1920, 1080, 128, 500
+    frames, gt = klt.synth_render(SEED, W, H, N, 0, F, ctx=gpu)
+    host = frames.cpu().numpy()
+    ogt = L.O.synth_gt(SEED, W, H, N, 0, F)
+    assert np.array_equal(gt.numpy(), ogt)
+    for f0 in (0, 251, 499):  # the workers take the GPU-rendered frames: they are the generator's
+        assert np.array_equal(host[f0], L.O.synth(SEED, W, H, N, f0, 1)[0][0]), f"frame {f0}"
+    fpath = str(tmp_path / "frames.npy")
+    np.save(fpath, host)
+    del host
+    cores = _host_cores()
+    ta = max(1, cores * 5 // 8)
+    tb = max(1, cores - ta)
+    worker = os.path.join(ROOT, "tests", "_loop_worker.py")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")  # CPU only
+    outs = {k: str(tmp_path / f"{k}.json") for k in ("exact", "sse2")}
+    procs = [subprocess.Popen([sys.executable, worker, str(W), str(H), str(N), str(F), str(SEED), k,
+                               "1" if k == "exact" else "0", str(th), outs[k], fpath], env=env)
+             for k, th in (("exact", ta), ("sse2", tb))]
+    try:
+        cfg = tbd.default_config(W, H)
+        loop = tbd.TbdLoop(cfg, ctx=gpu)
+        dets = [tbd.detections_from_gt(ogt[f]) for f in range(F)]
+        gm, grows, gpreds = [], [], []
+        for f in range(F):
+            m = loop.step(frames[f], f, dets[f], next_frame=frames[f + 1] if f + 1 < F else None)
+            gm.append({k: getattr(m, k) for k in METRIC_KEYS})
+            grows.append(_gpu_rows(loop.tracks()))
+            gpreds.append(loop.predictions())
+        batch = tbd.TbdLoop(cfg, ctx=gpu)  # the native frame loop over the same frames: the same metrics
+        ms = batch.run([frames[f] for f in range(F)], 0, dets)
+        assert [{k: getattr(m, k) for k in METRIC_KEYS} for m in ms] == gm
+        assert _gpu_rows(batch.tracks()) == grows[-1]
+        torch.cuda.synchronize()
+        del frames, batch, loop
+        t0 = time.time()
+        for p in procs:
+            p.wait(timeout=max(1.0, 900 - (time.time() - t0)))
+            assert p.returncode == 0, "oracle worker failed"
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    ex, ss = (json.load(open(outs[k])) for k in ("exact", "sse2"))
+    # the exact-order pipeline: every frame, bit-exact bookkeeping
+    for f in range(F):
+        assert gm[f] == ex["metrics"][f], f"frame {f}: metrics {gm[f]} vs oracle {ex['metrics'][f]}"
+        assert grows[f] == [tuple(r) for r in ex["rows"][f]], f"frame {f}: tracks differ"
+        op = {int(k): v for k, v in ex["preds"][f].items()}
+        assert gpreds[f].keys() == op.keys(), f"frame {f}: predicted tracks differ"
+        for k, (cx, cy) in gpreds[f].items():
+            assert max(abs(cx - op[k][0]), abs(cy - op[k][1])) <= 1e-4, f"frame {f} track {k}"
+    assert sum(m["redetected"] for m in gm) > 100 * 100 and sum(m["klt_predicted"] for m in gm) > 450 * 100
+    # the reference's SSE2 order, an independent loop
+    ls = LC.LoopStats()
+    for f in range(F):
+        ls.add(f, gm[f], ss["metrics"][f], grows[f], ss["rows"][f])
+    loop_sum = ls.summary()
+    call_sum = ex["shadow"]
+    report = {"config": {"width": W, "height": H, "objects": N, "frames": F, "seed": SEED,
+                         "oracle_threads": [ta, tb]},
+              "gpu_vs_sse2_loop": loop_sum, "per_call_exact_vs_sse2": call_sum}
+    out_dir = os.environ.get("GRAFT_REPO_ROOT")
+    if out_dir:  # the figures back from the GPU box (gpurun merges gpurun_out/)
+        os.makedirs(os.path.join(out_dir, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(out_dir, "gpurun_out", "loop_divergence_gpu.json"), "w") as fh:
+            json.dump(report, fh, indent=1)
+    assert loop_sum["frac_track_frames_pred_equal"] >= 0.995, report
+    assert loop_sum["frac_frames_tp_fn_fp_equal"] >= 0.99, report
+    assert call_sum["status_agree"] >= 0.995 and call_sum["frac_within_1e2"] >= 0.995, report
+    assert call_sum["status_disagree"] == 0 or call_sum["worst_disagreement_gate_margin"] <= 1e-3, report

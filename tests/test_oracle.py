@@ -168,6 +168,43 @@ def test_lk_sse2_vs_exact_accumulation_close():
     assert (d <= 1e-2).mean() >= 0.995
 
 
+def test_lk_gate_margins_and_threshold_clause():
+    """orc_lk_gate's margins (every status disagreement between
+    the two accumulation orders must lie within 1e-3 relative of a minEig /
+    bounds threshold).  A point whose minEig IS the threshold has margin 0; a
+    point far inside the frame with a strong texture has a large one; a point
+    whose window walks off the frame has its bounds margin; over 1080p points
+    every SSE2-vs-exact status disagreement sits at a threshold, including when
+    the threshold is placed at the points' own minimum eigenvalues."""
+    fr, _ = O.synth(20261015, 640, 480, 32, 0, 2)
+    P0, P1 = O.Pyramid(fr[0], (21, 21), 0), O.Pyramid(fr[1], (21, 21), 0)
+    pts = grid_points(480, 640, 16, 40)
+    _, _, me, _ = O.lk(P0, P1, pts, max_level=0, flags=8, accum=O.ACCUM_EXACT)  # level-0 minEig per point
+    i = int(np.argsort(me)[len(me) // 2])
+    g = np.empty(len(pts), np.float32)
+    _, st, _, _ = O.lk(P0, P1, pts, max_level=0, min_eig=float(me[i]), accum=O.ACCUM_EXACT, want_err=False, gate=g)
+    assert g[i] == 0.0 and st[i] == 1  # minEig == threshold passes (the gate is minEig < threshold)
+    assert (g[me > 2 * me[i]] > 0.01).all()  # 40 px inside the frame, minEig far from the threshold
+    # window origins (point - 10) just inside x >= -21, at x == cols, just inside y < rows
+    edge = np.float32([[-10.99, 100.0], [650.0, 200.0], [320.0, 489.995]])
+    ge = np.empty(3, np.float32)
+    _, st, _, _ = O.lk(P0, P1, edge, max_level=0, accum=O.ACCUM_EXACT, want_err=False, gate=ge)
+    assert st[1] == 0 and ge[1] == 0.0 and (ge <= 1e-3).all()
+    # the clause itself, at the 1080p loop's shape and with thresholds put among the points' minEig values
+    fr, _ = O.synth(20261015, 1920, 1080, 128, 0, 2)
+    A, B = O.Pyramid(fr[0], (21, 21), 2), O.Pyramid(fr[1], (21, 21), 2)
+    rng = np.random.default_rng(1)
+    pts = np.stack([rng.uniform(0, 1920, 8192), rng.uniform(0, 1080, 8192)], 1).astype(np.float32)
+    _, _, me, _ = O.lk(A, B, pts, max_level=0, flags=8, accum=O.ACCUM_EXACT)
+    for thr in (1e-4, float(np.quantile(me, 0.3)), float(np.quantile(me, 0.5))):
+        ga, gb = np.empty(len(pts), np.float32), np.empty(len(pts), np.float32)
+        a = O.lk(A, B, pts, max_level=2, min_eig=thr, accum=O.ACCUM_EXACT, want_err=False, gate=ga)
+        b = O.lk(A, B, pts, max_level=2, min_eig=thr, accum=O.ACCUM_SSE2, want_err=False, gate=gb)
+        dis = a[1] != b[1]
+        assert dis.mean() <= 0.005
+        assert (np.minimum(ga, gb)[dis] <= 1e-3).all()
+
+
 def test_lk_edge_cases():
     fr, _ = O.synth(5, 160, 120, 4, 0, 2)
     P0, P1 = O.Pyramid(fr[0]), O.Pyramid(fr[1])
