@@ -176,6 +176,14 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 #ifndef TBDK_LK_MULTI_WAVES
 #define TBDK_LK_MULTI_WAVES 1
 #endif
+// The interpolated (Ix, Iy) row pairs of the level (constant through its Newton
+// steps) kept in LDS instead of VGPRs (1): the level setup writes them once, each
+// step reads them back (one ds_read_b64 per row pair), so the kernel's register
+// peak drops by 2 * NP VGPRs and more waves fit per SIMD (tuning builds: 0 keeps
+// them in VGPRs)
+#ifndef TBDK_LK_GLDS
+#define TBDK_LK_GLDS 0
+#endif
 constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 
 #ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
@@ -194,7 +202,11 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
     constexpr int IM = FLY ? TBDK_LK_IPACK_FLY : TBDK_LK_IPACK;
     constexpr bool IPACK = IM == 1, ILIN = IM == 2;
+    constexpr bool GL = TBDK_LK_GLDS != 0;
+    // GL: this wave's (Ix, Iy) row pairs, [row pair][lane] (8 B per lane: b64 accesses)
+    __shared__ uint2 sg[GL ? NP * kMultiWaves : 1][64];
     const int lane = threadIdx.x & 63;
+    uint2(*const sgw)[64] = &sg[GL ? (threadIdx.x >> 6) * NP : 0];
     // point k of the wave owns lanes [1 + k*WW, 1 + (k+1)*WW); lane 0 (and any
     // lane past the last point) is idle with k == P and contributes 0
     const int k = lane == 0 ? P : (lane - 1) / WW;
@@ -305,6 +317,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 const int y1 = two ? bilin_s<0>(dy1, dy2, dw2, dw3, rnd14) : 0;
                 gxk[q] = pack_shr<W_BITS1>(x0, x1);
                 gyk[q] = pack_shr<W_BITS1>(y0, y1);
+                if constexpr (GL) sgw[q][lane] = make_uint2(gxk[q], gyk[q]);
                 if constexpr (ILIN) {
                     cgx = sdot2(ipq, gxk[q], cgx);
                     cgy = sdot2(ipq, gyk[q], cgy);
@@ -474,6 +487,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             }
             bilinear_weights(nextx - inx, nexty - iny, w0, w1);
             int b[2] = {0, 0};
+            if constexpr (GL) asm volatile("" ::: "memory");  // the (Ix, Iy) pairs are re-read from LDS every step
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 const int r = 2 * q;
@@ -495,8 +509,14 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                                                bilin_c(jp[r + 1], jp[r + 2], w0, w1, ic[r + 1]))
                                    : pack_diff(bilin_c(jp[r], jp[r + 1], w0, w1, ic[r]), 0);
                 }
-                b[0] = sdot2(d, gxk[q], b[0]);
-                b[1] = sdot2(d, gyk[q], b[1]);
+                uint32_t gx = gxk[q], gy = gyk[q];
+                if constexpr (GL) {
+                    const uint2 g = sgw[q][lane];
+                    gx = g.x;
+                    gy = g.y;
+                }
+                b[0] = sdot2(d, gx, b[0]);
+                b[1] = sdot2(d, gy, b[1]);
 #ifdef TBDK_LK_NEWTON_SB
                 if (q % TBDK_LK_NEWTON_SB == TBDK_LK_NEWTON_SB - 1) __builtin_amdgcn_sched_barrier(0);
 #endif
