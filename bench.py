@@ -243,13 +243,54 @@ def pin_rank(local_rank: int):
                 "reason": "the affinity mask is already GPU-local"}
     # every thread the process has so far (none is a HIP thread yet: pinning
     # precedes the first GPU call), so later threads inherit the mask
+    _pin_all_threads(allowed)
+    return {"pinned": True, "numa_node": node, "source": src, "cpus": len(allowed)}
+
+
+def _pin_all_threads(cpus):
     for tid in os.listdir("/proc/self/task"):
         try:
-            os.sched_setaffinity(int(tid), allowed)
+            os.sched_setaffinity(int(tid), cpus)
         except OSError:
             pass
-    os.sched_setaffinity(0, allowed)
-    return {"pinned": True, "numa_node": node, "source": src, "cpus": len(allowed)}
+    os.sched_setaffinity(0, cpus)
+
+
+def pin_rank_by_device(dev: int, sysroot: str = "/sys"):
+    """Second chance when sysfs could not name the GPU before HIP started: its
+    PCI address as the runtime reports it (torch device properties, after
+    device init), then that PCI device's local_cpulist / NUMA node.  Every
+    thread of the process is re-pinned (the runtime's included); no re-exec."""
+    import torch
+
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{int(getattr(pr, 'pci_domain_id', 0)):04x}:{int(pr.pci_bus_id):02x}:{int(pr.pci_device_id):02x}.0"
+    except (AttributeError, RuntimeError, TypeError, ValueError):
+        return {"pinned": False, "reason": "no PCI address from the runtime"}
+    d = os.path.join(sysroot, "bus/pci/devices", bdf)
+    cpus, node = [], -1
+    try:
+        node = int(open(os.path.join(d, "numa_node")).read())
+    except (OSError, ValueError):
+        pass
+    try:
+        cpus = parse_cpulist(open(os.path.join(d, "local_cpulist")).read())
+    except (OSError, ValueError):
+        if node >= 0:
+            try:
+                cpus = parse_cpulist(open(os.path.join(sysroot, f"devices/system/node/node{node}/cpulist")).read())
+            except (OSError, ValueError):
+                pass
+    if not cpus:
+        return {"pinned": False, "pci": bdf, "reason": "no local_cpulist / NUMA node for the GPU's PCI device"}
+    allowed = sorted(set(cpus) & os.sched_getaffinity(0))
+    if not allowed:
+        return {"pinned": False, "pci": bdf, "reason": "GPU-local CPUs outside the affinity mask"}
+    if set(allowed) == os.sched_getaffinity(0):
+        return {"pinned": False, "pci": bdf, "cpus": len(allowed), "reason": "the affinity mask is already GPU-local"}
+    _pin_all_threads(allowed)
+    return {"pinned": True, "pci": bdf, "numa_node": node, "source": "runtime PCI address", "cpus": len(allowed)}
 
 
 # ---- CPU baseline -----------------------------------------------------------------------------
@@ -829,6 +870,105 @@ def with_h2d(m: TbdMeasure, world: int, runs: int, skip: int):
             "api": "tbdk_tbd_run_host (pinned host frames, upload ring)"}
 
 
+def bounds_frame_leg(m: TbdMeasure, world: int, runs: int, skip: int):
+    """The KLT-propagated regime: the same sequence with the
+    tracker's bounds filter at the frame (W x H) instead of the reference's
+    hard-coded 1280 x 720 (tbd.cpp:218), so every object's track lives and is
+    propagated by PyrLK and GFTT runs on re-detection frames and depleted sets
+    only.  Frames [skip, nseq) through tbdk_tbd_run after `skip` warm-up frames,
+    a fresh loop per run, median of `runs`.  Never `value` (configs[2] keeps
+    the reference's filter)."""
+    from opencv_amd import tbd
+
+    a = m.args
+    cfg = tbd.default_config(a.width, a.height, win=a.win, max_level=a.max_level, redetect_every=a.redetect,
+                             bounds_xmax=a.width, bounds_ymax=a.height)
+    frames = [m.frames[f] for f in range(skip, m.nseq)]
+    packed = tbd.TbdLoop.pack_detections(m.dets[skip:m.nseq])
+    fps, per = [], None
+    for _ in range(runs):
+        loop = tbd.TbdLoop(cfg, ctx=m.ctx)
+        for f in range(skip):
+            loop.step(m.frames[f], f, m.dets[f], m.stream)
+        res = []
+        el = timed_on_all_ranks(lambda: res.extend(loop.run(frames, skip, None, m.stream, packed=packed)), world)
+        fps.append(replica_throughput(len(frames), world, el))
+        per = res
+        del loop
+    nf = max(1, len(per))
+    return {"median_fps": round(sorted(fps)[len(fps) // 2], 2), "runs_fps": [round(v, 1) for v in fps],
+            "unit": "frames/s", "frames": len(frames),
+            "per_frame": {"tracks": sum(x.ntracks for x in per) / nf, "lk_points": sum(x.lk_points for x in per) / nf,
+                          "gftt_rois": sum(x.redetected for x in per) / nf,
+                          "klt_predicted": sum(x.klt_predicted for x in per) / nf},
+            "tracker_bounds": f"0..{a.width} x 0..{a.height} (the frame)",
+            "note": "secondary: every track propagated by KLT (no 1280x720 filter churn); not BASELINE's config"}
+
+
+def copy_rate_at(ctx, traffic_bytes: int, reps: int = 25) -> dict:
+    """The hand-written stream copy (tbdk_hbm_copy) moving the same number of
+    bytes as a small kernel (read + write = traffic_bytes), timed the same way
+    (HIP events on the launch stream, best of `reps` after warm-up): what one
+    launch of that size can reach on this chip, launch latency included (a
+    11 MiB copy reaches ~3 TB/s, a 2 GiB one ~5.7 TB/s)."""
+    import torch
+    from opencv_amd import klt
+
+    n = max(16, (traffic_bytes // 2) // 16 * 16)
+    src = torch.ones(n, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    st = torch.cuda.current_stream()
+    best = None
+    for i in range(reps + 5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        klt.hbm_copy(dst, src, ctx=ctx, stream=st)
+        e1.record(st)
+        e1.synchronize()
+        if i >= 5:
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+    del src, dst
+    return {"bytes": 2 * n, "us": round(best * 1000, 2), "gbs": round(2 * n / (best / 1000) / 1e9, 1)}
+
+
+def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
+    """roofline_pyramid_4k: the u8 levels-only pyramid build (the TBD loop's
+    pyramid, 3 levels, win 21) of a 3840x2160 frame (BASELINE configs[4]'s size),
+    where the build's bytes are large enough for the HBM roofline to be the
+    bound: algorithmic bytes (pyr_build_bytes: frame read once, every padded
+    level written, level 2 reading level 1) / the build's HIP-event time (both
+    launches), mean over `builds` builds alternating two frames."""
+    import torch
+    from opencv_amd import klt
+
+    W, H, ml = 3840, 2160, 2
+    fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
+    P = klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=False)
+    for i in range(10):
+        P.build(fr[i & 1])
+    torch.cuda.synchronize()
+    ctx.timing_select(["pyr_build"])
+    ctx.timing_enable(True)
+    for i in range(builds):
+        P.build(fr[i & 1])
+    torch.cuda.synchronize()
+    c, ms = ctx.timing_query("pyr_build")
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    us = ms / c * 1000.0
+    b = pyr_build_bytes(W, H, ml + 1)
+    gbs = b / (us * 1e-6) / 1e9
+    del fr, P
+    cp = copy_rate_at(ctx, b)
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": b, "avg_us": round(us, 2), "builds": c,
+            "size_matched_copy": cp, "frac_size_matched_copy": round(gbs / cp["gbs"], 4),
+            "kernel": "pyr_build (levels only, u8, 3840x2160, 3 levels)",
+            "note": "algorithmic bytes (frame read once, padded levels written, level 2 reading level 1) / the "
+                    "build's HIP-event time (events on the launch stream around its launches)"}
+
+
 def kitti_leg(args, ctx, dev, world: int, rank: int):
     """BASELINE configs[3]: KITTI-shaped 1242x375 sequences, one per GPU (seed
     s + rank, sequences s..s+7 at 8 GPUs), 128 objects, the full loop; frames of
@@ -925,6 +1065,9 @@ def main(argv=None):
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary per-frame tbdk_tbd_step pass")
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (tbdk_tbd_run_host) variant")
     ap.add_argument("--no-kitti", action="store_true", help="skip the KITTI-shaped configs[3] measurement")
+    ap.add_argument("--no-bounds-frame", action="store_true",
+                    help="skip the secondary leg with the tracker's bounds at the frame (every object propagated)")
+    ap.add_argument("--no-pyr4k", action="store_true", help="skip the 4K u8 levels-only pyramid roofline leg")
     ap.add_argument("--kitti-frames", type=int, default=500)
     ap.add_argument("--no-farneback", action="store_true", help="skip the secondary dense Farneback measurement")
     ap.add_argument("--fb-width", type=int, default=3840)
@@ -941,6 +1084,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
     if args.no_secondary:
         args.no_step_api = args.no_h2d = args.no_kitti = args.no_farneback = args.no_f16 = args.no_hog = True
+        args.no_bounds_frame = args.no_pyr4k = True
         args.no_copy_peak = True
         args.repeats = 0
 
@@ -958,6 +1102,10 @@ def main(argv=None):
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    if not args.no_pin and not pin.get("pinned") and "already" not in pin.get("reason", ""):
+        first = pin.get("reason")
+        pin = pin_rank_by_device(dev)
+        pin["sysfs_before_init"] = first
 
     from opencv_amd import klt, tbd
 
@@ -1016,6 +1164,9 @@ def main(argv=None):
     if not args.no_h2d:
         progress("with-H2D variant", rank)
         line["with_h2d"] = with_h2d(m, world, 3, 20)
+    if not args.no_bounds_frame and args.bounds == "reference":
+        progress("bounds-frame variant", rank)
+        line["bounds_frame"] = bounds_frame_leg(m, world, 3, 20)
 
     # secondary: the same frames through the per-frame tbdk_tbd_step API (no
     # look-ahead), a fresh loop, no timing events; reported, never `value`
@@ -1083,8 +1234,11 @@ def main(argv=None):
     pyr = kstats.get("pyr_build", kstats_aside.get("pyr_build", nolaunch))
     pyr_gbs = pbb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     cnt = pmc_bytes(PYR_KERNELS)
+    cp_pyr = copy_rate_at(ctx, pbb) if not args.no_copy_peak else None
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pbb, "b_pyr_survey": pb,
+                "size_matched_copy": cp_pyr,
+                "frac_size_matched_copy": round(pyr_gbs / cp_pyr["gbs"], 4) if cp_pyr else None,
                 "kernel": "pyr_build",
                 "traffic": (cnt["fetch_raw"] + cnt["write"]) if cnt else None,
                 "traffic_fetch_x2": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,
@@ -1140,6 +1294,9 @@ def main(argv=None):
         # before any leg imports _oracle: every CPU baseline of the line runs the
         # -O3 -march=native build (native_oracle() is a no-op once _oracle is loaded)
         native_oracle()
+    if rank == 0 and not args.no_pyr4k:
+        progress("4K pyramid roofline")
+        line["roofline_pyramid_4k"] = pyramid_4k_leg(ctx, dev)
     if rank == 0 and not args.no_farneback:
         progress("Farneback secondary")
         line["farneback"] = farneback_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)

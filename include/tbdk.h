@@ -108,9 +108,12 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       eigenvalue strips as a fresh-start mismatch, forcing the re-walk
  *       rounds taken when a segment's fresh start differs from the
  *       reference's running box-filter sum (results equal).
- *   "pyr_fuse" (0/1, default 1): tbdk_pyr_build computes level 0's padded
- *       copy and level 1 in one launch; 0: one launch per level (results
- *       equal).
+ *   "pyr_fuse" (0/1/2, default 1): tbdk_pyr_build of a u8 pyramid: 1
+ *       computes level 0's padded copy and level 1 in one launch, then one
+ *       launch per level; 2 computes levels 0, 1 and 2 in one tiled launch (the
+ *       frame read once through LDS; pyramids whose level pads exceed size - 2
+ *       take 1; measured slower, kept for A/B runs); 0: one launch per level
+ *       (results equal).
  *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;

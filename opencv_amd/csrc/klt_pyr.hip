@@ -331,13 +331,338 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
     return hipGetLastError();
 }
 
+// ---- levels 0, 1 and 2 in one launch (pyr_fuse 2, the default) ----------------
+//
+// One workgroup per tile of TX x TY level-2 pixels (level 1: 2TX x 2TY, the
+// frame: 4TX x 4TY), every byte of the frame read once into LDS (16-byte loads
+// of the tile plus its halo, rows and columns reflect-101 at the frame's edges),
+// then from LDS:
+//   level 0: the tile's frame pixels written as the padded copy (16-byte stores);
+//   level 1: pyrDown_ over the tile plus a 2-pixel halo, separably (the
+//            horizontal [1 4 6 4 1] sums of the halo rows at the level-1 columns
+//            into LDS as int16, then the vertical taps and (s + 128) >> 8 -- the
+//            same integers as the 5x5 sum), halo entries outside the level at
+//            their reflect-101 coordinate (the reference makes level 2 from the
+//            isolated level 1 with BORDER_REFLECT_101, pyramids.cpp:795-800);
+//   level 2: pyrDown_ of the level-1 values in LDS.
+// The reflect-101 frame of each level: a pixel at distance 1..pad from an edge
+// is also stored at its mirror position outside the level (for rows, columns
+// and both), so every padded byte is written by the workgroup that owns its
+// source pixel (requires pad <= size - 2 on every level built here; other
+// pyramids take the two-role path).
+constexpr int kFusedThreads = 256;
+#ifndef TBDK_PYR_FUSED_STOP  // timing probes only: return after this phase (wrong results)
+#define TBDK_PYR_FUSED_STOP 99
+#endif
+
+struct PyrFusedArgs {
+    const uint8_t* src;
+    int spitch, w0, h0;
+    int vec16;                 // src and spitch 16-byte aligned
+    uint8_t* d[3];             // level data (padded origin)
+    int pitch[3], pad[3], w[3], h[3];
+    int nlv;                   // levels written here: 2 or 3
+    int tiles_x, ntiles;
+};
+
+// store one byte of level L at in-level (y, x) and at every mirror position of
+// the level's reflect-101 frame
+__device__ __forceinline__ void fused_put_mirrors(const PyrFusedArgs& a, int L, int y, int x, uint8_t v,
+                                                  bool skip_self)
+{
+    const int p = a.pad[L], w = a.w[L], h = a.h[L];
+    int ys[3], nys = 0, xs[3], nxs = 0;
+    ys[nys++] = y;
+    if (y >= 1 && y <= p) ys[nys++] = -y;
+    if (y >= h - 1 - p && y <= h - 2) ys[nys++] = 2 * (h - 1) - y;
+    xs[nxs++] = x;
+    if (x >= 1 && x <= p) xs[nxs++] = -x;
+    if (x >= w - 1 - p && x <= w - 2) xs[nxs++] = 2 * (w - 1) - x;
+    uint8_t* base = a.d[L] + (size_t)p * a.pitch[L] + p;
+    for (int i = 0; i < nys; ++i)
+        for (int j = 0; j < nxs; ++j)
+            if (!(skip_self && j == 0)) base[(ptrdiff_t)ys[i] * a.pitch[L] + xs[j]] = v;
+}
+
+// the row mirrors of a 16-byte chunk of level L at in-level (y, x0 .. x0+15),
+// plus the column mirrors of its bytes (x0 multiple of 16; n valid bytes)
+__device__ __forceinline__ void fused_put_chunk(const PyrFusedArgs& a, int L, int y, int x0, uint4 v, int n)
+{
+    const int p = a.pad[L], w = a.w[L], h = a.h[L];
+    uint8_t* base = a.d[L] + (size_t)p * a.pitch[L] + p;
+    int ys[3], nys = 0;
+    ys[nys++] = y;
+    if (y >= 1 && y <= p) ys[nys++] = -y;
+    if (y >= h - 1 - p && y <= h - 2) ys[nys++] = 2 * (h - 1) - y;
+    const bool aligned = ((p & 15) == 0) && n == 16;
+    for (int i = 0; i < nys; ++i) {
+        uint8_t* row = base + (ptrdiff_t)ys[i] * a.pitch[L];
+        if (aligned) {
+            *reinterpret_cast<uint4*>(row + x0) = v;
+        } else {
+            const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+            for (int k = 0; k < n; ++k) row[x0 + k] = (uint8_t)(q[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    // column mirrors: only chunks that touch the first / last pad + 1 columns
+    if (x0 <= p || x0 + n - 1 >= w - 1 - p) {
+        const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+        for (int k = 0; k < n; ++k) {
+            const int x = x0 + k;
+            if ((x >= 1 && x <= p) || (x >= w - 1 - p && x <= w - 2))
+                fused_put_mirrors(a, L, y, x, (uint8_t)(q[k >> 2] >> (8 * (k & 3))), true);
+        }
+    }
+}
+
+__device__ __forceinline__ int pyr_w5(int a, int b, int c, int d, int e) { return c * 6 + (b + d) * 4 + a + e; }
+
+__device__ __forceinline__ int byte_at(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, int k)
+{
+    const uint32_t w = k < 4 ? a : k < 8 ? b : k < 12 ? c : k < 16 ? d : e;
+    return (int)((w >> (8 * (k & 3))) & 255u);
+}
+
+// four horizontal pyrDown_ sums from the 11 bytes starting at byte `o` (0..7)
+// of the 20 LDS bytes at p (8-byte aligned): outputs k = 0..3 use bytes
+// o + 2k .. o + 2k + 4
+__device__ __forceinline__ void hsum4(const uint8_t* p, int o, int (&h)[4])
+{
+    const uint2 a = *reinterpret_cast<const uint2*>(p);
+    const uint2 b = *reinterpret_cast<const uint2*>(p + 8);
+    const uint32_t c = *reinterpret_cast<const uint32_t*>(p + 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int v[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) v[t] = byte_at(a.x, a.y, b.x, b.y, c, o + 2 * k + t);
+        h[k] = pyr_w5(v[0], v[1], v[2], v[3], v[4]);
+    }
+}
+
+template <int TX, int TY>
+__global__ __launch_bounds__(kFusedThreads) void pyr_fused_kernel(PyrFusedArgs a)
+{
+    // frame window: rows [4Y - 6, 4Y + 4TY + 3), columns [4X - 16, 4X + 4TX + 16)
+    constexpr int FH = 4 * TY + 9, FW = 4 * TX + 32;
+    // level-1 window: rows [2Y - 2, 2Y + 2TY + 1) (NY1), columns in GX1 groups of
+    // four from 2X - 4 (covers [2X - 2, 2X + 2TX]); stored with level-1 column l
+    // at LDS column l - (2X - 16), so the tile's own columns start 16-aligned
+    constexpr int NY1 = 2 * TY + 3, GX1 = TX / 2 + 2, HW = 4 * GX1, L1W = 2 * TX + 32;
+    __shared__ __attribute__((aligned(16))) uint8_t sF[FH * FW];   // the frame window; then the level-2 row sums
+    __shared__ __attribute__((aligned(16))) int16_t sH[FH * HW];   // horizontal level-1 sums
+    __shared__ __attribute__((aligned(16))) uint8_t sL1[NY1 * L1W];
+    int16_t* const sH2 = reinterpret_cast<int16_t*>(sF);             // [NY1][TX], after sF's last use
+    static_assert(NY1 * TX * 2 <= FH * FW, "level-2 sums alias the frame window");
+
+    const int tid = threadIdx.x;
+    const int t = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring tiles on one XCD (halo rows in its L2)
+    const int TXi = t % a.tiles_x, TYi = t / a.tiles_x;
+    const int X = TXi * TX, Y = TYi * TY;              // level-2 tile origin
+    const int F0x = 4 * X - 16, F0y = 4 * Y - 6;
+    const int w1 = a.w[1], h1 = a.h[1];
+
+    // ---- 1. the frame window into LDS (rows and columns reflect-101 at the frame's edges)
+    for (int i = tid; i < FH * (FW / 16); i += kFusedThreads) {
+        const int r = i / (FW / 16), c = i - r * (FW / 16);
+        const int gy = reflect101(F0y + r, a.h0), gx = F0x + 16 * c;
+        const uint8_t* srow = a.src + (size_t)gy * a.spitch;
+        uint4 v;
+        if (a.vec16 && gx >= 0 && gx + 15 < a.w0) {
+            v = *reinterpret_cast<const uint4*>(srow + gx);
+        } else {
+            uint32_t q[4];
+#pragma unroll
+            for (int dd = 0; dd < 4; ++dd) {
+                q[dd] = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[dd] |= (uint32_t)srow[reflect101(gx + 4 * dd + k, a.w0)] << (8 * k);
+            }
+            v = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+        *reinterpret_cast<uint4*>(sF + r * FW + 16 * c) = v;
+    }
+    __syncthreads();
+
+    if (TBDK_PYR_FUSED_STOP <= 1) return;
+    // ---- 2. level 0: the tile's frame pixels (window rows 6 .., columns 16 ..)
+    for (int i = tid; i < 4 * TY * (TX / 4); i += kFusedThreads) {
+        const int r = i / (TX / 4), c = i - r * (TX / 4);
+        const int y = 4 * Y + r, x = 4 * X + 16 * c;
+        if (y >= a.h0 || x >= a.w0) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(sF + (r + 6) * FW + 16 + 16 * c);
+        fused_put_chunk(a, 0, y, x, v, min(16, a.w0 - x));
+    }
+    if (TBDK_PYR_FUSED_STOP <= 2) return;
+    // ---- 3. horizontal level-1 sums of every window row, four level-1 columns
+    //      l0 .. l0+3 (l0 = 2X - 4 + 4g) per item, each at its reflect-101 column
+    for (int i = tid; i < FH * GX1; i += kFusedThreads) {
+        const int r = i / GX1, g = i - r * GX1;
+        const int l0 = 2 * X - 4 + 4 * g;
+        const uint8_t* row = sF + r * FW;
+        int h[4];
+        if (l0 >= 0 && l0 + 3 < w1) {
+            hsum4(row + 8 * g, 6, h);  // frame columns 2 l0 - 2 .. 2 l0 + 8 = window bytes 8g + 6 ..
+        } else {
+            // columns past w1 + 1 feed no level-2 pixel: clamped so their reflection stays in the window
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint8_t* q = row + (2 * reflect101(min(l0 + k, w1 + 1), w1) - 2 - F0x);
+                h[k] = pyr_w5(q[0], q[1], q[2], q[3], q[4]);
+            }
+        }
+        uint2 o;
+        o.x = (uint32_t)(uint16_t)h[0] | ((uint32_t)(uint16_t)h[1] << 16);
+        o.y = (uint32_t)(uint16_t)h[2] | ((uint32_t)(uint16_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(sH + r * HW + 4 * g) = o;
+    }
+    __syncthreads();
+    if (TBDK_PYR_FUSED_STOP <= 3) return;
+    // ---- 4. level-1 window values, rows at their reflect-101 rows
+    for (int i = tid; i < NY1 * GX1; i += kFusedThreads) {
+        const int r = i / GX1, g = i - r * GX1;
+        const int ry = reflect101(min(2 * Y - 2 + r, h1 + 1), h1);
+        const int16_t* hc = sH + (2 * ry - 2 - F0y) * HW + 4 * g;
+        int v[5][4];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint2 q = *reinterpret_cast<const uint2*>(hc + j * HW);
+            v[j][0] = (int)(int16_t)(q.x & 0xFFFFu);
+            v[j][1] = (int)(int16_t)(q.x >> 16);
+            v[j][2] = (int)(int16_t)(q.y & 0xFFFFu);
+            v[j][3] = (int)(int16_t)(q.y >> 16);
+        }
+        uint32_t o = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o |= (uint32_t)((pyr_w5(v[0][k], v[1][k], v[2][k], v[3][k], v[4][k]) + 128) >> 8) << (8 * k);
+        *reinterpret_cast<uint32_t*>(sL1 + r * L1W + 12 + 4 * g) = o;
+    }
+    __syncthreads();
+    if (TBDK_PYR_FUSED_STOP <= 4) return;
+    // ---- 5. level 1: the tile's pixels (window rows 2 .., LDS columns 16 ..)
+    for (int i = tid; i < 2 * TY * (TX / 8); i += kFusedThreads) {
+        const int r = i / (TX / 8), c = i - r * (TX / 8);
+        const int y = 2 * Y + r, x = 2 * X + 16 * c;
+        if (y >= h1 || x >= w1) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(sL1 + (r + 2) * L1W + 16 + 16 * c);
+        fused_put_chunk(a, 1, y, x, v, min(16, w1 - x));
+    }
+    if (a.nlv < 3) return;
+    // ---- 6. horizontal level-2 sums of the level-1 window rows, level-2 columns
+    //      X + 4q .. X + 4q + 3 (level-1 columns 2X + 8q - 2 .. = LDS bytes 8q + 14 ..)
+    for (int i = tid; i < NY1 * (TX / 4); i += kFusedThreads) {
+        const int r = i / (TX / 4), q4 = i - r * (TX / 4);
+        int h[4];
+        hsum4(sL1 + r * L1W + 8 * q4 + 8, 6, h);
+        uint2 o;
+        o.x = (uint32_t)(uint16_t)h[0] | ((uint32_t)(uint16_t)h[1] << 16);
+        o.y = (uint32_t)(uint16_t)h[2] | ((uint32_t)(uint16_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(sH2 + r * TX + 4 * q4) = o;
+    }
+    __syncthreads();
+    // ---- 7. level 2: the tile, four pixels per item
+    for (int i = tid; i < TY * (TX / 4); i += kFusedThreads) {
+        const int r = i / (TX / 4), c = i - r * (TX / 4);
+        const int y = Y + r, x = X + 4 * c;
+        if (y >= a.h[2] || x >= a.w[2]) continue;
+        const int16_t* hc = sH2 + (2 * r) * TX + 4 * c;
+        int v[5][4];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint2 q = *reinterpret_cast<const uint2*>(hc + j * TX);
+            v[j][0] = (int)(int16_t)(q.x & 0xFFFFu);
+            v[j][1] = (int)(int16_t)(q.x >> 16);
+            v[j][2] = (int)(int16_t)(q.y & 0xFFFFu);
+            v[j][3] = (int)(int16_t)(q.y >> 16);
+        }
+        uint32_t o = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o |= (uint32_t)((pyr_w5(v[0][k], v[1][k], v[2][k], v[3][k], v[4][k]) + 128) >> 8) << (8 * k);
+        const int n = min(4, a.w[2] - x);
+        const int p = a.pad[2], w = a.w[2], h = a.h[2];
+        uint8_t* base = a.d[2] + (size_t)p * a.pitch[2] + p;
+        int ys[3], nys = 0;
+        ys[nys++] = y;
+        if (y >= 1 && y <= p) ys[nys++] = -y;
+        if (y >= h - 1 - p && y <= h - 2) ys[nys++] = 2 * (h - 1) - y;
+        for (int j = 0; j < nys; ++j) {
+            uint8_t* row = base + (ptrdiff_t)ys[j] * a.pitch[2];
+            if (n == 4) *reinterpret_cast<uint32_t*>(row + x) = o;
+            else
+                for (int k = 0; k < n; ++k) row[x + k] = (uint8_t)(o >> (8 * k));
+        }
+        if (x <= p || x + n - 1 >= w - 1 - p)
+            for (int k = 0; k < n; ++k) {
+                const int xx = x + k;
+                if ((xx >= 1 && xx <= p) || (xx >= w - 1 - p && xx <= w - 2))
+                    fused_put_mirrors(a, 2, y, xx, (uint8_t)(o >> (8 * k)), true);
+            }
+    }
+}
+
+// the fused build applies when the frame window's 16-byte loads and stores
+// line up and every level it writes has room for a one-bounce reflect-101 frame
+static bool pyr_fused_ok(const tbdk_pyr& pyr)
+{
+    if (pyr.nlevels < 2 || pyr.cn > 1 || pyr.depth != TBDK_DEPTH_8U) return false;
+    const int nlv = pyr.nlevels >= 3 ? 3 : 2;
+    for (int l = 0; l < nlv; ++l) {
+        const tbdk_level& L = pyr.lv[l];
+        if (L.pad > L.width - 2 || L.pad > L.height - 2 || (L.pad & 15) || (L.pitch & 15) ||
+            (reinterpret_cast<uintptr_t>(L.data) & 15))
+            return false;
+    }
+    return true;
+}
+
+static hipError_t launch_pyr_fused(const uint8_t* src, int spitch, const tbdk_pyr& pyr, hipStream_t s, int* built)
+{
+    PyrFusedArgs a;
+    a.src = src;
+    a.spitch = spitch;
+    a.w0 = pyr.lv[0].width;
+    a.h0 = pyr.lv[0].height;
+    a.vec16 = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)spitch) & 15) == 0;
+    a.nlv = pyr.nlevels >= 3 ? 3 : 2;
+    for (int l = 0; l < 3; ++l) {
+        const tbdk_level& L = pyr.lv[l < a.nlv ? l : a.nlv - 1];
+        a.d[l] = L.data;
+        a.pitch[l] = L.pitch;
+        a.pad[l] = L.pad;
+        a.w[l] = L.width;
+        a.h[l] = L.height;
+    }
+    if (a.nlv < 3) {  // level-2 geometry still sizes the tiles
+        a.w[2] = (a.w[1] + 1) / 2;
+        a.h[2] = (a.h[1] + 1) / 2;
+    }
+    // big tiles when they alone give the chip ~2 workgroups per CU
+    const int w2 = (a.w[1] + 1) / 2, h2 = (a.h[1] + 1) / 2;
+    const long big = (long)((w2 + 63) / 64) * ((h2 + 15) / 16);
+    if (big >= 480) {
+        a.tiles_x = (w2 + 63) / 64;
+        a.ntiles = (int)big;
+        hipLaunchKernelGGL((pyr_fused_kernel<64, 16>), dim3(a.ntiles), dim3(kFusedThreads), 0, s, a);
+    } else {
+        a.tiles_x = (w2 + 31) / 32;
+        a.ntiles = a.tiles_x * ((h2 + 7) / 8);
+        hipLaunchKernelGGL((pyr_fused_kernel<32, 8>), dim3(a.ntiles), dim3(kFusedThreads), 0, s, a);
+    }
+    *built = a.nlv;
+    return hipGetLastError();
+}
+
 // every level of a u8 pyramid from the frame: levels 0 and 1 in one launch
 // (fuse), or one launch per level
-hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, bool fuse, hipStream_t s)
+hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, hipStream_t s)
 {
     hipError_t e;
     int level = 1;
-    if (fuse && pyr.nlevels >= 2) {
+    if (fuse >= 2 && pyr_fused_ok(pyr)) {
+        e = launch_pyr_fused(img, pitch, pyr, s, &level);
+    } else if (fuse && pyr.nlevels >= 2) {
         e = launch_pyr_fuse01(img, pitch, pyr, s);
         level = 2;
     } else {

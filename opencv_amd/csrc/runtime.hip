@@ -194,7 +194,8 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         return TBDK_OK;
     }
     if (std::strcmp(name, "pyr_fuse") == 0) {
-        ctx->opt_pyr_fuse = value != 0;
+        if (value < 0 || value > 2) return TBDK_EINVAL;
+        ctx->opt_pyr_fuse = (int)value;
         return TBDK_OK;
     }
     if (std::strcmp(name, "lk_scharr_fly") == 0) {
@@ -370,7 +371,7 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     } else if (pyr->depth == TBDK_DEPTH_32F) {
         e = launch_pyr_build_f32(img, pitch, 0, *pyr, s);
     } else {
-        e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse != 0, s);
+        e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse, s);
         if (e == hipSuccess && !(pyr->flags & TBDK_PYR_NO_DERIVS)) e = launch_scharr_levels(*pyr, s);
     }
     timing_end(ctx, rec, s);

@@ -72,7 +72,7 @@ struct tbdk_ctx {
     int device = 0;
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
-    int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): fused level launches (0: one per level)
+    int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): 1 the two-role launch + one per level, 2 levels 0-2 in one tiled launch (slower, A/B), 0 one launch per level
     int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     int opt_fb_prep_ahead = 1;  // tbdk_ctx_set_option("fb_prep_ahead"): Farneback level prep on a side stream
@@ -117,7 +117,7 @@ hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, u
 // Scharr derivative planes (interior only; the zero frame is written once at allocation)
 hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s);
 // every u8 level of pyr from the frame (fused launches where the levels allow)
-hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, bool fuse, hipStream_t s);
+hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, hipStream_t s);
 // the fp16 pyramid (klt_f16.hip): level 0 from a u8 (img_f16 = 0) or fp16 frame,
 // the fp16 pyrDown levels and the fp16 derivative pairs
 hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s);

@@ -214,3 +214,28 @@ def test_gpu_numa_cpus_fake_sysfs(tmp_path, monkeypatch):
     assert bench.gpu_numa_cpus(0, str(b)) == (0, list(range(16)), "drm:0000:05:00.0:local_cpulist")
     assert bench.gpu_numa_cpus(1, str(b)) == (1, list(range(16, 32)), "drm:0000:c1:00.0:numa_node")
     assert bench.gpu_numa_cpus(0, str(tmp_path / "empty")) is None
+
+
+def test_pin_by_runtime_pci_address_fake_sysfs(tmp_path, monkeypatch):
+    """bench.pin_rank_by_device: the runtime's PCI address (faked) -> the fake
+    sysfs tree's local_cpulist; the affinity change itself is stubbed"""
+    import types
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    _fake_sysfs(tmp_path)
+    props = types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x05, pci_device_id=0)
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: props)
+    pinned = []
+    monkeypatch.setattr(bench, "_pin_all_threads", lambda cpus: pinned.append(cpus))
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(64)))
+    r = bench.pin_rank_by_device(0, str(tmp_path))
+    assert r["pinned"] and r["pci"] == "0000:05:00.0" and pinned == [list(range(16))]
+    props.pci_bus_id = 0xC1  # no local_cpulist: its NUMA node's cpulist
+    r = bench.pin_rank_by_device(0, str(tmp_path))
+    assert r["pinned"] and r["numa_node"] == 1 and pinned[-1] == list(range(16, 32))
+    props.pci_bus_id = 0x99
+    assert not bench.pin_rank_by_device(0, str(tmp_path))["pinned"]

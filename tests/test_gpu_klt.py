@@ -121,6 +121,34 @@ def test_pyramid_frame_at_allocation_end(gpu, shape):
             assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"level {lvl} derivs {derivs}"
 
 
+@pytest.mark.parametrize("shape,maxlev,win", [((2160, 3840), 2, 21), ((2161, 3841), 3, 21), ((1079, 1919), 2, 21),
+                                             ((517, 1023), 2, 31), ((255, 257), 2, 21), ((140, 140), 2, 21),
+                                             ((1200, 300), 4, 7), ((375, 1242), 2, 45)])
+def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
+    """ctx option pyr_fuse: 2 (levels 0-2 in one tiled launch: edge tiles, partial
+    tiles, the mirrored reflect-101 frames, pads of 32 / 48 / 64), 1 (two-role
+    launch) and 0 (one launch per level): every padded level bit-exact with the
+    oracle's, levels-only and with derivative planes"""
+    K = klt()
+    img = np.random.default_rng(sum(shape)).integers(0, 256, shape, dtype=np.uint8)
+    R = None
+    try:
+        for mode in (2, 1, 0):
+            gpu.set_option("pyr_fuse", mode)
+            for derivs in (False, True):
+                P = K.build_pyramid(to_dev(img), (win, win), maxlev, ctx=gpu, derivs=derivs)
+                torch.cuda.synchronize()
+                if R is None:
+                    R = O.Pyramid(img, (win, win), maxlev, pad=P.pyr.lv[0].pad)
+                assert P.nlevels == R.nlevels
+                for lvl in range(P.nlevels):
+                    assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"mode {mode} level {lvl}"
+                if derivs:
+                    assert np.array_equal(P.deriv(0), O.scharr(R.level(0))), f"mode {mode} deriv"
+    finally:
+        gpu.set_option("pyr_fuse", 1)
+
+
 @pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])
 def test_lk_levels_only_equals_derivative_planes(gpu, win, maxlev):
     """PyrLK on levels-only pyramids (the window's Scharr values derived in the

@@ -1,6 +1,7 @@
-"""tbdk_pyr_build timing: levels-only pyramids (one fused launch) vs pyramids
-with derivative planes (fused levels + the Scharr launch), 1080p / KITTI / 4K,
-HIP events over 200 builds each."""
+"""tbdk_pyr_build timing by ctx option pyr_fuse (2: levels 0-2 in one tiled
+launch, 1: the two-role launch + one per level, 0: one launch per level),
+levels-only and with derivative planes (+ the Scharr launch), 1080p / KITTI /
+4K, HIP events over 200 builds each."""
 import os
 import sys
 
@@ -12,7 +13,7 @@ ctx = klt.Context.get(0)
 for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2), (1920, 1080, 3)):
     fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
     out = []
-    for derivs, fuse in ((False, 1), (False, 0), (True, 1)):
+    for derivs, fuse in ((False, 2), (False, 1), (False, 0), (True, 2), (True, 1)):
         ctx.set_option("pyr_fuse", fuse)
         P = klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=derivs)
         for _ in range(20):
@@ -28,5 +29,5 @@ for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2), (1920, 1080
         ctx.timing_select(None)
         out.append(ms / c * 1000)
     ctx.set_option("pyr_fuse", 1)
-    print(f"{W}x{H} maxLevel {ml}: levels only fused {out[0]:6.1f} us, per level {out[1]:6.1f} us; "
-          f"with Scharr planes {out[2]:6.1f} us")
+    print(f"{W}x{H} maxLevel {ml}: levels only: tiled {out[0]:6.1f} us, two-role {out[1]:6.1f} us, per level "
+          f"{out[2]:6.1f} us; with Scharr planes: tiled {out[3]:6.1f} us, two-role {out[4]:6.1f} us", flush=True)
