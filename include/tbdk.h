@@ -246,6 +246,16 @@ int tbdk_pyr_create_f32(tbdk_ctx* ctx, int width, int height, int max_level,
                         int win_w, int win_h, tbdk_pyr* pyr);
 int tbdk_pyr_build_u16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream);
 int tbdk_pyr_build_f32(tbdk_ctx* ctx, const float* img, int pitch, tbdk_pyr* pyr, void* stream);
+/* The fp32 pixel path on cn = 2..4 interleaved channels: CV_16UC3/C4 and
+ * CV_32FC3/C4 frames of cv::cuda::SparsePyrLKOpticalFlow (cudaoptflow/src/
+ * pyrlk.cpp:197-205), computed as the CPU path handles channels
+ * (lkpyramid.cpp:55-144, 178-695: windows of win_w * cn values, G and b over
+ * all of them).  Levels hold cn fp32 values per pixel, the derivative planes
+ * an (Ix, Iy) fp32 pair per value; tbdk_pyr_build / _build_u16 / _build_f32
+ * take frames of cn interleaved u8 / u16 / fp32 values per pixel;
+ * tbdk_lk_sparse (impl 0) tracks on two such pyramids. */
+int tbdk_pyr_create_f32_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_level,
+                           int win_w, int win_h, tbdk_pyr* pyr);
 
 /* Synchronous copy of level `level` to host memory (GpuMat::download
  * analogue; not for the hot path).  with_border != 0 copies the padded frame

@@ -57,6 +57,18 @@ struct GpuImage {
     int width = 0, height = 0, pitch = 0;  // pitch in bytes
 };
 
+// Element depths of a typed view (cv::Mat depth codes): the types
+// cv::cuda::SparsePyrLKOpticalFlow::calc accepts (cudaoptflow/src/pyrlk.cpp:189-205)
+constexpr int DEPTH_8U = 0, DEPTH_16U = 2, DEPTH_32F = 5;
+
+// Non-owning device image view with a depth and cn interleaved channels
+// (GpuMat of CV_8UC1..4 / CV_16UC1..4 / CV_32FC1..4 analogue)
+struct GpuMatView {
+    void* data = nullptr;
+    int width = 0, height = 0, pitch = 0;  // pitch in bytes
+    int depth = DEPTH_8U, cn = 1;
+};
+
 // One context per (host thread, device); owns GFTT scratch and timing records.
 class Context {
 public:
@@ -76,15 +88,18 @@ private:
 // gives the fp16 pixel path's pyramid (tbdk_pyr_create_f16).
 class Pyramid {
 public:
-    // depth TBDK_DEPTH_8U (cn 1..4 channels, interleaved), TBDK_DEPTH_16F or TBDK_DEPTH_32F (one channel)
+    // depth TBDK_DEPTH_8U or TBDK_DEPTH_32F (cn 1..4 channels, interleaved), TBDK_DEPTH_16F (one channel)
     Pyramid(Context& ctx, int width, int height, int max_level, Size win = {21, 21}, int depth = TBDK_DEPTH_8U,
             int cn = 1)
         : ctx_(&ctx)
     {
-        if (cn != 1 && depth != TBDK_DEPTH_8U) throw Error(TBDK_EINVAL, "Pyramid: multi-channel pyramids are 8U");
+        if (cn != 1 && depth == TBDK_DEPTH_16F) throw Error(TBDK_EINVAL, "Pyramid: fp16 pyramids are one-channel");
         if (depth == TBDK_DEPTH_16F)
             check(tbdk_pyr_create_f16(ctx.get(), width, height, max_level, win.width, win.height, &p_),
                   "tbdk_pyr_create_f16");
+        else if (depth == TBDK_DEPTH_32F && cn != 1)
+            check(tbdk_pyr_create_f32_cn(ctx.get(), width, height, cn, max_level, win.width, win.height, &p_),
+                  "tbdk_pyr_create_f32_cn");
         else if (depth == TBDK_DEPTH_32F)
             check(tbdk_pyr_create_f32(ctx.get(), width, height, max_level, win.width, win.height, &p_),
                   "tbdk_pyr_create_f32");
@@ -118,6 +133,24 @@ public:
     {
         if (width != p_.lv[0].width || height != p_.lv[0].height) throw Error(TBDK_EINVAL, "Pyramid::build_f32");
         check(tbdk_pyr_build_f32(ctx_->get(), data, pitch, &p_, stream), "tbdk_pyr_build_f32");
+    }
+    // any typed view the pyramid takes: u8 into either depth, u16 / fp32 into fp32
+    // pyramids, with the pyramid's channel count
+    void build(const GpuMatView& img, void* stream = nullptr)
+    {
+        if (img.width != p_.lv[0].width || img.height != p_.lv[0].height || img.cn != channels())
+            throw Error(TBDK_EINVAL, "Pyramid::build");
+        if (img.depth == DEPTH_8U)
+            check(tbdk_pyr_build(ctx_->get(), static_cast<const uint8_t*>(img.data), img.pitch, &p_, stream),
+                  "tbdk_pyr_build");
+        else if (img.depth == DEPTH_16U)
+            check(tbdk_pyr_build_u16(ctx_->get(), static_cast<const uint16_t*>(img.data), img.pitch, &p_, stream),
+                  "tbdk_pyr_build_u16");
+        else if (img.depth == DEPTH_32F)
+            check(tbdk_pyr_build_f32(ctx_->get(), static_cast<const float*>(img.data), img.pitch, &p_, stream),
+                  "tbdk_pyr_build_f32");
+        else
+            throw Error(TBDK_EINVAL, "Pyramid::build: depth");
     }
     int depth() const { return p_.depth; }
     int channels() const { return p_.cn > 1 ? p_.cn : 1; }
@@ -165,8 +198,28 @@ public:
         if (n == 0) return;  // reference: empty prevPts releases the outputs (pyrlk.cpp:221-227)
         for (int i = 0; i < 2; ++i) {
             const GpuImage& im = i == 0 ? prevImg : nextImg;
-            if (!pyr_[i] || pyr_[i]->get().lv[0].width != im.width || pyr_[i]->get().lv[0].height != im.height)
+            if (!pyr_[i] || pyr_[i]->get().lv[0].width != im.width || pyr_[i]->get().lv[0].height != im.height ||
+                pyr_[i]->depth() != TBDK_DEPTH_8U || pyr_[i]->channels() != 1)
                 pyr_[i].reset(new Pyramid(*ctx_, im.width, im.height, max_level_, win_));
+            pyr_[i]->build(im, stream);
+        }
+        calc(*pyr_[0], *pyr_[1], prevPts, nextPts, status, err, n, stream);
+    }
+
+    // Typed images (the CUDA class's accepted types, pyrlk.cpp:189-205): CV_8UC1..4
+    // on the u8 path, CV_16UC1..4 / CV_32FC1..4 on the fp32 pixel path; both
+    // images of one type.  The pyramids are cached per (size, depth, channels).
+    void calc(const GpuMatView& prevImg, const GpuMatView& nextImg, const float* prevPts, float* nextPts,
+              uint8_t* status, float* err, int n, void* stream = nullptr)
+    {
+        if (n == 0) return;
+        if (prevImg.depth != nextImg.depth || prevImg.cn != nextImg.cn) throw Error(TBDK_EINVAL, "calc: types");
+        const int pdepth = prevImg.depth == DEPTH_8U ? TBDK_DEPTH_8U : TBDK_DEPTH_32F;
+        for (int i = 0; i < 2; ++i) {
+            const GpuMatView& im = i == 0 ? prevImg : nextImg;
+            if (!pyr_[i] || pyr_[i]->get().lv[0].width != im.width || pyr_[i]->get().lv[0].height != im.height ||
+                pyr_[i]->depth() != pdepth || pyr_[i]->channels() != im.cn)
+                pyr_[i].reset(new Pyramid(*ctx_, im.width, im.height, max_level_, win_, pdepth, im.cn));
             pyr_[i]->build(im, stream);
         }
         calc(*pyr_[0], *pyr_[1], prevPts, nextPts, status, err, n, stream);

@@ -184,6 +184,14 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 #ifndef TBDK_LK_GLDS
 #define TBDK_LK_GLDS 0
 #endif
+// A launch ends with its slowest wave: the few points that run to 30 Newton
+// steps on a level (and the waves that carry them) finish long after the
+// rest.  A wave that has taken more than TBDK_LK_PRIO_STEPS steps raises its
+// issue priority (s_setprio), so on a shared SIMD its instructions go first and
+// the straggler runs near its lone-wave speed (0: off)
+#ifndef TBDK_LK_PRIO_STEPS
+#define TBDK_LK_PRIO_STEPS 0
+#endif
 constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 
 #ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
@@ -228,6 +236,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         outy = a.next_pts[2 * i + 1];
     }
     int status = 1, nit = 0;
+#if TBDK_LK_PRIO_STEPS > 0
+    int wsteps = 0;  // Newton steps this wave has run (wave-uniform)
+#endif
 #if defined(TBDK_LK_PROBE_RELOADS) && TBDK_LK_PROBE_RELOADS == 2
     int nrl = 0;
 #endif
@@ -464,6 +475,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < a.max_count; ++j) {
             if (!any_lane(act)) break;
+#if TBDK_LK_PRIO_STEPS > 0
+            if (++wsteps == TBDK_LK_PRIO_STEPS) __builtin_amdgcn_s_setprio(3);
+#endif
             const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
             if (act && (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h)) {
                 if (level == 0) status = 0;

@@ -342,6 +342,13 @@ int tbdk_pyr_create_f32(tbdk_ctx* ctx, int width, int height, int max_level, int
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_32F, 0, pyr);
 }
 
+int tbdk_pyr_create_f32_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_level, int win_w, int win_h,
+                           tbdk_pyr* pyr)
+{
+    if (cn < 1 || cn > 4) return TBDK_EINVAL;
+    return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_32F, 0, pyr, cn);
+}
+
 int tbdk_pyr_create_f16(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h, tbdk_pyr* pyr)
 {
     return pyr_create(ctx, width, height, max_level, win_w, win_h, TBDK_DEPTH_16F, 0, pyr);
@@ -360,11 +367,14 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
 {
     const int cn = pyr && pyr->cn > 1 ? pyr->cn : 1;
     if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pitch < pyr->lv[0].width * cn) return TBDK_EINVAL;
+    if (cn > 1 && pyr->depth == TBDK_DEPTH_16F) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     hipError_t e;
-    if (cn > 1) {
+    if (cn > 1 && pyr->depth == TBDK_DEPTH_32F) {
+        e = launch_pyr_build_f32_cn(img, pitch, 0, *pyr, s);
+    } else if (cn > 1) {
         e = launch_pyr_cn(img, pitch, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_16F) {
         e = launch_pyr_build_f16(img, pitch, 0, *pyr, s);
@@ -394,13 +404,15 @@ int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* 
 static int pyr_build_f32_from(tbdk_ctx* ctx, const void* img, int pitch, int bytes_per_px, int kind, tbdk_pyr* pyr,
                               void* stream)
 {
+    const int cn = pyr && pyr->cn > 1 ? pyr->cn : 1;
     if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pyr->depth != TBDK_DEPTH_32F ||
-        pitch < bytes_per_px * pyr->lv[0].width || pitch % bytes_per_px != 0)
+        pitch < bytes_per_px * cn * pyr->lv[0].width || pitch % bytes_per_px != 0)
         return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
-    hipError_t e = launch_pyr_build_f32(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s);
+    hipError_t e = cn > 1 ? launch_pyr_build_f32_cn(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s)
+                          : launch_pyr_build_f32(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);
 }
@@ -479,7 +491,7 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     const bool f32 = prev->depth == TBDK_DEPTH_32F;
     const bool f16 = prev->depth == TBDK_DEPTH_16F || f32;  // the float pixel paths
     const int cn = prev->cn > 1 ? prev->cn : 1;
-    if (cn != (next->cn > 1 ? next->cn : 1) || (cn > 1 && f16)) return TBDK_EINVAL;
+    if (cn != (next->cn > 1 ? next->cn : 1) || (cn > 1 && f16 && !f32)) return TBDK_EINVAL;
     const int pad_needed = p->win_w > p->win_h ? p->win_w + 2 : p->win_h + 2;
     int max_level = p->max_level;
     if (prev->nlevels - 1 < max_level) max_level = prev->nlevels - 1;
@@ -520,6 +532,14 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     // auto: several points per wave when the window has an instantiation, else the
     // one-point-per-wave strip kernel, else the generic LDS kernel (no derivative planes)
     if (p->impl < 0 || p->impl > 3) return TBDK_EINVAL;
+    if (cn > 1 && f32) {  // multi-channel 16U / 32F frames: the fp32 cn kernel (klt_cn_f32.hip)
+        if (p->impl != 0 || !have_d || lk_cn_f32_smem_bytes(p->win_w, p->win_h, cn) > 160 * 1024) return TBDK_EINVAL;
+        a.cn = cn;
+        int rec = timing_begin(ctx, "lk_sparse", s);
+        hipError_t e = launch_lk_cn_f32(a, s);
+        timing_end(ctx, rec, s);
+        return map_err(e);
+    }
     if (cn > 1) {  // multi-channel frames: one kernel (klt_cn.hip), on the derivative planes
         if (p->impl != 0 || !have_d || lk_cn_smem_bytes(p->win_w, p->win_h, cn) > 160 * 1024) return TBDK_EINVAL;
         a.cn = cn;

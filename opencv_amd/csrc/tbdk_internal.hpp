@@ -170,6 +170,9 @@ int map_status(hipError_t e);
 hipError_t launch_pyr_cn(const uint8_t* img, int pitch, const tbdk_pyr& pyr, hipStream_t s);
 hipError_t launch_lk_cn(const LkArgs& a, hipStream_t s);
 size_t lk_cn_smem_bytes(int win_w, int win_h, int cn);
+hipError_t launch_lk_cn_f32(const LkArgs& a, hipStream_t s);
+size_t lk_cn_f32_smem_bytes(int win_w, int win_h, int cn);
+hipError_t launch_pyr_build_f32_cn(const uint8_t* img, int pitch, int kind, const tbdk_pyr& pyr, hipStream_t s);
 
 size_t lk_smem_bytes(int win_w, int win_h);
 hipError_t launch_lk_sparse(const LkArgs& a, hipStream_t s);

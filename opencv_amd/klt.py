@@ -100,19 +100,24 @@ class Pyramid:
                  dtype: torch.dtype = torch.uint8, derivs: bool = True, channels: int = 1):
         """derivs=False (u8 only): levels without derivative planes
         (tbdk_pyr_create_levels); PyrLK then derives the window's Scharr values
-        itself, with the same results.  channels 2..4 (u8 only): interleaved
-        multi-channel frames (tbdk_pyr_create_cn)."""
+        itself, with the same results.  channels 2..4: interleaved multi-channel
+        frames, u8 (tbdk_pyr_create_cn) or the fp32 pixel path for 16U / 32F
+        frames (tbdk_pyr_create_f32_cn)."""
         if dtype not in (torch.uint8, torch.float16, torch.float32):
             raise _lib.TbdkError("Pyramid dtype must be torch.uint8, torch.float16 or torch.float32")
         if not derivs and dtype != torch.uint8:
             raise _lib.TbdkError("levels-only pyramids are u8")
-        if channels != 1 and (dtype != torch.uint8 or not derivs):
-            raise _lib.TbdkError("multi-channel pyramids are u8 with derivative planes")
+        if channels != 1 and (dtype == torch.float16 or not derivs):
+            raise _lib.TbdkError("multi-channel pyramids are u8 or fp32, with derivative planes")
         self.ctx = ctx
         self.dtype = dtype
         self.channels = int(channels)
         self.pyr = _lib.Pyr()
-        if channels != 1:
+        if channels != 1 and dtype == torch.float32:
+            _lib.check(ctx.lib.tbdk_pyr_create_f32_cn(ctx.handle, int(width), int(height), int(channels),
+                                                      int(max_level), int(win[0]), int(win[1]), C.byref(self.pyr)),
+                       "tbdk_pyr_create_f32_cn")
+        elif channels != 1:
             _lib.check(ctx.lib.tbdk_pyr_create_cn(ctx.handle, int(width), int(height), int(channels), int(max_level),
                                                   int(win[0]), int(win[1]), C.byref(self.pyr)), "tbdk_pyr_create_cn")
         else:
@@ -129,14 +134,19 @@ class Pyramid:
 
     def build(self, img: torch.Tensor, stream=None) -> "Pyramid":
         """From a 2-D uint8 frame (either depth) or, for an fp16 pyramid, a float16 frame;
-        a multi-channel pyramid from an (H, W, C) uint8 frame."""
+        a multi-channel pyramid from an (H, W, C) uint8 frame (fp32 multi-channel
+        pyramids also uint16 / float32)."""
         if self.channels != 1:
-            if img.dim() != 3 or not img.is_cuda or img.dtype != torch.uint8 or \
+            ok_types = (torch.uint8, torch.uint16, torch.float32) if self.dtype == torch.float32 else (torch.uint8,)
+            if img.dim() != 3 or not img.is_cuda or img.dtype not in ok_types or \
                     tuple(img.shape) != (self.height, self.width, self.channels) or img.stride(2) != 1 or \
                     img.stride(1) != self.channels:
-                raise _lib.TbdkError("Pyramid.build expects an (H, W, C) uint8 device tensor of the pyramid's size")
-            _lib.check(self.ctx.lib.tbdk_pyr_build(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)),
-                                                   C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
+                raise _lib.TbdkError("Pyramid.build expects an (H, W, C) device tensor of the pyramid's size and "
+                                     "depth")
+            fn = {torch.uint8: self.ctx.lib.tbdk_pyr_build, torch.uint16: self.ctx.lib.tbdk_pyr_build_u16,
+                  torch.float32: self.ctx.lib.tbdk_pyr_build_f32}[img.dtype]
+            _lib.check(fn(self.ctx.handle, C.c_void_p(img.data_ptr()), int(img.stride(0)) * img.element_size(),
+                          C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build (multi-channel)")
             return self
         if self.dtype == torch.float32 and img.dim() == 2 and img.is_cuda and img.stride(1) == 1 and \
                 img.dtype in (torch.uint16, torch.float32):

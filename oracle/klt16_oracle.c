@@ -102,50 +102,69 @@ void orc16_scharr(const uint16_t* src, int w, int h, int pitch, uint16_t* dst)
     }
 }
 
-/* one pyrDown level of the fp32 pixel path (the same order, no rounding) */
-void orc32_pyr_down(const float* src, int sw, int sh, int spitch, float* dst, int dw, int dh, int dpitch)
+/* one pyrDown level of the fp32 pixel path (the same order, no rounding), cn
+ * interleaved channels (pitches in elements): every channel filtered on its
+ * own, the 5 taps cn elements apart (pyrDown_ on CV_32FC(cn), pyramids.cpp:722-857) */
+void orc32_pyr_down_cn(const float* src, int sw, int sh, int spitch, int cn, float* dst, int dw, int dh, int dpitch)
 {
     for (int y = 0; y < dh; ++y)
-        for (int x = 0; x < dw; ++x) {
-            float r[5];
-            for (int j = 0; j < 5; ++j) {
-                const float* row = src + (size_t)orc_reflect101(2 * y + j - 2, sh) * spitch;
-                float s0 = row[orc_reflect101(2 * x - 2, sw)];
-                float s1 = row[orc_reflect101(2 * x - 1, sw)];
-                float s2 = row[orc_reflect101(2 * x, sw)];
-                float s3 = row[orc_reflect101(2 * x + 1, sw)];
-                float s4 = row[orc_reflect101(2 * x + 2, sw)];
-                r[j] = s2 * 6.f + (s1 + s3) * 4.f + s0 + s4;
+        for (int x = 0; x < dw; ++x)
+            for (int c = 0; c < cn; ++c) {
+                float r[5];
+                for (int j = 0; j < 5; ++j) {
+                    const float* row = src + (size_t)orc_reflect101(2 * y + j - 2, sh) * spitch;
+                    float s0 = row[orc_reflect101(2 * x - 2, sw) * cn + c];
+                    float s1 = row[orc_reflect101(2 * x - 1, sw) * cn + c];
+                    float s2 = row[orc_reflect101(2 * x, sw) * cn + c];
+                    float s3 = row[orc_reflect101(2 * x + 1, sw) * cn + c];
+                    float s4 = row[orc_reflect101(2 * x + 2, sw) * cn + c];
+                    r[j] = s2 * 6.f + (s1 + s3) * 4.f + s0 + s4;
+                }
+                dst[(size_t)y * dpitch + (size_t)x * cn + c] =
+                    (r[2] * 6.f + (r[1] + r[3]) * 4.f + r[0] + r[4]) * (1.f / 256.f);
             }
-            dst[(size_t)y * dpitch + x] = (r[2] * 6.f + (r[1] + r[3]) * 4.f + r[0] + r[4]) * (1.f / 256.f);
-        }
 }
 
-/* calcSharrDeriv's formula on an fp32 level: dst (h x w x 2) fp32 (Ix, Iy) */
-void orc32_scharr(const float* src, int w, int h, int pitch, float* dst)
+void orc32_pyr_down(const float* src, int sw, int sh, int spitch, float* dst, int dw, int dh, int dpitch)
+{
+    orc32_pyr_down_cn(src, sw, sh, spitch, 1, dst, dw, dh, dpitch);
+}
+
+/* calcSharrDeriv's formula on an fp32 level of cn interleaved channels
+ * (lkpyramid.cpp:55-144: neighbours cn elements apart, rows / columns
+ * reflect-101): dst (h x w x cn x 2) fp32 (Ix, Iy) per element */
+void orc32_scharr_cn(const float* src, int w, int h, int pitch, int cn, float* dst)
 {
     for (int y = 0; y < h; ++y) {
         const float* r0 = src + (size_t)orc_reflect101(y - 1, h) * pitch;
         const float* r1 = src + (size_t)y * pitch;
         const float* r2 = src + (size_t)orc_reflect101(y + 1, h) * pitch;
-        for (int x = 0; x < w; ++x) {
-            float t0[3], t1[3];
-            for (int k = 0; k < 3; ++k) {
-                const int c = orc_reflect101(x + k - 1, w);
-                t0[k] = (r0[c] + r2[c]) * 3.f + r1[c] * 10.f;
-                t1[k] = r2[c] - r0[c];
+        for (int x = 0; x < w; ++x)
+            for (int ch = 0; ch < cn; ++ch) {
+                float t0[3], t1[3];
+                for (int k = 0; k < 3; ++k) {
+                    const int c = orc_reflect101(x + k - 1, w) * cn + ch;
+                    t0[k] = (r0[c] + r2[c]) * 3.f + r1[c] * 10.f;
+                    t1[k] = r2[c] - r0[c];
+                }
+                const size_t o = (((size_t)y * w + x) * cn + ch) * 2;
+                dst[o] = t0[2] - t0[0];
+                dst[o + 1] = (t1[2] + t1[0]) * 3.f + t1[1] * 10.f;
             }
-            dst[((size_t)y * w + x) * 2] = t0[2] - t0[0];
-            dst[((size_t)y * w + x) * 2 + 1] = (t1[2] + t1[0]) * 3.f + t1[1] * 10.f;
-        }
     }
 }
 
+void orc32_scharr(const float* src, int w, int h, int pitch, float* dst)
+{
+    orc32_scharr_cn(src, w, h, pitch, 1, dst);
+}
+
 typedef struct orc16_level {
-    const void* px;     /* h x w fp16 (or fp32 with f32) */
-    const void* d;      /* h x w x 2 fp16 / fp32 (Ix, Iy), or NULL for a J-only level */
+    const void* px;     /* h x w (x cn) fp16 (or fp32 with f32) */
+    const void* d;      /* h x w (x cn) x 2 fp16 / fp32 (Ix, Iy), or NULL for a J-only level */
     int w, h;
     int f32;            /* the fp32 pixel path: the same algorithm on fp32 levels */
+    int cn;             /* interleaved channels (0 or 1: one); fp32 only */
 } orc16_level;
 
 typedef struct orc16_pyr {
@@ -153,16 +172,21 @@ typedef struct orc16_pyr {
     orc16_level lv[8];
 } orc16_pyr;
 
-static inline float px16(const orc16_level* L, int x, int y)
+static inline int lcn(const orc16_level* L) { return L->cn > 1 ? L->cn : 1; }
+
+/* channel ch of pixel (x, y), coordinates reflect-101 (the padded level's frame) */
+static inline float px16(const orc16_level* L, int x, int y, int ch)
 {
-    const size_t k = (size_t)orc_reflect101(y, L->h) * L->w + orc_reflect101(x, L->w);
+    const int cn = lcn(L);
+    const size_t k = ((size_t)orc_reflect101(y, L->h) * L->w + orc_reflect101(x, L->w)) * cn + ch;
     return L->f32 ? ((const float*)L->px)[k] : orc16_h2f(((const uint16_t*)L->px)[k]);
 }
 
-static inline float dv16(const orc16_level* L, int x, int y, int c)
+/* derivative c (0: Ix, 1: Iy) of channel ch at (x, y); zero outside the level */
+static inline float dv16(const orc16_level* L, int x, int y, int ch, int c)
 {
     if (x < 0 || y < 0 || x >= L->w || y >= L->h) return 0.f; /* BORDER_CONSTANT 0 frame */
-    const size_t k = ((size_t)y * L->w + x) * 2 + c;
+    const size_t k = (((size_t)y * L->w + x) * lcn(L) + ch) * 2 + c;
     return L->f32 ? ((const float*)L->d)[k] : orc16_h2f(((const uint16_t*)L->d)[k]);
 }
 
@@ -199,10 +223,14 @@ typedef struct orc16_job {
 static void lk16_point(const orc16_job* jb, int i, float* buf)
 {
     const int WW = jb->prm->winW, WH = jb->prm->winH, flags = jb->prm->flags;
+    /* cn channels: a window row is WW * cn elements (column e = pixel e / cn,
+     * channel e % cn), G and b sum over all of them, as the CPU path does
+     * (lkpyramid.cpp:233-252, 268-420: winSize.width * cn per row) */
+    const int cn = lcn(&jb->prev->lv[0]), WE = WW * cn;
     float* iv = buf;
-    float* gx = iv + WW * WH;
-    float* gy = gx + WW * WH;
-    float* col = gy + WW * WH;
+    float* gx = iv + WE * WH;
+    float* gy = gx + WE * WH;
+    float* col = gy + WE * WH;
     const float FLT_SCALE = 1.f / (1 << 20);
     const float halfx = (WW - 1) * 0.5f, halfy = (WH - 1) * 0.5f;
     const float p0x = jb->prevPts[2 * i], p0y = jb->prevPts[2 * i + 1];
@@ -246,25 +274,27 @@ static void lk16_point(const orc16_job* jb, int i, float* buf)
         weights16(prevx - ipx, prevy - ipy, w);
         float s[3];
         for (int v = 0; v < 3; ++v) {
-            for (int x = 0; x < WW; ++x) {
+            for (int e = 0; e < WE; ++e) {
+                const int x = e / cn, ch = e - x * cn;
                 float acc = 0.f;
                 for (int r = 0; r < WH; ++r) {
                     const int X = ipx + x, Y = ipy + r;
-                    const size_t k = (size_t)r * WW + x;
+                    const size_t k = (size_t)r * WE + e;
                     if (v == 0) {
-                        iv[k] = bil(w, px16(I, X, Y), px16(I, X + 1, Y), px16(I, X, Y + 1), px16(I, X + 1, Y + 1), 0.f);
-                        gx[k] = bil(w, dv16(I, X, Y, 0), dv16(I, X + 1, Y, 0), dv16(I, X, Y + 1, 0),
-                                    dv16(I, X + 1, Y + 1, 0), 0.f);
-                        gy[k] = bil(w, dv16(I, X, Y, 1), dv16(I, X + 1, Y, 1), dv16(I, X, Y + 1, 1),
-                                    dv16(I, X + 1, Y + 1, 1), 0.f);
+                        iv[k] = bil(w, px16(I, X, Y, ch), px16(I, X + 1, Y, ch), px16(I, X, Y + 1, ch),
+                                    px16(I, X + 1, Y + 1, ch), 0.f);
+                        gx[k] = bil(w, dv16(I, X, Y, ch, 0), dv16(I, X + 1, Y, ch, 0), dv16(I, X, Y + 1, ch, 0),
+                                    dv16(I, X + 1, Y + 1, ch, 0), 0.f);
+                        gy[k] = bil(w, dv16(I, X, Y, ch, 1), dv16(I, X + 1, Y, ch, 1), dv16(I, X, Y + 1, ch, 1),
+                                    dv16(I, X + 1, Y + 1, ch, 1), 0.f);
                     }
                     const float a = v == 2 ? gy[k] : gx[k], b = v == 0 ? gx[k] : gy[k];
                     acc = fmaf(a, b, acc);
                 }
-                col[x] = acc;
+                col[e] = acc;
             }
             float t = col[0];
-            for (int x = 1; x < WW; ++x) t += col[x];
+            for (int e = 1; e < WE; ++e) t += col[e];
             s[v] = t;
         }
         const float A11 = s[0] * FLT_SCALE, A12 = s[1] * FLT_SCALE, A22 = s[2] * FLT_SCALE;
@@ -289,19 +319,20 @@ static void lk16_point(const orc16_job* jb, int i, float* buf)
             weights16(nextx - inx, nexty - iny, w);
             float b[2];
             for (int v = 0; v < 2; ++v) {
-                for (int x = 0; x < WW; ++x) {
+                for (int e = 0; e < WE; ++e) {
+                    const int x = e / cn, ch = e - x * cn;
                     float acc = 0.f;
                     for (int r = 0; r < WH; ++r) {
                         const int X = inx + x, Y = iny + r;
-                        const size_t k = (size_t)r * WW + x;
-                        const float d = bil(w, px16(J, X, Y), px16(J, X + 1, Y), px16(J, X, Y + 1),
-                                            px16(J, X + 1, Y + 1), -iv[k]);
+                        const size_t k = (size_t)r * WE + e;
+                        const float d = bil(w, px16(J, X, Y, ch), px16(J, X + 1, Y, ch), px16(J, X, Y + 1, ch),
+                                            px16(J, X + 1, Y + 1, ch), -iv[k]);
                         acc = fmaf(d, v == 0 ? gx[k] : gy[k], acc);
                     }
-                    col[x] = acc;
+                    col[e] = acc;
                 }
                 float t = col[0];
-                for (int x = 1; x < WW; ++x) t += col[x];
+                for (int e = 1; e < WE; ++e) t += col[e];
                 b[v] = t * (32.f * FLT_SCALE);
             }
             const float ddx = (A12 * b[1] - A22 * b[0]) * D;
@@ -326,18 +357,20 @@ static void lk16_point(const orc16_job* jb, int i, float* buf)
                 status = 0;
             } else {
                 weights16(npx - inx, npy - iny, w);
-                for (int x = 0; x < WW; ++x) {
-                    float e = 0.f;
+                for (int e = 0; e < WE; ++e) {
+                    const int x = e / cn, ch = e - x * cn;
+                    float ev = 0.f;
                     for (int r = 0; r < WH; ++r) {
                         const int X = inx + x, Y = iny + r;
-                        e += fabsf(bil(w, px16(J, X, Y), px16(J, X + 1, Y), px16(J, X, Y + 1), px16(J, X + 1, Y + 1),
-                                       -iv[(size_t)r * WW + x]));
+                        ev += fabsf(bil(w, px16(J, X, Y, ch), px16(J, X + 1, Y, ch), px16(J, X, Y + 1, ch),
+                                        px16(J, X + 1, Y + 1, ch), -iv[(size_t)r * WE + e]));
                     }
-                    col[x] = e;
+                    col[e] = ev;
                 }
                 float t = col[0];
-                for (int x = 1; x < WW; ++x) t += col[x];
-                errv = (t * 32.f) * (1.f / (float)(32 * WW * WH));
+                for (int e = 1; e < WE; ++e) t += col[e];
+                /* lkpyramid.cpp:690: errval / (32 * winSize.width * cn * winSize.height) */
+                errv = (t * 32.f) * (1.f / (float)(32 * WW * cn * WH));
             }
         }
     }
@@ -351,8 +384,9 @@ static void lk16_point(const orc16_job* jb, int i, float* buf)
 static void* lk16_worker(void* arg)
 {
     const orc16_job* jb = (const orc16_job*)arg;
-    const int area = jb->prm->winW * jb->prm->winH;
-    float* buf = (float*)malloc(sizeof(float) * ((size_t)area * 3 + (size_t)jb->prm->winW));
+    const int cn = lcn(&jb->prev->lv[0]);
+    const int area = jb->prm->winW * cn * jb->prm->winH;
+    float* buf = (float*)malloc(sizeof(float) * ((size_t)area * 3 + (size_t)jb->prm->winW * cn));
     for (int i = jb->begin; i < jb->end; ++i) lk16_point(jb, i, buf);
     free(buf);
     return NULL;
@@ -369,7 +403,8 @@ int orc16_lk(const orc16_pyr* prev, const orc16_pyr* next, const float* prevPts,
     if (next->nlevels - 1 < maxLevel) maxLevel = next->nlevels - 1;
     for (int l = 0; l <= maxLevel; ++l)
         if (prev->lv[l].w != next->lv[l].w || prev->lv[l].h != next->lv[l].h || !prev->lv[l].d ||
-            prev->lv[l].f32 != next->lv[l].f32)
+            prev->lv[l].f32 != next->lv[l].f32 || lcn(&prev->lv[l]) != lcn(&next->lv[l]) ||
+            (lcn(&prev->lv[l]) > 1 && !prev->lv[l].f32))
             return -2;
     const double eps = prm->epsilon < 0. ? 0. : (prm->epsilon > 10. ? 10. : prm->epsilon);
     int nth = prm->nthreads > 0 ? prm->nthreads : 1;

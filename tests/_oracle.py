@@ -157,7 +157,8 @@ def lk(prev: Pyramid, nxt: Pyramid, pts: np.ndarray, win=(21, 21), max_level=3, 
 # ---- the fp16 pixel path (oracle/klt16_oracle.c) ------------------------------
 
 class Level16(C.Structure):
-    _fields_ = [("px", C.c_void_p), ("d", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("f32", C.c_int)]
+    _fields_ = [("px", C.c_void_p), ("d", C.c_void_p), ("w", C.c_int), ("h", C.c_int), ("f32", C.c_int),
+                ("cn", C.c_int)]
 
 
 class OPyr16(C.Structure):
@@ -171,6 +172,9 @@ def _lib16():
         lib.orc16_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         lib.orc32_pyr_down.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
         lib.orc32_scharr.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.orc32_pyr_down_cn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                          C.c_int]
+        lib.orc32_scharr_cn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         lib.orc16_lk.restype = C.c_int
         lib.orc16_lk.argtypes = [C.POINTER(OPyr16), C.POINTER(OPyr16), C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_int, C.POINTER(LkParams), C.c_void_p]
@@ -199,22 +203,26 @@ def scharr16(img: np.ndarray) -> np.ndarray:
 
 
 def pyr_down32(img: np.ndarray) -> np.ndarray:
-    """the fp32 pixel path's pyrDown (pyr_down16's order, no rounding)."""
+    """the fp32 pixel path's pyrDown (pyr_down16's order, no rounding); (H, W)
+    or (H, W, cn) interleaved channels, each filtered on its own."""
     lib = _lib16()
     img = np.ascontiguousarray(img, dtype=np.float32)
-    h, w = img.shape
-    out = np.empty(((h + 1) // 2, (w + 1) // 2), dtype=np.float32)
-    lib.orc32_pyr_down(_ptr(img), w, h, w, _ptr(out), out.shape[1], out.shape[0], out.shape[1])
+    h, w = img.shape[:2]
+    cn = 1 if img.ndim == 2 else img.shape[2]
+    out = np.empty(((h + 1) // 2, (w + 1) // 2) + img.shape[2:], dtype=np.float32)
+    lib.orc32_pyr_down_cn(_ptr(img), w, h, w * cn, cn, _ptr(out), out.shape[1], out.shape[0], out.shape[1] * cn)
     return out
 
 
 def scharr32(img: np.ndarray) -> np.ndarray:
-    """calcSharrDeriv's formula in fp32 on an fp32 level: (H, W, 2) float32 (Ix, Iy)."""
+    """calcSharrDeriv's formula in fp32 on an fp32 level: (H, W, 2) float32 (Ix, Iy);
+    (H, W, cn) interleaved channels -> (H, W, 2 cn), (Ix_c, Iy_c) per channel."""
     lib = _lib16()
     img = np.ascontiguousarray(img, dtype=np.float32)
-    h, w = img.shape
-    out = np.empty((h, w, 2), dtype=np.float32)
-    lib.orc32_scharr(_ptr(img), w, h, w, _ptr(out))
+    h, w = img.shape[:2]
+    cn = 1 if img.ndim == 2 else img.shape[2]
+    out = np.empty((h, w, 2 * cn), dtype=np.float32)
+    lib.orc32_scharr_cn(_ptr(img), w, h, w * cn, cn, _ptr(out))
     return out
 
 
@@ -222,7 +230,8 @@ class Pyramid16:
     """fp16 oracle pyramid: levels (float16) and their fp16 derivative planes;
     the level rule of cv::buildOpticalFlowPyramid (lkpyramid.cpp:782-787).
     f32=True: the fp32 pixel path (float32 levels and derivative pairs; a
-    uint8 / uint16 / float32 frame converts exactly)."""
+    uint8 / uint16 / float32 frame converts exactly); an (H, W, cn) frame
+    (f32 only) gives interleaved cn-channel levels."""
 
     def __init__(self, img: np.ndarray, win=(21, 21), max_level=3, f32: bool = False):
         dt = np.float32 if f32 else np.float16
@@ -237,10 +246,12 @@ class Pyramid16:
             self.levels.append(down(self.levels[-1]))
         self.derivs = [sch(L) for L in self.levels]
         self.nlevels = len(self.levels)
+        self.cn = 1 if l0.ndim == 2 else l0.shape[2]
+        assert self.cn == 1 or f32, "multi-channel frames: the fp32 pixel path only"
         self.p = OPyr16()
         self.p.nlevels = self.nlevels
         for i, (L, D) in enumerate(zip(self.levels, self.derivs)):
-            self.p.lv[i] = Level16(L.ctypes.data, D.ctypes.data, L.shape[1], L.shape[0], int(f32))
+            self.p.lv[i] = Level16(L.ctypes.data, D.ctypes.data, L.shape[1], L.shape[0], int(f32), self.cn)
 
 
 def lk16(prev: Pyramid16, nxt: Pyramid16, pts: np.ndarray, win=(21, 21), max_level=3, max_count=30, eps=0.01,

@@ -68,6 +68,44 @@ int main(int argc, char** argv)
             std::printf("fp16 tracked-correctly %d\n", good16);
             if (good16 * 10 < n * 8 || P.depth() != TBDK_DEPTH_16F) return 7;
         }
+        {  // CV_32FC3 / CV_16UC4 frames through the typed calc (the fp32 pixel path, cn channels)
+            std::vector<uint8_t> hb((size_t)W * H);
+            (void)hipMemcpy(hb.data(), d1, hb.size(), hipMemcpyDeviceToHost);
+            std::vector<float> fa((size_t)W * H * 3), fb3((size_t)W * H * 3);
+            std::vector<uint16_t> ua((size_t)W * H * 4), ub((size_t)W * H * 4);
+            for (size_t k = 0; k < (size_t)W * H; ++k) {
+                const float va = h[k], vb = hb[k];
+                fa[3 * k] = va, fa[3 * k + 1] = 0.5f * va + 10.f, fa[3 * k + 2] = 255.f - va;
+                fb3[3 * k] = vb, fb3[3 * k + 1] = 0.5f * vb + 10.f, fb3[3 * k + 2] = 255.f - vb;
+                for (int c = 0; c < 4; ++c) {
+                    ua[4 * k + c] = (uint16_t)(h[k] * 257 / (c + 1));
+                    ub[4 * k + c] = (uint16_t)(hb[k] * 257 / (c + 1));
+                }
+            }
+            void *dfa, *dfb, *dua, *dub;
+            if (hipMalloc(&dfa, fa.size() * 4) || hipMalloc(&dfb, fb3.size() * 4) || hipMalloc(&dua, ua.size() * 2) ||
+                hipMalloc(&dub, ub.size() * 2))
+                return 4;
+            (void)hipMemcpy(dfa, fa.data(), fa.size() * 4, hipMemcpyHostToDevice);
+            (void)hipMemcpy(dfb, fb3.data(), fb3.size() * 4, hipMemcpyHostToDevice);
+            (void)hipMemcpy(dua, ua.data(), ua.size() * 2, hipMemcpyHostToDevice);
+            (void)hipMemcpy(dub, ub.data(), ub.size() * 2, hipMemcpyHostToDevice);
+            const tbdk::GpuMatView views[2][2] = {
+                {{dfa, W, H, W * 12, tbdk::DEPTH_32F, 3}, {dfb, W, H, W * 12, tbdk::DEPTH_32F, 3}},
+                {{dua, W, H, W * 8, tbdk::DEPTH_16U, 4}, {dub, W, H, W * 8, tbdk::DEPTH_16U, 4}}};
+            for (int t = 0; t < 2; ++t) {
+                lk->calc(views[t][0], views[t][1], pts, nxt, st, nullptr, n);
+                (void)hipMemcpy(p1.data(), nxt, 8 * (size_t)n, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(s.data(), st, n, hipMemcpyDeviceToHost);
+                int goodc = 0;
+                for (int i = 0; i < n; ++i)
+                    if (s[i] && std::abs(p1[2 * i] - p0[2 * i] - 1.5f) < 0.1f &&
+                        std::abs(p1[2 * i + 1] - p0[2 * i + 1] + 0.5f) < 0.1f)
+                        ++goodc;
+                std::printf("%s tracked-correctly %d\n", t == 0 ? "32FC3" : "16UC4", goodc);
+                if (goodc * 10 < n * 8) return 12;
+            }
+        }
         // dense Farneback through the facade: the interior flow is the shift
         float* flow;
         if (hipMalloc(&flow, (size_t)W * H * 8)) return 4;

@@ -14,6 +14,8 @@ identities the reference's arithmetic implies:
     and its error is gray's x 1/cn; permuting the channels changes nothing;
   * in the reference's SSE2 order, the cn copies (g, g, g) track as gray up to
     the float rounding of the sums."""
+import os
+
 import numpy as np
 import pytest
 
@@ -106,3 +108,64 @@ def test_multichannel_known_translation(dx, dy):
     ok = st == 1
     assert ok.mean() > 0.95
     assert np.abs(nxt[ok] - (pts[ok] + np.float32([dx, dy]))).max() < 0.05
+
+
+# ---- the fp32 pixel path on cn channels (oracle/klt16_oracle.c, CV_16UC3/C4 and
+# CV_32FC3/C4 frames of cv::cuda::SparsePyrLKOpticalFlow, cudaoptflow/src/pyrlk.cpp:197-205)
+
+
+def _f32_frames(cn, seed=5, w=160, h=120):
+    a, b = _frames(seed, w, h)
+    rng = np.random.default_rng(seed)
+    noise = [rng.normal(0, 3, a.shape).astype(np.float32) for _ in range(cn - 1)]
+    fa = np.stack([a.astype(np.float32)] + [a * 0.5 + 20 + n for n in noise], 2).astype(np.float32)
+    fb = np.stack([b.astype(np.float32)] + [b * 0.5 + 20 + n for n in noise], 2).astype(np.float32)
+    return fa, fb
+
+
+@pytest.mark.parametrize("cn", [2, 3, 4])
+def test_f32_pyramid_and_scharr_are_per_channel(cn):
+    fa, _ = _f32_frames(cn)
+    P = O.Pyramid16(fa, (21, 21), 3, f32=True)
+    Ps = [O.Pyramid16(np.ascontiguousarray(fa[:, :, c]), (21, 21), 3, f32=True) for c in range(cn)]
+    assert P.nlevels == Ps[0].nlevels and P.cn == cn
+    for lvl in range(P.nlevels):
+        for c in range(cn):
+            assert np.array_equal(P.levels[lvl][:, :, c].view(np.uint32), Ps[c].levels[lvl].view(np.uint32))
+            assert np.array_equal(P.derivs[lvl][:, :, 2 * c:2 * c + 2].view(np.uint32),
+                                  Ps[c].derivs[lvl].view(np.uint32))
+
+
+@pytest.mark.parametrize("cn", [2, 3, 4])
+def test_f32_constant_channels_track_exactly_as_gray(cn):
+    """a constant channel's interpolated derivatives are exactly 0, so its G and b
+    terms are +0 and every running sum keeps its value: points, status,
+    iterations and minEig equal the one-channel run bit for bit, wherever the
+    constant channels sit"""
+    a, b = _frames()
+    fa, fb = a.astype(np.float32), b.astype(np.float32)
+    pts = grid_points(a.shape[0], a.shape[1], 9, 4)
+    g = O.lk16(O.Pyramid16(fa, f32=True), O.Pyramid16(fb, f32=True), pts)
+    gm = O.lk16(O.Pyramid16(fa, f32=True), O.Pyramid16(fb, f32=True), pts, flags=O.OPTFLOW_LK_GET_MIN_EIGENVALS)
+    z = np.full(a.shape, 77.25, np.float32)
+    for pos in range(cn):
+        chans_a, chans_b = [z] * cn, [z] * cn
+        chans_a[pos], chans_b[pos] = fa, fb
+        A, B = O.Pyramid16(np.stack(chans_a, 2), f32=True), O.Pyramid16(np.stack(chans_b, 2), f32=True)
+        m = O.lk16(A, B, pts)
+        assert np.array_equal(m[0].view(np.uint32), g[0].view(np.uint32)), pos
+        assert np.array_equal(m[1], g[1]) and np.array_equal(m[3], g[3])
+        mm = O.lk16(A, B, pts, flags=O.OPTFLOW_LK_GET_MIN_EIGENVALS)
+        assert np.array_equal(mm[2].view(np.uint32), gm[2].view(np.uint32))
+
+
+@pytest.mark.parametrize("cn,dx,dy", [(3, 3, -2), (4, -2, 1)])
+def test_f32_multichannel_known_translation(cn, dx, dy):
+    img = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "basketball_pair.npz"))["a"]
+    a, b = shifted_pair(img, dx, dy)
+    fa = np.stack([a.astype(np.float32) * (c + 1) / cn for c in range(cn)], 2).astype(np.float32)
+    fb = np.stack([b.astype(np.float32) * (c + 1) / cn for c in range(cn)], 2).astype(np.float32)
+    pts = grid_points(a.shape[0], a.shape[1], 24, 48)
+    nx, st, err, _ = O.lk16(O.Pyramid16(fa, f32=True), O.Pyramid16(fb, f32=True), pts)
+    e = np.abs(nx - (pts + np.float32([dx, dy]))).max(1)
+    assert st.mean() > 0.95 and np.median(e[st == 1]) < 0.05

@@ -22,7 +22,7 @@ for o in range(NOBJ):
 base = np.concatenate(pts).astype(np.float32)
 P0 = klt.Pyramid(ctx, W, H, 2, derivs=False).build(frames[0])
 P1 = klt.Pyramid(ctx, W, H, 2, derivs=False).build(frames[1])
-lk = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30)
+lk = klt.SparsePyrLKOpticalFlow((21, 21), 2, int(os.environ.get("LK_ITERS", "30")))  # criteria maxCount
 out = []
 for n in [int(v) for v in (sys.argv[1:] or ["6000", "12000", "18000", "32000", "131000"])]:
     d = torch.from_numpy(np.resize(base, (n, 2)).astype(np.float32)).cuda()
@@ -37,4 +37,4 @@ for n in [int(v) for v in (sys.argv[1:] or ["6000", "12000", "18000", "32000", "
     c, ms = ctx.timing_query("lk_sparse")
     ctx.timing_enable(False)
     out.append(f"n {n}: {ms / c * 1000:.1f} us")
-print(os.path.basename(os.environ.get("TBDK_LIB", "libtbdk.so")), "; ".join(out), flush=True)
+print(os.path.basename(os.environ.get("TBDK_LIB", "libtbdk.so")), "maxCount", lk.iters, "; ".join(out), flush=True)
