@@ -398,7 +398,17 @@ def cpu_baseline_line(frames_host, gt, args, restore_affinity=None):
         fps1, n1 = cpu_baseline(frames_host, gt, args, args.cpu_baseline_seconds_1t, 1)
     finally:
         os.sched_setaffinity(0, pinned)
-    return {"value": round(fps, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+    cal = None
+    try:  # the restatement against the real reference on a shape-matched input
+        c = json.load(open(os.path.join(ROOT, "profiles", "r04_cpu_calibration.json")))["results"]
+        cal = {"restatement_over_reference_lk_1t": c["lk_1080p_128x256_1t_ms"]["ratio"],
+               "restatement_over_reference_lk_8t": c["lk_1080p_128x256_8t_ms"]["ratio"],
+               "source": "profiles/r04_cpu_calibration.json (tools/calibrate_cpu.py vs BASELINE.md §2)",
+               "note": "PyrLK per call, 1080p x 32k points: the C restatement is this many times slower than the "
+                       "reference's SSE2 build (shape-matched input; the restatement's input iterates more)"}
+    except (OSError, KeyError, ValueError):
+        pass
+    return {"value": round(fps, 3), "unit": "frames/s", "cores": cores, "kind": "port", "calibration": cal,
             "value_1_thread": round(fps1, 4), "frames_1_thread": n1, "host": info,
             "build": "oracle/ sources -O3 -march=native -ffp-contract=off, built on this host" if lib else
                      "oracle/liboracle.so as shipped (-O2; the native build failed)",

@@ -663,8 +663,16 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         return TBDK_OK;
     };
-    rc = launch_early_gftt();
-    if (rc != TBDK_OK) return rc;
+    // ctx option tbd_early_order: 0 launches the early GFTT first in the step, 1
+    // right after the critical (refreshed-set) PyrLK, 2 after the fit and the
+    // next pyramid, just before the host waits (its host work then runs while
+    // the device tracks; the early GFTT stream still waits for this frame's
+    // pyramid, taken above)
+    const int early_order = t->ctx->opt_tbd_early_order;
+    if (early_order == 0) {
+        rc = launch_early_gftt();
+        if (rc != TBDK_OK) return rc;
+    }
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents, h_lists) were last read by uploads issued before the
@@ -750,6 +758,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                              nB * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + nA);
             if (rc != TBDK_OK) return rc;
         }
+        if (early_order == 1) {
+            rc = launch_early_gftt();
+            if (rc != TBDK_OK) return rc;
+        }
         hipError_t e = hipSuccess;  // zero-copy without a look-ahead wait sets it nowhere below
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
             e = hipStreamWaitEvent(s, t->la_done, 0);
@@ -768,6 +780,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
         if (next) {  // runs on the device while this step waits for the fit and tracks
             rc = enqueue_next_pyr();
+            if (rc != TBDK_OK) return rc;
+        }
+        if (early_order == 2) {
+            rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
         }
         auto ts0 = clk::now();
@@ -899,6 +915,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             t->la_lk = true;
         }
     } else {
+        if (early_order != 0) {
+            rc = launch_early_gftt();
+            if (rc != TBDK_OK) return rc;
+        }
         if (next) {
             // the next pyramid is rebuilt over the previous frame's, which the
             // previous step's look-ahead PyrLK (on la_s) may still be reading
