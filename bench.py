@@ -492,10 +492,23 @@ def farneback_secondary(ctx, args, device, cpu: bool):
 
 
 def pyr_f16_bytes(w: int, h: int, nlevels: int) -> int:
-    """Algorithmic HBM bytes of one fp16 pyramid build from a u8 frame: frame
-    read (1 B/px) and level 0 written (2 B/px); per further level the previous
-    level read and the level written (2 B/px each); per level its fp16 (Ix, Iy)
-    plane written (4 B/px) from the level read (2 B/px)."""
+    """Algorithmic HBM bytes of one fp16 pyramid build from a u8 frame, the
+    bytes that must move: the frame read once (1 B/px), every level written
+    once (2 B/px) and every level above 0 read once for the next level and its
+    own Scharr plane (2 B/px), every fp16 (Ix, Iy) plane written (4 B/px).
+    (Rounds 1-3 counted level 0 and each level's Scharr source as separate
+    reads, as the one-launch-per-plane build does: pyr_f16_bytes_per_plane.)"""
+    sizes = []
+    for _ in range(nlevels):
+        sizes.append(w * h)
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return sizes[0] + 2 * sum(sizes) + 2 * sum(sizes[1:]) + 4 * sum(sizes)
+
+
+def pyr_f16_bytes_per_plane(w: int, h: int, nlevels: int) -> int:
+    """the rounds 1-3 count: frame read and level 0 written (3 B/px), per
+    further level the previous level read and the level written, per level its
+    Scharr source read and plane written (6 B/px)"""
     sizes = []
     for _ in range(nlevels):
         sizes.append(w * h)
@@ -569,7 +582,10 @@ def lk_f16_secondary(ctx, args, device, cpu: bool):
                         "note": "VALU-bound (fp32 FMA on fp16 taps, no MFMA); algorithmic flops per SURVEY.md §8(d)"},
            "roofline_pyramid": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb,
-                                "kernel": "pyr_build (fp16 levels + fp16 Scharr planes)"},
+                                "bytes_per_launch_per_plane_count": pyr_f16_bytes_per_plane(w, h, nlev),
+                                "avg_us": round(pk["avg_us"], 2),
+                                "kernel": "pyr_build (fp16 levels + fp16 Scharr planes; klt_pyr_fp.hip, "
+                                          f"{nlev} role-split launches)"},
            "kernels": kern}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))

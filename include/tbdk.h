@@ -113,7 +113,13 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       launch per level; 2 computes levels 0, 1 and 2 in one tiled launch (the
  *       frame read once through LDS; pyramids whose level pads exceed size - 2
  *       take 1; measured slower, kept for A/B runs); 0: one launch per level
- *       (results equal).
+ *       (results equal).  fp16 / fp32 pyramids: >= 1 builds L levels in L
+ *       role-split launches (level 0's copy, level 1 and level 0's Scharr
+ *       plane from the frame, then level i and plane i-1 from level i-1);
+ *       0 takes one launch per level and one for every plane (results equal).
+ *   "pyr_rows" (1/2/4, default 4): rows per thread of the u8 two-role
+ *       launch (pyr_fuse 1): level 0's 16-byte copies of that many rows, level
+ *       1 in row pairs sharing their 7 frame rows when > 1 (results equal).
  *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;
@@ -161,6 +167,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       system-scope flag in pinned memory that the host polls, instead of an
  *       event recorded behind the fit (whose marker held the next frame's
  *       pyramid back; results equal).
+ *   "tbd_early_order" (0/1/2, default 2): where a step launches its early
+ *       GFTT: 0 first, 1 after the critical refreshed-set PyrLK, 2 after the
+ *       fit and the next frame's pyramid, before the host waits for the fit
+ *       (its host-side setup then overlaps the GPU's critical chain; results
+ *       equal).
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
  *       pyramids carry Scharr derivative planes and PyrLK reads them instead of
  *       deriving the window's values (results equal; A/B runs).

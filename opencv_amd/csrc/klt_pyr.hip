@@ -192,7 +192,9 @@ struct PyrRolesArgs {
     int nA;              // blocks of role A (role B: the rest)
     int wa4, wb4;        // items per padded row of roles A (4 or 16 bytes) and B (4 pixels)
     int a16;             // role A copies 16 bytes per thread (source, copy and pitches 16-byte aligned, pad % 16 == 0)
+    int ra, rb;          // rows per thread: role A (16-byte path, 1..kRowsA), role B (1 or 2)
 };
+constexpr int kRowsA = 4;
 
 __device__ __forceinline__ int pyr5(int a, int b, int c, int d, int e) { return c * 6 + (b + d) * 4 + a + e; }
 
@@ -213,32 +215,96 @@ __device__ __forceinline__ int pyr_down_at(const PyrRolesArgs& a, int y, int x)
 
 __device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 255u); }
 
+// role B's fast-path horizontal taps: bytes c0 .. c0 + 10 of a row (c0 = 2 mod 4)
+// as the [1 4 6 4 1] sums of four level-1 columns
+__device__ __forceinline__ void pyr_row_h4(const uint8_t* row, int base, int* hs)
+{
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(row + base);
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    const uint32_t s0 = __builtin_amdgcn_alignbyte(w1, w0, 2), s1 = __builtin_amdgcn_alignbyte(w2, w1, 2),
+                   s2 = __builtin_amdgcn_alignbyte(w3, w2, 2);
+    int px[11];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        px[k] = byte_of(s0, k);
+        px[4 + k] = byte_of(s1, k);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) px[8 + k] = byte_of(s2, k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hs[k] = pyr5(px[2 * k], px[2 * k + 1], px[2 * k + 2], px[2 * k + 3], px[2 * k + 4]);
+}
+
+// role B, one padded level-1 row py, 4 pixels from padded column 4t
+__device__ __forceinline__ void pyr_role_b_row(const PyrRolesArgs& a, int py, int t)
+{
+    const int y = reflect101(py - a.pad1, a.h1);
+    const int x0 = reflect101(4 * t - a.pad1, a.w1);
+    uint32_t v = 0;
+    // fast path: four consecutive in-image pixels whose taps need no reflection.
+    // x0 even (the pads are multiples of 16) puts the taps' first byte c0 at
+    // offset 2 of an aligned dword, so the four aligned dwords read per row end
+    // with the dword holding byte c0 + 10 < sw: no byte past the row's last
+    // in-image dword is touched (a frame ending at its allocation's last byte
+    // with sw % 4 == 0 is safe; sw % 4 != 0 needs a dword pitch, a.vec).
+    const bool fast = a.vec && 2 * y - 2 >= 0 && 2 * y + 2 < a.sh && 4 * t - a.pad1 == x0 && 2 * x0 - 2 >= 0 &&
+                      2 * x0 + 8 < a.sw && x0 + 3 < a.w1 && (x0 & 1) == 0;
+    if (fast) {
+        const int base = (2 * x0 - 2) & ~3;
+        int hs[5][4];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pyr_row_h4(a.src + (size_t)(2 * y + j - 2) * a.spitch, base, hs[j]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v |= (uint32_t)((pyr5(hs[0][k], hs[1][k], hs[2][k], hs[3][k], hs[4][k]) + 128) >> 8) << (8 * k);
+    } else {
+#pragma nounroll
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)pyr_down_at(a, y, reflect101(4 * t + k - a.pad1, a.w1)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(a.d1 + (size_t)py * a.p1 + 4 * t) = v;
+}
+
 __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
 {
     int b = blockIdx.x;
     const int tid = threadIdx.x;
-    if (b < a.nA) {  // ---- role A: the padded copy of the source
+    if (b < a.nA) {  // ---- role A: the padded copy of the source, a.ra rows per thread
         const int item = b * kRoleThreads + tid;
-        const int py = item / a.wa4, t = item - py * a.wa4;
-        if (py >= a.sh + 2 * a.cpad) return;
-        const uint8_t* srow = a.src + (size_t)reflect101(py - a.cpad, a.sh) * a.spitch;
-        if (a.a16) {  // 16 bytes per thread: one dwordx4 load and store in the frame's interior
+        const int pg = item / a.wa4, t = item - pg * a.wa4;
+        const int hp = a.sh + 2 * a.cpad;
+        if (a.a16) {  // 16 bytes per row: dwordx4 loads (all rows first) and stores in the frame's interior
             const int x0 = 16 * t - a.cpad;
-            uint4 v;
+            const int py0 = pg * a.ra;
+            if (py0 >= hp) return;
+            const int nr = hp - py0 < a.ra ? hp - py0 : a.ra;
+            uint4 v[kRowsA];
             if (x0 >= 0 && x0 + 15 < a.sw) {
-                v = *reinterpret_cast<const uint4*>(srow + x0);
-            } else {
-                uint32_t q[4];
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    q[d] = 0;
-                    for (int k = 0; k < 4; ++k) q[d] |= (uint32_t)srow[reflect101(x0 + 4 * d + k, a.sw)] << (8 * k);
+                for (int r = 0; r < kRowsA; ++r)
+                    if (r < nr)
+                        v[r] = *reinterpret_cast<const uint4*>(
+                            a.src + (size_t)reflect101(py0 + r - a.cpad, a.sh) * a.spitch + x0);
+            } else {
+                for (int r = 0; r < nr; ++r) {
+                    const uint8_t* srow = a.src + (size_t)reflect101(py0 + r - a.cpad, a.sh) * a.spitch;
+                    uint32_t q[4];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        q[d] = 0;
+                        for (int k = 0; k < 4; ++k)
+                            q[d] |= (uint32_t)srow[reflect101(x0 + 4 * d + k, a.sw)] << (8 * k);
+                    }
+                    v[r] = make_uint4(q[0], q[1], q[2], q[3]);
                 }
-                v = make_uint4(q[0], q[1], q[2], q[3]);
             }
-            *reinterpret_cast<uint4*>(a.copy + (size_t)py * a.cpitch + 16 * t) = v;
+#pragma unroll
+            for (int r = 0; r < kRowsA; ++r)
+                if (r < nr) *reinterpret_cast<uint4*>(a.copy + (size_t)(py0 + r) * a.cpitch + 16 * t) = v[r];
             return;
         }
+        const int py = pg;  // 4 bytes per thread, one row
+        if (py >= hp) return;
+        const uint8_t* srow = a.src + (size_t)reflect101(py - a.cpad, a.sh) * a.spitch;
         const int x0 = 4 * t - a.cpad;
         uint32_t v;
         if (a.vec && (x0 & 3) == 0 && x0 >= 0 && x0 + 3 < a.sw) {
@@ -251,58 +317,42 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
         return;
     }
     b -= a.nA;
-    {  // ---- role B: the level below, 4 pixels per thread
+    {  // ---- role B: the level below, 4 pixels of a.rb rows per thread
         const int item = b * kRoleThreads + tid;
-        const int py = item / a.wb4, t = item - py * a.wb4;
-        if (py >= a.h1 + 2 * a.pad1) return;
-        const int y = reflect101(py - a.pad1, a.h1);
-        const int x0 = reflect101(4 * t - a.pad1, a.w1);
-        uint32_t v = 0;
-        // fast path: four consecutive in-image pixels whose taps need no reflection.
-        // x0 even (the pads are multiples of 16) puts the taps' first byte c0 at
-        // offset 2 of an aligned dword, so the four aligned dwords read per row end
-        // with the dword holding byte c0 + 10 < sw: no byte past the row's last
-        // in-image dword is touched (a frame ending at its allocation's last byte
-        // with sw % 4 == 0 is safe; sw % 4 != 0 needs a dword pitch, a.vec).
-        const bool fast = a.vec && 2 * y - 2 >= 0 && 2 * y + 2 < a.sh && 4 * t - a.pad1 == x0 && 2 * x0 - 2 >= 0 &&
-                          2 * x0 + 8 < a.sw && x0 + 3 < a.w1 && (x0 & 1) == 0;
-        if (fast) {
-            const int c0 = 2 * x0 - 2, base = c0 & ~3, o = 2;  // c0 - base
-            int h[4] = {0, 0, 0, 0};
+        const int pg = item / a.wb4, t = item - pg * a.wb4;
+        const int hp1 = a.h1 + 2 * a.pad1;
+        const int py0 = pg * a.rb;
+        if (py0 >= hp1) return;
+        if (a.rb == 2) {
+            // two in-image rows y, y + 1 share their 7 source rows
+            const int y = py0 - a.pad1, x0 = 4 * t - a.pad1;
+            if (a.vec && y >= 1 && 2 * y + 4 < a.sh && y + 1 < a.h1 && x0 >= 1 && 2 * x0 + 8 < a.sw &&
+                x0 + 3 < a.w1 && (x0 & 1) == 0) {
+                const int base = (2 * x0 - 2) & ~3;
+                int hs[7][4];
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(a.src + (size_t)(2 * y + j - 2) * a.spitch + base);
-                const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-                // bytes c0 .. c0 + 10 as three dwords
-                const uint32_t s0 = __builtin_amdgcn_alignbyte(w1, w0, o), s1 = __builtin_amdgcn_alignbyte(w2, w1, o),
-                               s2 = __builtin_amdgcn_alignbyte(w3, w2, o);
-                int px[11];
+                for (int j = 0; j < 7; ++j) pyr_row_h4(a.src + (size_t)(2 * y + j - 2) * a.spitch, base, hs[j]);
+                uint32_t v0 = 0, v1 = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    px[k] = byte_of(s0, k);
-                    px[4 + k] = byte_of(s1, k);
+                    v0 |= (uint32_t)((pyr5(hs[0][k], hs[1][k], hs[2][k], hs[3][k], hs[4][k]) + 128) >> 8) << (8 * k);
+                    v1 |= (uint32_t)((pyr5(hs[2][k], hs[3][k], hs[4][k], hs[5][k], hs[6][k]) + 128) >> 8) << (8 * k);
                 }
-#pragma unroll
-                for (int k = 0; k < 3; ++k) px[8 + k] = byte_of(s2, k);
-                const int kj = j == 2 ? 6 : (j == 1 || j == 3) ? 4 : 1;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h[k] += kj * pyr5(px[2 * k], px[2 * k + 1], px[2 * k + 2], px[2 * k + 3],
-                                                                px[2 * k + 4]);
+                *reinterpret_cast<uint32_t*>(a.d1 + (size_t)py0 * a.p1 + 4 * t) = v0;
+                *reinterpret_cast<uint32_t*>(a.d1 + (size_t)(py0 + 1) * a.p1 + 4 * t) = v1;
+                return;
             }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v |= (uint32_t)((h[k] + 128) >> 8) << (8 * k);
-        } else {
-#pragma nounroll
-            for (int k = 0; k < 4; ++k)
-                v |= (uint32_t)pyr_down_at(a, y, reflect101(4 * t + k - a.pad1, a.w1)) << (8 * k);
+            pyr_role_b_row(a, py0, t);
+            if (py0 + 1 < hp1) pyr_role_b_row(a, py0 + 1, t);
+            return;
         }
-        *reinterpret_cast<uint32_t*>(a.d1 + (size_t)py * a.p1 + 4 * t) = v;
-        return;
+        pyr_role_b_row(a, py0, t);
     }
 }
 
 // levels 0 and 1 of pyr from the frame in one launch
-static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_pyr& pyr, hipStream_t s)
+static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_pyr& pyr, hipStream_t s, int rows_a,
+                                    int rows_b)
 {
     PyrRolesArgs a;
     const tbdk_level& S = pyr.lv[0];
@@ -325,8 +375,10 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
               (uintptr_t)S.pitch | (uintptr_t)S.pad) & 15) == 0 && S.pitch >= ((S.width + 2 * S.pad + 15) & ~15);
     a.wa4 = a.a16 ? (S.width + 2 * S.pad + 15) / 16 : (S.width + 2 * S.pad + 3) / 4;
     a.wb4 = (D1.width + 2 * D1.pad + 3) / 4;
-    a.nA = blocks((long)a.wa4 * (S.height + 2 * S.pad));
-    const int nB = blocks((long)a.wb4 * (D1.height + 2 * D1.pad));
+    a.ra = a.a16 ? rows_a : 1;
+    a.rb = rows_b;
+    a.nA = blocks((long)a.wa4 * ((S.height + 2 * S.pad + a.ra - 1) / a.ra));
+    const int nB = blocks((long)a.wb4 * ((D1.height + 2 * D1.pad + a.rb - 1) / a.rb));
     hipLaunchKernelGGL(pyr_build_kernel, dim3(a.nA + nB), dim3(kRoleThreads), 0, s, a);
     return hipGetLastError();
 }
@@ -656,14 +708,15 @@ static hipError_t launch_pyr_fused(const uint8_t* src, int spitch, const tbdk_py
 
 // every level of a u8 pyramid from the frame: levels 0 and 1 in one launch
 // (fuse), or one launch per level
-hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, hipStream_t s)
+hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, hipStream_t s)
 {
     hipError_t e;
     int level = 1;
     if (fuse >= 2 && pyr_fused_ok(pyr)) {
         e = launch_pyr_fused(img, pitch, pyr, s, &level);
     } else if (fuse && pyr.nlevels >= 2) {
-        e = launch_pyr_fuse01(img, pitch, pyr, s);
+        rows = rows < 1 ? 1 : rows > kRowsA ? kRowsA : rows;
+        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1);
         level = 2;
     } else {
         e = launch_pad_copy(img, pitch, pyr.lv[0], s);

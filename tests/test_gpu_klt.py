@@ -127,14 +127,16 @@ def test_pyramid_frame_at_allocation_end(gpu, shape):
 def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
     """ctx option pyr_fuse: 2 (levels 0-2 in one tiled launch: edge tiles, partial
     tiles, the mirrored reflect-101 frames, pads of 32 / 48 / 64), 1 (two-role
-    launch) and 0 (one launch per level): every padded level bit-exact with the
+    launch, 4 / 2 / 1 rows per thread: ctx option pyr_rows) and 0 (one launch
+    per level): every padded level bit-exact with the
     oracle's, levels-only and with derivative planes"""
     K = klt()
     img = np.random.default_rng(sum(shape)).integers(0, 256, shape, dtype=np.uint8)
     R = None
     try:
-        for mode in (2, 1, 0):
+        for mode, rows in ((2, 4), (1, 4), (1, 2), (1, 1), (0, 4)):
             gpu.set_option("pyr_fuse", mode)
+            gpu.set_option("pyr_rows", rows)  # rows per thread of the two-role launch
             for derivs in (False, True):
                 P = K.build_pyramid(to_dev(img), (win, win), maxlev, ctx=gpu, derivs=derivs)
                 torch.cuda.synchronize()
@@ -142,11 +144,12 @@ def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
                     R = O.Pyramid(img, (win, win), maxlev, pad=P.pyr.lv[0].pad)
                 assert P.nlevels == R.nlevels
                 for lvl in range(P.nlevels):
-                    assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"mode {mode} level {lvl}"
+                    assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"mode {mode}/{rows} level {lvl}"
                 if derivs:
-                    assert np.array_equal(P.deriv(0), O.scharr(R.level(0))), f"mode {mode} deriv"
+                    assert np.array_equal(P.deriv(0), O.scharr(R.level(0))), f"mode {mode}/{rows} deriv"
     finally:
         gpu.set_option("pyr_fuse", 1)
+        gpu.set_option("pyr_rows", 4)
 
 
 @pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])

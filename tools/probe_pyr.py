@@ -13,8 +13,10 @@ ctx = klt.Context.get(0)
 for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2), (1920, 1080, 3)):
     fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
     out = []
-    for derivs, fuse in ((False, 2), (False, 1), (False, 0), (True, 2), (True, 1)):
+    for derivs, fuse, rows in ((False, 2, 4), (False, 1, 4), (False, 0, 4), (True, 2, 4), (True, 1, 4), (False, 1, 1),
+                               (False, 1, 2)):
         ctx.set_option("pyr_fuse", fuse)
+        ctx.set_option("pyr_rows", rows)
         P = klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=derivs)
         for _ in range(20):
             P.build(fr[0])
@@ -29,5 +31,7 @@ for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2), (1920, 1080
         ctx.timing_select(None)
         out.append(ms / c * 1000)
     ctx.set_option("pyr_fuse", 1)
-    print(f"{W}x{H} maxLevel {ml}: levels only: tiled {out[0]:6.1f} us, two-role {out[1]:6.1f} us, per level "
-          f"{out[2]:6.1f} us; with Scharr planes: tiled {out[3]:6.1f} us, two-role {out[4]:6.1f} us", flush=True)
+    ctx.set_option("pyr_rows", 4)
+    print(f"{W}x{H} maxLevel {ml}: levels only: tiled {out[0]:6.1f} us, two-role {out[1]:6.1f} us (4 rows/thread; "
+          f"1: {out[5]:6.1f}, 2: {out[6]:6.1f}), per level {out[2]:6.1f} us; with Scharr planes: tiled "
+          f"{out[3]:6.1f} us, two-role {out[4]:6.1f} us", flush=True)
