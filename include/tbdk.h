@@ -119,7 +119,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       0 takes one launch per level and one for every plane (results equal).
  *   "pyr_rows" (1/2/4, default 4): rows per thread of the u8 two-role
  *       launch (pyr_fuse 1): level 0's 16-byte copies of that many rows, level
- *       1 in row pairs sharing their 7 frame rows when > 1 (results equal).
+ *       1 in row pairs sharing their 7 frame rows when > 1; and of the fp16 /
+ *       fp32 role-split launches (copies and Scharr planes that many rows,
+ *       levels in pairs at most; results equal).
  *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;

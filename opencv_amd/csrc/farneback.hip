@@ -655,12 +655,17 @@ constexpr int kFbSlots = kFbStrip + kFbStrip / 4;
 #define TBDK_FB_TK 2  // output columns per horizontal task (2: twice the threads in the solve phase)
 #endif
 constexpr int kFbTK = TBDK_FB_TK;
+// 1 (tuning builds): 4-column horizontal tasks in half-waves, outputs handed
+// to the other half by v_permlane32_swap (requires kFbTK == 2 and the deferred solve)
+#ifndef TBDK_FB_HX
+#define TBDK_FB_HX 0
+#endif
+static_assert(!TBDK_FB_HX || kFbTK == 2, "TBDK_FB_HX takes 2-column solves");
 static_assert(kFbTK == 2 || kFbTK == 4, "tasks of 2 or 4 columns");
-template <int M, bool GAUSS>
+template <int M, bool GAUSS, int TK = kFbTK>
 __device__ __forceinline__ void fb_hsums(const FbIterArgs& a, const float (*vb)[5][kFbSlots], int r, int o0,
-                                         float (&out)[5][kFbTK])
+                                         float (&out)[5][TK])
 {
-    constexpr int TK = kFbTK;
     const int g0 = o0 & ~3, sk = o0 - g0;  // the box sums' group start, slides to o0 (0 or 2)
 #pragma unroll
     for (int ch = 0; ch < 5; ++ch) {
@@ -821,7 +826,7 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
 {
     constexpr int K = 2 * M + 1;
     constexpr int OW = fb_ow(M);
-    constexpr int NQ = (OW + kFbTK - 1) / kFbTK;  // horizontal tasks per row
+    [[maybe_unused]] constexpr int NQ = (OW + kFbTK - 1) / kFbTK;  // horizontal tasks per row
     constexpr int RR = kFbRB + 2 * M;     // M ring rows
     constexpr int VC = 4;                 // centres per thread in the vertical pass
     __shared__ float mr[5 * RR * kFbStrip];
@@ -906,7 +911,32 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
         if (more) fb_rows_b<NR>(a, rs, x, ybase, 2 * M + s0 + kFbRB, half, A, B);
         fb_lds_barrier();
         const int nb = min(kFbRB, nrows - s0);
-#if TBDK_FB_DEFER
+#if TBDK_FB_DEFER && TBDK_FB_HX
+        {
+            // tasks of 4 columns in lanes 0-31 of each wave (half the LDS reads of
+            // two 2-column tasks); v_permlane32_swap hands outputs 2-3 to lanes
+            // 32-63, so every lane still solves 2 (bit-identical sums: the box
+            // sums restart at the same columns)
+            constexpr int NQ4 = (OW + 3) / 4;
+            const int lane = tid & 63, task = (tid >> 6) * 32 + (lane & 31);
+            const bool in = task < nb * NQ4;
+            const int r = in ? task / NQ4 : 0, q = in ? task - r * NQ4 : 0;
+            float o4[5][4];
+            if (lane < 32) fb_hsums<M, GAUSS, 4>(a, vb, r, 4 * q, o4);
+#pragma unroll
+            for (int ch = 0; ch < 5; ++ch) {
+                const auto p2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, o4[ch][0]),
+                                                                 __builtin_bit_cast(unsigned, o4[ch][2]), false, false);
+                const auto p3 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, o4[ch][1]),
+                                                                 __builtin_bit_cast(unsigned, o4[ch][3]), false, false);
+                pend[ch][0] = lane < 32 ? o4[ch][0] : __builtin_bit_cast(float, p2[0]);
+                pend[ch][1] = lane < 32 ? o4[ch][1] : __builtin_bit_cast(float, p3[0]);
+            }
+            pend_o0 = 4 * q + (lane < 32 ? 0 : 2);
+            pend_ok = in && ox0 + pend_o0 < a.w;
+            pend_y = y0 + s0 + r;
+        }
+#elif TBDK_FB_DEFER
         {
             const bool in = tid < nb * NQ;
             const int r = in ? tid / NQ : 0, q = in ? tid - r * NQ : 0;

@@ -56,6 +56,7 @@ struct Job {
     Src s;
     Dst d;
     int ux, rows, bx, b0;  // threads per row, rows, blocks per row, first block
+    int rpt;               // rows per thread (<= kCopyRows / kDownRows / kScharrRows by role)
 };
 
 struct Jobs {
@@ -144,7 +145,7 @@ __device__ __forceinline__ void role_copy(const Job& j, int t, int py0)
 {
     typedef Run<8, KIND> R;
     uint32_t raw[kCopyRows][R::NA];
-    const int nr = j.rows - py0 < kCopyRows ? j.rows - py0 : kCopyRows;
+    const int nr = j.rows - py0 < j.rpt ? j.rows - py0 : j.rpt;
 #pragma unroll
     for (int k = 0; k < kCopyRows; ++k)
         if (k < nr) row_raw<8, KIND>(j.s, py0 + k - j.d.pad, 8 * t - j.d.pad, raw[k]);
@@ -244,7 +245,9 @@ __device__ __forceinline__ void role_down(const Job& j, int t, int py0)
 {
     const int cx = 4 * t - j.d.pad;
     const int y0 = py0 - j.d.pad;
-    if (y0 >= 0 && y0 + 2 <= j.d.h && cx >= 0 && cx + 4 <= j.d.w) {
+    if (j.rpt == 1) {
+        down_row<KIND, F32>(j, t, py0);
+    } else if (y0 >= 0 && y0 + 2 <= j.d.h && cx >= 0 && cx + 4 <= j.d.w) {
         uint32_t raw[7][Run<11, KIND>::NA];
 #pragma unroll
         for (int k = 0; k < 7; ++k) row_raw<11, KIND>(j.s, 2 * y0 - 2 + k, 2 * cx - 2, raw[k]);
@@ -266,10 +269,11 @@ __device__ __forceinline__ void role_scharr(const Job& j, int t, int y0)
     typedef Run<10, KIND> R;
     const int x0 = 8 * t;
     uint32_t raw[kScharrRows + 2][R::NA];
+    const int nr = j.s.h - y0 < j.rpt ? j.s.h - y0 : j.rpt;
 #pragma unroll
-    for (int k = 0; k < kScharrRows + 2; ++k) row_raw<10, KIND>(j.s, y0 - 1 + k, x0 - 1, raw[k]);
+    for (int k = 0; k < kScharrRows + 2; ++k)
+        if (k < nr + 2) row_raw<10, KIND>(j.s, y0 - 1 + k, x0 - 1, raw[k]);
     const int n = j.s.w - x0;
-    const int nr = j.s.h - y0 < kScharrRows ? j.s.h - y0 : kScharrRows;
 #pragma unroll
     for (int rr = 0; rr < kScharrRows; ++rr) {
         if (rr >= nr) break;
@@ -319,9 +323,9 @@ __device__ __forceinline__ void role_scharr(const Job& j, int t, int y0)
 template <int KIND, bool F32>
 __device__ __forceinline__ void run_role(const Job& j, int t, int rg)
 {
-    if (j.role == R_COPY) role_copy<KIND, F32>(j, t, rg * kCopyRows);
-    else if (j.role == R_DOWN) role_down<KIND, F32>(j, t, rg * kDownRows);
-    else role_scharr<KIND, F32>(j, t, rg * kScharrRows);
+    if (j.role == R_COPY) role_copy<KIND, F32>(j, t, rg * j.rpt);
+    else if (j.role == R_DOWN) role_down<KIND, F32>(j, t, rg * j.rpt);
+    else role_scharr<KIND, F32>(j, t, rg * j.rpt);
 }
 
 template <bool F32>
@@ -360,7 +364,7 @@ Dst level_dst(const tbdk_level& L)
     return Dst{L.data, L.pitch, L.width, L.height, L.pad};
 }
 
-void add_job(Jobs& js, int& nb, int role, int kind, const Src& s, const Dst& d)
+void add_job(Jobs& js, int& nb, int role, int kind, const Src& s, const Dst& d, int rows)
 {
     Job& j = js.j[js.n++];
     j.role = role;
@@ -377,16 +381,19 @@ void add_job(Jobs& js, int& nb, int role, int kind, const Src& s, const Dst& d)
         j.ux = (s.w + 7) / 8;
         j.rows = s.h;
     }
-    const int per = role == R_COPY ? kCopyRows : role == R_DOWN ? kDownRows : kScharrRows;
+    const int cap = role == R_COPY ? kCopyRows : role == R_DOWN ? kDownRows : kScharrRows;
+    j.rpt = rows < 1 ? 1 : rows > cap ? cap : rows;
     j.bx = (j.ux + 255) / 256;
     j.b0 = nb;
-    nb += j.bx * ((j.rows + per - 1) / per);
+    nb += j.bx * ((j.rows + j.rpt - 1) / j.rpt);
 }
 
 }  // namespace
 
-// kind: K_U8 / K_U16 / K_F32 / K_F16 frame; f32: fp32 levels (else fp16)
-hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, hipStream_t s)
+// kind: K_U8 / K_U16 / K_F32 / K_F16 frame; f32: fp32 levels (else fp16); rows: rows per thread
+// (ctx option pyr_rows; the level-1 rows go in pairs at most)
+hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, int rows,
+                               hipStream_t s)
 {
     const int es = f32 ? 4 : 2;
     const int L = pyr.nlevels;
@@ -396,14 +403,14 @@ hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32
         js.n = 0;
         int nb = 0;
         if (i == 1) {
-            add_job(js, nb, R_COPY, kind, fr, level_dst(pyr.lv[0]));
-            if (L > 1) add_job(js, nb, R_DOWN, kind, fr, level_dst(pyr.lv[1]));
-            add_job(js, nb, R_SCHARR, kind, fr, level_dst(pyr.dv[0]));
+            add_job(js, nb, R_COPY, kind, fr, level_dst(pyr.lv[0]), rows);
+            if (L > 1) add_job(js, nb, R_DOWN, kind, fr, level_dst(pyr.lv[1]), rows);
+            add_job(js, nb, R_SCHARR, kind, fr, level_dst(pyr.dv[0]), rows);
         } else {
             const int lk = f32 ? K_F32 : K_F16;
             const Src ls = level_src(pyr.lv[i - 1], es);
-            if (i < L) add_job(js, nb, R_DOWN, lk, ls, level_dst(pyr.lv[i]));
-            add_job(js, nb, R_SCHARR, lk, ls, level_dst(pyr.dv[i - 1]));
+            if (i < L) add_job(js, nb, R_DOWN, lk, ls, level_dst(pyr.lv[i]), rows);
+            add_job(js, nb, R_SCHARR, lk, ls, level_dst(pyr.dv[i - 1]), rows);
         }
         if (f32) hipLaunchKernelGGL(pyr_fp_jobs_kernel<true>, dim3(nb), dim3(256), 0, s, js);
         else hipLaunchKernelGGL(pyr_fp_jobs_kernel<false>, dim3(nb), dim3(256), 0, s, js);

@@ -387,10 +387,10 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     } else if (cn > 1) {
         e = launch_pyr_cn(img, pitch, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_16F) {
-        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, false, *pyr, s)
+        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, false, *pyr, ctx->opt_pyr_rows, s)
                               : launch_pyr_build_f16(img, pitch, 0, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_32F) {
-        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, true, *pyr, s)
+        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, true, *pyr, ctx->opt_pyr_rows, s)
                               : launch_pyr_build_f32(img, pitch, 0, *pyr, s);
     } else {
         e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse, ctx->opt_pyr_rows, s);
@@ -409,7 +409,7 @@ int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* 
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     const uint8_t* p = reinterpret_cast<const uint8_t*>(img);
-    hipError_t e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(p, pitch, 3, false, *pyr, s)
+    hipError_t e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(p, pitch, 3, false, *pyr, ctx->opt_pyr_rows, s)
                                      : launch_pyr_build_f16(p, pitch, 1, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);
@@ -426,7 +426,7 @@ static int pyr_build_f32_from(tbdk_ctx* ctx, const void* img, int pitch, int byt
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     hipError_t e = cn > 1 ? launch_pyr_build_f32_cn(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s)
-               : ctx->opt_pyr_fuse ? launch_pyr_build_fp(static_cast<const uint8_t*>(img), pitch, kind, true, *pyr, s)
+               : ctx->opt_pyr_fuse ? launch_pyr_build_fp(static_cast<const uint8_t*>(img), pitch, kind, true, *pyr, ctx->opt_pyr_rows, s)
                                    : launch_pyr_build_f32(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);

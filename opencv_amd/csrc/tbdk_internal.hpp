@@ -126,7 +126,8 @@ hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, cons
 // fp32 pixel path: src_kind 0 u8, 1 u16, 2 fp32 frame
 hipError_t launch_pyr_build_f32(const uint8_t* img, int pitch, int src_kind, const tbdk_pyr& pyr, hipStream_t s);
 // role-split fp16 / fp32 pyramid build (klt_pyr_fp.hip); kind: 0 u8, 1 u16, 2 f32, 3 f16 frame
-hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, hipStream_t s);
+hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, int rows,
+                               hipStream_t s);
 
 // ---- kernels (klt_lk.hip) ----
 struct LkLevel {

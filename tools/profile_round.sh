@@ -26,4 +26,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python3 "$root/tools/pmc_json.py" "$out/FETCH_SIZE/pmc_counter_collection.csv" "$out/WRITE_SIZE/pmc_counter_collection.csv" \
     "$out/pmc.json" \
-    "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (kernel trace only), bench.py --steps 60 --sequence-frames 100 --no-cpu-baseline --no-step-api --repeats 0 --no-h2d --no-kitti --fb-pairs 3 --f16-pairs 3 --hog-frames 10; per-launch means; FETCH_SIZE/WRITE_SIZE are KiB; fetch_bytes doubles FETCH_SIZE (gfx950 reports 1/2 of wide coalesced reads, MI355X_MICROARCH.md HBM section; other access widths uncalibrated); Infinity-Cache hits are included in these memory-side counters."
+    "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (kernel trace only), bench.py --steps 60 --sequence-frames 100 --no-cpu-baseline --no-step-api --repeats 0 --no-h2d --no-kitti --fb-pairs 3 --f16-pairs 3 --hog-frames 10; per-launch means; FETCH_SIZE/WRITE_SIZE are KiB; fetch_bytes = 2 x FETCH_SIZE (the guide's gfx950 correction for wide 16-B-per-lane reads, MI355X_MICROARCH.md HBM section), fetch_size_kib is the raw count that bench.py's roofline traffic uses (its kernels load <= 4 B per lane); Infinity-Cache hits are included in these memory-side counters."
