@@ -117,6 +117,9 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       role-split launches (level 0's copy, level 1 and level 0's Scharr
  *       plane from the frame, then level i and plane i-1 from level i-1);
  *       0 takes one launch per level and one for every plane (results equal).
+ *   "pyr_xcd" (0/1, default 1): the u8 two-role and fp16 / fp32 role-split
+ *       pyramid launches deal each role's blocks to the 8 XCDs in contiguous
+ *       row bands, so rows a role reads twice share one XCD's L2 (results equal).
  *   "pyr_rows" (1/2/4, default 4): rows per thread of the u8 two-role
  *       launch (pyr_fuse 1): level 0's 16-byte copies of that many rows, level
  *       1 in row pairs sharing their 7 frame rows when > 1; and of the fp16 /

@@ -193,6 +193,8 @@ struct PyrRolesArgs {
     int wa4, wb4;        // items per padded row of roles A (4 or 16 bytes) and B (4 pixels)
     int a16;             // role A copies 16 bytes per thread (source, copy and pitches 16-byte aligned, pad % 16 == 0)
     int ra, rb;          // rows per thread: role A (16-byte path, 1..kRowsA), role B (1 or 2)
+    int nAr, nB;         // blocks of role A (nA - nAr alignment blocks idle) and of role B
+    int xcd;             // deal each role's blocks to the XCDs in contiguous row bands (nA % 8 == 0)
 };
 constexpr int kRowsA = 4;
 
@@ -269,6 +271,8 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
     int b = blockIdx.x;
     const int tid = threadIdx.x;
     if (b < a.nA) {  // ---- role A: the padded copy of the source, a.ra rows per thread
+        if (b >= a.nAr) return;
+        if (a.xcd) b = xcd_swizzle(b, a.nAr);
         const int item = b * kRoleThreads + tid;
         const int pg = item / a.wa4, t = item - pg * a.wa4;
         const int hp = a.sh + 2 * a.cpad;
@@ -317,6 +321,7 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
         return;
     }
     b -= a.nA;
+    if (a.xcd) b = xcd_swizzle(b, a.nB);
     {  // ---- role B: the level below, 4 pixels of a.rb rows per thread
         const int item = b * kRoleThreads + tid;
         const int pg = item / a.wb4, t = item - pg * a.wb4;
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
 
 // levels 0 and 1 of pyr from the frame in one launch
 static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_pyr& pyr, hipStream_t s, int rows_a,
-                                    int rows_b)
+                                    int rows_b, int xcd)
 {
     PyrRolesArgs a;
     const tbdk_level& S = pyr.lv[0];
@@ -377,9 +382,11 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
     a.wb4 = (D1.width + 2 * D1.pad + 3) / 4;
     a.ra = a.a16 ? rows_a : 1;
     a.rb = rows_b;
-    a.nA = blocks((long)a.wa4 * ((S.height + 2 * S.pad + a.ra - 1) / a.ra));
-    const int nB = blocks((long)a.wb4 * ((D1.height + 2 * D1.pad + a.rb - 1) / a.rb));
-    hipLaunchKernelGGL(pyr_build_kernel, dim3(a.nA + nB), dim3(kRoleThreads), 0, s, a);
+    a.nAr = blocks((long)a.wa4 * ((S.height + 2 * S.pad + a.ra - 1) / a.ra));
+    a.nA = xcd ? (a.nAr + 7) & ~7 : a.nAr;
+    a.nB = blocks((long)a.wb4 * ((D1.height + 2 * D1.pad + a.rb - 1) / a.rb));
+    a.xcd = xcd;
+    hipLaunchKernelGGL(pyr_build_kernel, dim3(a.nA + a.nB), dim3(kRoleThreads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -708,7 +715,8 @@ static hipError_t launch_pyr_fused(const uint8_t* src, int spitch, const tbdk_py
 
 // every level of a u8 pyramid from the frame: levels 0 and 1 in one launch
 // (fuse), or one launch per level
-hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, hipStream_t s)
+hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, int xcd,
+                             hipStream_t s)
 {
     hipError_t e;
     int level = 1;
@@ -716,7 +724,7 @@ hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr,
         e = launch_pyr_fused(img, pitch, pyr, s, &level);
     } else if (fuse && pyr.nlevels >= 2) {
         rows = rows < 1 ? 1 : rows > kRowsA ? kRowsA : rows;
-        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1);
+        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1, xcd);
         level = 2;
     } else {
         e = launch_pad_copy(img, pitch, pyr.lv[0], s);

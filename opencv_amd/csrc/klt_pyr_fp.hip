@@ -57,11 +57,13 @@ struct Job {
     Dst d;
     int ux, rows, bx, b0;  // threads per row, rows, blocks per row, first block
     int rpt;               // rows per thread (<= kCopyRows / kDownRows / kScharrRows by role)
+    int nb;                // blocks of the job (b0 is a multiple of 8: job block b runs on XCD b % 8)
 };
 
 struct Jobs {
     Job j[3];
     int n;
+    int xcd;  // deal each job's blocks to the XCDs in contiguous row bands (xcd_swizzle)
 };
 
 __device__ __forceinline__ int reflect101(int p, int len)
@@ -335,7 +337,8 @@ __global__ void __launch_bounds__(256) pyr_fp_jobs_kernel(Jobs js)
     int i = 0;
     while (i + 1 < js.n && b >= js.j[i + 1].b0) ++i;
     const Job& j = js.j[i];
-    const int rb = b - j.b0;
+    if (b - j.b0 >= j.nb) return;  // alignment gap before the next job
+    const int rb = js.xcd ? xcd_swizzle(b - j.b0, j.nb) : b - j.b0;
     const int row = rb / j.bx;  // row group
     const int t = (rb - row * j.bx) * 256 + (int)threadIdx.x;
     if (t >= j.ux) return;
@@ -384,8 +387,9 @@ void add_job(Jobs& js, int& nb, int role, int kind, const Src& s, const Dst& d, 
     const int cap = role == R_COPY ? kCopyRows : role == R_DOWN ? kDownRows : kScharrRows;
     j.rpt = rows < 1 ? 1 : rows > cap ? cap : rows;
     j.bx = (j.ux + 255) / 256;
-    j.b0 = nb;
-    nb += j.bx * ((j.rows + j.rpt - 1) / j.rpt);
+    j.b0 = (nb + 7) & ~7;
+    j.nb = j.bx * ((j.rows + j.rpt - 1) / j.rpt);
+    nb = j.b0 + j.nb;
 }
 
 }  // namespace
@@ -393,7 +397,7 @@ void add_job(Jobs& js, int& nb, int role, int kind, const Src& s, const Dst& d, 
 // kind: K_U8 / K_U16 / K_F32 / K_F16 frame; f32: fp32 levels (else fp16); rows: rows per thread
 // (ctx option pyr_rows; the level-1 rows go in pairs at most)
 hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, int rows,
-                               hipStream_t s)
+                               int xcd, hipStream_t s)
 {
     const int es = f32 ? 4 : 2;
     const int L = pyr.nlevels;
@@ -401,6 +405,7 @@ hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32
     for (int i = 1; i <= L; ++i) {
         Jobs js;
         js.n = 0;
+        js.xcd = xcd;
         int nb = 0;
         if (i == 1) {
             add_job(js, nb, R_COPY, kind, fr, level_dst(pyr.lv[0]), rows);

@@ -203,6 +203,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_pyr_fuse = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "pyr_xcd") == 0) {
+        ctx->opt_pyr_xcd = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "pyr_rows") == 0) {
         if (value != 1 && value != 2 && value != 4) return TBDK_EINVAL;
         ctx->opt_pyr_rows = (int)value;
@@ -387,13 +391,13 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     } else if (cn > 1) {
         e = launch_pyr_cn(img, pitch, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_16F) {
-        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, false, *pyr, ctx->opt_pyr_rows, s)
+        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, false, *pyr, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s)
                               : launch_pyr_build_f16(img, pitch, 0, *pyr, s);
     } else if (pyr->depth == TBDK_DEPTH_32F) {
-        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, true, *pyr, ctx->opt_pyr_rows, s)
+        e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(img, pitch, 0, true, *pyr, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s)
                               : launch_pyr_build_f32(img, pitch, 0, *pyr, s);
     } else {
-        e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse, ctx->opt_pyr_rows, s);
+        e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s);
         if (e == hipSuccess && !(pyr->flags & TBDK_PYR_NO_DERIVS)) e = launch_scharr_levels(*pyr, s);
     }
     timing_end(ctx, rec, s);
@@ -409,7 +413,7 @@ int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* 
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     const uint8_t* p = reinterpret_cast<const uint8_t*>(img);
-    hipError_t e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(p, pitch, 3, false, *pyr, ctx->opt_pyr_rows, s)
+    hipError_t e = ctx->opt_pyr_fuse ? launch_pyr_build_fp(p, pitch, 3, false, *pyr, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s)
                                      : launch_pyr_build_f16(p, pitch, 1, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);
@@ -426,7 +430,7 @@ static int pyr_build_f32_from(tbdk_ctx* ctx, const void* img, int pitch, int byt
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
     hipError_t e = cn > 1 ? launch_pyr_build_f32_cn(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s)
-               : ctx->opt_pyr_fuse ? launch_pyr_build_fp(static_cast<const uint8_t*>(img), pitch, kind, true, *pyr, ctx->opt_pyr_rows, s)
+               : ctx->opt_pyr_fuse ? launch_pyr_build_fp(static_cast<const uint8_t*>(img), pitch, kind, true, *pyr, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s)
                                    : launch_pyr_build_f32(static_cast<const uint8_t*>(img), pitch, kind, *pyr, s);
     timing_end(ctx, rec, s);
     return map_err(e);

@@ -72,6 +72,7 @@ struct tbdk_ctx {
     int device = 0;
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
+    int opt_pyr_xcd = 1;       // tbdk_ctx_set_option("pyr_xcd"): pyramid roles' row bands per XCD
     int opt_pyr_rows = 4;      // tbdk_ctx_set_option("pyr_rows"): rows per thread of the two-role u8 build (1, 2, 4)
     int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): 1 the two-role launch + one per level, 2 levels 0-2 in one tiled launch (slower, A/B), 0 one launch per level
     int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
@@ -119,7 +120,8 @@ hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, u
 // Scharr derivative planes (interior only; the zero frame is written once at allocation)
 hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s);
 // every u8 level of pyr from the frame (fused launches where the levels allow)
-hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, hipStream_t s);
+hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, int xcd,
+                             hipStream_t s);
 // the fp16 pyramid (klt_f16.hip): level 0 from a u8 (img_f16 = 0) or fp16 frame,
 // the fp16 pyrDown levels and the fp16 derivative pairs
 hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s);
@@ -127,7 +129,7 @@ hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, cons
 hipError_t launch_pyr_build_f32(const uint8_t* img, int pitch, int src_kind, const tbdk_pyr& pyr, hipStream_t s);
 // role-split fp16 / fp32 pyramid build (klt_pyr_fp.hip); kind: 0 u8, 1 u16, 2 f32, 3 f16 frame
 hipError_t launch_pyr_build_fp(const uint8_t* img, int pitch, int kind, bool f32, const tbdk_pyr& pyr, int rows,
-                               hipStream_t s);
+                               int xcd, hipStream_t s);
 
 // ---- kernels (klt_lk.hip) ----
 struct LkLevel {

@@ -134,9 +134,10 @@ def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
     img = np.random.default_rng(sum(shape)).integers(0, 256, shape, dtype=np.uint8)
     R = None
     try:
-        for mode, rows in ((2, 4), (1, 4), (1, 2), (1, 1), (0, 4)):
+        for mode, rows, xcd in ((2, 4, 1), (1, 4, 1), (1, 2, 0), (1, 1, 1), (1, 4, 0), (0, 4, 1)):
             gpu.set_option("pyr_fuse", mode)
             gpu.set_option("pyr_rows", rows)  # rows per thread of the two-role launch
+            gpu.set_option("pyr_xcd", xcd)  # row bands per XCD
             for derivs in (False, True):
                 P = K.build_pyramid(to_dev(img), (win, win), maxlev, ctx=gpu, derivs=derivs)
                 torch.cuda.synchronize()
@@ -150,6 +151,7 @@ def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
     finally:
         gpu.set_option("pyr_fuse", 1)
         gpu.set_option("pyr_rows", 4)
+        gpu.set_option("pyr_xcd", 1)
 
 
 @pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])

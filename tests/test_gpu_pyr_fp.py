@@ -77,9 +77,10 @@ def test_pyr_fp_bit_exact(gpu, store, kind, layout, shape, maxlev, win):
     R = O.Pyramid16(img, (win, win), maxlev, f32=store == "f32")
     view = np.uint16 if store == "f16" else np.uint32
     try:
-        for mode, rows in ((1, 4), (1, 2), (1, 1), (0, 4)):
+        for mode, rows, xcd in ((1, 4, 1), (1, 2, 1), (1, 1, 0), (0, 4, 1)):
             gpu.set_option("pyr_fuse", mode)
             gpu.set_option("pyr_rows", rows)  # rows per thread of the role-split build
+            gpu.set_option("pyr_xcd", xcd)  # row bands per XCD
             P = _build(gpu, dev, kind, store, (win, win), maxlev)
             torch.cuda.synchronize()
             assert P.nlevels == R.nlevels
@@ -95,3 +96,4 @@ def test_pyr_fp_bit_exact(gpu, store, kind, layout, shape, maxlev, win):
     finally:
         gpu.set_option("pyr_fuse", 1)
         gpu.set_option("pyr_rows", 4)
+        gpu.set_option("pyr_xcd", 1)

@@ -1,6 +1,7 @@
 """tbdk_pyr_build timing by ctx options pyr_fuse (2: levels 0-2 in one tiled
 launch, 1: the two-role launch + one per level, 0: one launch per level) and
-pyr_rows (rows per thread of the two-role launch), levels-only and with
+pyr_rows (rows per thread of the two-role launch) and pyr_xcd (row bands per
+XCD), levels-only and with
 derivative planes, 1080p / KITTI / 4K.  HIP events over 100 builds per
 variant, the variants interleaved over 5 rounds; per variant the median and
 min of the rounds' means."""
@@ -13,9 +14,9 @@ import torch
 from opencv_amd import klt
 
 ctx = klt.Context.get(0)
-VARIANTS = [("tiled", False, 2, 4), ("two-role r4", False, 1, 4), ("two-role r2", False, 1, 2),
-            ("two-role r1", False, 1, 1), ("per level", False, 0, 4), ("planes two-role r4", True, 1, 4),
-            ("planes two-role r1", True, 1, 1)]
+VARIANTS = [("tiled", False, 2, 4, 1), ("two-role r4", False, 1, 4, 1), ("two-role r4 noxcd", False, 1, 4, 0),
+            ("two-role r2", False, 1, 2, 1), ("two-role r1", False, 1, 1, 1), ("two-role r1 noxcd", False, 1, 1, 0),
+            ("per level", False, 0, 4, 1), ("planes two-role r4", True, 1, 4, 1)]
 
 
 def timed(P, frames, n=100):
@@ -35,13 +36,15 @@ for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2)):
     pyrs = {v[0]: klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=v[1]) for v in VARIANTS}
     res = {v[0]: [] for v in VARIANTS}
     for rnd in range(6):
-        for name, derivs, fuse, rows in VARIANTS:
+        for name, derivs, fuse, rows, xcd in VARIANTS:
             ctx.set_option("pyr_fuse", fuse)
             ctx.set_option("pyr_rows", rows)
+            ctx.set_option("pyr_xcd", xcd)
             t = timed(pyrs[name], fr, 20 if rnd == 0 else 100)
             if rnd:
                 res[name].append(t)
     ctx.set_option("pyr_fuse", 1)
     ctx.set_option("pyr_rows", 4)
+    ctx.set_option("pyr_xcd", 1)
     print(f"{W}x{H} maxLevel {ml}: " + ", ".join(f"{k} {statistics.median(v):.1f} (min {min(v):.1f})"
                                                  for k, v in res.items()) + " us", flush=True)
