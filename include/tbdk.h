@@ -120,11 +120,12 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *   "pyr_xcd" (0/1, default 1): the u8 two-role and fp16 / fp32 role-split
  *       pyramid launches deal each role's blocks to the 8 XCDs in contiguous
  *       row bands, so rows a role reads twice share one XCD's L2 (results equal).
- *   "pyr_rows" (1/2/4, default 4): rows per thread of the u8 two-role
- *       launch (pyr_fuse 1): level 0's 16-byte copies of that many rows, level
- *       1 in row pairs sharing their 7 frame rows when > 1; and of the fp16 /
+ *   "pyr_rows" (1/2/4, default 1): rows per thread of the u8 two-role
+ *       launch (pyr_fuse 1: level 0's 16-byte copies of that many rows, level
+ *       1 in row pairs sharing their 7 frame rows when > 1) and of the fp16 /
  *       fp32 role-split launches (copies and Scharr planes that many rows,
- *       levels in pairs at most; results equal).
+ *       levels in pairs at most); more than 1 measured slower (fewer waves
+ *       to hide the loads' latency), kept for A/B runs (results equal).
  *   "lk_scharr_fly" (0/1, default 0): the several-points-per-wave PyrLK
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;

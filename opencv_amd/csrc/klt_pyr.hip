@@ -289,7 +289,11 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
                         v[r] = *reinterpret_cast<const uint4*>(
                             a.src + (size_t)reflect101(py0 + r - a.cpad, a.sh) * a.spitch + x0);
             } else {
-                for (int r = 0; r < nr; ++r) {
+                // unrolled with constant indices: a runtime index into v[] makes the
+                // compiler move v[] to LDS (16 KB per workgroup, each load waited on)
+#pragma unroll
+                for (int r = 0; r < kRowsA; ++r) {
+                    if (r >= nr) break;
                     const uint8_t* srow = a.src + (size_t)reflect101(py0 + r - a.cpad, a.sh) * a.spitch;
                     uint32_t q[4];
 #pragma unroll

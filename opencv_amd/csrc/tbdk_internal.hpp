@@ -73,7 +73,7 @@ struct tbdk_ctx {
     bool timing = false;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
     int opt_pyr_xcd = 1;       // tbdk_ctx_set_option("pyr_xcd"): pyramid roles' row bands per XCD
-    int opt_pyr_rows = 4;      // tbdk_ctx_set_option("pyr_rows"): rows per thread of the two-role u8 build (1, 2, 4)
+    int opt_pyr_rows = 1;      // tbdk_ctx_set_option("pyr_rows"): rows per thread of the two-role u8 build (1, 2, 4)
     int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): 1 the two-role launch + one per level, 2 levels 0-2 in one tiled launch (slower, A/B), 0 one launch per level
     int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0

@@ -1,8 +1,8 @@
 """GPU parity of the role-split floating-point pyramid build (klt_pyr_fp.hip,
 ctx option pyr_fuse >= 1, the default) against the oracle
 (oracle/klt16_oracle.c: orc16_pyr_down / orc16_scharr and the fp32 twins) and
-against the one-launch-per-plane build (pyr_fuse=0), at 4 / 2 / 1 rows per
-thread (ctx option pyr_rows): fp16 levels from u8 and
+against the one-launch-per-plane build (pyr_fuse=0), at 1 / 2 / 4 rows per
+thread (ctx option pyr_rows), with and without the XCD row bands (pyr_xcd): fp16 levels from u8 and
 fp16 frames, fp32 levels from u8, u16 and fp32 frames; padded levels (reflect-101
 frames) and derivative planes bit-exact.  Layouts: dense frames, frames whose
 last byte ends their allocation (the dword fast path's last-row rule), and
@@ -77,7 +77,7 @@ def test_pyr_fp_bit_exact(gpu, store, kind, layout, shape, maxlev, win):
     R = O.Pyramid16(img, (win, win), maxlev, f32=store == "f32")
     view = np.uint16 if store == "f16" else np.uint32
     try:
-        for mode, rows, xcd in ((1, 4, 1), (1, 2, 1), (1, 1, 0), (0, 4, 1)):
+        for mode, rows, xcd in ((1, 1, 1), (1, 1, 0), (1, 4, 1), (1, 2, 0), (0, 1, 1)):
             gpu.set_option("pyr_fuse", mode)
             gpu.set_option("pyr_rows", rows)  # rows per thread of the role-split build
             gpu.set_option("pyr_xcd", xcd)  # row bands per XCD
@@ -91,9 +91,9 @@ def test_pyr_fp_bit_exact(gpu, store, kind, layout, shape, maxlev, win):
                 ry = [O.load().orc_reflect101(y - pad, hh) for y in range(hh + 2 * pad)]
                 rx = [O.load().orc_reflect101(x - pad, ww) for x in range(ww + 2 * pad)]
                 full = P.level(i, with_border=True)
-                assert np.array_equal(full.view(view), ref[np.ix_(ry, rx)].view(view)), f"mode {mode}/{rows} level {i}"
-                assert np.array_equal(P.deriv(i).view(view), R.derivs[i].view(view)), f"mode {mode}/{rows} deriv {i}"
+                assert np.array_equal(full.view(view), ref[np.ix_(ry, rx)].view(view)), f"mode {mode}/{rows}/{xcd} level {i}"
+                assert np.array_equal(P.deriv(i).view(view), R.derivs[i].view(view)), f"mode {mode}/{rows}/{xcd} deriv {i}"
     finally:
         gpu.set_option("pyr_fuse", 1)
-        gpu.set_option("pyr_rows", 4)
+        gpu.set_option("pyr_rows", 1)
         gpu.set_option("pyr_xcd", 1)

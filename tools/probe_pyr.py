@@ -14,6 +14,16 @@ import torch
 from opencv_amd import klt
 
 ctx = klt.Context.get(0)
+only = sys.argv[1:]  # optional variant names (a library without pyr_rows / pyr_xcd: "two-role r4" etc. still run)
+
+
+def opt(name, v):
+    try:
+        ctx.set_option(name, v)
+    except Exception:  # option unknown to this library build
+        pass
+
+
 VARIANTS = [("tiled", False, 2, 4, 1), ("two-role r4", False, 1, 4, 1), ("two-role r4 noxcd", False, 1, 4, 0),
             ("two-role r2", False, 1, 2, 1), ("two-role r1", False, 1, 1, 1), ("two-role r1 noxcd", False, 1, 1, 0),
             ("per level", False, 0, 4, 1), ("planes two-role r4", True, 1, 4, 1)]
@@ -33,18 +43,20 @@ def timed(P, frames, n=100):
 
 for (W, H, ml) in ((1920, 1080, 2), (1242, 375, 2), (3840, 2160, 2)):
     fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
-    pyrs = {v[0]: klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=v[1]) for v in VARIANTS}
+    pyrs = {v[0]: klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=v[1]) for v in VARIANTS if not only or v[0] in only}
     res = {v[0]: [] for v in VARIANTS}
     for rnd in range(6):
         for name, derivs, fuse, rows, xcd in VARIANTS:
-            ctx.set_option("pyr_fuse", fuse)
-            ctx.set_option("pyr_rows", rows)
-            ctx.set_option("pyr_xcd", xcd)
+            if only and name not in only:
+                continue
+            opt("pyr_fuse", fuse)
+            opt("pyr_rows", rows)
+            opt("pyr_xcd", xcd)
             t = timed(pyrs[name], fr, 20 if rnd == 0 else 100)
             if rnd:
                 res[name].append(t)
-    ctx.set_option("pyr_fuse", 1)
-    ctx.set_option("pyr_rows", 4)
-    ctx.set_option("pyr_xcd", 1)
+    opt("pyr_fuse", 1)
+    opt("pyr_rows", 1)
+    opt("pyr_xcd", 1)
     print(f"{W}x{H} maxLevel {ml}: " + ", ".join(f"{k} {statistics.median(v):.1f} (min {min(v):.1f})"
-                                                 for k, v in res.items()) + " us", flush=True)
+                                                 for k, v in res.items() if v) + " us", flush=True)

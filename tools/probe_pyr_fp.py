@@ -34,11 +34,10 @@ for (W, H, ml) in ((1920, 1080, 2), (3840, 2160, 2)):
             continue
         frames = [f.to(src) for f in fr]
         P = klt.Pyramid(ctx, W, H, ml, (21, 21), store)
-        res = {(1, 4, 1): [], (1, 4, 0): [], (1, 2, 1): [], (1, 1, 1): [], (1, 1, 0): [], (0, 4, 1): []}
+        res = {(1, 1): [], (1, 0): [], (0, 1): []}
         for rnd in range(6):  # variants interleaved; round 0 warms up
-            for fuse, rows, xcd in res:
+            for fuse, xcd in res:
                 ctx.set_option("pyr_fuse", fuse)
-                ctx.set_option("pyr_rows", rows)
                 ctx.set_option("pyr_xcd", xcd)
                 n = 20 if rnd == 0 else 100
                 ctx.timing_select(["pyr_build"])
@@ -50,14 +49,11 @@ for (W, H, ml) in ((1920, 1080, 2), (3840, 2160, 2)):
                 ctx.timing_enable(False)
                 ctx.timing_select(None)
                 if rnd:
-                    res[fuse, rows, xcd].append(ms / c * 1000)
+                    res[fuse, xcd].append(ms / c * 1000)
         ctx.set_option("pyr_fuse", 1)
-        ctx.set_option("pyr_rows", 4)
         ctx.set_option("pyr_xcd", 1)
         mb = min_bytes(P, frames[0].element_size())
         med = {k: statistics.median(v) for k, v in res.items()}
-        best = min(med[k] for k in med if k[0] == 1)
-        print(f"{W}x{H} {str(store)[6:]} levels from {str(src)[6:]} ({mb / 1e6:.1f} MB): role-split rows 4/2/1 "
-              f"{med[1, 4, 1]:.1f} / {med[1, 2, 1]:.1f} / {med[1, 1, 1]:.1f} us, without XCD bands rows 4/1 "
-              f"{med[1, 4, 0]:.1f} / {med[1, 1, 0]:.1f} (best {mb / best / 1e3:.0f} GB/s), per plane "
-              f"{med[0, 4, 1]:.1f} us", flush=True)
+        print(f"{W}x{H} {str(store)[6:]} levels from {str(src)[6:]} ({mb / 1e6:.1f} MB): role-split "
+              f"{med[1, 1]:.1f} us ({mb / med[1, 1] / 1e3:.0f} GB/s), without XCD bands {med[1, 0]:.1f}, "
+              f"per plane {med[0, 1]:.1f} us", flush=True)
