@@ -215,7 +215,7 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
         gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
         gpu.set_option("tbd_early_la", 1)
-        gpu.set_option("tbd_early_order", 2)
+        gpu.set_option("tbd_early_order", 0)
     base = res[0, 0, 0, 0]
     for key, r in res.items():
         assert r[0] == base[0], key
