@@ -1,8 +1,9 @@
 #!/usr/bin/env bash
-# pmc_pyr_fp.sh <outdir> [probe filter, default 3840x2160:float16:uint8] -- counters of the
-# role-split fp pyramid build (tools/probe_pyr_fp.py, one configuration): one rocprofv3 --pmc
-# pass per counter group (<= 8 SQ + GRBM, then FETCH_SIZE, then WRITE_SIZE), kernel trace only;
-# summary per (kernel, grid size) in <outdir>/summary.json.  Run on the GPU box.
+# pmc_pyr_fp.sh <outdir> [probe filter, default 3840x2160:float16:uint8 | u8] -- counters of the
+# role-split fp pyramid build (tools/probe_pyr_fp.py, one configuration) or, with "u8", of the
+# u8 two-role levels-only build (tools/probe_pyr.py "two-role r1": 1080p, KITTI, 4K): one
+# rocprofv3 --pmc pass per counter group (<= 8 SQ + GRBM, then FETCH_SIZE, then WRITE_SIZE),
+# kernel trace only; summary per (kernel, grid size) in <outdir>/summary.json.  GPU box.
 set -euo pipefail
 root=$(pwd); out=$root/$1; cfg=${2:-3840x2160:float16:uint8}
 mkdir -p "$out"; cd /tmp; export TMPDIR=/tmp
@@ -10,8 +11,13 @@ i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i + 1))
-    timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/p$i" -o pmc \
-        -- python3 "$root/tools/probe_pyr_fp.py" "$cfg" > "$out/p$i.log" 2>&1
+    if [ "$cfg" = u8 ]; then
+        timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/p$i" -o pmc \
+            -- python3 "$root/tools/probe_pyr.py" "two-role r1" > "$out/p$i.log" 2>&1
+    else
+        timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/p$i" -o pmc \
+            -- python3 "$root/tools/probe_pyr_fp.py" "$cfg" > "$out/p$i.log" 2>&1
+    fi
 done
 python3 - "$out" <<'PY'
 import collections, csv, glob, json, os, sys
