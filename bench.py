@@ -570,6 +570,7 @@ def lk_f16_secondary(ctx, args, device, cpu: bool):
     flops = lk_flops(npts * nlev, iters / n, args.win)  # per launch (one pair)
     tf = flops / (lkk["avg_us"] * 1e-6) / 1e12
     pb = pyr_f16_bytes(w, h, nlev)
+    ptr = pmc_pyr_traffic("f16", [("pyr_fp_jobs_kernel<false>", nlev)])  # counters of the role-split build
     gbs = pb / (pk["avg_us"] * 1e-6) / 1e9
     out = {"value": round(n / wall, 2), "unit": "pairs/s", "points_per_s": round(n * npts / wall, 1),
            "ms_per_pair": round(1000 * wall / n, 3), "dtype": "f16 pixels, f32 arithmetic",
@@ -583,6 +584,8 @@ def lk_f16_secondary(ctx, args, device, cpu: bool):
            "roofline_pyramid": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pb,
                                 "bytes_per_launch_per_plane_count": pyr_f16_bytes_per_plane(w, h, nlev),
+                                "traffic": ptr[0], "traffic_fetch_x2": ptr[1], "traffic_source": ptr[2],
+                                "traffic_over_algorithmic": round(ptr[0] / pb, 3) if ptr[0] else None,
                                 "avg_us": round(pk["avg_us"], 2),
                                 "kernel": "pyr_build (fp16 levels + fp16 Scharr planes; klt_pyr_fp.hip, "
                                           f"{nlev} role-split launches)"},
@@ -958,6 +961,32 @@ def copy_rate_at(ctx, traffic_bytes: int, reps: int = 25) -> dict:
     return {"bytes": 2 * n, "us": round(best * 1000, 2), "gbs": round(2 * n / (best / 1000) / 1e9, 1)}
 
 
+def pmc_pyr_traffic(kind: str, kernels):
+    """HBM counter bytes per build of a pyramid build from the newest committed
+    profiles/rNN_pmc_pyr_<kind>.json (tools/pmc_pyr_fp.sh: FETCH_SIZE and
+    WRITE_SIZE passes over the probe, per kernel and grid size): for each kernel
+    name fragment, the entry of the largest grid (the 4K build), fetch + write;
+    (raw, fetch doubled, source file) or (None, None, None)."""
+    d = os.path.join(ROOT, "profiles")
+    try:
+        files = sorted(f for f in os.listdir(d) if f.endswith(f"_pmc_pyr_{kind}.json"))
+    except OSError:
+        return None, None, None
+    if not files:
+        return None, None, None
+    summ = json.load(open(os.path.join(d, files[-1])))
+    raw = dbl = 0.0
+    for frag, n in kernels:
+        ent = [(int(k.rsplit("grid=", 1)[1]), v) for k, v in summ.items()
+               if frag in k and "grid=" in k and "fetch_mb" in v and "write_mb" in v]
+        if len(ent) < n:
+            return None, None, None
+        for _, v in sorted(ent, key=lambda e: -e[0])[:n]:
+            raw += (v["fetch_mb"] + v["write_mb"]) * 1e6
+            dbl += (2 * v["fetch_mb"] + v["write_mb"]) * 1e6
+    return round(raw), round(dbl), files[-1]
+
+
 def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
     """roofline_pyramid_4k: the u8 levels-only pyramid build (the TBD loop's
     pyramid, 3 levels, win 21) of a 3840x2160 frame (BASELINE configs[4]'s size),
@@ -987,8 +1016,11 @@ def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
     gbs = b / (us * 1e-6) / 1e9
     del fr, P
     cp = copy_rate_at(ctx, b)
+    tr, tr2, src = pmc_pyr_traffic("u8", [("pyr_build_kernel", 1), ("pyr_down_padded_kernel", 1)])
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": b, "avg_us": round(us, 2), "builds": c,
+            "traffic": tr, "traffic_fetch_x2": tr2, "traffic_source": src,
+            "traffic_over_algorithmic": round(tr / b, 3) if tr else None,
             "size_matched_copy": cp, "frac_size_matched_copy": round(gbs / cp["gbs"], 4),
             "kernel": "pyr_build (levels only, u8, 3840x2160, 3 levels)",
             "note": "algorithmic bytes (frame read once, padded levels written, level 2 reading level 1) / the "
