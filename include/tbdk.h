@@ -178,6 +178,8 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       fit and the next frame's pyramid, before the host waits for the fit
  *       (its host-side setup then overlaps the GPU's critical chain; measured
  *       no faster over whole sequences; results equal).
+ *   "tbd_early_prio" (0/1, default 0; taken by tbdk_tbd_create): the early
+ *       GFTT's stream at the lowest (0) or highest (1) priority (results equal).
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
  *       pyramids carry Scharr derivative planes and PyrLK reads them instead of
  *       deriving the window's values (results equal; A/B runs).

@@ -171,6 +171,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_early_la = value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_early_prio") == 0) {
+        ctx->opt_tbd_early_prio = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_early_order") == 0) {
         if (value < 0 || value > 2) return TBDK_EINVAL;
         ctx->opt_tbd_early_order = (int)value;

@@ -456,7 +456,11 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     // the critical PyrLK measured no difference either)
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->la_s, hipStreamNonBlocking, prio_least);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking, prio_least);
+    // the early GFTT at the lowest priority (ctx option tbd_early_prio, read here:
+    // 1 = the highest, for launch orders that put it behind the critical PyrLK)
+    if (e == hipSuccess)
+        e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking,
+                                        ctx->opt_tbd_early_prio ? prio_greatest : prio_least);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);

@@ -193,13 +193,15 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
     res = {}
     try:
-        for early, spec, ela, order in ((2, 1, 1, 0), (2, 1, 0, 0), (2, 1, 2, 0), (2, 0, 1, 0), (1, 1, 1, 0),
-                                        (1, 1, 2, 0), (1, 0, 1, 0), (0, 1, 1, 0), (0, 0, 0, 0), (2, 1, 1, 1),
-                                        (2, 1, 1, 2), (1, 0, 2, 2)):
+        for early, spec, ela, order, prio in ((2, 1, 1, 0, 0), (2, 1, 0, 0, 0), (2, 1, 2, 0, 0), (2, 0, 1, 0, 0),
+                                              (1, 1, 1, 0, 0), (1, 1, 2, 0, 0), (1, 0, 1, 0, 0), (0, 1, 1, 0, 0),
+                                              (0, 0, 0, 0, 0), (2, 1, 1, 1, 0), (2, 1, 1, 2, 0), (1, 0, 2, 2, 0),
+                                              (2, 1, 1, 1, 1), (2, 1, 1, 0, 1)):
             gpu.set_option("tbd_early_gftt", early)
             gpu.set_option("tbd_spec_lookahead", spec)
             gpu.set_option("tbd_early_la", ela)
             gpu.set_option("tbd_early_order", order)  # where the step launches the early GFTT
+            gpu.set_option("tbd_early_prio", prio)  # its stream's priority (read by the loop's creation)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms, preds = [], []
             if api == "run":
@@ -209,21 +211,22 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
                     nxt = frames[f + 1] if api == "ahead" and f + 1 < F else None
                     ms.append(loop.step(frames[f], f, dets[f], next_frame=nxt))
                     preds.append(loop.predictions())
-            res[early, spec, ela, order] = ([_mkey(m) for m in ms], preds, loop.tracks(),
+            res[early, spec, ela, order, prio] = ([_mkey(m) for m in ms], preds, loop.tracks(),
                                             sum(m.early_gftt for m in ms))
     finally:
         gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
         gpu.set_option("tbd_early_la", 1)
         gpu.set_option("tbd_early_order", 0)
-    base = res[0, 0, 0, 0]
+        gpu.set_option("tbd_early_prio", 0)
+    base = res[0, 0, 0, 0, 0]
     for key, r in res.items():
         assert r[0] == base[0], key
         assert r[1] == base[1], key
         assert r[2] == base[2], key
-    assert res[1, 1, 1, 0][3] > 2 * F and base[3] == 0  # the early path was taken (and off means off)
-    assert res[2, 1, 1, 0][3] > res[1, 1, 1, 0][3] + F  # re-detection guesses confirmed
-    assert res[2, 1, 1, 1][3] == res[2, 1, 1, 2][3] == res[2, 1, 1, 0][3]
+    assert res[1, 1, 1, 0, 0][3] > 2 * F and base[3] == 0  # the early path was taken (and off means off)
+    assert res[2, 1, 1, 0, 0][3] > res[1, 1, 1, 0, 0][3] + F  # re-detection guesses confirmed
+    assert res[2, 1, 1, 1, 0][3] == res[2, 1, 1, 2, 0][3] == res[2, 1, 1, 0, 0][3] == res[2, 1, 1, 1, 1][3]
 
 
 def test_tbd_zero_copy_matches_copies(gpu):
