@@ -403,7 +403,7 @@ def cpu_baseline_line(frames_host, gt, args, restore_affinity=None):
         c = json.load(open(os.path.join(ROOT, "profiles", "r04_cpu_calibration.json")))["results"]
         cal = {"restatement_over_reference_lk_1t": c["lk_1080p_128x256_1t_ms"]["ratio"],
                "restatement_over_reference_lk_8t": c["lk_1080p_128x256_8t_ms"]["ratio"],
-               "source": "profiles/r04_cpu_calibration.json (tools/calibrate_cpu.py vs BASELINE.md §2)",
+               "source": "profiles/r04_cpu_calibration.json (tests/calibrate_cpu.py vs BASELINE.md §2)",
                "note": "PyrLK per call, 1080p x 32k points: the C restatement is this many times slower than the "
                        "reference's SSE2 build (shape-matched input; the restatement's input iterates more)"}
     except (OSError, KeyError, ValueError):

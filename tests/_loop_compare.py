@@ -1,6 +1,6 @@
 """Loop-level comparison of the TBD loop in the GPU's accumulation order with
 the reference's SSE2 order (TEST INFRASTRUCTURE ONLY; used by
-tests/test_gpu_tbd_e2e.py and tools/loop_divergence.py).
+tests/test_gpu_tbd_e2e.py and tests/loop_divergence_cpu.py).
 
 The GPU's PyrLK sums G and b exactly (integers) and rounds once; the reference
 adds float products in SSE2 lane order (video/src/lkpyramid.cpp:278-316,

@@ -5,7 +5,7 @@ maxLevel 3, 128 boxes x 256 points), 1 and 8 threads, in the SSE2 accumulation
 order, so the bench's cpu_baseline (a "port") can be read against the
 reference itself: ratio = restatement time / reference time on that input.
 
-  TBDK_ORACLE_LIB=<-O3 -march=native build> python tools/calibrate_cpu.py
+  TBDK_ORACLE_LIB=<-O3 -march=native build> python tests/calibrate_cpu.py
 """
 import json
 import os

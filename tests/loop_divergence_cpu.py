@@ -4,7 +4,7 @@ loop in the reference's SSE2 order, over a whole configs[2]-shaped sequence
 exact-order oracle (tests/test_gpu_tbd_e2e.py), so these figures are the
 GPU-vs-reference-order divergence.
 
-  python tools/loop_divergence.py [--frames 500] [--threads 8] [--seed 20261015] [--out f.json]
+  python tests/loop_divergence_cpu.py [--frames 500] [--threads 8] [--seed 20261015] [--out f.json]
 """
 import argparse
 import json

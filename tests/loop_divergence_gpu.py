@@ -4,7 +4,7 @@ beside the one tests/test_gpu_tbd_e2e.py asserts (same procedure: GPU-rendered
 frames handed to two CPU oracle workers, tests/_loop_worker.py; the oracle runs
 here only as the checker).  Writes gpurun_out/loop_divergence_<W>x<H>_<seed>.json.
 
-  python tools/loop_divergence_gpu.py W H OBJECTS FRAMES SEED
+  python tests/loop_divergence_gpu.py W H OBJECTS FRAMES SEED
 """
 import json
 import os
