@@ -63,7 +63,10 @@ struct FitOut {
 // One wave per live track, kFitWaves tracks per workgroup.  Fit terms follow
 // getRTMatrix's non-full-affine branch (float products summed in double),
 // accumulated wave-parallel in a fixed order (box_fit.hpp: wave_fit_similarity).
-constexpr int kFitWaves = 8;
+#ifndef TBDK_FIT_WAVES
+#define TBDK_FIT_WAVES 8  // tracks (waves) per fit workgroup (tuning builds)
+#endif
+constexpr int kFitWaves = TBDK_FIT_WAVES;
 __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry* __restrict__ ents, int nents,
                                                                  float2* __restrict__ slot_pts,
                                                                  const float2* __restrict__ slot_next,
