@@ -190,3 +190,36 @@ def test_f32_cn_calc_on_frames_and_vs_u8_cn(gpu):
     both = (s8 == 1) & (s32 == 1)
     d = np.abs(r8.next_pts.cpu().numpy() - r32.next_pts.cpu().numpy())[both].max(1)
     assert (s8 == s32).mean() >= 0.99 and (d <= 1e-2).mean() >= 0.99
+
+
+def test_f32_4k_bit_exact_sample(gpu):
+    """the fp32 pixel path at configs[4]'s size: 4K float32 frames (u8 scale plus
+    noise), 512 objects x 256 points, 3 levels; both pyramids whole (the
+    role-split build, klt_pyr_fp.hip) and LK on a seeded 8192-point sample"""
+    from opencv_amd import klt
+
+    W, H, nobj = 3840, 2160, 512
+    fr, gt = klt.synth_render(20261015, W, H, nobj, 0, 2, ctx=gpu)
+    rng = np.random.default_rng(5)
+    f = [(x.cpu().numpy().astype(np.float32) + rng.normal(0, 0.25, (H, W))).astype(np.float32) for x in fr]
+    pts = box_points(gt[0].numpy(), 256)
+    assert len(pts) == nobj * 256
+    P0, P1 = _dev_pyr(gpu, f[0], (21, 21), 2), _dev_pyr(gpu, f[1], (21, 21), 2)
+    lk = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30)
+    r = lk.calc(P0, P1, to_dev(pts), want_iters=True)
+    torch.cuda.synchronize()
+    R0, R1 = O.Pyramid16(f[0], (21, 21), 2, f32=True), O.Pyramid16(f[1], (21, 21), 2, f32=True)
+    for P, R in ((P0, R0), (P1, R1)):
+        assert P.nlevels == R.nlevels == 3
+        for i in range(3):
+            assert np.array_equal(P.level(i).view(np.uint32), R.levels[i].view(np.uint32)), f"level {i}"
+            assert np.array_equal(P.deriv(i).view(np.uint32), R.derivs[i].view(np.uint32)), f"deriv {i}"
+    idx = np.sort(np.random.default_rng(4).choice(len(pts), 8192, replace=False))
+    nx, st, er, it = O.lk16(R0, R1, pts[idx], (21, 21), 2, nthreads=16)
+    g_st = r.status.cpu().numpy()[idx]
+    assert np.array_equal(g_st, st)
+    ok = st == 1
+    assert np.array_equal(r.next_pts.cpu().numpy()[idx][ok].view(np.uint32), nx[ok].view(np.uint32))
+    assert np.array_equal(r.err.cpu().numpy()[idx][ok].view(np.uint32), er[ok].view(np.uint32))
+    assert np.array_equal(r.iters.cpu().numpy()[idx], it)
+    assert st.mean() > 0.9
