@@ -74,8 +74,8 @@ def pyr_build_bytes(w: int, h: int, nlevels: int, pad: int = 32) -> int:
 
 def max_over_ranks(value: float, world: int, device=None) -> float:
     """Max of a per-rank wall time over all ranks (the contract's job time).
-    Collective only when world > 1; the tensor lives on `device` (cuda for
-    RCCL, cpu for gloo)."""
+    Collective only when world > 1; the tensor lives on `device` (cpu: the
+    bench's group is gloo, see main())."""
     if world <= 1:
         return value
     import torch
@@ -739,6 +739,26 @@ def progress(msg: str, rank: int = 0):
         print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
+def init_rank_group(world: int, rank: int, local: int) -> None:
+    """Select the rank's GPU and, at world > 1, join the job's process group.
+
+    The replicas exchange nothing on the data path: the
+    contract's barriers and the max-over-ranks time go over a gloo (host)
+    group, so no RCCL communicator creates GPU streams.  HIP maps a process's
+    streams onto its 4 hardware queues in creation order, and the TBD loop
+    drops from ~4.8k to ~3k frames/s when more than four streams exist before
+    its own."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(0)
+
+
 def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_leg=None):
     """The bench contract, independent of what a step is: the rank's own
     sequence (seed + rank), W untimed warm-up steps, then EXACTLY K steps
@@ -856,7 +876,7 @@ def timed_on_all_ranks(fn, world):
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    return max_over_ranks(el, world, device="cuda")
+    return max_over_ranks(el, world, device="cpu")
 
 
 def sequence_repeats(m: TbdMeasure, world: int, runs: int, skip: int):
@@ -1153,12 +1173,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    init_rank_group(world, rank, local)
     dev = torch.cuda.current_device()
     if not args.no_pin and not pin.get("pinned") and "already" not in pin.get("reason", ""):
         first = pin.get("reason")
@@ -1183,7 +1198,7 @@ def main(argv=None):
     # host load between the timed region and the secondary GPU legs left those
     # legs measuring a cooled-down device (whole-sequence repeats ~9 % below
     # the timed region right after it)
-    line, ms = run_contract(args, world, rank, m, torch.cuda.synchronize, "cuda", cpu_leg=None)
+    line, ms = run_contract(args, world, rank, m, torch.cuda.synchronize, "cpu", cpu_leg=None)
     nb = 60  # frames handed to the CPU baseline (it stops at its time budget)
     cpu_in = (m.frames[:nb].cpu().numpy(), m.gtn[:nb]) if (rank == 0 and world == 1 and
                                                           not args.no_cpu_baseline) else None

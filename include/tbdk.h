@@ -272,7 +272,14 @@ int tbdk_pyr_build_f32(tbdk_ctx* ctx, const float* img, int pitch, tbdk_pyr* pyr
  * all of them).  Levels hold cn fp32 values per pixel, the derivative planes
  * an (Ix, Iy) fp32 pair per value; tbdk_pyr_build / _build_u16 / _build_f32
  * take frames of cn interleaved u8 / u16 / fp32 values per pixel;
- * tbdk_lk_sparse (impl 0) tracks on two such pyramids. */
+ * tbdk_lk_sparse (impl 0) tracks on two such pyramids.
+ * Semantics are the CPU path's, not the CUDA class's: err is the L1 mean over
+ * 32 * win_w * cn * win_h (lkpyramid.cpp:690; pyrlk.cu:555 divides by
+ * min(cn, 3) * win_w * win_h instead, and reads 16U frames through normalised
+ * [0, 1] textures), and the minEigThreshold gate applies to the raw values (the
+ * CUDA class has none).  cn = 2 is accepted here, as buildOpticalFlowPyramid /
+ * calcOpticalFlowPyrLK accept it; the typed-frame facades reject it as the
+ * CUDA class does (pyrlk.cpp:142,228). */
 int tbdk_pyr_create_f32_cn(tbdk_ctx* ctx, int width, int height, int cn, int max_level,
                            int win_w, int win_h, tbdk_pyr* pyr);
 

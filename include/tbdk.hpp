@@ -214,6 +214,9 @@ public:
     {
         if (n == 0) return;
         if (prevImg.depth != nextImg.depth || prevImg.cn != nextImg.cn) throw Error(TBDK_EINVAL, "calc: types");
+        // the CUDA class asserts cn 1, 3 or 4 on its frames (pyrlk.cpp:142,228);
+        // prebuilt Pyramids (below) take any count, as calcOpticalFlowPyrLK does
+        if (prevImg.cn != 1 && prevImg.cn != 3 && prevImg.cn != 4) throw Error(TBDK_EINVAL, "calc: channels");
         const int pdepth = prevImg.depth == DEPTH_8U ? TBDK_DEPTH_8U : TBDK_DEPTH_32F;
         for (int i = 0; i < 2; ++i) {
             const GpuMatView& im = i == 0 ? prevImg : nextImg;

@@ -194,6 +194,17 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 #endif
 constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 
+// Probe builds (-DTBDK_LK_TRACE, tools/probe_lk_trace.py): every wave appends
+// one record of six u64 to a device buffer set by tbdk_probe_lk_trace():
+// start / end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32, n << 32 | wave,
+// the launch's point-list key, Newton steps | reloads << 16 | max iters << 32.
+// Not in the product library.
+#ifdef TBDK_LK_TRACE
+__device__ unsigned long long* g_lk_trace;
+__device__ unsigned int g_lk_trace_n;
+__device__ unsigned int g_lk_trace_cap;
+#endif
+
 #ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
 #define TBDK_MULTI_BOUNDS __launch_bounds__(64 * TBDK_LK_MULTI_WAVES, TBDK_LK_MULTI_MINW)
 #else
@@ -223,6 +234,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     const int i = k < P ? seg_point(a, wave * P + k) : -1;
     const bool valid = i >= 0;
     if (!any_lane(valid)) return;  // wave-uniform
+#ifdef TBDK_LK_TRACE
+    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
+    int tr_steps = 0, tr_reloads = 0;
+#endif
     const int e4 = 4 * (k * WW + WW), s4 = 4 * (k * WW);  // last lane of the point, lane before its first
     const int rnd9 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 5 - 1));
     const int rnd14 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 1));
@@ -475,6 +490,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < a.max_count; ++j) {
             if (!any_lane(act)) break;
+#ifdef TBDK_LK_TRACE
+            ++tr_steps;
+#endif
 #if TBDK_LK_PRIO_STEPS > 0
             if (++wsteps == TBDK_LK_PRIO_STEPS) __builtin_amdgcn_s_setprio(3);
 #endif
@@ -492,6 +510,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             if (TBDK_LK_PROBE_RELOADS == 1 || (TBDK_LK_PROBE_RELOADS != 3 && any_lane(moved))) {
 #else
             if (any_lane(moved)) {  // uniform: reload the J columns (unchanged for points that did not move)
+#endif
+#ifdef TBDK_LK_TRACE
+                ++tr_reloads;
 #endif
                 const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
 #pragma unroll
@@ -626,6 +647,29 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         }
     }
 
+#ifdef TBDK_LK_TRACE
+    {
+        int mx = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) mx = max(mx, __builtin_amdgcn_readlane(valid ? nit : 0, 1 + q * WW));
+        const unsigned long long tr_t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
+        if (lane == 0) {
+            const unsigned r = atomicAdd(&g_lk_trace_n, 1u);
+            if (r < g_lk_trace_cap) {
+                unsigned long long* o = g_lk_trace + 6ull * r;
+                o[0] = tr_t0;
+                o[1] = tr_t1;
+                o[2] = hw | ((unsigned long long)xcc << 32);
+                o[3] = ((unsigned long long)(unsigned)a.n << 32) | (unsigned)wave;
+                o[4] = (unsigned long long)(uintptr_t)(a.seg_list ? (const void*)a.seg_list : (const void*)a.prev_pts);
+                o[5] = (unsigned)tr_steps | ((unsigned long long)(unsigned)tr_reloads << 16) |
+                       ((unsigned long long)(unsigned)mx << 32);
+            }
+        }
+    }
+#endif
     if (valid && x == 0) {
         a.next_pts[2 * i] = outx;
         a.next_pts[2 * i + 1] = outy;
@@ -673,3 +717,20 @@ hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s)
 }
 
 }  // namespace tbdk
+
+#ifdef TBDK_LK_TRACE
+extern "C" int tbdk_probe_lk_trace(void* buf, unsigned cap)
+{
+    unsigned long long* p = static_cast<unsigned long long*>(buf);
+    const unsigned zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace), &p, sizeof(p)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace_cap), &cap, sizeof(cap)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace_n), &zero, sizeof(zero)) != hipSuccess)
+        return -2;
+    return 0;
+}
+extern "C" int tbdk_probe_lk_trace_count(unsigned* n)
+{
+    return hipMemcpyFromSymbol(n, HIP_SYMBOL(tbdk::g_lk_trace_n), sizeof(*n)) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -394,7 +394,7 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
     return hipGetLastError();
 }
 
-// ---- levels 0, 1 and 2 in one launch (pyr_fuse 2, the default) ----------------
+// ---- levels 0, 1 and 2 in one launch (pyr_fuse 2, opt-in for A/B runs) -------
 //
 // One workgroup per tile of TX x TY level-2 pixels (level 1: 2TX x 2TY, the
 // frame: 4TX x 4TY), every byte of the frame read once into LDS (16-byte loads

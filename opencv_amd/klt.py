@@ -386,7 +386,10 @@ class SparsePyrLKOpticalFlow:
 
     def _as_pyr(self, img) -> Pyramid:
         if isinstance(img, Pyramid):
-            return img
+            return img  # prebuilt pyramids: any channel count, as calcOpticalFlowPyrLK
+        if torch.is_tensor(img) and img.dim() == 3 and img.shape[2] == 2:
+            # the CUDA class takes 1, 3 or 4 channels (CV_Assert, cudaoptflow/src/pyrlk.cpp:142,228)
+            raise _lib.TbdkError("SparsePyrLKOpticalFlow.calc: frames must have 1, 3 or 4 channels")
         return build_pyramid(img, self.win, self.max_level, self.ctx)
 
     def calc(self, prevImg, nextImg, prevPts: torch.Tensor, nextPts: torch.Tensor | None = None,

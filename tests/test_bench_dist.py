@@ -49,6 +49,51 @@ def test_replica_timing_world_size_2():
     assert all(abs(r[2] - 480 * 2 / 2.0) < 1e-12 for r in res)  # frames of all ranks / max time
 
 
+def _group_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = []
+    torch.cuda.set_device = lambda d: dev.append(d)  # no GPU here; record the selection
+    bench.init_rank_group(world, rank, rank)
+    backend = dist.get_backend()
+    el = bench.max_over_ranks([1.0, 4.0][rank], world, device="cpu")
+    q.put((rank, backend, dev, el))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_group_is_host_only_world_size_2():
+    """bench.init_rank_group at world size 2: each rank selects its own GPU and
+    the job's group is gloo, so no RCCL communicator (and none of its GPU
+    streams) exists before the TBD loop's own streams — HIP's creation-order
+    queue mapping cannot push the loop onto a shared hardware queue
+    (DESIGN.md §8)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == ["gloo", "gloo"]
+    assert [r[2] for r in res] == [[0], [1]]
+    assert [r[3] for r in res] == [4.0, 4.0]
+
+
+def test_bench_creates_no_rccl_group():
+    """No code path of bench.py creates an RCCL (nccl) process group."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'init_process_group("nccl"' not in src and "init_process_group('nccl'" not in src
+
+
 def test_single_rank_needs_no_collective():
     sys.path.insert(0, ROOT)
     import bench

@@ -149,7 +149,8 @@ def test_f32_cn_pyramid_bit_exact(gpu, kind, cn):
 
 
 @pytest.mark.parametrize("kind,cn,win,maxlev", [("f32", 3, 21, 3), ("f32", 4, 21, 2), ("u16", 3, 15, 2),
-                                                ("u16", 4, 31, 1), ("f32", 3, 7, 0), ("u16", 4, 9, 3)])
+                                                ("u16", 4, 31, 1), ("f32", 3, 7, 0), ("u16", 4, 9, 3),
+                                                ("u16", 4, 45, 1)])  # > 64 KB of LDS: the opt-in path
 def test_f32_cn_lk_bit_exact(gpu, kind, cn, win, maxlev):
     from opencv_amd import klt
 

@@ -291,3 +291,48 @@ def test_tbd_run_host_matches_run(gpu):
         got += [_mkey(m) for m in loop.run_host(src[9:], 9, dets[9:])]
         assert got == want
         assert loop.tracks() == ref.tracks()
+
+
+def test_tbd_lookahead_then_no_tracks(gpu):
+    """Detections vanish for a stretch, so a step that issued look-ahead PyrLK
+    (speculative, and on re-detection frames the early rows') ends with every
+    track deleted, and the next step has no tracks: it skips KLT and rebuilds
+    the next pyramid over the frame that look-ahead PyrLK may still be reading
+    (tbd_loop.hip, the wait on la_done in the no-KLT branch).  Then detections
+    return and new tracks start.  Frames, predictions and tracks equal the
+    same sequence with the look-ahead off, through run and per-step ahead."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 640, 480, 16, 40
+    frames, gt = klt.synth_render(17, W, H, N, 0, F, ctx=gpu)
+    dets = []
+    for f in range(F):
+        d = tbd.detections_from_gt(gt[f].numpy())
+        dets.append(d[:0].copy() if 10 <= f < 26 else d)
+    c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=5)
+    res = {}
+    try:
+        for spec, ela in ((1, 1), (1, 2), (0, 0)):
+            gpu.set_option("tbd_spec_lookahead", spec)
+            gpu.set_option("tbd_early_la", ela)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = [_mkey(m) for m in loop.run(frames, 0, dets)]
+            ahead = tbd.TbdLoop(c, ctx=gpu)
+            ma, pa = [], []
+            for f in range(F):
+                ma.append(_mkey(ahead.step(frames[f], f, dets[f], next_frame=frames[f + 1] if f + 1 < F else None)))
+                pa.append(ahead.predictions())
+            torch.cuda.synchronize()
+            assert ms == ma, (spec, ela)
+            assert loop.tracks() == ahead.tracks(), (spec, ela)
+            res[spec, ela] = (ms, pa, loop.tracks())
+    finally:
+        gpu.set_option("tbd_spec_lookahead", 1)
+        gpu.set_option("tbd_early_la", 1)
+    base = res[0, 0]
+    for key, r in res.items():
+        assert r == base, key
+    nt = [m[6] for m in base[0]]
+    gap = [f for f in range(11, 26) if nt[f - 1] > 0 and nt[f] == 0]
+    assert gap, f"no step ended with every track deleted: {nt}"  # the no-track step follows it
+    assert nt[-1] > 0 and sum(m[7] for m in base[0][27:]) > 0  # tracking resumed after the gap
