@@ -92,24 +92,55 @@ def replica_throughput(steps: int, world: int, max_elapsed: float) -> float:
     return steps * world / max_elapsed
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/rNN_pmc.json, separate --pmc passes, see tools/profile_round.sh):
-    FETCH_SIZE + WRITE_SIZE as counted.  The guide's x2 applies to wide (16 B
-    per lane) streaming reads; these kernels load 4 B per lane (or less), and the
-    pyramid's counts match its known read / write sets without it.
-    None when no summary covers the kernel."""
+def _pmc_summaries(suffix: str):
     d = os.path.join(ROOT, "profiles")
     try:
-        files = sorted(f for f in os.listdir(d) if f.endswith("_pmc.json"))
+        return d, sorted(f for f in os.listdir(d) if f.endswith(suffix))
     except OSError:
-        return None, None
+        return d, []
+
+
+def pmc_traffic(kernel_substr: str, suffix: str = "_pmc_loop.json"):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (separate --pmc passes, tools/profile_round.sh): FETCH_SIZE + WRITE_SIZE as
+    counted.  The loop's kernels read profiles/rNN_pmc_loop.json, whose passes
+    run only the contract's legs (bench.py --no-secondary: the 1080p x 128 loop),
+    so no other configuration's launches of the same kernel (the 4K pyramid leg,
+    the bounds-at-frame leg) enter the means; the secondaries' kernels read
+    rNN_pmc.json (suffix).  The guide's x2 applies to wide (16 B per lane)
+    streaming reads; these kernels load 4 B per lane (or less), and the
+    pyramid's counts match its known read / write sets without it (DESIGN.md
+    §7).  None when no summary covers the kernel."""
+    d, files = _pmc_summaries(suffix)
     for f in reversed(files):
         k = json.load(open(os.path.join(d, f)))["kernels"]
         for name, v in k.items():
             if kernel_substr in name and v.get("fetch_bytes") is not None and v.get("write_bytes") is not None:
                 return v["fetch_size_kib"] * 1024 + v["write_bytes"], f
     return None, None
+
+
+def ktrace_grid_us(frags, pick: str = "max_grid"):
+    """Kernel-trace durations (rocprofv3's GPU start / end: no launch cost) per
+    kernel and grid from the newest committed profiles/rNN_ktrace_grid.json
+    (tools/ktrace_by_grid.py over the profiled bench run): for each kernel name
+    fragment the entry of the largest grid (pick "max_grid": the 4K leg's
+    launches) or of the most dispatches (pick "most": the loop's); (sum of
+    their mean durations in us, [(kernel, grid, dispatches, avg_us)], source)
+    or (None, None, None)."""
+    d, files = _pmc_summaries("_ktrace_grid.json")
+    if not files:
+        return None, None, None
+    ents = json.load(open(os.path.join(d, files[-1])))["entries"]
+    tot, used = 0.0, []
+    for frag in frags:
+        c = [e for e in ents if frag in e["kernel"]]
+        if not c:
+            return None, None, None
+        e = max(c, key=(lambda e: e["grid"]) if pick == "max_grid" else (lambda e: e["dispatches"]))
+        tot += e["avg_us"]
+        used.append((e["kernel"], e["grid"], e["dispatches"], e["avg_us"]))
+    return round(tot, 3), used, files[-1]
 
 
 # ---- host cores and rank pinning --------------------------------------------------------------
@@ -460,7 +491,7 @@ def farneback_secondary(ctx, args, device, cpu: bool):
     gbs = it_bytes / (kern["fb_iter"]["ms_per_pair"] * n * 1e-3) / 1e9 if kern["fb_iter"]["launches"] else 0.0
     # PMC bytes per fb_iter launch (the committed summary's mean over a pair's
     # launches, all levels) x launches per pair -> HBM bytes per pair
-    per_launch, traffic_src = pmc_traffic("fb_iter_kernel<6, false>")
+    per_launch, traffic_src = pmc_traffic("fb_iter_kernel<6, false>", "_pmc.json")
     launches_per_pair = kern["fb_iter"]["launches"] / n
     traffic = per_launch * launches_per_pair if per_launch is not None else None
     alg_pair = it_bytes / n
@@ -1037,11 +1068,14 @@ def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
     del fr, P
     cp = copy_rate_at(ctx, b)
     tr, tr2, src = pmc_pyr_traffic("u8", [("pyr_build_kernel", 1), ("pyr_down_padded_kernel", 1)])
+    kt_us, kt_used, kt_src = ktrace_grid_us(("pyr_build_kernel", "pyr_down_padded_kernel"), "max_grid")
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": b, "avg_us": round(us, 2), "builds": c,
             "traffic": tr, "traffic_fetch_x2": tr2, "traffic_source": src,
             "traffic_over_algorithmic": round(tr / b, 3) if tr else None,
             "size_matched_copy": cp, "frac_size_matched_copy": round(gbs / cp["gbs"], 4),
+            "kernel_trace_us": kt_us, "kernel_trace_launches": kt_used, "kernel_trace_source": kt_src,
+            "frac_kernel_trace": round(b / (kt_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4) if kt_us else None,
             "kernel": "pyr_build (levels only, u8, 3840x2160, 3 levels)",
             "note": "algorithmic bytes (frame read once, padded levels written, level 2 reading level 1) / the "
                     "build's HIP-event time (events on the launch stream around its launches)"}
@@ -1080,14 +1114,11 @@ PYR_KERNELS = ("pyr_build_kernel", "pad_copy_kernel", "pyr_down_padded_kernel", 
 
 
 def pmc_bytes(kernel_substrs):
-    """Sum over kernels of the committed PMC summary's per-launch bytes (raw
-    FETCH_SIZE, FETCH_SIZE x2 as the guide's wide-read correction, WRITE_SIZE);
-    None when no summary covers them."""
-    d = os.path.join(ROOT, "profiles")
-    try:
-        files = sorted(f for f in os.listdir(d) if f.endswith("_pmc.json"))
-    except OSError:
-        return None
+    """Sum over kernels of the committed loop-only PMC summary's per-launch
+    bytes (profiles/rNN_pmc_loop.json, see pmc_traffic; raw FETCH_SIZE,
+    FETCH_SIZE x2 as the guide's wide-read correction, WRITE_SIZE); None when
+    no summary covers them."""
+    d, files = _pmc_summaries("_pmc_loop.json")
     for f in reversed(files):
         k = json.load(open(os.path.join(d, f)))["kernels"]
         hit = [(n, v) for n, v in k.items() if any(s in n for s in kernel_substrs)
@@ -1308,10 +1339,13 @@ def main(argv=None):
     pyr_gbs = pbb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     cnt = pmc_bytes(PYR_KERNELS)
     cp_pyr = copy_rate_at(ctx, pbb) if not args.no_copy_peak else None
+    kt_us, kt_used, kt_src = ktrace_grid_us(("pyr_build_kernel", "pyr_down_padded_kernel"), "most")
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pbb, "b_pyr_survey": pb,
                 "size_matched_copy": cp_pyr,
                 "frac_size_matched_copy": round(pyr_gbs / cp_pyr["gbs"], 4) if cp_pyr else None,
+                "kernel_trace_us": kt_us, "kernel_trace_launches": kt_used, "kernel_trace_source": kt_src,
+                "frac_kernel_trace": round(pbb / (kt_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4) if kt_us else None,
                 "kernel": "pyr_build",
                 "traffic": (cnt["fetch_raw"] + cnt["write"]) if cnt else None,
                 "traffic_fetch_x2": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,

@@ -194,15 +194,20 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 #endif
 constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 
-// Probe builds (-DTBDK_LK_TRACE, tools/probe_lk_trace.py): every wave appends
-// one record of six u64 to a device buffer set by tbdk_probe_lk_trace():
+// Probe builds (-DTBDK_LK_TRACE, tools/probe_lk_trace.py): every wave writes
+// one record of sixteen u64 (at its launch's base + its wave index, no atomics:
+// a device-wide atomic counter serialises the waves' exits) to a device buffer
+// set by tbdk_probe_lk_trace():
 // start / end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32, n << 32 | wave,
-// the launch's point-list key, Newton steps | reloads << 16 | max iters << 32.
+// the launch's point-list key, Newton steps | reloads << 16 | max iters << 32,
+// then 16 u32 phase stamps (ticks after start): per level L, [4L] its start,
+// [4L+1] the setup's G sums done, [4L+2] the first J window loaded (the probe
+// waits for it there), [4L+3] its Newton steps done; [12] the error pass done.
 // Not in the product library.
 #ifdef TBDK_LK_TRACE
 __device__ unsigned long long* g_lk_trace;
-__device__ unsigned int g_lk_trace_n;
 __device__ unsigned int g_lk_trace_cap;
+static unsigned g_lk_trace_next;  // host: records handed out so far
 #endif
 
 #ifdef TBDK_LK_MULTI_MINW  // waves per SIMD the register allocation must allow (tuning builds)
@@ -237,6 +242,13 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #ifdef TBDK_LK_TRACE
     const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
     int tr_steps = 0, tr_reloads = 0;
+    auto tr_stamp = [&](int idx) {
+        const unsigned r = a.trace_base + (unsigned)wave;
+        const unsigned d = (unsigned)(__builtin_amdgcn_s_memrealtime() - tr_t0);
+        if (lane == 0 && r < g_lk_trace_cap) reinterpret_cast<unsigned*>(g_lk_trace + 16ull * r + 6)[idx] = d;
+    };
+#else
+    auto tr_stamp = [](int) {};
 #endif
     const int e4 = 4 * (k * WW + WW), s4 = 4 * (k * WW);  // last lane of the point, lane before its first
     const int rnd9 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 5 - 1));
@@ -261,6 +273,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 
     for (int level = a.max_level; level >= 0; --level) {
         const LkLevel L = a.lv[level];
+        tr_stamp(4 * level);
         const float sc = (float)(1. / (1 << level));
         float prevx = p0x * sc, prevy = p0y * sc;
         float nextx, nexty;
@@ -463,6 +476,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             if (k >= P) acc[0] = acc[1] = acc[2] = 0;
             float s[3];
             seg_sum_exact<3>(acc, e4, s4, s);
+            tr_stamp(4 * level + 1);
             // J columns at the first Newton position, loaded after the G sums (with
             // the loads in flight during the sums the kernel needs 148 VGPRs, 3
             // waves per SIMD; this way 116, 4 waves)
@@ -471,6 +485,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + pinx + x + L.jpad) : 0u;
 #pragma unroll
                 for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+#ifdef TBDK_LK_TRACE
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+                tr_stamp(4 * level + 2);
             }
             // A = float(exact sum) * 2^-20   (lkpyramid.cpp:438-440)
             A11 = s[0] * FLT_SCALE;
@@ -586,6 +604,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             }
         }
 
+        tr_stamp(4 * level + 3);
         if (level == 0 && a.err && (a.flags & TBDK_OPTFLOW_LK_GET_MIN_EIGENVALS) == 0) {
             bool want = valid && status;
             const float npx = outx - halfx, npy = outy - halfy;
@@ -643,6 +662,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 if (k >= P) e = 0;
                 const float errval = (float)seg_sum_small(e, e4, s4);
                 if (want) errv = errval * 1.f / (float)(32 * WW * WH);
+                tr_stamp(12);
             }
         }
     }
@@ -656,9 +676,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
         const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
         if (lane == 0) {
-            const unsigned r = atomicAdd(&g_lk_trace_n, 1u);
+            const unsigned r = a.trace_base + (unsigned)wave;
             if (r < g_lk_trace_cap) {
-                unsigned long long* o = g_lk_trace + 6ull * r;
+                unsigned long long* o = g_lk_trace + 16ull * r;
                 o[0] = tr_t0;
                 o[1] = tr_t1;
                 o[2] = hw | ((unsigned long long)xcc << 32);
@@ -702,11 +722,19 @@ hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s)
     if (!lk_multi_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
     const int per_wg = kMultiWaves * (64 / a.win_w);  // waves of P points
     const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * kMultiWaves);
+#ifdef TBDK_LK_TRACE
+    LkArgs at = a;
+    at.trace_base = g_lk_trace_next;
+    g_lk_trace_next += grid.x * kMultiWaves;
+    const LkArgs& la = at;
+#else
+    const LkArgs& la = a;
+#endif
     switch (a.win_w) {
-#define TBDK_CASE(W)                                                                   \
-    case W:                                                                            \
-        if (fly) hipLaunchKernelGGL((lk_multi_kernel<W, W, true>), grid, block, 0, s, a);  \
-        else hipLaunchKernelGGL((lk_multi_kernel<W, W, false>), grid, block, 0, s, a); \
+#define TBDK_CASE(W)                                                                    \
+    case W:                                                                             \
+        if (fly) hipLaunchKernelGGL((lk_multi_kernel<W, W, true>), grid, block, 0, s, la);  \
+        else hipLaunchKernelGGL((lk_multi_kernel<W, W, false>), grid, block, 0, s, la); \
         break;
         TBDK_MULTI_WINDOWS(TBDK_CASE)
 #undef TBDK_CASE
@@ -722,15 +750,19 @@ hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s)
 extern "C" int tbdk_probe_lk_trace(void* buf, unsigned cap)
 {
     unsigned long long* p = static_cast<unsigned long long*>(buf);
-    const unsigned zero = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace), &p, sizeof(p)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace_cap), &cap, sizeof(cap)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace_n), &zero, sizeof(zero)) != hipSuccess)
+    cap /= 16;  // records of sixteen u64
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace), &p, sizeof(p)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(tbdk::g_lk_trace_cap), &cap, sizeof(cap)) != hipSuccess)
         return -2;
+    tbdk::g_lk_trace_next = 0;
     return 0;
 }
+// records handed out since tbdk_probe_lk_trace (waves that exit early, with no
+// valid point, leave theirs zero)
 extern "C" int tbdk_probe_lk_trace_count(unsigned* n)
 {
-    return hipMemcpyFromSymbol(n, HIP_SYMBOL(tbdk::g_lk_trace_n), sizeof(*n)) == hipSuccess ? 0 : -2;
+    *n = tbdk::g_lk_trace_next;
+    return 0;
 }
 #endif

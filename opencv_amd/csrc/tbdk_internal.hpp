@@ -157,6 +157,9 @@ struct LkArgs {
     uint8_t* status;
     float* err;
     int32_t* iters;
+#ifdef TBDK_LK_TRACE
+    unsigned trace_base;  // probe builds: first trace record of this launch (klt_lk_multi.hip)
+#endif
 };
 
 // launch index -> point index under the segmented layout, -1 if none

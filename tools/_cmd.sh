@@ -1,6 +1,8 @@
-set -e
-R=$GRAFT_REPO_ROOT
-cd $R
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b22.json 2> gpurun_out/b22.err
-python3 -c "
-import json; d=json.loads(open('gpurun_out/b22.json').read().strip().splitlines()[-1]); print(d['value'], d['sequence']['runs_fps'], d['with_h2d']['runs_fps'], d['step_api'], d['kitti']['value'], d['roofline']['frac'])"
+mkdir -p gpurun_out/tl
+root=$(pwd); cd /tmp; export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $root/gpurun_out/tl -o kt -- python3 $root/bench.py --no-secondary --no-cpu-baseline > $root/gpurun_out/tl/bench.json 2> $root/gpurun_out/tl/bench.err || exit 1
+cd $root
+f=$(find gpurun_out/tl -name "*kernel_trace.csv" | head -1)
+python3 tools/timeline.py gpurun_out/tl --first pyr_build_kernel --skip 100 --frames 4 > gpurun_out/tl/timeline.txt
+python3 tools/gaps.py $f > gpurun_out/tl/gaps.txt
+head -30 gpurun_out/tl/timeline.txt

@@ -20,19 +20,22 @@ import torch
 
 from opencv_amd import klt, tbd
 
-CAP = 1 << 20
+CAP = 1 << 19  # records
 TICK_US = 0.01
 
 
 def arm(lib, buf):
-    assert lib.tbdk_probe_lk_trace(C.c_void_p(buf.data_ptr()), C.c_uint(CAP)) == 0
+    buf.zero_()
+    torch.cuda.synchronize()
+    assert lib.tbdk_probe_lk_trace(C.c_void_p(buf.data_ptr()), C.c_uint(16 * CAP)) == 0
 
 
 def records(lib, buf):
     n = C.c_uint()
     assert lib.tbdk_probe_lk_trace_count(C.byref(n)) == 0
     n = min(n.value, CAP)
-    return buf[: 6 * n].view(-1, 6).cpu().numpy().view(np.uint64)
+    r = buf[: 16 * n].view(-1, 16).cpu().numpy().view(np.uint64)
+    return r[r[:, 0] != 0]  # waves with no valid point exit before recording
 
 
 def split_launches(r):
@@ -83,10 +86,23 @@ def summarize(rec, label=""):
         o[int(b)] -= 1
     o = np.cumsum(o)[:nb]
     last = np.argsort(en)[-5:][::-1]
+    ph = rec[:, 6:14].copy().view(np.uint32).astype(np.float64) * TICK_US  # (waves, 16) phase stamps
+    phs = []
+    for L in (2, 1, 0):
+        a0, a1, a2, a3 = ph[:, 4 * L], ph[:, 4 * L + 1], ph[:, 4 * L + 2], ph[:, 4 * L + 3]
+        ok = a3 > 0
+        if ok.sum():
+            phs.append(f"L{L}: setup {np.mean(a1[ok] - a0[ok]):.2f} jload {np.mean(a2[ok] - a1[ok]):.2f} "
+                       f"newton {np.mean(a3[ok] - a2[ok]):.2f}")
+    e = ph[:, 12]
+    ok = e > 0
+    if ok.sum():
+        phs.append(f"err {np.mean(e[ok] - ph[ok, 3]):.2f}")
     s = (f"{label} waves {len(rec)} span {span:.1f} us; ends p50 {q(.5):.1f} p90 {q(.9):.1f} p99 {q(.99):.1f}; "
          f"starts max {st.max():.1f}; dur p50 {np.median(dur):.1f} p90 {np.percentile(dur, 90):.1f} max {dur.max():.1f}; "
          f"waves/SIMD mean {occ:.2f} (SIMDs used {uniq}); resident peak {o.max():.0f}; "
          f"steps mean {steps.mean():.1f} max {steps.max()}; reloads mean {rel.mean():.2f}; maxit mean {mit.mean():.1f}\n")
+    s += "   phases (mean us): " + "; ".join(phs) + "\n"
     s += "   occupancy by 10%% of span: " + " ".join(
         f"{o[int(i * nb / 10):int((i + 1) * nb / 10)].mean() / 1024:.2f}" for i in range(10)) + "\n"
     s += "   last waves (start, dur, steps, reloads, maxit): " + "; ".join(
@@ -163,7 +179,7 @@ def run_standalone(lib, buf):
 
 def main():
     lib = C.CDLL(os.environ["TBDK_LIB"])
-    buf = torch.zeros(6 * CAP, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(16 * CAP, dtype=torch.int64, device="cuda")
     mode = sys.argv[1] if len(sys.argv) > 1 else "loop"
     os.makedirs("gpurun_out", exist_ok=True)
     if mode == "standalone":
