@@ -39,11 +39,43 @@ def main():
     c, n = c.cpu().numpy(), n.cpu().numpy()
     pts = np.concatenate([c[i, :n[i]] for i in range(len(rois))]).astype(np.float32)
     box = np.concatenate([np.full(n[i], i) for i in range(len(rois))])
+    rank = np.concatenate([np.arange(n[i]) for i in range(len(rois))])  # GFTT order: strongest corner first
+    bx = np.array(rois, dtype=np.float64)
+    bdist = np.minimum.reduce([pts[:, 0] - bx[box, 0], pts[:, 1] - bx[box, 1], bx[box, 0] + bx[box, 2] - 1 - pts[:, 0],
+                               bx[box, 1] + bx[box, 3] - 1 - pts[:, 1]])  # to the box's border, px
     P = [klt.Pyramid(ctx, W, H, 2, derivs=False).build(frames[i]) for i in range(3)]
     lk = klt.SparsePyrLKOpticalFlow((21, 21), 2, 30)
     r01 = lk.calc(P[0], P[1], torch.from_numpy(pts).cuda(), want_iters=True)
     torch.cuda.synchronize()
     ok = r01.status.cpu().numpy() == 1
+    it0 = r01.iters.cpu().numpy()
+    print(f"fresh corners 0->1: corr(iterations, rank in box) {np.corrcoef(it0, rank)[0, 1]:.3f}, "
+          f"corr(iterations, distance to box border) {np.corrcoef(it0, bdist)[0, 1]:.3f}, "
+          f"corr(iterations, border distance < 11) {np.corrcoef(it0, bdist < 11)[0, 1]:.3f}; iterations by border "
+          f"distance <11 / >=11: {it0[bdist < 11].mean():.2f} / {it0[bdist >= 11].mean():.2f}", flush=True)
+    nb0 = int(sys.argv[1]) if len(sys.argv) > 1 else 68
+    s0 = box < nb0
+    q0, it0s, rk0, bd0 = pts[s0], it0[s0], rank[s0], bdist[s0]
+    o0 = {"natural": np.arange(len(q0)), "oracle": np.argsort(-it0s, kind="stable"),
+          "border_first": np.lexsort((np.arange(len(q0)), bd0 >= 11)),
+          "weak_first_in_box": np.lexsort((-rk0, box[s0]))}
+    r0 = {k: [] for k in o0}
+    for rnd in range(5):
+        for name, o in o0.items():
+            d = torch.from_numpy(q0[o]).cuda()
+            for _ in range(3):
+                lk.calc(P[0], P[1], d)
+            torch.cuda.synchronize()
+            ctx.timing_select(["lk_sparse"])
+            ctx.timing_enable(True)
+            for _ in range(20):
+                lk.calc(P[0], P[1], d)
+            torch.cuda.synchronize()
+            cnt, ms = ctx.timing_query("lk_sparse")
+            ctx.timing_enable(False)
+            r0[name].append(ms / cnt * 1000)
+    print(f"fresh corners 0->1, {len(q0)} points: " + "; ".join(f"{k} {np.median(v):.1f} us" for k, v in r0.items()),
+          flush=True)
     p1 = r01.next_pts.cpu().numpy()[ok]
     it01 = r01.iters.cpu().numpy()[ok]
     b1 = box[ok]
