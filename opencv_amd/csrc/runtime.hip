@@ -167,7 +167,7 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_early_la") == 0) {
-        if (value < 0 || value > 3) return TBDK_EINVAL;
+        if (value < 0 || value > 2) return TBDK_EINVAL;
         ctx->opt_tbd_early_la = value;
         return TBDK_OK;
     }

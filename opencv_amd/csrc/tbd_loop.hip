@@ -269,14 +269,7 @@ struct tbdk_tbd {
     unsigned* d_fitcnt = nullptr;
     int fit_tag = 0;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
-    hipEvent_t early_ev[2] = {nullptr, nullptr};  // an early GFTT of row set k complete
-    // the next frame's early GFTT launched by this step (tbd_early_la 3 with the
-    // next frame's detections known, tbdk_tbd_run): its ROIs and row map, for the
-    // next step to adopt when its frame is pre_frame
-    bool pre_early = false;
-    const uint8_t* pre_frame = nullptr;
-    std::vector<tbdk_roi> pre_erois;
-    std::unordered_map<uint64_t, int> pre_erow_of;
+    hipEvent_t early_done = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
     std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
@@ -299,10 +292,8 @@ namespace {
 
 // Cross-stream edge: stream s waits for event ev only while ev's work is still
 // pending.  A wait enqueues a barrier packet that the consumer queue's
-// packet processor resolves before the next kernel starts (several us on the
-// frame's chain: the critical PyrLK behind the early GFTT's rows, the fit
-// behind the look-ahead PyrLK, which have usually finished by then); work that
-// is complete when the edge is enqueued needs none (its results are visible to
+// packet processor resolves before the next kernel starts; work that is
+// complete when the edge is enqueued needs none (its results are visible to
 // every later dispatch).  Event completion is monotonic, so the query cannot
 // skip a wait that is needed.
 hipError_t wait_if_pending(hipStream_t s, hipEvent_t ev)
@@ -336,8 +327,7 @@ int release(tbdk_tbd* t)
     if (t->pyr_ready) (void)hipEventDestroy(t->pyr_ready);
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
     if (t->early_s) (void)hipStreamDestroy(t->early_s);
-    for (int k = 0; k < 2; ++k)
-        if (t->early_ev[k]) (void)hipEventDestroy(t->early_ev[k]);
+    if (t->early_done) (void)hipEventDestroy(t->early_done);
     gftt_scratch_free(t->gftt);
     gftt_scratch_free(t->gftt2);
     if (t->up_s) (void)hipStreamSynchronize(t->up_s);
@@ -452,7 +442,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
     hm(reinterpret_cast<void**>(&t->h_tab), sizeof(GfttRoi) * S);
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
-    hm(reinterpret_cast<void**>(&t->h_spec), 2 * sizeof(int32_t) * S);  // speculative slots + early rows (tbd_early_la 3)
+    hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_ers), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
     if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
@@ -460,7 +450,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     sm(reinterpret_cast<void**>(&t->d_fit), t->h_fit, sizeof(FitOut) * S);
     sm(reinterpret_cast<void**>(&t->d_tab), t->h_tab, sizeof(GfttRoi) * S);
     sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
-    sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, 2 * sizeof(int32_t) * S);
+    sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_ers), t->h_ers, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
     t->fit_flag = t->zc && ctx->opt_tbd_fit_flag != 0;
@@ -503,7 +493,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess)
         e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking,
                                         ctx->opt_tbd_early_prio ? prio_greatest : prio_least);
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&t->early_ev[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -564,8 +554,7 @@ namespace {
 // while the host tracker runs), and its PyrLK of the unchanged point sets
 // behind the post-tracker GFTT; the next step skips what was done.
 int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets, int ndets,
-              const uint8_t* next, int next_pitch, tbdk_frame_metrics* metrics, hipStream_t s,
-              const tbdk_detection* next_dets = nullptr, int next_ndets = -1)
+              const uint8_t* next, int next_pitch, tbdk_frame_metrics* metrics, hipStream_t s)
 {
     if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width ||
         (next && next_pitch < t->cfg.width))
@@ -619,52 +608,50 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // PyrLK and fit); the
     // post-tracker phase takes its corners for every refreshed set whose box
     // equals one of these ROIs.
+    t->erois.clear();
+    t->erow_of.clear();
     const int S = c.max_tracks;
     const int erow0 = S * (1 + t->eb);  // this step's early GFTT rows (the previous step's: the other set)
-    hipEvent_t early_done = t->early_ev[t->eb];
     bool early_launched = false;
-    // the ROIs of frame `fid`'s early GFTT (detections dd[0, nd)): the new tracks'
-    // boxes, and on re-detection frames the guessed refreshed boxes
-    auto early_rois = [&](const tbdk_detection* dd, int nd, int fid, bool all_new, std::vector<tbdk_roi>& rois,
-                          std::unordered_map<uint64_t, int>& row_of) {
-        rois.clear();
-        row_of.clear();
-        for (int i = 0; i < nd && (int)rois.size() < c.max_tracks; ++i) {
-            const tbdk_detection& d = dd[i];
+    auto launch_early_gftt = [&]() -> int {
+        if (!c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
+        const bool all_new = t->tracker->getTracks().empty();
+        for (int i = 0; i < ndets && (int)t->erois.size() < c.max_tracks; ++i) {
+            const tbdk_detection& d = dets[i];
             const bool beyond = d.x >= c.bounds_xmax || d.y >= c.bounds_ymax || d.x + d.width < c.bounds_xmin ||
                                 d.y + d.height < c.bounds_ymin;
             if (!all_new && !beyond) continue;
             const int x0 = std::max(d.x, 0), y0 = std::max(d.y, 0);
             const int x1 = std::min(d.x + d.width, c.width), y1 = std::min(d.y + d.height, c.height);
             if (x1 - x0 < 3 || y1 - y0 < 3) continue;
-            if (!row_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)rois.size()).second) continue;
-            rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+            if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+            t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
         }
         // re-detection frames: every existing track's set is refreshed in its box
         // after updateAssignedTracks (tbd.cpp:948-965), which depends only on the
         // assigned detection and the track's box history; speculate the detection
         // of largest overlap with the track's last box and GFTT that box early
         // (a track assigned otherwise, or not at all, takes the post-tracker GFTT)
-        if (t->ctx->opt_tbd_early_gftt >= 2 && !all_new && fid % c.redetect_every == 0 && nd > 0) {
+        if (t->ctx->opt_tbd_early_gftt >= 2 && !all_new && frame_id % c.redetect_every == 0 && ndets > 0) {
             auto& order = t->det_order;
-            order.resize((size_t)nd);
+            order.resize((size_t)ndets);
             int maxw = 0;
-            for (int i = 0; i < nd; ++i) {
+            for (int i = 0; i < ndets; ++i) {
                 order[(size_t)i] = i;
-                maxw = std::max(maxw, dd[i].width);
+                maxw = std::max(maxw, dets[i].width);
             }
-            std::sort(order.begin(), order.end(), [&](int a, int b) { return dd[a].x < dd[b].x; });
+            std::sort(order.begin(), order.end(), [&](int a, int b) { return dets[a].x < dets[b].x; });
             for (const auto& tr : t->tracker->getTracks()) {
-                if ((int)rois.size() >= c.max_tracks) break;
+                if ((int)t->erois.size() >= c.max_tracks) break;
                 if (t->slot_of.find(tr.id) == t->slot_of.end()) continue;
                 const tbd::Rect& lb = tr.bboxes.back();
                 if (lb.x >= c.bounds_xmax || lb.y >= c.bounds_ymax) continue;  // deleted by the bounds filter
                 auto lo = std::lower_bound(order.begin(), order.end(), lb.x - maxw,
-                                           [&](int a, int x) { return dd[a].x < x; });
+                                           [&](int a, int x) { return dets[a].x < x; });
                 int best = -1;
                 double bo = 0.0;
-                for (auto it = lo; it != order.end() && dd[*it].x <= lb.x + lb.width; ++it) {
-                    const tbdk_detection& d = dd[*it];
+                for (auto it = lo; it != order.end() && dets[*it].x <= lb.x + lb.width; ++it) {
+                    const tbdk_detection& d = dets[*it];
                     const double o = tbd::computeBoundingBoxOverlap(lb, tbd::Rect(d.x, d.y, d.width, d.height));
                     if (o > bo) {
                         bo = o;
@@ -672,7 +659,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                     }
                 }
                 if (best < 0) continue;
-                const tbdk_detection& d = dd[best];
+                const tbdk_detection& d = dets[best];
                 const unsigned nprior = tr.historyLength < 4 ? (unsigned)tr.historyLength : 4u;
                 unsigned wsum = 0, hsum = 0;
                 for (unsigned k = tr.bboxes.size() - nprior; k < tr.bboxes.size(); ++k) {
@@ -685,48 +672,29 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 const int x0 = std::max(r.x, 0), y0 = std::max(r.y, 0);
                 const int x1 = std::min(r.x + r.width, c.width), y1 = std::min(r.y + r.height, c.height);
                 if (x1 - x0 < 3 || y1 - y0 < 3) continue;
-                if (!row_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)rois.size()).second) continue;
-                rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+                if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+                t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
         }
-    };
-    // GFTT of `rois` on level 0 of pyramid Q into row set `set` (table h_etab[set],
-    // rows S (1 + set) ..) on early_s, completion recorded on early_ev[set]
-    auto launch_early_set = [&](const std::vector<tbdk_roi>& rois, const tbdk_pyr& Q, int set) -> int {
-        GfttPlan eplan;
-        GfttRoi* htab = t->h_etab[set];
-        int rc2 = gftt_prepare(rois.data(), (int)rois.size(), c.width, c.height, &gp, htab, &eplan);
-        if (rc2 != TBDK_OK) return rc2;
-        hipStream_t es = t->early_s;  // ordered behind the pyramid it reads by the caller
-        const GfttRoi* dtab = t->zc ? t->d_etab + (htab - t->h_etab[0]) : t->d_etab;
-        if (!t->zc) {
-            hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * rois.size(), hipMemcpyHostToDevice, es);
-            if (e != hipSuccess) return map_status(e);
-        }
-        const tbdk_level& L0 = Q.lv[0];
-        const int row0 = S * (1 + set);
-        rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
-                          reinterpret_cast<float*>(t->slot_pts + (size_t)row0 * kSlotPts), t->slot_counts + row0, es,
-                          nullptr, kSlotPts);
-        if (rc2 != TBDK_OK) return rc2;
-        return map_status(hipEventRecord(t->early_ev[set], es));
-    };
-    // the previous step launched this frame's early GFTT (same frame, same row set)
-    if (t->pre_early && t->pre_frame == frame && la_valid) {
-        t->erois.swap(t->pre_erois);
-        t->erow_of.swap(t->pre_erow_of);
-        early_launched = true;
-    } else {
-        t->erois.clear();
-        t->erow_of.clear();
-    }
-    t->pre_early = false;
-    auto launch_early_gftt = [&]() -> int {
-        if (early_launched || !c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
-        early_rois(dets, ndets, frame_id, t->tracker->getTracks().empty(), t->erois, t->erow_of);
         if (!t->erois.empty()) {
-            const int r2 = launch_early_set(t->erois, P, t->eb);
-            if (r2 != TBDK_OK) return r2;
+            GfttPlan eplan;
+            GfttRoi* htab = t->h_etab[t->eb];
+            int rc2 = gftt_prepare(t->erois.data(), (int)t->erois.size(), c.width, c.height, &gp, htab, &eplan);
+            if (rc2 != TBDK_OK) return rc2;
+            hipStream_t es = t->early_s;  // ordered at the top of the step
+            const GfttRoi* dtab = t->zc ? t->d_etab + (htab - t->h_etab[0]) : t->d_etab;
+            if (!t->zc) {
+                hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * t->erois.size(),
+                                              hipMemcpyHostToDevice, es);
+                if (e != hipSuccess) return map_status(e);
+            }
+            const tbdk_level& L0 = P.lv[0];
+            rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
+                              reinterpret_cast<float*>(t->slot_pts + (size_t)erow0 * kSlotPts), t->slot_counts + erow0,
+                              es, nullptr, kSlotPts);
+            if (rc2 != TBDK_OK) return rc2;
+            const hipError_t e = hipEventRecord(t->early_done, es);
+            if (e != hipSuccess) return map_status(e);
             early_launched = true;
         }
         return TBDK_OK;
@@ -915,38 +883,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 klt_pred++;
             }
         }
-        // ---- the next frame's early GFTT, launched here (tbd_early_la 3, the next
-        // frame's detections known): on a frame that is not a re-detection frame
-        // its ROIs are the next detections beyond the tracker's bounds, which
-        // need no tracker state (a step after which no track is left would also
-        // GFTT the detections inside the bounds: those then take the
-        // post-tracker GFTT).  Launched before the look-ahead PyrLK, its 512-thread
-        // workgroups get their CUs before the PyrLK waves fill them (launched
-        // after, they wait for those waves to drain); the next step adopts it
-        // (same frame, row set eb ^ 1: free once this step's fit has compacted
-        // the rows it last held).
-        if (next && next_dets && next_ndets >= 0 && t->ctx->opt_tbd_early_la == 3 && c.use_klt &&
-            t->ctx->opt_tbd_early_gftt && (frame_id + 1) % c.redetect_every != 0 && !tracks.empty()) {
-            early_rois(next_dets, next_ndets, frame_id + 1, false, t->pre_erois, t->pre_erow_of);
-            if (!t->pre_erois.empty()) {
-                e = wait_if_pending(t->early_s, t->la_ready);
-                if (e != hipSuccess) return map_status(e);
-                rc = launch_early_set(t->pre_erois, Pnext, t->eb ^ 1);
-                if (rc != TBDK_OK) return rc;
-                t->pre_early = true;
-                t->pre_frame = next;
-            }
-        }
         // ---- speculative look-ahead PyrLK (see tbdk_tbd::spec_list): runs while the
-        // host tracks; the post-tracker phase adds the unchanged sets it missed.
-        // With tbd_early_la 3 the early GFTT rows below join the same launch (one
-        // pool of waves instead of two launches queued on la_s).
-        const int ela = t->ctx->opt_tbd_early_la;
-        const int ne = (int)t->erois.size();
-        const bool do_ers = next && early_launched && ne > 0 &&
-                            (ela >= 2 || (ela == 1 && frame_id % c.redetect_every == 0));
-        int ns = 0;
+        // host tracks; the post-tracker phase adds the unchanged sets it missed
         if (next && t->ctx->opt_tbd_spec_la && frame_id % c.redetect_every != 0) {
+            int ns = 0;
             k = 0;
             for (const auto& tr : tracks) {
                 auto it = t->slot_of.find(tr.id);
@@ -961,46 +901,40 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                     continue;
                 t->h_spec[ns++] = it->second;
             }
-        }
-        const int nmerge = (do_ers && ela == 3) ? ne : 0;  // early rows appended to the speculative list
-        for (int q = 0; q < nmerge; ++q) t->h_spec[ns + q] = erow0 + q;
-        if (ns + nmerge > 0) {
-            hipStream_t ls = t->la_s;
-            e = wait_if_pending(ls, t->la_ready);
-            if (e == hipSuccess && nmerge > 0) e = wait_if_pending(ls, early_done);
-            if (e == hipSuccess && !t->zc)
-                e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * (ns + nmerge), hipMemcpyHostToDevice, ls);
-            if (e != hipSuccess) return map_status(e);
-            rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
-                             reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             (ns + nmerge) * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec);
-            if (rc != TBDK_OK) return rc;
-            e = hipEventRecord(t->la_done, ls);
-            if (e != hipSuccess) return map_status(e);
-            for (int q = 0; q < ns; ++q) {
-                t->spec_member[(size_t)t->h_spec[q]] = 1;
-                t->spec_list.push_back(t->h_spec[q]);
+            if (ns > 0) {
+                hipStream_t ls = t->la_s;
+                e = wait_if_pending(ls, t->la_ready);
+                if (e == hipSuccess && !t->zc)
+                    e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
+                if (e != hipSuccess) return map_status(e);
+                rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
+                                 reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                                 ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec);
+                if (rc != TBDK_OK) return rc;
+                e = hipEventRecord(t->la_done, ls);
+                if (e != hipSuccess) return map_status(e);
+                for (int q = 0; q < ns; ++q) {
+                    t->spec_member[(size_t)t->h_spec[q]] = 1;
+                    t->spec_list.push_back(t->h_spec[q]);
+                }
+                t->la_lk = true;
             }
-            for (int q = 0; q < nmerge; ++q) {
-                t->ers_row[(size_t)(erow0 + q)] = 1;
-                t->ers_list.push_back(erow0 + q);
-            }
-            t->la_lk = true;
         }
         // ---- look-ahead PyrLK of this step's early GFTT rows (option
         // tbd_early_la; 1: re-detection frames, where the speculative PyrLK above
         // does not run and the device would idle through the host tracker step,
-        // 2: every frame, 3: every frame, in the speculative launch above).  Each
-        // early row is the corner set a track refreshed in this step's ROI will
-        // be tracked from in the next step (new tracks, the re-detection guesses
-        // the tracker confirms), so the next step's PyrLK of the refreshed sets
-        // skips the rows tracked here: the same points, the same pyramids (this
-        // frame's and the look-ahead), the same results.
-        if (do_ers && nmerge == 0) {
+        // 2: every frame).  Each early row is the corner set a track refreshed in
+        // this step's ROI will be tracked from in the next step (new tracks, the
+        // re-detection guesses the tracker confirms), so the next step's PyrLK
+        // of the refreshed sets skips the rows tracked here: the same points, the
+        // same pyramids (this frame's and the look-ahead), the same results.
+        const int ela = t->ctx->opt_tbd_early_la;
+        const int ne = (int)t->erois.size();
+        if (next && early_launched && ne > 0 && (ela >= 2 || (ela == 1 && frame_id % c.redetect_every == 0))) {
             for (int q = 0; q < ne; ++q) t->h_ers[q] = erow0 + q;
             hipStream_t ls = t->la_s;
             e = wait_if_pending(ls, t->la_ready);
-            if (e == hipSuccess) e = wait_if_pending(ls, early_done);
+            if (e == hipSuccess) e = wait_if_pending(ls, t->early_done);
             if (e == hipSuccess && !t->zc)
                 e = hipMemcpyAsync(t->d_ers, t->h_ers, sizeof(int32_t) * ne, hipMemcpyHostToDevice, ls);
             if (e != hipSuccess) return map_status(e);
@@ -1107,7 +1041,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // look-ahead PyrLK): the GFTT heads the next frame's critical path, so it is
     // queued first and the PyrLK fills the device around it.
     if (early_launched) {
-        hipError_t e = wait_if_pending(t->side, early_done);
+        hipError_t e = wait_if_pending(t->side, t->early_done);
         if (e != hipSuccess) return map_status(e);
     }
     if (nroi > 0) {
@@ -1221,11 +1155,9 @@ int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first
     if (nframes > 0 && det_offsets[nframes] > det_offsets[0] && !dets) return TBDK_EINVAL;
     for (int i = 0; i < nframes; ++i) {
         const uint8_t* next = i + 1 < nframes ? frames[i + 1] : nullptr;
-        const bool nd = next && dets;
         int rc = step_impl(t, frames[i], pitch, first_frame_id + i, dets ? dets + det_offsets[i] : nullptr,
                            det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr,
-                           static_cast<hipStream_t>(stream), nd ? dets + det_offsets[i + 1] : nullptr,
-                           nd ? det_offsets[i + 2] - det_offsets[i + 1] : -1);
+                           static_cast<hipStream_t>(stream));
         if (rc != TBDK_OK) return rc;
     }
     return TBDK_OK;
@@ -1278,11 +1210,9 @@ int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int 
         if (e == hipSuccess && i + 2 < nframes) e = upload(i + 2);  // ring[(i + 2) % 3] held frame i - 1
         if (e != hipSuccess) return map_status(e);
         const uint8_t* next = i + 1 < nframes ? t->ring[(i + 1) % 3] : nullptr;
-        const bool nd = next && dets;
         int rc = step_impl(t, t->ring[i % 3], t->ring_pitch, first_frame_id + i,
                            dets ? dets + det_offsets[i] : nullptr, det_offsets[i + 1] - det_offsets[i], next,
-                           t->ring_pitch, metrics ? metrics + i : nullptr, s, nd ? dets + det_offsets[i + 1] : nullptr,
-                           nd ? det_offsets[i + 2] - det_offsets[i + 1] : -1);
+                           t->ring_pitch, metrics ? metrics + i : nullptr, s);
         if (rc != TBDK_OK) return rc;
         e = hipEventRecord(t->freed[i % 3], s);
         if (e != hipSuccess) return map_status(e);

@@ -193,8 +193,7 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
     res = {}
     try:
-        for early, spec, ela, order, prio in ((2, 1, 1, 0, 0), (2, 1, 0, 0, 0), (2, 1, 2, 0, 0), (2, 1, 3, 0, 0),
-                                              (1, 1, 3, 0, 0), (2, 0, 3, 0, 0), (2, 0, 1, 0, 0),
+        for early, spec, ela, order, prio in ((2, 1, 1, 0, 0), (2, 1, 0, 0, 0), (2, 1, 2, 0, 0), (2, 0, 1, 0, 0),
                                               (1, 1, 1, 0, 0), (1, 1, 2, 0, 0), (1, 0, 1, 0, 0), (0, 1, 1, 0, 0),
                                               (0, 0, 0, 0, 0), (2, 1, 1, 1, 0), (2, 1, 1, 2, 0), (1, 0, 2, 2, 0),
                                               (2, 1, 1, 1, 1), (2, 1, 1, 0, 1)):
@@ -286,17 +285,12 @@ def test_tbd_run_host_matches_run(gpu):
     ref = tbd.TbdLoop(c, ctx=gpu)
     want = [_mkey(m) for m in ref.run(frames, 0, dets)]
     host = frames.cpu().pin_memory()
-    try:
-        for ela in (1, 3):  # 3: the next frame's early GFTT launched a step ahead
-            gpu.set_option("tbd_early_la", ela)
-            for src in (host, frames.cpu()):
-                loop = tbd.TbdLoop(c, ctx=gpu)
-                got = [_mkey(m) for m in loop.run_host(src[:9], 0, dets[:9])]
-                got += [_mkey(m) for m in loop.run_host(src[9:], 9, dets[9:])]
-                assert got == want, ela
-                assert loop.tracks() == ref.tracks()
-    finally:
-        gpu.set_option("tbd_early_la", 1)
+    for src in (host, frames.cpu()):
+        loop = tbd.TbdLoop(c, ctx=gpu)
+        got = [_mkey(m) for m in loop.run_host(src[:9], 0, dets[:9])]
+        got += [_mkey(m) for m in loop.run_host(src[9:], 9, dets[9:])]
+        assert got == want
+        assert loop.tracks() == ref.tracks()
 
 
 def test_tbd_lookahead_then_no_tracks(gpu):
@@ -318,7 +312,7 @@ def test_tbd_lookahead_then_no_tracks(gpu):
     c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=5)
     res = {}
     try:
-        for spec, ela in ((1, 1), (1, 2), (1, 3), (0, 0)):
+        for spec, ela in ((1, 1), (1, 2), (0, 0)):
             gpu.set_option("tbd_spec_lookahead", spec)
             gpu.set_option("tbd_early_la", ela)
             loop = tbd.TbdLoop(c, ctx=gpu)
