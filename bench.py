@@ -641,6 +641,73 @@ def lk_f16_secondary(ctx, args, device, cpu: bool):
     return out
 
 
+def dense_lk_secondary(ctx, args, device, cpu: bool):
+    """SURVEY §8 (f-4): dense PyrLK, cv::cuda::DensePyrLKOpticalFlow's interface
+    with its defaults (win 13, maxLevel 3, 30 iterations) on synthetic 1080p
+    pairs, computed as the CPU calcOpticalFlowPyrLK at every pixel
+    (tbdk_lk_dense: per pair the next frame's pyramid with Scharr planes, the
+    case images of the previous one, the PyrLK of all 2.07 M pixels).
+    Pairs/s and pixels/s, the per-point-setup path (ctx option lk_dense_case 0)
+    beside it, and the oracle on a pixel sample.  Reported, never `value`."""
+    import numpy as np
+    import torch
+    from opencv_amd import klt
+
+    w, h, n = args.width, args.height, args.dense_pairs
+    frames, _ = klt.synth_render(args.seed + 17, w, h, args.objects, 0, n + 1, device=device, ctx=ctx)
+    win, ml = (13, 13), 3
+    lk = klt.DensePyrLKOpticalFlow.create(win, ml, 30)
+    pyrs = [klt.Pyramid(ctx, w, h, ml, win) for _ in range(2)]
+    flow = torch.empty((h, w, 2), dtype=torch.float32, device=frames.device)
+
+    def run():
+        pyrs[0].build(frames[0])
+        for i in range(n):
+            pyrs[(i + 1) % 2].build(frames[i + 1])
+            lk.calc(pyrs[i % 2], pyrs[(i + 1) % 2], flow)
+
+    res = {}
+    try:
+        for mode in (1, 0):
+            ctx.set_option("lk_dense_case", mode)
+            run()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            res[mode] = (time.perf_counter() - t0) / n
+    finally:
+        ctx.set_option("lk_dense_case", 1)
+    out = {"value": round(1.0 / res[1], 2), "unit": "pairs/s", "mpix_per_s": round(w * h / res[1] / 1e6, 1),
+           "ms_per_pair": round(1000 * res[1], 3), "dtype": "u8",
+           "per_point_setup": {"value": round(1.0 / res[0], 2), "unit": "pairs/s",
+                               "note": "ctx option lk_dense_case 0: the sparse kernel's per-point window setup over "
+                                       "the pixel grid (round 4's dense path)"},
+           "config": {"workload": f"dense PyrLK {w}x{h} synthetic pairs (cv::cuda::DensePyrLKOpticalFlow defaults)",
+                      "win": 13, "max_level": ml, "iters": 30, "pairs": n,
+                      "per_pair": "next pyramid (levels + Scharr planes) + case images + PyrLK of every pixel"}}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        a_, b_ = frames[0].cpu().numpy(), frames[1].cpu().numpy()
+        threads = min(16, os.cpu_count() or 1)
+        ys, xs = np.mgrid[0:h:16, 0:w:16]
+        sample = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.float32)
+        t1 = time.perf_counter()
+        P0, P1 = O.Pyramid(a_, win, ml), O.Pyramid(b_, win, ml)
+        tp = (time.perf_counter() - t1) / 2
+        t1 = time.perf_counter()
+        O.lk(P0, P1, sample, win=win, max_level=ml, accum=O.ACCUM_SSE2, nthreads=threads, want_err=False)
+        tl = (time.perf_counter() - t1) * (w * h) / len(sample)
+        out["cpu_baseline"] = {"value": round(1.0 / (tp + tl), 4), "unit": "pairs/s", "cores": threads,
+                               "kind": "port",
+                               "sample": f"oracle/klt_oracle.c: one pyramid (1 thread) + calcOpticalFlowPyrLK of "
+                                         f"{len(sample)} grid pixels (every 16th row and column, {threads} threads, "
+                                         "SSE2 order), LK time scaled to all pixels"}
+    del frames, pyrs, flow
+    return out
+
+
 def hog_secondary(ctx, args, device, cpu: bool):
     """The sample's detection step in GPU mode (samples/gpu/tbd.cpp:384-443,
     596-606): cv::cuda::HOG 48x96 people detector, 15 levels, scale 1.05, hit
@@ -1187,12 +1254,15 @@ def main(argv=None):
     ap.add_argument("--f16-pairs", type=int, default=10)
     ap.add_argument("--no-copy-peak", action="store_true", help="skip the measured HBM stream-copy peak")
     ap.add_argument("--no-hog", action="store_true", help="skip the secondary HOG detector measurement")
+    ap.add_argument("--no-dense", action="store_true", help="skip the secondary dense PyrLK measurement")
+    ap.add_argument("--dense-pairs", type=int, default=5)
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
     ap.add_argument("--hog-frames", type=int, default=60)
     args = ap.parse_args(argv)
     if args.no_secondary:
         args.no_step_api = args.no_h2d = args.no_kitti = args.no_farneback = args.no_f16 = args.no_hog = True
+        args.no_dense = True
         args.no_bounds_frame = args.no_pyr4k = True
         args.no_copy_peak = True
         args.repeats = 0
@@ -1410,6 +1480,9 @@ def main(argv=None):
     if rank == 0 and not args.no_f16:
         progress("fp16 PyrLK secondary")
         line["lk_f16"] = lk_f16_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
+    if rank == 0 and not args.no_dense:
+        progress("dense PyrLK secondary")
+        line["dense_lk"] = dense_lk_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_hog:
         progress("HOG secondary")
         line["hog"] = hog_secondary(ctx, args, dev, cpu=world == 1 and not args.no_cpu_baseline)

@@ -218,10 +218,20 @@ static unsigned g_lk_trace_next;  // host: records handed out so far
 
 // FLY: the Scharr derivatives of the window are computed from the u8 level in
 // the level setup instead of read from the pyramid's derivative planes (same
-// values; the planes need not exist)
-template <int WW, int WH, bool FLY>
+// values; the planes need not exist).
+// DENSE (klt_dense.hip, cv::cuda::DensePyrLKOpticalFlow): the points are the
+// pixel grid, and a point's interpolated window (I x32, Ix, Iy) is read from
+// the level's case images instead of interpolated in the setup: the window of
+// pixel (x, y) at level L has the sub-pixel phase (x mod 2^L, y mod 2^L) / 2^L
+// and origin (x >> L, y >> L) - half, so every window element is element
+// (y >> L) - half + r, (x >> L) - half + c of the case image of that phase,
+// the same integers the planes setup computes (the phase's weights applied to
+// the same pyramid and derivative-plane values).  The Newton steps are this
+// kernel's.  Outputs: the flow (next - pixel) and the status plane.
+template <int WW, int WH, bool FLY, bool DENSE = false>
 __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 {
+    static_assert(!DENSE || (!FLY && TBDK_LK_IPACK == 1), "dense mode: the planes instance's packed I pairs");
     constexpr int P = 64 / WW;         // points per wave
     constexpr int NP = (WH + 1) / 2;   // packed row pairs (rows 2q, 2q+1)
     constexpr int IM = FLY ? TBDK_LK_IPACK_FLY : TBDK_LK_IPACK;
@@ -236,7 +246,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     const int k = lane == 0 ? P : (lane - 1) / WW;
     const int x = k < P ? lane - 1 - k * WW : 0;
     const int wave = xcd_swizzle(blockIdx.x, gridDim.x) * kMultiWaves + (threadIdx.x >> 6);
-    const int i = k < P ? seg_point(a, wave * P + k) : -1;
+    const int i = k >= P ? -1 : DENSE ? (wave * P + k < a.n ? wave * P + k : -1) : seg_point(a, wave * P + k);
     const bool valid = i >= 0;
     if (!any_lane(valid)) return;  // wave-uniform
 #ifdef TBDK_LK_TRACE
@@ -256,7 +266,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 
     const float FLT_SCALE = 1.f / (1 << 20);
     const float halfx = (WW - 1) * 0.5f, halfy = (WH - 1) * 0.5f;
-    const float p0x = valid ? a.prev_pts[2 * i] : 0.f, p0y = valid ? a.prev_pts[2 * i + 1] : 0.f;
+    const int gy = DENSE && valid ? i / a.dense_w : 0, gx = DENSE && valid ? i - gy * a.dense_w : 0;  // DENSE: the pixel
+    const float p0x = DENSE ? (float)gx : valid ? a.prev_pts[2 * i] : 0.f;
+    const float p0y = DENSE ? (float)gy : valid ? a.prev_pts[2 * i + 1] : 0.f;
     float outx = 0.f, outy = 0.f;
     if ((a.flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) && valid) {
         outx = a.next_pts[2 * i];
@@ -445,6 +457,28 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                     dxa = dxc;
                     dya = dyc;
                     ra = rc;
+                }
+            } else if constexpr (DENSE) {
+                // the window from case image (gx, gy) mod 2^level: element (r, x) at
+                // level position (ipy + r, ipx + x); per row pair two 8-byte loads
+                // of (I x32 | Ix << 16, Iy) and the same packing as pair_step
+                const int msk = (1 << level) - 1;
+                // (inactive lanes: the case-0 image's top-left corner, in bounds)
+                const int64_t cbase = act ? (int64_t)(((gy & msk) << level) | (gx & msk)) * L.cstride +
+                                                (int64_t)ipy * L.cpitch + ipx + x
+                                          : -(int64_t)(WH / 2) * L.cpitch - WW / 2;
+                const uint2* cw = L.C + cbase;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const int r = 2 * q;
+                    const uint2 e0 = cw[(int64_t)r * L.cpitch];
+                    const uint2 e1 = r + 1 < WH ? cw[(int64_t)(r + 1) * L.cpitch] : make_uint2(0u, 0u);
+                    ipk[q] = __builtin_amdgcn_perm(e1.x, e0.x, 0x05040100u);  // (I x32 of rows r, r+1)
+                    gxk[q] = __builtin_amdgcn_perm(e1.x, e0.x, 0x07060302u);  // (Ix of rows r, r+1)
+                    gyk[q] = __builtin_amdgcn_perm(e1.y, e0.y, 0x05040100u);  // (Iy of rows r, r+1)
+                    acc[0] = sdot2(gxk[q], gxk[q], acc[0]);
+                    acc[1] = sdot2(gxk[q], gyk[q], acc[1]);
+                    acc[2] = sdot2(gyk[q], gyk[q], acc[2]);
                 }
             } else {
                 uint32_t ip[WH + 1], dxp[WH + 1], dyp[WH + 1];
@@ -690,6 +724,12 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         }
     }
 #endif
+    if (DENSE && valid && x == 0) {
+        *reinterpret_cast<float2*>(reinterpret_cast<uint8_t*>(a.flow) + (size_t)gy * a.flow_pitch + 8 * (size_t)gx) =
+            make_float2(outx - (float)gx, outy - (float)gy);
+        if (a.dstatus) a.dstatus[(size_t)gy * a.dstatus_pitch + gx] = (uint8_t)status;
+        return;
+    }
     if (valid && x == 0) {
         a.next_pts[2 * i] = outx;
         a.next_pts[2 * i + 1] = outy;
@@ -735,6 +775,24 @@ hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s)
     case W:                                                                             \
         if (fly) hipLaunchKernelGGL((lk_multi_kernel<W, W, true>), grid, block, 0, s, la);  \
         else hipLaunchKernelGGL((lk_multi_kernel<W, W, false>), grid, block, 0, s, la); \
+        break;
+        TBDK_MULTI_WINDOWS(TBDK_CASE)
+#undef TBDK_CASE
+    default:
+        return hipErrorNotSupported;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_lk_multi_dense(const LkArgs& a, hipStream_t s)
+{
+    if (!lk_multi_supported(a.win_w, a.win_h)) return hipErrorNotSupported;
+    const int per_wg = kMultiWaves * (64 / a.win_w);  // waves of P points
+    const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * kMultiWaves);
+    switch (a.win_w) {
+#define TBDK_CASE(W)                                                                          \
+    case W:                                                                                   \
+        hipLaunchKernelGGL((lk_multi_kernel<W, W, false, true>), grid, block, 0, s, a);       \
         break;
         TBDK_MULTI_WINDOWS(TBDK_CASE)
 #undef TBDK_CASE

@@ -117,6 +117,7 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     fb_release(ctx);
     hog_release(ctx);
     if (ctx->dense_buf) (void)hipFree(ctx->dense_buf);
+    if (ctx->dcase_buf) (void)hipFree(ctx->dcase_buf);
     delete ctx;
     return TBDK_OK;
 }
@@ -214,6 +215,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
     if (std::strcmp(name, "pyr_rows") == 0) {
         if (value != 1 && value != 2 && value != 4) return TBDK_EINVAL;
         ctx->opt_pyr_rows = (int)value;
+        return TBDK_OK;
+    }
+    if (std::strcmp(name, "lk_dense_case") == 0) {
+        ctx->opt_lk_dense_case = value != 0;
         return TBDK_OK;
     }
     if (std::strcmp(name, "lk_scharr_fly") == 0) {
@@ -501,11 +506,12 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
 
 int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts,
                       float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
-                      const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list)
+                      const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list,
+                      const LkDense* dense)
 {
     if (!ctx || !prev || !next || !p || n < 0) return TBDK_EINVAL;
     if (n == 0) return TBDK_OK;
-    if (!prev_pts || !next_pts || !status) return TBDK_EINVAL;
+    if (dense ? !dense->flow : (!prev_pts || !next_pts || !status)) return TBDK_EINVAL;
     if (p->win_w <= 2 || p->win_h <= 2 || p->win_w > 63 || p->win_h > 63 || p->max_level < 0) return TBDK_EINVAL;
     if (prev->nlevels <= 0 || next->nlevels <= 0) return TBDK_EINVAL;
     if (prev->depth != next->depth ||
@@ -552,6 +558,24 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     bool have_d = true;
     for (int l = 0; l <= max_level; ++l)
         if (!a.lv[l].D || a.lv[l].dpad < pad_needed) have_d = false;
+    if (dense) {  // dense mode (klt_dense.hip): the planes instance of the several-points-per-wave kernel
+        if (cn > 1 || f16 || p->impl != 0 || !have_d || !lk_multi_supported(p->win_w, p->win_h) || seg_counts)
+            return TBDK_EINVAL;
+        for (int l = 0; l <= max_level; ++l) {
+            a.lv[l].C = dense->C[l];
+            a.lv[l].cstride = dense->cstride[l];
+            a.lv[l].cpitch = dense->cpitch[l];
+        }
+        a.dense_w = dense->w;
+        a.flow = dense->flow;
+        a.flow_pitch = dense->flow_pitch;
+        a.dstatus = dense->status;
+        a.dstatus_pitch = dense->status_pitch;
+        int rec = timing_begin(ctx, "lk_sparse", s);
+        hipError_t e = launch_lk_multi_dense(a, s);
+        timing_end(ctx, rec, s);
+        return map_err(e);
+    }
     // auto: several points per wave when the window has an instantiation, else the
     // one-point-per-wave strip kernel, else the generic LDS kernel (no derivative planes)
     if (p->impl < 0 || p->impl > 3) return TBDK_EINVAL;

@@ -97,6 +97,9 @@ struct tbdk_ctx {
     tbdk::GfttScratch gftt;  // grown on demand, or up front by tbdk_gftt_reserve
     tbdk::FbScratch* fb = nullptr;  // dense Farneback planes (farneback.hip)
     void* dense_buf = nullptr;      // dense PyrLK grid / next points / status (klt_dense.hip)
+    void* dcase_buf = nullptr;      // dense PyrLK case images (klt_dense.hip)
+    size_t dcase_cap = 0;           // bytes
+    int opt_lk_dense_case = 1;      // tbdk_ctx_set_option("lk_dense_case"): dense PyrLK from case images
     tbdk::HogScratch* hog = nullptr;  // HOG level image, gradients, blocks, hits (hog.hip)
     int64_t dense_cap = 0;          // pixels
 };
@@ -138,6 +141,11 @@ struct LkLevel {
     const uint8_t* J;
     const uint8_t* D;   // derivative plane of I (int16x2 per pixel), may be null
     int w, h, ipitch, jpitch, ipad, jpad, dpitch, dpad;
+    // dense mode (klt_dense.hip): the level's case images, element (y, x) of case
+    // c at C[c * cstride + y * cpitch + x] for y, x from -border on
+    const uint2* C;
+    int64_t cstride;
+    int cpitch;
 };
 
 struct LkArgs {
@@ -157,6 +165,14 @@ struct LkArgs {
     uint8_t* status;
     float* err;
     int32_t* iters;
+    // dense mode: point k of the launch is pixel (k % dense_w, k / dense_w);
+    // outputs the flow (next - pixel, CV_32FC2, flow_pitch bytes) and the status
+    // plane (dstatus_pitch bytes; may be null)
+    int dense_w;
+    float* flow;
+    int flow_pitch;
+    uint8_t* dstatus;
+    int dstatus_pitch;
 #ifdef TBDK_LK_TRACE
     unsigned trace_base;  // probe builds: first trace record of this launch (klt_lk_multi.hip)
 #endif
@@ -172,10 +188,24 @@ __device__ __forceinline__ int seg_point(const LkArgs& a, int k)
     return j < a.seg_counts[s] ? s * a.seg_stride + j : -1;
 }
 
+// dense mode of lk_internal (klt_dense.hip): the case images of every level
+// and the flow / status outputs
+struct LkDense {
+    const uint2* C[TBDK_MAX_LEVELS];
+    int64_t cstride[TBDK_MAX_LEVELS];
+    int cpitch[TBDK_MAX_LEVELS];
+    int w;
+    float* flow;
+    int flow_pitch;
+    uint8_t* status;
+    int status_pitch;
+};
+
 // argument checking + kernel choice shared by tbdk_lk_sparse and the TBD loop
 int lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts, float* next_pts,
                 uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
-                const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list = nullptr);
+                const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list = nullptr,
+                const LkDense* dense = nullptr);
 int map_status(hipError_t e);
 // multi-channel u8 pyramids and PyrLK (klt_cn.hip)
 hipError_t launch_pyr_cn(const uint8_t* img, int pitch, const tbdk_pyr& pyr, hipStream_t s);
@@ -195,6 +225,8 @@ hipError_t launch_lk_strip(const LkArgs& a, hipStream_t s);
 bool lk_multi_supported(int win_w, int win_h);
 // fly: Scharr derivatives computed in the kernel (no derivative planes read)
 hipError_t launch_lk_multi(const LkArgs& a, bool fly, hipStream_t s);
+// dense mode of the several-points-per-wave kernel (klt_dense.hip: case images in a.lv[].C)
+hipError_t launch_lk_multi_dense(const LkArgs& a, hipStream_t s);
 // the fp16 pixel path (klt_f16.hip)
 bool lk_f16_supported(int win_w, int win_h);
 hipError_t launch_lk_f16(const LkArgs& a, bool f32, hipStream_t s);  // fp16 or (f32) fp32 pixel path

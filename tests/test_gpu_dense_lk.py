@@ -70,3 +70,29 @@ def test_dense_ignores_use_initial_flow(gpu):
     out = klt.DensePyrLKOpticalFlow.create(useInitialFlow=True).calc(a, b, flow=seeded)
     torch.cuda.synchronize()
     assert torch.equal(ref, out)
+
+
+@pytest.mark.parametrize("w,h,win,max_level", [(640, 480, 13, 3), (331, 187, 21, 2), (200, 150, 7, 4)])
+def test_dense_case_images_equal_per_point_setup(gpu, w, h, win, max_level):
+    """The dense path's case images (every window read from the per-phase
+    interpolated images, ctx option lk_dense_case = 1, the default) against the
+    per-point setup of the sparse kernels over the pixel grid (lk_dense_case =
+    0): the same flow and status at every pixel, the flow of failed points
+    included."""
+    from opencv_amd import klt
+
+    fr, _ = O.synth(7 + w, w, h, 12, 0, 2)
+    a, b = torch.from_numpy(fr[0]).cuda(), torch.from_numpy(fr[1]).cuda()
+    out = {}
+    try:
+        for mode in (1, 0):
+            gpu.set_option("lk_dense_case", mode)
+            lk = klt.DensePyrLKOpticalFlow.create((win, win), max_level, 30)
+            flow, status = lk.calc(a, b, want_status=True)
+            torch.cuda.synchronize()
+            out[mode] = (flow.cpu().numpy(), status.cpu().numpy())
+    finally:
+        gpu.set_option("lk_dense_case", 1)
+    assert np.array_equal(out[1][1], out[0][1])
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    assert out[1][1].mean() > 0.5
