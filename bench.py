@@ -431,12 +431,17 @@ def cpu_baseline_line(frames_host, gt, args, restore_affinity=None):
         os.sched_setaffinity(0, pinned)
     cal = None
     try:  # the restatement against the real reference on a shape-matched input
-        c = json.load(open(os.path.join(ROOT, "profiles", "r04_cpu_calibration.json")))["results"]
-        cal = {"restatement_over_reference_lk_1t": c["lk_1080p_128x256_1t_ms"]["ratio"],
-               "restatement_over_reference_lk_8t": c["lk_1080p_128x256_8t_ms"]["ratio"],
-               "source": "profiles/r04_cpu_calibration.json (tests/calibrate_cpu.py vs BASELINE.md §2)",
-               "note": "PyrLK per call, 1080p x 32k points: the C restatement is this many times slower than the "
-                       "reference's SSE2 build (shape-matched input; the restatement's input iterates more)"}
+        c = json.load(open(os.path.join(ROOT, "profiles", "r05_cpu_calibration.json")))
+        m = c["inputs"]["matched_iterations"]["results"]
+        r1, r8 = m["lk_1080p_128x256_1t_ms"], m["lk_1080p_128x256_8t_ms"]
+        cal = {"restatement_over_reference_lk_1t": r1["ratio"], "restatement_over_reference_lk_8t": r8["ratio"],
+               "per_iteration_1t": r1["ratio_per_iteration"], "per_iteration_8t": r8["ratio_per_iteration"],
+               "mean_iters_restatement": r1["mean_iters"], "mean_iters_reference": r1["reference_mean_iters"],
+               "source": "profiles/r05_cpu_calibration.json (tests/calibrate_cpu.py vs BASELINE.md §2)",
+               "note": "PyrLK per call, 1080p x 32k points on an input blurred to the reference figure's iteration "
+                       "count (13.4 per point against its 8-12): the C restatement is this many times slower than "
+                       "the reference's SSE2 build per call, and per Newton iteration at the reference's 12 and 8 "
+                       "iterations per point"}
     except (OSError, KeyError, ValueError):
         pass
     return {"value": round(fps, 3), "unit": "frames/s", "cores": cores, "kind": "port", "calibration": cal,
