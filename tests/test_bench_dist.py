@@ -284,3 +284,28 @@ def test_pin_by_runtime_pci_address_fake_sysfs(tmp_path, monkeypatch):
     assert r["pinned"] and r["numa_node"] == 1 and pinned[-1] == list(range(16, 32))
     props.pci_bus_id = 0x99
     assert not bench.pin_rank_by_device(0, str(tmp_path))["pinned"]
+
+
+def test_loop_traffic_fields_from_committed_loop_summary():
+    """the loop's traffic fields come from the newest
+    committed loop-only PMC summary (profiles/rNN_pmc_loop.json: only
+    configs[2]'s launches counted) and reproduce from it: the levels-only
+    1080p build's counter bytes are within 10 % of its algorithmic bytes
+    (round 4's name-keyed means, with the 4K legs mixed in, gave 1.68x), and
+    PyrLK's per-launch bytes stay below two full pyramids (SURVEY §8d's
+    B_lk bound).  The kernel-trace helper finds the loop's and the 4K build's
+    grids in the committed per-grid summary."""
+    import bench
+
+    p = bench.pmc_bytes(["pyr_build_kernel", "pyr_down_padded_kernel"])
+    assert p is not None and p["source"].endswith("_pmc_loop.json")
+    alg = bench.pyr_build_bytes(1920, 1080, 3)
+    ratio = (p["fetch_raw"] + p["write"]) / alg
+    assert 0.85 < ratio < 1.1, ratio
+    lk, src = bench.pmc_traffic("lk_multi_kernel")
+    assert src is not None and src.endswith("_pmc_loop.json")
+    assert 0 < lk < 2 * alg
+    us, used, gsrc = bench.ktrace_grid_us(["pyr_build_kernel", "pyr_down_padded_kernel"], pick="max_grid")
+    assert us is not None and gsrc.endswith("_ktrace_grid.json") and len(used) == 2
+    us1, used1, _ = bench.ktrace_grid_us(["pyr_build_kernel", "pyr_down_padded_kernel"], pick="most")
+    assert us1 is not None and us1 < us  # the loop's 1080p grids take less time than the 4K leg's
