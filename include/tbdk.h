@@ -326,7 +326,14 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
  *   status : device u8 plane (status_pitch bytes) or NULL
  * TBDK_OPTFLOW_USE_INITIAL_FLOW is ignored, as in the reference (dense() never
  * reads the incoming flow); win_w/win_h <= 2 is TBDK_EINVAL (pyrlk.cpp:243).
- * Scratch (17 B per pixel) is owned by the context and grown on demand. */
+ * With 8-bit one-channel pyramids carrying derivative planes (pads >= win + 2)
+ * and an odd square window of 7..31, the previous pyramid's windows come from
+ * per-phase case images (8 B per level position and sub-pixel phase: about one
+ * frame of entries per level, ~71 MB at 1080p, win 13, maxLevel 3); otherwise
+ * per-pixel scratch (17 B per pixel).  Either buffer is owned by the context
+ * and grown on demand (growth frees the old buffer, which waits for the
+ * device), so dense calls on one context must not overlap on different
+ * streams: order them, or give each stream its own context. */
 int tbdk_lk_dense(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, float* flow, int flow_pitch,
                   uint8_t* status, int status_pitch, const tbdk_lk_params* params, void* stream);
 
