@@ -725,6 +725,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // ones after it completes.
     std::vector<tbd::Track>& tracks = t->tracker->getTracks();
     int nents = 0, klt_points = 0, klt_pred = 0, lk_points = 0, nA = 0, nB = 0;
+    bool merged = false;  // the unchanged and refreshed sets in one PyrLK launch
     int64_t lk_iters = 0;
     t->preds.clear();
     const bool run_klt = c.use_klt && t->have_prev && !tracks.empty();
@@ -757,7 +758,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             hipError_t e = hipMemcpyAsync(t->d_pre, t->h_pre, bytes, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) return map_status(e);
         }
-        if (nA > 0) {
+        // the unchanged sets go first, overlapping the previous step's
+        // post-tracker work; when that work is already complete (the first frame
+        // of a run, steps without look-ahead) both kinds of sets wait for nothing
+        // and one launch of nA + nB sets replaces two back-to-back ones
+        merged = nA > 0 && nB > 0 && hipEventQuery(t->post_done) == hipSuccess;
+        if (nA > 0 && !merged) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
                              nA * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists);
@@ -789,9 +795,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     };
     if (run_klt) {
         if (nB > 0) {
+            const int first = merged ? 0 : nA, nsets = merged ? nA + nB : nB;
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             nB * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + nA);
+                             nsets * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + first);
             if (rc != TBDK_OK) return rc;
         }
         if (early_order == 1) {
