@@ -72,7 +72,8 @@ def test_dense_ignores_use_initial_flow(gpu):
     assert torch.equal(ref, out)
 
 
-@pytest.mark.parametrize("w,h,win,max_level", [(640, 480, 13, 3), (331, 187, 21, 2), (200, 150, 7, 4)])
+@pytest.mark.parametrize("w,h,win,max_level", [(640, 480, 13, 3), (331, 187, 21, 2), (200, 150, 7, 4), (160, 120, 31, 5),
+                                                (64, 48, 9, 0), (97, 61, 15, 3)])
 def test_dense_case_images_equal_per_point_setup(gpu, w, h, win, max_level):
     """The dense path's case images (every window read from the per-phase
     interpolated images, ctx option lk_dense_case = 1, the default) against the
