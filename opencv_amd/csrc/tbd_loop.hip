@@ -34,10 +34,10 @@
 #include <functional>
 #include <new>
 #include <queue>
-#include <unordered_map>
 #include <vector>
 
 #include "box_fit.hpp"
+#include "flat_map.hpp"
 #include "tbd_tracker.hpp"
 #include "tbdk_internal.hpp"
 
@@ -249,7 +249,7 @@ struct tbdk_tbd {
     GfttRoi* d_etab = nullptr;
     int eb = 0;  // early-row set of this step
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
-    std::unordered_map<uint64_t, int> erow_of;    // ROI box -> early corner row
+    FlatMap<uint64_t> erow_of;                    // ROI box -> early corner row
     std::vector<int> det_order;                   // scratch: detections by left edge
     GfttScratch gftt;   // the early GFTT's (early_s); the loop's own, not the context's
     GfttScratch gftt2;  // the post-tracker GFTT's (side), so the next step's early GFTT need not wait for it
@@ -273,8 +273,8 @@ struct tbdk_tbd {
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
     std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
-    std::unordered_map<unsigned, int> slot_of;     // track id -> slot
-    std::unordered_map<unsigned, int> npts_of;     // track id -> corners after last fit
+    FlatMap<unsigned> slot_of;                     // track id -> slot
+    FlatMap<unsigned> npts_of;                     // track id -> corners after last fit
     std::vector<tbd::Detection> dets;
     std::vector<tbd::Prediction> preds;
     std::vector<tbdk_roi> rois;
@@ -515,6 +515,10 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         return TBDK_ENOMEM;
     }
     for (int s = 0; s < cfg->max_tracks; ++s) t->free_slots.push(s);
+    // at most max_tracks live entries each (tracks holding a slot; early ROIs)
+    t->slot_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
+    t->npts_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
+    t->erow_of = FlatMap<uint64_t>(4 * (size_t)cfg->max_tracks);
     rc = gftt_reserve(t->gftt, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc == TBDK_OK) rc = gftt_reserve(t->gftt2, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc != TBDK_OK) {
@@ -624,7 +628,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             const int x0 = std::max(d.x, 0), y0 = std::max(d.y, 0);
             const int x1 = std::min(d.x + d.width, c.width), y1 = std::min(d.y + d.height, c.height);
             if (x1 - x0 < 3 || y1 - y0 < 3) continue;
-            if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+            if (!t->erow_of.insert(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size())) continue;
             t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
         }
         // re-detection frames: every existing track's set is refreshed in its box
@@ -643,7 +647,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             std::sort(order.begin(), order.end(), [&](int a, int b) { return dets[a].x < dets[b].x; });
             for (const auto& tr : t->tracker->getTracks()) {
                 if ((int)t->erois.size() >= c.max_tracks) break;
-                if (t->slot_of.find(tr.id) == t->slot_of.end()) continue;
+                if (!t->slot_of.find(tr.id)) continue;
                 const tbd::Rect& lb = tr.bboxes.back();
                 if (lb.x >= c.bounds_xmax || lb.y >= c.bounds_ymax) continue;  // deleted by the bounds filter
                 auto lo = std::lower_bound(order.begin(), order.end(), lb.x - maxw,
@@ -672,7 +676,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 const int x0 = std::max(r.x, 0), y0 = std::max(r.y, 0);
                 const int x1 = std::min(r.x + r.width, c.width), y1 = std::min(r.y + r.height, c.height);
                 if (x1 - x0 < 3 || y1 - y0 < 3) continue;
-                if (!t->erow_of.emplace(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size()).second) continue;
+                if (!t->erow_of.insert(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->erois.size())) continue;
                 t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
         }
@@ -739,9 +743,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     lp.impl = 0;
     if (run_klt) {
         for (const auto& tr : tracks) {
-            auto it = t->slot_of.find(tr.id);
-            if (it == t->slot_of.end()) continue;
-            const int slot = it->second;
+            const int* it = t->slot_of.find(tr.id);
+            if (!it) continue;
+            const int slot = *it;
             const tbd::Rect& b = tr.bboxes.back();
             const int src = t->src_row[(size_t)slot];
             t->h_ents[nents++] = FitEntry{slot, b.x, b.y, b.width, b.height, src};
@@ -882,9 +886,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         int k = 0;
         for (const auto& tr : tracks) {
-            if (t->slot_of.find(tr.id) == t->slot_of.end()) continue;
+            if (!t->slot_of.find(tr.id)) continue;
             const FitOut& o = t->h_fit[k++];
-            t->npts_of[tr.id] = o.n;
+            t->npts_of.set(tr.id, o.n);
             if (o.valid) {
                 t->preds.push_back(tbd::Prediction{tr.id, 1, o.cx, o.cy});
                 klt_pred++;
@@ -896,8 +900,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             int ns = 0;
             k = 0;
             for (const auto& tr : tracks) {
-                auto it = t->slot_of.find(tr.id);
-                if (it == t->slot_of.end()) continue;
+                const int* it = t->slot_of.find(tr.id);
+                if (!it) continue;
                 const FitOut& o = t->h_fit[k++];
                 if (o.n < c.min_points || !o.valid) continue;
                 const tbd::Rect& bb = tr.bboxes.back();  // predictNewLocationsOfTracks + filterTracksOutOfBounds
@@ -906,7 +910,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 if (r.x + r.width < c.bounds_xmin || r.x >= c.bounds_xmax || r.y + r.height < c.bounds_ymin ||
                     r.y >= c.bounds_ymax)
                     continue;
-                t->h_spec[ns++] = it->second;
+                t->h_spec[ns++] = *it;
             }
             if (ns > 0) {
                 hipStream_t ls = t->la_s;
@@ -993,10 +997,9 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
     }
     for (unsigned id : t->tracker->deletedIds) {
-        auto it = t->slot_of.find(id);
-        if (it != t->slot_of.end()) {
-            t->free_slots.push(it->second);
-            t->slot_of.erase(it);
+        if (const int* it = t->slot_of.find(id)) {
+            t->free_slots.push(*it);
+            t->slot_of.erase(id);
         }
         t->npts_of.erase(id);
     }
@@ -1008,32 +1011,32 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const int prow0 = 3 * S;  // the post-tracker GFTT's rows
     if (c.use_klt) {
         for (const auto& tr : t->tracker->getTracks()) {
-            auto it = t->slot_of.find(tr.id);
-            bool is_new = it == t->slot_of.end();
+            const int* it = t->slot_of.find(tr.id);
+            bool is_new = !it;
             int slot;
             if (is_new) {
                 if (t->free_slots.empty()) continue;  // slot pool exhausted: track runs on the motion model
                 slot = t->free_slots.top();
                 t->free_slots.pop();
-                t->slot_of[tr.id] = slot;
+                t->slot_of.set(tr.id, slot);
             } else {
-                slot = it->second;
-                auto np = t->npts_of.find(tr.id);
-                const int n = np == t->npts_of.end() ? 0 : np->second;
+                slot = *it;
+                const int* np = t->npts_of.find(tr.id);
+                const int n = np ? *np : 0;
                 if (frame_id % c.redetect_every != 0 && n >= c.min_points) continue;
             }
             const tbd::Rect& b = tr.bboxes.back();
             int x0 = std::max(b.x, 0), y0 = std::max(b.y, 0);
             int x1 = std::min(b.x + b.width, c.width), y1 = std::min(b.y + b.height, c.height);
             t->refreshed[(size_t)slot] = 1;
-            t->npts_of[tr.id] = c.max_corners;  // refreshed at the next fit
+            t->npts_of.set(tr.id, c.max_corners);  // refreshed at the next fit
             t->src_list.push_back(slot);
             if (x1 - x0 < 3 || y1 - y0 < 3) {  // nothing to detect in: empty point set
                 t->rois.push_back(tbdk_roi{0, 0, 1, 1});
             } else {
-                auto er = t->erow_of.find(box_key(x0, y0, x1 - x0, y1 - y0));
-                if (er != t->erow_of.end()) {  // the early GFTT ran on this ROI of this frame
-                    t->src_row[(size_t)slot] = erow0 + er->second;
+                if (const int* er = t->erow_of.find(box_key(x0, y0, x1 - x0, y1 - y0))) {
+                    // the early GFTT ran on this ROI of this frame
+                    t->src_row[(size_t)slot] = erow0 + *er;
                     nearly++;
                     continue;
                 }
@@ -1079,11 +1082,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (c.use_klt && !t->tracker->getTracks().empty()) {
             int n = 0;  // unchanged sets the speculative PyrLK did not cover
             for (const auto& tr : t->tracker->getTracks()) {
-                auto it = t->slot_of.find(tr.id);
-                if (it == t->slot_of.end() || t->refreshed[(size_t)it->second]) continue;
-                t->la_member[(size_t)it->second] = 1;
-                t->la_list.push_back(it->second);
-                if (!t->spec_member[(size_t)it->second]) t->h_la[n++] = it->second;
+                const int* it = t->slot_of.find(tr.id);
+                if (!it || t->refreshed[(size_t)*it]) continue;
+                t->la_member[(size_t)*it] = 1;
+                t->la_list.push_back(*it);
+                if (!t->spec_member[(size_t)*it]) t->h_la[n++] = *it;
             }
             if (n > 0) {
                 // on la_s, after the fit and the pyramid (la_ready) and behind the
@@ -1264,12 +1267,12 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
         o.pred_h = tr.predPosition.height;
         o.age = (int32_t)tr.age;
         o.total_visible = (int32_t)tr.totalVisibleCount;
-        auto it = t->slot_of.find(tr.id);
-        if (it == t->slot_of.end()) {
+        const int* it = t->slot_of.find(tr.id);
+        if (!it) {
             o.npoints = 0;
         } else {  // a refreshed set is still its GFTT row
-            const int src = t->src_row[(size_t)it->second];
-            o.npoints = std::max(0, counts[(size_t)(src >= 0 ? src : it->second)]);
+            const int src = t->src_row[(size_t)*it];
+            o.npoints = std::max(0, counts[(size_t)(src >= 0 ? src : *it)]);
         }
         o.max_confidence = tr.maxConfidence;
         o.bbox_overlap = tr.bboxOverlap;

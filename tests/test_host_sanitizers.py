@@ -37,3 +37,16 @@ def test_tracker_and_driver_under_asan_ubsan():
     assert p.returncode == 0, out[-4000:]
     assert "AddressSanitizer" not in out and "runtime error" not in out, out[-4000:]
     assert " passed" in out and " failed" not in out
+
+
+def test_flat_map_matches_unordered_map_under_asan_ubsan(tmp_path):
+    """The TBD loop's lookup tables (opencv_amd/csrc/flat_map.hpp: track id ->
+    slot, track id -> corner count, early box -> row) against std::unordered_map
+    over random insert / set / erase / find / clear sequences, host-built with
+    AddressSanitizer + UndefinedBehaviorSanitizer."""
+    exe = str(tmp_path / "flat_map_check")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=undefined", "-I", os.path.join(ROOT, "opencv_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "cpp", "flat_map_check.cpp"), "-o", exe])
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "flat_map ok" in p.stdout, p.stdout + p.stderr
