@@ -553,6 +553,31 @@ int tbdk_tbd_tracking_write(tbdk_tbd* t, const uint32_t* history_ages, int nages
 
 namespace {
 
+// Host-phase profile of step_impl (probe builds, -DTBDK_STEP_PROFILE): the
+// time between successive marks, summed over steps, read by
+// tbdk_probe_step_profile (tools/probe_step_host.py)
+#ifdef TBDK_STEP_PROFILE
+constexpr int kStepMarks = 12;
+double g_step_prof[kStepMarks];
+long g_step_prof_n = 0;
+#define STEP_MARK(i) (sp_t[(i)] = std::chrono::steady_clock::now(), sp_set[(i)] = true)
+// sub-segments of the speculative PyrLK block: SUB_MARK(k) adds the time since
+// the previous SUB_MARK (or SUB_START) to g_sub_prof[k]
+double g_sub_prof[8];
+long g_sub_n = 0;
+#define SUB_START() (sub_t0 = std::chrono::steady_clock::now())
+#define SUB_MARK(k)                                                                                          \
+    do {                                                                                                     \
+        const auto sub_t1 = std::chrono::steady_clock::now();                                                \
+        g_sub_prof[(k)] += std::chrono::duration<double, std::micro>(sub_t1 - sub_t0).count();             \
+        sub_t0 = sub_t1;                                                                                     \
+    } while (0)
+#else
+#define STEP_MARK(i) ((void)0)
+#define SUB_START() ((void)0)
+#define SUB_MARK(k) ((void)0)
+#endif
+
 // One frame.  With next != nullptr the step also enqueues look-ahead work for
 // the next frame: its pyramid behind this frame's fit (the device has it to run
 // while the host tracker runs), and its PyrLK of the unchanged point sets
@@ -565,6 +590,13 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         return TBDK_EINVAL;
     using clk = std::chrono::steady_clock;
     const auto t_step0 = clk::now();
+#ifdef TBDK_STEP_PROFILE
+    clk::time_point sp_t[kStepMarks];
+    bool sp_set[kStepMarks] = {};
+    sp_t[0] = t_step0;
+    sp_set[0] = true;
+    clk::time_point sub_t0 = t_step0;
+#endif
     double launch_us = 0.0;
     const tbdk_tbd_config& c = t->cfg;
     tbdk_pyr& P = t->pyr[t->cur];
@@ -713,6 +745,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         rc = launch_early_gftt();
         if (rc != TBDK_OK) return rc;
     }
+    STEP_MARK(1);
 
     // No host wait here: the pinned staging buffers written before this step's
     // fit sync (h_ents, h_lists) were last read by uploads issued before the
@@ -782,6 +815,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     t->src_list.clear();
 
 
+    STEP_MARK(2);
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
     {  // the previous step's early and post-tracker GFTT (their rows) before the refreshed sets
         hipError_t e = wait_if_pending(s, t->post_done);
@@ -805,6 +839,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                              nsets * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + first);
             if (rc != TBDK_OK) return rc;
         }
+        STEP_MARK(3);
         if (early_order == 1) {
             rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
@@ -834,6 +869,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (rc != TBDK_OK) return rc;
         }
         auto ts0 = clk::now();
+        STEP_MARK(4);
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
         // the one host wait of the frame, on the critical path: poll instead of
         // a blocking synchronize (its wake-up latency is part of every frame).
@@ -877,6 +913,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         wait_us += std::chrono::duration<double, std::micro>(clk::now() - ts0).count();
         if (e != hipSuccess) return map_status(e);
         synced = true;
+        STEP_MARK(5);
         for (int k = 0; k < nents; ++k) {
             const FitOut& o = t->h_fit[k];
             // map back: entries were filled in track order, skipping slotless tracks
@@ -894,9 +931,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 klt_pred++;
             }
         }
+        STEP_MARK(6);
         // ---- speculative look-ahead PyrLK (see tbdk_tbd::spec_list): runs while the
         // host tracks; the post-tracker phase adds the unchanged sets it missed
         if (next && t->ctx->opt_tbd_spec_la && frame_id % c.redetect_every != 0) {
+            SUB_START();
             int ns = 0;
             k = 0;
             for (const auto& tr : tracks) {
@@ -912,23 +951,31 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                     continue;
                 t->h_spec[ns++] = *it;
             }
+            SUB_MARK(0);
             if (ns > 0) {
                 hipStream_t ls = t->la_s;
                 e = wait_if_pending(ls, t->la_ready);
                 if (e == hipSuccess && !t->zc)
                     e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
                 if (e != hipSuccess) return map_status(e);
+                SUB_MARK(1);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
                                  ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec);
                 if (rc != TBDK_OK) return rc;
+                SUB_MARK(2);
                 e = hipEventRecord(t->la_done, ls);
                 if (e != hipSuccess) return map_status(e);
+                SUB_MARK(3);
                 for (int q = 0; q < ns; ++q) {
                     t->spec_member[(size_t)t->h_spec[q]] = 1;
                     t->spec_list.push_back(t->h_spec[q]);
                 }
                 t->la_lk = true;
+                SUB_MARK(4);
+#ifdef TBDK_STEP_PROFILE
+                g_sub_n++;
+#endif
             }
         }
         // ---- look-ahead PyrLK of this step's early GFTT rows (option
@@ -978,6 +1025,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
     }
 
+    STEP_MARK(7);
     // ---- host tracker step (cv::tbd::Tracker::performTrackingStep)
     t->dets.resize((size_t)ndets);
     for (int i = 0; i < ndets; ++i) {
@@ -992,6 +1040,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     t->tracker->performTrackingStep(t->dets, frame_id, t->preds.data(), (int)t->preds.size(),
                                     t->traj ? &t->traj->map : nullptr);
     const double tracker_us = std::chrono::duration<double, std::micro>(clk::now() - tt0).count();
+    STEP_MARK(8);
     if (!synced) {  // no fit this step: order the previous step's uploads before reusing h_tab
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) return map_status(e);
@@ -1045,6 +1094,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             t->src_row[(size_t)slot] = prow0 + nroi++;
         }
     }
+    STEP_MARK(9);
     // ---- the post-tracker GFTT (side stream, behind the early GFTT whose rows
     // the next step reads and whose scratch it reuses).  With a next frame, the
     // PyrLK of the point sets this leaves unchanged is enqueued after it (the
@@ -1075,6 +1125,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         hipError_t e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
     }
+    STEP_MARK(10);
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
     // set was not refreshed just now (exactly the next step's unchanged sets)
     if (next) {
@@ -1114,6 +1165,21 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     t->eb ^= 1;
     t->have_prev = true;
 
+    STEP_MARK(11);
+#ifdef TBDK_STEP_PROFILE
+    {  // segments between consecutive marks that were both reached
+        int prev = 0;
+        bool all = true;
+        for (int i = 1; i < kStepMarks; ++i) all = all && sp_set[i];
+        if (all) {
+            for (int i = 1; i < kStepMarks; ++i) {
+                g_step_prof[i] += std::chrono::duration<double, std::micro>(sp_t[i] - sp_t[prev]).count();
+                prev = i;
+            }
+            g_step_prof_n++;
+        }
+    }
+#endif
     if (metrics) {
         const tbd::Tracker& tk = *t->tracker;
         metrics->tp = tk.truePositives.back();
@@ -1140,6 +1206,28 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
 }  // namespace
 
 extern "C" {
+
+#ifdef TBDK_STEP_PROFILE
+// average us per profiled step of each segment [mark i-1, mark i) into out[1..];
+// out[0] = the number of steps; the sums are reset
+int tbdk_probe_step_profile(double* out, int cap)
+{
+    if (!out || cap < kStepMarks) return TBDK_EINVAL;
+    out[0] = (double)g_step_prof_n;
+    for (int i = 1; i < kStepMarks; ++i) {
+        out[i] = g_step_prof_n ? g_step_prof[i] / g_step_prof_n : 0.0;
+        g_step_prof[i] = 0.0;
+    }
+    g_step_prof_n = 0;
+    if (cap >= kStepMarks + 6) {  // the speculative block's sub-segments, per block run
+        out[kStepMarks] = (double)g_sub_n;
+        for (int k = 0; k < 5; ++k) out[kStepMarks + 1 + k] = g_sub_n ? g_sub_prof[k] / g_sub_n : 0.0;
+    }
+    for (double& v : g_sub_prof) v = 0.0;
+    g_sub_n = 0;
+    return TBDK_OK;
+}
+#endif
 
 int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
                   int ndets, tbdk_frame_metrics* metrics, void* stream)
