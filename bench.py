@@ -1387,7 +1387,10 @@ def main(argv=None):
         flops_per_launch, achieved = 0.0, 0.0
     lk_every = kstats_aside.get("lk_sparse", {}).get("avg_us")
     # the auto choice is lk_multi_kernel (several points per wave) for the odd square windows it covers
-    traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true>")  # the loop's FLY instance
+    # the loop's FLY instance (lk_multi_kernel<W, W, true, false>: FLY, not the dense mode)
+    traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true, false>")
+    if traffic is None:  # summaries written before the dense mode's template argument existed
+        traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true>")
     if traffic is None:
         traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",

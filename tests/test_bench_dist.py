@@ -302,7 +302,7 @@ def test_loop_traffic_fields_from_committed_loop_summary():
     alg = bench.pyr_build_bytes(1920, 1080, 3)
     ratio = (p["fetch_raw"] + p["write"]) / alg
     assert 0.85 < ratio < 1.1, ratio
-    lk, src = bench.pmc_traffic("lk_multi_kernel")
+    lk, src = bench.pmc_traffic("lk_multi_kernel<21, 21, true, false>")  # the name bench.main looks up
     assert src is not None and src.endswith("_pmc_loop.json")
     assert 0 < lk < 2 * alg
     us, used, gsrc = bench.ktrace_grid_us(["pyr_build_kernel", "pyr_down_padded_kernel"], pick="max_grid")
