@@ -99,6 +99,15 @@ int tbdk_ctx_create(int device, tbdk_ctx** out)
         // that with 4 hardware queues neither shares one with the caller's stream
         fb_create_streams(c);
         hog_create_lanes(c);
+        // then the TBD loop's streams (tbdk_tbd_create): the post-tracker
+        // stream at the highest priority, the look-ahead and early-GFTT streams
+        // at the lowest (on gfx950 the range is normal..high)
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+            if (hipStreamCreateWithPriority(&c->tbd_side, hipStreamNonBlocking, hi) != hipSuccess) c->tbd_side = nullptr;
+            if (hipStreamCreateWithPriority(&c->tbd_la, hipStreamNonBlocking, lo) != hipSuccess) c->tbd_la = nullptr;
+            if (hipStreamCreateWithPriority(&c->tbd_early, hipStreamNonBlocking, lo) != hipSuccess) c->tbd_early = nullptr;
+        }
     }
     *out = c;
     return TBDK_OK;
@@ -118,6 +127,8 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx)
     hog_release(ctx);
     if (ctx->dense_buf) (void)hipFree(ctx->dense_buf);
     if (ctx->dcase_buf) (void)hipFree(ctx->dcase_buf);
+    for (hipStream_t st : {ctx->tbd_side, ctx->tbd_la, ctx->tbd_early})
+        if (st) (void)hipStreamDestroy(st);
     delete ctx;
     return TBDK_OK;
 }

@@ -269,6 +269,7 @@ struct tbdk_tbd {
     unsigned* d_fitcnt = nullptr;
     int fit_tag = 0;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
+    bool own_side = false, own_la = false, own_early = false;  // created here, not the context's
     hipEvent_t early_done = nullptr;
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
@@ -319,14 +320,14 @@ int release(tbdk_tbd* t)
     if (t->la_s) (void)hipStreamSynchronize(t->la_s);
     if (t->la_done) (void)hipEventDestroy(t->la_done);
     if (t->la_ready) (void)hipEventDestroy(t->la_ready);
-    if (t->la_s) (void)hipStreamDestroy(t->la_s);
+    if (t->la_s && t->own_la) (void)hipStreamDestroy(t->la_s);
     if (t->eig_done) (void)hipEventDestroy(t->eig_done);
-    if (t->side) (void)hipStreamDestroy(t->side);
+    if (t->side && t->own_side) (void)hipStreamDestroy(t->side);
     for (int i = 0; i < 2; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
     if (t->pyr_ready) (void)hipEventDestroy(t->pyr_ready);
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
-    if (t->early_s) (void)hipStreamDestroy(t->early_s);
+    if (t->early_s && t->own_early) (void)hipStreamDestroy(t->early_s);
     if (t->early_done) (void)hipEventDestroy(t->early_done);
     gftt_scratch_free(t->gftt);
     gftt_scratch_free(t->gftt2);
@@ -478,7 +479,10 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     // look-ahead PyrLK it shares the device with
     int prio_least = 0, prio_greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_greatest);
+    // the context's streams when it has them (see tbdk_ctx::tbd_side), else our own
+    if (e == hipSuccess && ctx->tbd_side) t->side = ctx->tbd_side;
+    else if (e == hipSuccess && (e = hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_greatest)) == hipSuccess)
+        t->own_side = true;
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->post_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
@@ -486,13 +490,19 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     // the look-ahead PyrLK at the lowest priority (on gfx950 the range is
     // normal..high, so this is the default; a high-priority caller stream for
     // the critical PyrLK measured no difference either)
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->la_s, hipStreamNonBlocking, prio_least);
+    if (e == hipSuccess && ctx->tbd_la) t->la_s = ctx->tbd_la;
+    else if (e == hipSuccess && (e = hipStreamCreateWithPriority(&t->la_s, hipStreamNonBlocking, prio_least)) == hipSuccess)
+        t->own_la = true;
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->eig_done, hipEventDisableTiming);
     // the early GFTT at the lowest priority (ctx option tbd_early_prio, read here:
     // 1 = the highest, for launch orders that put it behind the critical PyrLK)
-    if (e == hipSuccess)
+    if (e == hipSuccess && ctx->tbd_early && !ctx->opt_tbd_early_prio) {
+        t->early_s = ctx->tbd_early;
+    } else if (e == hipSuccess) {
         e = hipStreamCreateWithPriority(&t->early_s, hipStreamNonBlocking,
                                         ctx->opt_tbd_early_prio ? prio_greatest : prio_least);
+        if (e == hipSuccess) t->own_early = true;
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);

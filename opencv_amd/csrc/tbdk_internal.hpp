@@ -102,6 +102,13 @@ struct tbdk_ctx {
     int opt_lk_dense_case = 1;      // tbdk_ctx_set_option("lk_dense_case"): dense PyrLK from case images
     tbdk::HogScratch* hog = nullptr;  // HOG level image, gradients, blocks, hits (hog.hip)
     int64_t dense_cap = 0;          // pixels
+    // the TBD loop's side streams (post-tracker work, look-ahead PyrLK, early
+    // GFTT), created once with the context so that every loop of the context
+    // gets the same stream -> hardware-queue mapping (HIP deals streams to the
+    // few hardware queues in creation order; a loop created after other
+    // streams otherwise lands on a different, often slower, mapping).  Loops
+    // on one context share them (stream order only adds dependencies).
+    hipStream_t tbd_side = nullptr, tbd_la = nullptr, tbd_early = nullptr;
 };
 
 namespace tbdk {
