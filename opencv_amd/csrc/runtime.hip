@@ -31,12 +31,20 @@ static uint64_t sample_hash(uint64_t x)
     return x ^ (x >> 31);
 }
 
+// is `name` in the ",a,b," selection (no allocation: the launch sites call
+// this once per launch while timing is on)
+static bool timing_selected(const std::string& only, const char* name)
+{
+    const size_t n = std::strlen(name);
+    for (size_t p = only.find(name); p != std::string::npos; p = only.find(name, p + 1))
+        if (p > 0 && only[p - 1] == ',' && p + n < only.size() && only[p + n] == ',') return true;
+    return false;
+}
+
 int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
 {
     if (!ctx->timing) return -1;
-    if (!ctx->timing_only.empty() &&
-        ctx->timing_only.find("," + std::string(name) + ",") == std::string::npos)
-        return -1;
+    if (!ctx->timing_only.empty() && !timing_selected(ctx->timing_only, name)) return -1;
     int64_t* calls = nullptr;
     for (auto& c : ctx->timing_calls)
         if (c.first == name) calls = &c.second;
