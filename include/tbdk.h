@@ -173,11 +173,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       system-scope flag in pinned memory that the host polls, instead of an
  *       event recorded behind the fit (whose marker held the next frame's
  *       pyramid back; results equal).
- *   "tbd_early_order" (0/1/2, default 0): where a step launches its early
- *       GFTT: 0 first, 1 after the critical refreshed-set PyrLK, 2 after the
- *       fit and the next frame's pyramid, before the host waits for the fit
- *       (its host-side setup then overlaps the GPU's critical chain; measured
- *       no faster over whole sequences; results equal).
+ *   "tbd_early_order" (0/1/2, default 1): where a step launches its early
+ *       GFTT: 0 first, 1 after the critical refreshed-set PyrLK (its host
+ *       setup no longer delays that launch, and the PyrLK waves are dispatched
+ *       ahead of the GFTT's), 2 after the fit and the next frame's pyramid,
+ *       before the host waits for the fit (results equal).
  *   "tbd_early_prio" (0/1, default 0; taken by tbdk_tbd_create): the early
  *       GFTT's stream at the lowest (0) or highest (1) priority (results equal).
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's

@@ -85,7 +85,7 @@ struct tbdk_ctx {
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")
     int opt_tbd_zero_copy = 1;   // tbdk_ctx_set_option("tbd_zero_copy"), read by tbdk_tbd_create
     int opt_tbd_fit_flag = 1;    // tbdk_ctx_set_option("tbd_fit_flag"), read by tbdk_tbd_create
-    int opt_tbd_early_order = 0;  // tbdk_ctx_set_option("tbd_early_order"): where the early GFTT is launched in a step
+    int opt_tbd_early_order = 1;  // tbdk_ctx_set_option("tbd_early_order"): where the early GFTT is launched in a step (round 5: 1)
     int opt_tbd_early_prio = 0;  // tbdk_ctx_set_option("tbd_early_prio"), read by tbdk_tbd_create
     int opt_tbd_early_la = 1;    // tbdk_ctx_set_option("tbd_early_la"): look-ahead PyrLK of early GFTT rows
     int opt_tbd_pyr_derivs = 0;  // tbdk_ctx_set_option("tbd_pyr_derivs"): loop pyramids with Scharr planes (A/B)

@@ -217,7 +217,7 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
         gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
         gpu.set_option("tbd_early_la", 1)
-        gpu.set_option("tbd_early_order", 0)
+        gpu.set_option("tbd_early_order", 1)  # the default
         gpu.set_option("tbd_early_prio", 0)
     base = res[0, 0, 0, 0, 0]
     for key, r in res.items():
