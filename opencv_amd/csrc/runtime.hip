@@ -107,15 +107,6 @@ int tbdk_ctx_create(int device, tbdk_ctx** out)
         // that with 4 hardware queues neither shares one with the caller's stream
         fb_create_streams(c);
         hog_create_lanes(c);
-        // then the TBD loop's streams (tbdk_tbd_create): the post-tracker
-        // stream at the highest priority, the look-ahead and early-GFTT streams
-        // at the lowest (on gfx950 the range is normal..high)
-        int lo = 0, hi = 0;
-        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
-            if (hipStreamCreateWithPriority(&c->tbd_side, hipStreamNonBlocking, hi) != hipSuccess) c->tbd_side = nullptr;
-            if (hipStreamCreateWithPriority(&c->tbd_la, hipStreamNonBlocking, lo) != hipSuccess) c->tbd_la = nullptr;
-            if (hipStreamCreateWithPriority(&c->tbd_early, hipStreamNonBlocking, lo) != hipSuccess) c->tbd_early = nullptr;
-        }
     }
     *out = c;
     return TBDK_OK;

@@ -479,6 +479,15 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     // look-ahead PyrLK it shares the device with
     int prio_least = 0, prio_greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    if (e == hipSuccess) {  // the context's loop streams, made by its first loop (see tbdk_ctx::tbd_side)
+        std::lock_guard<std::mutex> lk(ctx->tbd_mu);
+        if (!ctx->tbd_side && hipStreamCreateWithPriority(&ctx->tbd_side, hipStreamNonBlocking, prio_greatest) != hipSuccess)
+            ctx->tbd_side = nullptr;
+        if (!ctx->tbd_la && hipStreamCreateWithPriority(&ctx->tbd_la, hipStreamNonBlocking, prio_least) != hipSuccess)
+            ctx->tbd_la = nullptr;
+        if (!ctx->tbd_early && hipStreamCreateWithPriority(&ctx->tbd_early, hipStreamNonBlocking, prio_least) != hipSuccess)
+            ctx->tbd_early = nullptr;
+    }
     // the context's streams when it has them (see tbdk_ctx::tbd_side), else our own
     if (e == hipSuccess && ctx->tbd_side) t->side = ctx->tbd_side;
     else if (e == hipSuccess && (e = hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_greatest)) == hipSuccess)

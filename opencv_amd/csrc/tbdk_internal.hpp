@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -103,11 +104,15 @@ struct tbdk_ctx {
     tbdk::HogScratch* hog = nullptr;  // HOG level image, gradients, blocks, hits (hog.hip)
     int64_t dense_cap = 0;          // pixels
     // the TBD loop's side streams (post-tracker work, look-ahead PyrLK, early
-    // GFTT), created once with the context so that every loop of the context
-    // gets the same stream -> hardware-queue mapping (HIP deals streams to the
-    // few hardware queues in creation order; a loop created after other
-    // streams otherwise lands on a different, often slower, mapping).  Loops
-    // on one context share them (stream order only adds dependencies).
+    // GFTT), created by the context's first loop and kept for every later one,
+    // so that each loop gets the first loop's stream -> hardware-queue mapping
+    // (HIP deals streams to the few hardware queues as they are created; a
+    // loop created after other streams otherwise lands on a different, often
+    // slower, mapping).  Not at context creation: streams created then shift
+    // the queue the caller's stream gets at its first use (HOG's lanes then
+    // shared it: 1.36k -> 0.92k frames/s).  Loops on one context share them
+    // (stream order only adds dependencies).
+    std::mutex tbd_mu;
     hipStream_t tbd_side = nullptr, tbd_la = nullptr, tbd_early = nullptr;
 };
 
