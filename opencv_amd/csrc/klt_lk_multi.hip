@@ -717,7 +717,9 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 o[1] = tr_t1;
                 o[2] = hw | ((unsigned long long)xcc << 32);
                 o[3] = ((unsigned long long)(unsigned)a.n << 32) | (unsigned)wave;
-                o[4] = (unsigned long long)(uintptr_t)(a.seg_list ? (const void*)a.seg_list : (const void*)a.prev_pts);
+                o[4] = a.seg_ninl > 0 ? (1ull << 48) | ((unsigned long long)a.seg_ninl << 16) | a.seg_inl[0]
+                                      : (unsigned long long)(uintptr_t)(a.seg_list ? (const void*)a.seg_list
+                                                                                   : (const void*)a.prev_pts);
                 o[5] = (unsigned)tr_steps | ((unsigned long long)(unsigned)tr_reloads << 16) |
                        ((unsigned long long)(unsigned)mx << 32);
             }

@@ -213,6 +213,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_pyr_derivs = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_fit_inline") == 0) {
+        ctx->opt_tbd_fit_inline = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "pyr_fuse") == 0) {
         if (value < 0 || value > 2) return TBDK_EINVAL;
         ctx->opt_pyr_fuse = (int)value;
@@ -233,6 +237,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
     }
     if (std::strcmp(name, "lk_scharr_fly") == 0) {
         ctx->opt_lk_scharr_fly = value != 0;
+        return TBDK_OK;
+    }
+    if (std::strcmp(name, "lk_seg_inline") == 0) {
+        ctx->opt_lk_seg_inline = value != 0;
         return TBDK_OK;
     }
     if (std::strcmp(name, "lk_impl") == 0) {  // kernel used when tbdk_lk_params.impl is 0 (auto)
@@ -517,7 +525,7 @@ int tbdk_lk_sparse(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, co
 int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts,
                       float* next_pts, uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
                       const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list,
-                      const LkDense* dense)
+                      const LkDense* dense, const int32_t* seg_list_host)
 {
     if (!ctx || !prev || !next || !p || n < 0) return TBDK_EINVAL;
     if (n == 0) return TBDK_OK;
@@ -563,6 +571,16 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
     a.seg_list = seg_list;
     a.seg_stride = seg_stride > 0 ? seg_stride : 1;
     if ((seg_counts && seg_stride <= 0) || (seg_list && !seg_counts)) return TBDK_EINVAL;
+    if (seg_list && seg_list_host && ctx->opt_lk_seg_inline) {  // the list into the kernel arguments
+        const int nseg = (int)(((int64_t)n + a.seg_stride - 1) / a.seg_stride);
+        bool fits = nseg <= kSegInline;
+        for (int k = 0; fits && k < nseg; ++k) fits = (uint32_t)seg_list_host[k] <= 0xFFFFu;
+        if (fits) {
+            for (int k = 0; k < nseg; ++k) a.seg_inl[k] = (uint16_t)seg_list_host[k];
+            a.seg_ninl = nseg;
+            a.seg_list = nullptr;
+        }
+    }
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     bool have_d = true;

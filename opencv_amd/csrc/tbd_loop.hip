@@ -51,6 +51,20 @@ struct FitEntry {
     int src;         // >= 0: a refreshed set, its corners (and PyrLK results) in GFTT row src
 };
 
+// the fit table carried in the kernel arguments (ctx option tbd_fit_inline): the
+// zero-copy table lives in pinned host memory, where each fit wave's first load
+// is a round trip over the host link on the frame's critical chain
+struct FitEntryC {
+    uint16_t slot;
+    int16_t src;
+    int16_t x, y;
+    uint16_t w, h;
+};
+constexpr int kFitInline = 256;
+struct FitInline {
+    FitEntryC e[kFitInline];
+};
+
 struct FitOut {
     double cx, cy;  // KLT-propagated centroid
     double scale;
@@ -74,7 +88,8 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
                                                                  const int32_t* __restrict__ slot_iters,
                                                                  int32_t* __restrict__ slot_counts,
                                                                  FitOut* __restrict__ out, int min_fit,
-                                                                 unsigned* __restrict__ fit_cnt, int32_t* flag, int tag)
+                                                                 unsigned* __restrict__ fit_cnt, int32_t* flag, int tag,
+                                                                 int inl, const FitInline fi)
 {
     __shared__ float2 s_a[kFitWaves][kSlotPts], s_b[kFitWaves][kSlotPts];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -82,7 +97,13 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
     if (e < nents) {
         float2* sa = s_a[wv];
         float2* sb = s_b[wv];
-        const FitEntry E = ents[e];
+        FitEntry E;
+        if (inl) {
+            const FitEntryC c = fi.e[e];
+            E = FitEntry{c.slot, c.x, c.y, c.w, c.h, c.src};
+        } else {
+            E = ents[e];
+        }
         const int row = E.src >= 0 ? E.src : E.slot;  // where the tracked set and its PyrLK results are
         const int c0 = slot_counts[row];
         const int cnt = c0 < 0 ? 0 : c0;  // -1: GFTT candidate overflow, no corners
@@ -180,6 +201,7 @@ struct tbdk_tbd {
     int32_t* slot_iters = nullptr;
     int32_t* slot_counts = nullptr;
     FitEntry* d_ents = nullptr;
+    FitInline fit_inl;  // this step's fit table as kernel arguments
     FitOut* d_fit = nullptr;
     GfttRoi* d_tab = nullptr;  // device mirror of h_tab
     // post-tracker work (the GFTT of refreshed sets the early GFTT missed) runs on `side`, so the next
@@ -822,7 +844,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (nA > 0 && !merged) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             nA * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists);
+                             nA * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists, nullptr, t->h_lists);
             if (rc != TBDK_OK) return rc;
         }
     }
@@ -855,7 +877,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             const int first = merged ? 0 : nA, nsets = merged ? nA + nB : nB;
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             nsets * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + first);
+                             nsets * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + first, nullptr,
+                             t->h_lists + first);
             if (rc != TBDK_OK) return rc;
         }
         STEP_MARK(3);
@@ -870,11 +893,23 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         const bool by_flag = t->fit_flag && nents > 0;
         const int tag = by_flag ? ++t->fit_tag : 0;
+        int inl = t->ctx->opt_tbd_fit_inline && nents <= kFitInline ? 1 : 0;
+        for (int q = 0; q < nents && inl; ++q) {  // the table into the kernel arguments, if it fits
+            const FitEntry& f = t->h_ents[q];
+            const bool fits = f.slot >= 0 && f.slot <= 0xFFFF && f.src >= -0x8000 && f.src <= 0x7FFF &&
+                              f.x >= -0x8000 && f.x <= 0x7FFF && f.y >= -0x8000 && f.y <= 0x7FFF && f.w >= 0 &&
+                              f.w <= 0xFFFF && f.h >= 0 && f.h <= 0xFFFF;
+            if (fits)
+                t->fit_inl.e[q] = FitEntryC{(uint16_t)f.slot, (int16_t)f.src, (int16_t)f.x, (int16_t)f.y,
+                                            (uint16_t)f.w, (uint16_t)f.h};
+            else
+                inl = 0;
+        }
         int rec = timing_begin(t->ctx, "tbd_fit", s);
         hipLaunchKernelGGL(tbd_fit_kernel, dim3((nents + kFitWaves - 1) / kFitWaves), dim3(64 * kFitWaves), 0, s,
                            t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points,
-                           by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag);
+                           by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag, inl, t->fit_inl);
         timing_end(t->ctx, rec, s);
         if (!t->zc) e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && !by_flag) e = hipEventRecord(t->fit_done, s);
@@ -980,7 +1015,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 SUB_MARK(1);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                 ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec);
+                                 ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec, nullptr, t->h_spec);
                 if (rc != TBDK_OK) return rc;
                 SUB_MARK(2);
                 e = hipEventRecord(t->la_done, ls);
@@ -1017,7 +1052,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (e != hipSuccess) return map_status(e);
             rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                             ne * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_ers);
+                             ne * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_ers, nullptr, t->h_ers);
             if (rc != TBDK_OK) return rc;
             e = hipEventRecord(t->la_done, ls);
             if (e != hipSuccess) return map_status(e);
@@ -1170,7 +1205,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 if (e != hipSuccess) return map_status(e);
                 rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la);
+                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la, nullptr, t->h_la);
                 if (rc != TBDK_OK) return rc;
                 e = hipEventRecord(t->la_done, ls);
                 if (e != hipSuccess) return map_status(e);

@@ -78,6 +78,7 @@ struct tbdk_ctx {
     int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): 1 the two-role launch + one per level, 2 levels 0-2 in one tiled launch (slower, A/B), 0 one launch per level
     int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
+    int opt_lk_seg_inline = 1;  // tbdk_ctx_set_option("lk_seg_inline"): segment lists in the kernel arguments
     int opt_fb_prep_ahead = 1;  // tbdk_ctx_set_option("fb_prep_ahead"): Farneback level prep on a side stream
     int opt_hog_level_streams = 3;  // tbdk_ctx_set_option("hog_level_streams"): lanes of detectMultiScale
     int opt_hog_window_tiled = 1;  // tbdk_ctx_set_option("hog_window_tiled"): LDS-tiled window pass
@@ -90,6 +91,7 @@ struct tbdk_ctx {
     int opt_tbd_early_prio = 0;  // tbdk_ctx_set_option("tbd_early_prio"), read by tbdk_tbd_create
     int opt_tbd_early_la = 1;    // tbdk_ctx_set_option("tbd_early_la"): look-ahead PyrLK of early GFTT rows
     int opt_tbd_pyr_derivs = 0;  // tbdk_ctx_set_option("tbd_pyr_derivs"): loop pyramids with Scharr planes (A/B)
+    int opt_tbd_fit_inline = 1;  // tbdk_ctx_set_option("tbd_fit_inline"): the fit table in the kernel arguments
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
     std::vector<std::pair<std::string, int64_t>> timing_calls;  // selected launches per name (sampled or not)
@@ -160,6 +162,8 @@ struct LkLevel {
     int cpitch;
 };
 
+constexpr int kSegInline = 256;  // segment list entries LkArgs can carry itself
+
 struct LkArgs {
     LkLevel lv[TBDK_MAX_LEVELS];
     // optional segmented layout: point i = seg * seg_stride + j is valid iff
@@ -168,6 +172,7 @@ struct LkArgs {
     const int32_t* seg_counts;
     const int32_t* seg_list;
     int seg_stride;
+    int seg_ninl;  // > 0: the segment list is seg_inl[0, seg_ninl) instead of seg_list
     int max_level, win_w, win_h, max_count, flags, n;
     int cn;  // channels (klt_cn.hip; the one-channel kernels ignore it)
     double eps2;
@@ -185,6 +190,10 @@ struct LkArgs {
     int flow_pitch;
     uint8_t* dstatus;
     int dstatus_pitch;
+    // the segment list carried in the kernel arguments (ctx option lk_seg_inline):
+    // the TBD loop's lists live in pinned host memory (zero-copy), where every
+    // wave's first load would be a round trip over the host link
+    uint16_t seg_inl[kSegInline];
 #ifdef TBDK_LK_TRACE
     unsigned trace_base;  // probe builds: first trace record of this launch (klt_lk_multi.hip)
 #endif
@@ -196,7 +205,7 @@ __device__ __forceinline__ int seg_point(const LkArgs& a, int k)
     if (k >= a.n) return -1;
     if (!a.seg_counts) return k;
     const int seg = k / a.seg_stride, j = k - seg * a.seg_stride;
-    const int s = a.seg_list ? a.seg_list[seg] : seg;
+    const int s = a.seg_ninl > 0 ? (int)a.seg_inl[seg] : a.seg_list ? a.seg_list[seg] : seg;
     return j < a.seg_counts[s] ? s * a.seg_stride + j : -1;
 }
 
@@ -217,7 +226,7 @@ struct LkDense {
 int lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next, const float* prev_pts, float* next_pts,
                 uint8_t* status, float* err, int32_t* iters, int n, const tbdk_lk_params* p,
                 const int32_t* seg_counts, int seg_stride, void* stream, const int32_t* seg_list = nullptr,
-                const LkDense* dense = nullptr);
+                const LkDense* dense = nullptr, const int32_t* seg_list_host = nullptr);
 int map_status(hipError_t e);
 // multi-channel u8 pyramids and PyrLK (klt_cn.hip)
 hipError_t launch_pyr_cn(const uint8_t* img, int pitch, const tbdk_pyr& pyr, hipStream_t s);

@@ -271,6 +271,34 @@ def test_tbd_fit_flag_matches_event(gpu):
     assert res[0] == res[1]
 
 
+def test_tbd_inline_kernel_args_match_tables(gpu):
+    """The PyrLK segment lists and the fit table carried in the kernel
+    arguments (ctx options lk_seg_inline, tbd_fit_inline; the defaults) and
+    read from the staged tables give the same frames, zero-copy or not."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 40, 14
+    frames, gt = klt.synth_render(10, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
+    res = []
+    try:
+        for seg, fit, zc in ((1, 1, 1), (0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0)):
+            gpu.set_option("lk_seg_inline", seg)
+            gpu.set_option("tbd_fit_inline", fit)
+            gpu.set_option("tbd_zero_copy", zc)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            res.append(([_mkey(m) for m in ms], loop.tracks()))
+    finally:
+        gpu.set_option("lk_seg_inline", 1)
+        gpu.set_option("tbd_fit_inline", 1)
+        gpu.set_option("tbd_zero_copy", 1)
+    assert sum(m[0] > 0 for m in res[0][0]) > F // 2  # frames with true positives
+    for r in res[1:]:
+        assert r == res[0]
+
+
 def test_tbd_run_host_matches_run(gpu):
     """tbdk_tbd_run_host (frames uploaded from pinned host memory through the
     three-frame device ring) gives the same frames as tbdk_tbd_run on the same

@@ -1,5 +1,6 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tbd.py tests/test_gpu_hog.py > gpurun_out/t_tbd.log 2>&1; tail -2 gpurun_out/t_tbd.log
-grep -q " passed" gpurun_out/t_tbd.log && ! grep -q "failed" gpurun_out/t_tbd.log || exit 1
-timeout -k 10 800 python -u bench.py --no-cpu-baseline > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err || exit 1
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_short.json 2> gpurun_out/bench_short.err || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tbd.py tests/test_gpu_tbd_e2e.py > gpurun_out/t_fit.log 2>&1; tail -2 gpurun_out/t_fit.log
+grep -q " passed" gpurun_out/t_fit.log && ! grep -q "failed" gpurun_out/t_fit.log || exit 1
+L=opencv_amd/lib/libtbdk.so
+bash tools/ab.sh 3 all=$L nofit=$L,--ctx-option=tbd_fit_inline=0 none=$L,--ctx-option=tbd_fit_inline=0,--ctx-option=lk_seg_inline=0 || exit 1
+bash tools/ab.sh 3 dall=$L,--steps=20,--warmup=5 dnofit=$L,--ctx-option=tbd_fit_inline=0,--steps=20,--warmup=5 || exit 1

@@ -14,6 +14,12 @@ import statistics
 import sys
 
 
+def kernel_key(name: str) -> str:
+    """The demangled name without its parameter list ("(anonymous namespace)::"
+    dropped first, so that its parenthesis does not end the name)."""
+    return name.replace("(anonymous namespace)::", "").split("(")[0]
+
+
 def summarize(path, substrs=()):
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -21,7 +27,7 @@ def summarize(path, substrs=()):
         if substrs and not any(s in name for s in substrs):
             continue
         g = int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y") or 1) * int(r.get("Grid_Size_Z") or 1)
-        per[(name.split("(")[0], g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
+        per[(kernel_key(name), g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
     out = []
     for (name, g), d in sorted(per.items()):
         out.append({"kernel": name, "grid": g, "dispatches": len(d), "avg_us": round(sum(d) / len(d), 3),
