@@ -1,6 +1,2 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tbd.py tests/test_gpu_tbd_e2e.py > gpurun_out/t_fit.log 2>&1; tail -2 gpurun_out/t_fit.log
-grep -q " passed" gpurun_out/t_fit.log && ! grep -q "failed" gpurun_out/t_fit.log || exit 1
-L=opencv_amd/lib/libtbdk.so
-bash tools/ab.sh 3 all=$L nofit=$L,--ctx-option=tbd_fit_inline=0 none=$L,--ctx-option=tbd_fit_inline=0,--ctx-option=lk_seg_inline=0 || exit 1
-bash tools/ab.sh 3 dall=$L,--steps=20,--warmup=5 dnofit=$L,--ctx-option=tbd_fit_inline=0,--steps=20,--warmup=5 || exit 1
+bash tools/profile_round.sh r05 > gpurun_out/prof_r05.log 2>&1 || { tail -5 gpurun_out/prof_r05.log; exit 1; }
