@@ -22,6 +22,9 @@ __global__ void rate_kernel(int* out, long long* cyc, int seed)
         else if constexpr (OP == 3) asm volatile("v_pk_add_u16 %0, %8, %0\nv_pk_add_u16 %1, %8, %1\nv_pk_add_u16 %2, %8, %2\nv_pk_add_u16 %3, %8, %3\nv_pk_add_u16 %4, %8, %4\nv_pk_add_u16 %5, %8, %5\nv_pk_add_u16 %6, %8, %6\nv_pk_add_u16 %7, %8, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
         else if constexpr (OP == 4) asm volatile("v_ashrrev_i32_sdwa %0, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %1, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %2, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %3, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %4, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %5, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %6, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\nv_ashrrev_i32_sdwa %7, 9, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
         else if constexpr (OP == 5) asm volatile("v_add_u32_dpp %0, %8, %0 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %1, %8, %1 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %2, %8, %2 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %3, %8, %3 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %4, %8, %4 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %5, %8, %5 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %6, %8, %6 row_shr:1 row_mask:0xf bank_mask:0xf\nv_add_u32_dpp %7, %8, %7 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
+        else if constexpr (OP == 6) asm volatile("v_dot4_u32_u8 %0, %8, %8, %0\nv_dot4_u32_u8 %1, %8, %8, %1\nv_dot4_u32_u8 %2, %8, %8, %2\nv_dot4_u32_u8 %3, %8, %8, %3\nv_dot4_u32_u8 %4, %8, %8, %4\nv_dot4_u32_u8 %5, %8, %8, %5\nv_dot4_u32_u8 %6, %8, %8, %6\nv_dot4_u32_u8 %7, %8, %8, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
+        else if constexpr (OP == 7) asm volatile("v_dot2_u32_u16 %0, %8, %8, %0\nv_dot2_u32_u16 %1, %8, %8, %1\nv_dot2_u32_u16 %2, %8, %8, %2\nv_dot2_u32_u16 %3, %8, %8, %3\nv_dot2_u32_u16 %4, %8, %8, %4\nv_dot2_u32_u16 %5, %8, %8, %5\nv_dot2_u32_u16 %6, %8, %8, %6\nv_dot2_u32_u16 %7, %8, %8, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
+        else if constexpr (OP == 8) asm volatile("v_mad_u32_u24 %0, %8, %8, %0\nv_mad_u32_u24 %1, %8, %8, %1\nv_mad_u32_u24 %2, %8, %8, %2\nv_mad_u32_u24 %3, %8, %8, %3\nv_mad_u32_u24 %4, %8, %8, %4\nv_mad_u32_u24 %5, %8, %8, %5\nv_mad_u32_u24 %6, %8, %8, %6\nv_mad_u32_u24 %7, %8, %8, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));
     }
     long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -70,6 +73,9 @@ int main()
         run<3>("v_pk_add_u16", w);
         run<4>("v_ashrrev sdwa", w);
         run<5>("v_add_u32 dpp", w);
+        run<6>("v_dot4_u32_u8", w);
+        run<7>("v_dot2_u32_u16", w);
+        run<8>("v_mad_u32_u24", w);
     }
     return 0;
 }
