@@ -56,12 +56,23 @@ __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(k >= 0 
 
 }  // namespace
 
-__device__ __forceinline__ int roi_of_cblock(const GfttRoi* rois, int nroi, int b)
+// ROI r of the launch: from the kernel arguments when the table travels there
+// (GfttArgs::inl), else from the table in memory
+__device__ __forceinline__ GfttRoi roi_at(const GfttArgs& a, int r)
 {
-    int lo = 0, hi = nroi - 1;
+    if (a.ninl > 0) {
+        const GfttRoiC c = a.inl[r];
+        return GfttRoi{c.x, c.y, c.w, c.h, c.off, c.moff, c.cblk};
+    }
+    return a.rois[r];
+}
+
+__device__ __forceinline__ int roi_of_cblock(const GfttArgs& a, int b)
+{
+    int lo = 0, hi = a.nroi - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (rois[mid].cblk <= b) lo = mid;
+        if ((a.ninl > 0 ? a.inl[mid].cblk : a.rois[mid].cblk) <= b) lo = mid;
         else hi = mid - 1;
     }
     return lo;
@@ -288,8 +299,8 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     __shared__ double s_drift[3][64];
     __shared__ int s_best[kEigWaves];
     __shared__ int s_bad;
-    const int r = roi_of_cblock(a.rois, a.nroi, blockIdx.x);
-    const GfttRoi R = a.rois[r];
+    const int r = roi_of_cblock(a, blockIdx.x);
+    const GfttRoi R = roi_at(a, r);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int H = R.h;
@@ -838,7 +849,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
     float2* bxy = acc + a.max_corners;
     uint8_t* img = reinterpret_cast<uint8_t*>(acc + ((a.max_corners + 65) & ~1));  // 16-byte aligned
     const int r = blockIdx.x;
-    const GfttRoi R = a.rois[r];
+    const GfttRoi R = roi_at(a, r);
     const int tid = threadIdx.x;
     __shared__ int s_total;
     GFTT_STAMP(0);

@@ -213,6 +213,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_pyr_derivs = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "gftt_inline") == 0) {
+        ctx->opt_gftt_inline = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_fit_inline") == 0) {
         ctx->opt_tbd_fit_inline = value != 0;
         return TBDK_OK;
@@ -748,7 +752,7 @@ int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px)
 
 int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois,
                 const GfttPlan& plan, const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
-                hipEvent_t after_eig, int corner_stride)
+                hipEvent_t after_eig, int corner_stride, const GfttRoi* h_rois)
 {
     if (corner_stride != 0 && corner_stride < p->max_corners) return TBDK_EINVAL;
     int rc = gftt_reserve(sc, ctx->device, plan.nroi, plan.total);
@@ -771,6 +775,18 @@ int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, c
     a.corner_stride = corner_stride ? corner_stride : p->max_corners;
     a.counts = counts;
     a.eig_redo = ctx->opt_gftt_eig_redo;
+    a.ninl = 0;
+    if (h_rois && ctx->opt_gftt_inline && plan.nroi <= kGfttInline) {  // the table into the kernel arguments
+        bool fits = true;
+        for (int r = 0; fits && r < plan.nroi; ++r) {
+            const GfttRoi& R = h_rois[r];
+            fits = R.x >= 0 && R.y >= 0 && R.w >= 0 && R.h >= 0 && R.x <= 0xFFFF && R.y <= 0xFFFF && R.w <= 0xFFFF &&
+                   R.h <= 0xFFFF;
+            if (fits)
+                a.inl[r] = GfttRoiC{(uint16_t)R.x, (uint16_t)R.y, (uint16_t)R.w, (uint16_t)R.h, R.off, R.moff, R.cblk};
+        }
+        if (fits) a.ninl = plan.nroi;
+    }
     gftt_plan(a, plan.max_area);
     hipError_t e;
     if (!gftt_generic(p)) {
@@ -816,7 +832,7 @@ int tbdk_gftt_rois(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int
     hipError_t e = hipMemcpyAsync(ctx->gftt.rois, tab.data(), sizeof(GfttRoi) * (size_t)nroi, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
     return gftt_launch(ctx, ctx->gftt, img, pitch, static_cast<const GfttRoi*>(ctx->gftt.rois), plan, p, corners,
-                       counts, s);
+                       counts, s, nullptr, 0, tab.data());
 }
 
 int tbdk_corner_min_eig_val(tbdk_ctx* ctx, const uint8_t* img, int width, int height, int pitch, float* dst,

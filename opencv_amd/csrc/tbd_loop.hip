@@ -768,7 +768,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             const tbdk_level& L0 = P.lv[0];
             rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
                               reinterpret_cast<float*>(t->slot_pts + (size_t)erow0 * kSlotPts), t->slot_counts + erow0,
-                              es, nullptr, kSlotPts);
+                              es, nullptr, kSlotPts, htab);
             if (rc2 != TBDK_OK) return rc2;
             const hipError_t e = hipEventRecord(t->early_done, es);
             if (e != hipSuccess) return map_status(e);
@@ -1169,7 +1169,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         const tbdk_level& L0 = P.lv[0];
         rc = gftt_launch(t->ctx, t->gftt2, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, t->d_tab, plan, &gp,
                          reinterpret_cast<float*>(t->slot_pts + (size_t)prow0 * kSlotPts), t->slot_counts + prow0,
-                         t->side, next ? t->eig_done : nullptr, kSlotPts);
+                         t->side, next ? t->eig_done : nullptr, kSlotPts, t->h_tab);
         if (rc != TBDK_OK) return rc;
     }
     // post_done also after an early GFTT none of whose ROIs was used: the next

@@ -92,6 +92,7 @@ struct tbdk_ctx {
     int opt_tbd_early_la = 1;    // tbdk_ctx_set_option("tbd_early_la"): look-ahead PyrLK of early GFTT rows
     int opt_tbd_pyr_derivs = 0;  // tbdk_ctx_set_option("tbd_pyr_derivs"): loop pyramids with Scharr planes (A/B)
     int opt_tbd_fit_inline = 1;  // tbdk_ctx_set_option("tbd_fit_inline"): the fit table in the kernel arguments
+    int opt_gftt_inline = 1;     // tbdk_ctx_set_option("gftt_inline"): GFTT ROI tables in the kernel arguments
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
     std::vector<std::pair<std::string, int64_t>> timing_calls;  // selected launches per name (sampled or not)
@@ -286,6 +287,12 @@ struct GfttRoi {
 constexpr int kGfttStrip = 56;
 constexpr int kGfttHalo = 4;
 __host__ __device__ constexpr int gftt_epitch(int w) { return (w + 7) & ~7; }
+// a ROI table entry carried in the kernel arguments (GfttArgs::inl)
+struct GfttRoiC {
+    uint16_t x, y, w, h;
+    int off, moff, cblk;
+};
+constexpr int kGfttInline = 128;
 struct GfttArgs {
     const uint8_t* img;
     int pitch;
@@ -303,6 +310,11 @@ struct GfttArgs {
     int corner_stride;
     int32_t* counts;  // nroi (-1: candidate overflow)
     int eig_redo;     // test option: walk every eig strip segment in sequence
+    // > 0: the ROI table is inl[0, nroi) instead of rois (ctx option gftt_inline):
+    // the TBD loop's tables live in pinned host memory, where the eigenvalue
+    // kernel's binary search over them is a chain of host-link round trips
+    int ninl;
+    GfttRoiC inl[kGfttInline];
 };
 constexpr int kGfttCap = 16384;  // candidates per ROI (LDS-resident for the sort)
 // scratch sizes for (rois, pixels): strips <= px/60 + rois; local-maximum words
@@ -324,9 +336,12 @@ int gftt_prepare(const tbdk_roi* rois, int nroi, int width, int height, const tb
 // scratch sized for max_rois ROIs of max_px pixels in total (grows only)
 int gftt_reserve(GfttScratch& sc, int device, int max_rois, int64_t max_px);
 void gftt_scratch_free(GfttScratch& sc);
+// h_rois (optional): a host-readable copy of the table, carried in the kernel
+// arguments when it fits (ctx option gftt_inline)
 int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, const GfttRoi* d_rois, const GfttPlan& plan,
                 const tbdk_gftt_params* p, float* corners, int32_t* counts, hipStream_t s,
-                hipEvent_t after_eig = nullptr, int corner_stride = 0);  // 0: max_corners
+                hipEvent_t after_eig = nullptr, int corner_stride = 0,  // 0: max_corners
+                const GfttRoi* h_rois = nullptr);
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig = nullptr);
 hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s);  // eigenvalue planes only
 hipError_t launch_gftt_select(const GfttArgs& a, hipStream_t s);

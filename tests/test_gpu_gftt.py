@@ -59,6 +59,24 @@ def test_gftt_1080p_128_boxes(gpu):
     assert (n > 0).all()
 
 
+@pytest.mark.parametrize("inline", [1, 0])
+def test_gftt_roi_table_in_args_or_memory(gpu, inline):
+    """The ROI table carried in the kernel arguments (ctx option gftt_inline,
+    up to 128 ROIs) and read from device memory (the option off, or more ROIs
+    than the arguments hold) give the oracle's corner lists."""
+    fr, gt = O.synth(20261016, 1920, 1080, 128, 0, 1)
+    boxes = [tuple(int(v) for v in g[1:]) for g in gt[0] if g[0]]
+    halves = [(x, y, max(w // 2, 3), max(h // 2, 3)) for x, y, w, h in boxes]
+    gpu.set_option("gftt_inline", inline)
+    try:
+        for rois in (boxes[:128], (boxes + halves)[:200]):
+            c, n = detect(gpu, fr[0], rois, 128, 0.01, 3.0)
+            check(fr[0], rois, c, n, 128, 0.01, 3.0)
+            assert (n > 0).sum() > len(rois) // 2
+    finally:
+        gpu.set_option("gftt_inline", 1)
+
+
 @pytest.mark.parametrize("shape", [(480, 640), (37, 61), (3, 3), (1, 7), (9, 1), (1080, 1920), (130, 121),
                                    (17, 200), (33, 58), (34, 59), (33, 56), (34, 57), (2, 2)])
 @pytest.mark.parametrize("redo", [0, 1])

@@ -272,8 +272,9 @@ def test_tbd_fit_flag_matches_event(gpu):
 
 
 def test_tbd_inline_kernel_args_match_tables(gpu):
-    """The PyrLK segment lists and the fit table carried in the kernel
-    arguments (ctx options lk_seg_inline, tbd_fit_inline; the defaults) and
+    """The PyrLK segment lists, the fit table and the GFTT ROI tables carried
+    in the kernel arguments (ctx options lk_seg_inline, tbd_fit_inline,
+    gftt_inline; the defaults) and
     read from the staged tables give the same frames, zero-copy or not."""
     from opencv_amd import klt, tbd
 
@@ -283,9 +284,10 @@ def test_tbd_inline_kernel_args_match_tables(gpu):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
     res = []
     try:
-        for seg, fit, zc in ((1, 1, 1), (0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0)):
+        for seg, fit, gf, zc in ((1, 1, 1, 1), (0, 0, 0, 1), (1, 0, 1, 1), (0, 1, 0, 1), (1, 1, 1, 0)):
             gpu.set_option("lk_seg_inline", seg)
             gpu.set_option("tbd_fit_inline", fit)
+            gpu.set_option("gftt_inline", gf)
             gpu.set_option("tbd_zero_copy", zc)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
@@ -293,6 +295,7 @@ def test_tbd_inline_kernel_args_match_tables(gpu):
     finally:
         gpu.set_option("lk_seg_inline", 1)
         gpu.set_option("tbd_fit_inline", 1)
+        gpu.set_option("gftt_inline", 1)
         gpu.set_option("tbd_zero_copy", 1)
     assert sum(m[0] > 0 for m in res[0][0]) > F // 2  # frames with true positives
     for r in res[1:]:

@@ -96,7 +96,7 @@ int main()
     unsigned long long* dtacc;
     CK(hipMalloc(&dtacc, 8 * 8 * nroi));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_tacc), &dtacc, sizeof(dtacc)));
-    tbdk::GfttArgs a;
+    tbdk::GfttArgs a{};
     a.img = dimg;
     a.pitch = W;
     a.rois = drois;
