@@ -245,6 +245,8 @@ struct tbdk_tbd {
     hipStream_t la_stream = nullptr;
     bool la_pyr = false;             // pyr[cur] already holds la_frame's pyramid
     bool la_lk = false;              // ... and the la_member slots are tracked into it
+    int la_defer_n = 0;              // look-ahead PyrLK left to the next step (h_la's first la_defer_n slots)
+    bool la_defer_eig = false;       // ... behind the post-tracker GFTT's eigenvalue kernel
     // pinned host staging (reuse rules: see tbdk_tbd_step)
     // [fit entries: S FitEntry][LK slot lists: S int32 (unchanged sets, then refreshed ones)]
     void* h_pre = nullptr;
@@ -815,6 +817,26 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     lp.flags = 0;
     lp.min_eig_threshold = c.min_eig_threshold;
     lp.impl = 0;
+    // the look-ahead PyrLK of the n unchanged sets in h_la, pyramid A -> B, on
+    // la_s behind the look-ahead pyramid and (eig) the post-tracker GFTT's
+    // eigenvalue kernel
+    auto launch_la = [&](int n, bool eig, tbdk_pyr& A, tbdk_pyr& B) -> int {
+        hipStream_t ls = t->la_s;
+        hipError_t e = wait_if_pending(ls, t->la_ready);
+        if (e == hipSuccess && eig) e = wait_if_pending(ls, t->eig_done);
+        if (e == hipSuccess && !t->zc)
+            e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
+        if (e != hipSuccess) return map_status(e);
+        const int r = lk_internal(t->ctx, &A, &B, reinterpret_cast<const float*>(t->slot_pts),
+                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                                  n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la, nullptr, t->h_la);
+        if (r != TBDK_OK) return r;
+        return map_status(hipEventRecord(t->la_done, ls));
+    };
+    // the previous step's deferred look-ahead PyrLK (ctx option tbd_la_defer),
+    // launched below once this step's critical PyrLK is; dropped with the look-ahead
+    const int la_defer = la_lk ? t->la_defer_n : 0;
+    t->la_defer_n = 0;
     if (run_klt) {
         for (const auto& tr : tracks) {
             const int* it = t->slot_of.find(tr.id);
@@ -879,6 +901,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
                              nsets * kSlotPts, &lp, t->slot_counts, kSlotPts, s, t->d_lists + first, nullptr,
                              t->h_lists + first);
+            if (rc != TBDK_OK) return rc;
+        }
+        if (la_defer > 0) {
+            rc = launch_la(la_defer, t->la_defer_eig, Pprev, P);
             if (rc != TBDK_OK) return rc;
         }
         STEP_MARK(3);
@@ -1183,7 +1209,6 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
     // set was not refreshed just now (exactly the next step's unchanged sets)
     if (next) {
-        hipError_t e = hipSuccess;
         if (c.use_klt && !t->tracker->getTracks().empty()) {
             int n = 0;  // unchanged sets the speculative PyrLK did not cover
             for (const auto& tr : t->tracker->getTracks()) {
@@ -1197,18 +1222,15 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 // on la_s, after the fit and the pyramid (la_ready) and behind the
                 // GFTT eigenvalue kernel: its many large workgroups would otherwise
                 // wait for the long-lived PyrLK waves to drain
-                hipStream_t ls = t->la_s;
-                e = wait_if_pending(ls, t->la_ready);
-                if (e == hipSuccess && nroi > 0) e = wait_if_pending(ls, t->eig_done);
-                if (e == hipSuccess && !t->zc)
-                    e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
-                if (e != hipSuccess) return map_status(e);
-                rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
-                                 reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                 n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la, nullptr, t->h_la);
-                if (rc != TBDK_OK) return rc;
-                e = hipEventRecord(t->la_done, ls);
-                if (e != hipSuccess) return map_status(e);
+                if (t->ctx->opt_tbd_la_defer) {
+                    // launched by the next step right after its critical PyrLK
+                    // (off the host chain between this fit and that launch)
+                    t->la_defer_n = n;
+                    t->la_defer_eig = nroi > 0;
+                } else {
+                    rc = launch_la(n, nroi > 0, P, Pnext);
+                    if (rc != TBDK_OK) return rc;
+                }
                 t->la_lk = true;
             }
         }

@@ -271,6 +271,36 @@ def test_tbd_fit_flag_matches_event(gpu):
     assert res[0] == res[1]
 
 
+def test_tbd_deferred_lookahead_matches(gpu):
+    """The look-ahead PyrLK of the unchanged sets launched by the next step
+    right after its critical PyrLK (ctx option tbd_la_defer) gives the same
+    frames as launched at the end of its own step, through tbdk_tbd_run and
+    per-frame steps with and without an announced next frame."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 40, 16
+    frames, gt = klt.synth_render(12, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=4)
+    res = []
+    try:
+        for d in (0, 1):
+            gpu.set_option("tbd_la_defer", d)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            stepped = tbd.TbdLoop(c, ctx=gpu)
+            mt = []
+            for f in range(F):  # the look-ahead announced on two frames of three
+                nxt = frames[f + 1] if f + 1 < F and f % 3 != 2 else None
+                mt.append(_mkey(stepped.step(frames[f], f, dets[f], next_frame=nxt)))
+            res.append(([_mkey(m) for m in ms], loop.tracks(), mt, stepped.tracks()))
+    finally:
+        gpu.set_option("tbd_la_defer", 0)
+    assert res[0] == res[1]
+    assert res[0][0] == res[0][2]
+    assert sum(m[7] for m in res[0][0]) > 0
+
+
 def test_tbd_inline_kernel_args_match_tables(gpu):
     """The PyrLK segment lists, the fit table and the GFTT ROI tables carried
     in the kernel arguments (ctx options lk_seg_inline, tbd_fit_inline,
