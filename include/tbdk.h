@@ -183,6 +183,16 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
  *       pyramids carry Scharr derivative planes and PyrLK reads them instead of
  *       deriving the window's values (results equal; A/B runs).
+ *   "lk_seg_inline", "tbd_fit_inline", "gftt_inline" (0/1, default 1): the TBD
+ *       loop's PyrLK segment lists (up to 256), the fit's per-track table (up
+ *       to 256 tracks) and GFTT ROI tables (up to 128 ROIs, also in
+ *       tbdk_gftt_rois) travel in the kernel arguments instead of being read
+ *       from the staged tables (with zero copy: pinned host memory, one
+ *       host-link round trip per first read); larger tables are read from
+ *       memory (results equal).
+ *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
+ *       sets is launched by the next step right after its critical PyrLK
+ *       instead of at the end of its own step (results equal; A/B runs).
  *   "timing_every" (>= 1, default 1): HIP events on a pseudo-random 1/N of the
  *       launches of each kernel selected for timing: launch i (counted per
  *       kernel name from tbdk_timing_enable) is timed iff splitmix64(i) % N == 0
