@@ -190,6 +190,9 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       from the staged tables (with zero copy: pinned host memory, one
  *       host-link round trip per first read); larger tables are read from
  *       memory (results equal).
+ *   "tbd_fit_wgpub" (0/1, default 1): with the fit flag, each fit workgroup
+ *       publishes its tracks' results with one system-scope release (wave 0
+ *       stores them), not one release per wave (results equal).
  *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
  *       sets is launched by the next step right after its critical PyrLK
  *       instead of at the end of its own step (results equal; A/B runs).

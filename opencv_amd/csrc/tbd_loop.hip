@@ -89,9 +89,10 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
                                                                  int32_t* __restrict__ slot_counts,
                                                                  FitOut* __restrict__ out, int min_fit,
                                                                  unsigned* __restrict__ fit_cnt, int32_t* flag, int tag,
-                                                                 int inl, const FitInline fi)
+                                                                 int inl, const FitInline fi, int wg_pub)
 {
     __shared__ float2 s_a[kFitWaves][kSlotPts], s_b[kFitWaves][kSlotPts];
+    __shared__ FitOut s_out[kFitWaves];  // wg_pub: the workgroup's results, published by wave 0
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int e = blockIdx.x * kFitWaves + wv;
     if (e < nents) {
@@ -158,23 +159,30 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
                 o.scale = sqrt(f.p * f.p + f.q * f.q);
                 o.valid = (o.scale > 0.5 && o.scale < 2.0 && isfinite(o.cx) && isfinite(o.cy)) ? 1 : 0;
             }
-            out[e] = o;
+            if (flag && wg_pub) s_out[wv] = o;
+            else out[e] = o;
         }
-        // every wave that wrote a FitOut releases it at system scope itself: the
-        // workgroup barrier below orders waves only at workgroup scope, and thread
-        // 0's release waits only for its own wave's stores
-        if (flag) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // without wg_pub every wave that wrote a FitOut releases it at system
+        // scope itself: the workgroup barrier below orders waves only at
+        // workgroup scope, and thread 0's release waits only for its own wave's
+        // stores (each release writes the XCD's L2 back)
+        if (flag && !wg_pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (flag) {
         // publish: after the workgroup's barrier one thread counts the
         // workgroup's results at system scope; the last workgroup resets the
         // count for the next launch (stream-ordered) and raises the frame's tag
         __syncthreads();
+        const int first = blockIdx.x * kFitWaves;
+        const int nin = nents - first < kFitWaves ? nents - first : kFitWaves;
+        if (wg_pub && threadIdx.x < 64) {  // wave 0 stores the workgroup's results and releases them once
+            if ((int)threadIdx.x < nin) out[first + threadIdx.x] = s_out[threadIdx.x];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
         if (threadIdx.x == 0) {
-            const int first = blockIdx.x * kFitWaves;
-            const unsigned nin = (unsigned)(nents - first < kFitWaves ? nents - first : kFitWaves);
-            const unsigned prev = __hip_atomic_fetch_add(fit_cnt, nin, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (prev + nin == (unsigned)nents) {
+            const unsigned prev =
+                __hip_atomic_fetch_add(fit_cnt, (unsigned)nin, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (prev + (unsigned)nin == (unsigned)nents) {
                 *fit_cnt = 0u;
                 __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -935,7 +943,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         hipLaunchKernelGGL(tbd_fit_kernel, dim3((nents + kFitWaves - 1) / kFitWaves), dim3(64 * kFitWaves), 0, s,
                            t->d_ents, nents, t->slot_pts, t->slot_next,
                            t->slot_status, t->slot_iters, t->slot_counts, t->d_fit, c.min_fit_points,
-                           by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag, inl, t->fit_inl);
+                           by_flag ? t->d_fitcnt : nullptr, by_flag ? t->d_flag : nullptr, tag, inl, t->fit_inl,
+                           t->ctx->opt_tbd_fit_wgpub);
         timing_end(t->ctx, rec, s);
         if (!t->zc) e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && !by_flag) e = hipEventRecord(t->fit_done, s);
