@@ -217,6 +217,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_fit_wgpub = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_la_pyr_side") == 0) {
+        ctx->opt_tbd_la_pyr_side = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_la_defer") == 0) {
         ctx->opt_tbd_la_defer = value != 0;
         return TBDK_OK;

@@ -223,6 +223,7 @@ struct tbdk_tbd {
     // behind the post-tracker GFTT
     hipEvent_t fit_done = nullptr;   // this frame's predictions are on the host
     hipEvent_t la_ready = nullptr;   // look-ahead pyramid complete (recorded on the step's stream)
+    hipEvent_t lk_issued = nullptr;  // tbd_la_pyr_side: this step's PyrLK launches (on the step's stream) done
     hipEvent_t la_done = nullptr;    // look-ahead PyrLK complete (recorded on la_s)
     // the look-ahead PyrLK runs on its own stream behind the GFTT eigenvalue
     // kernel, so the refreshed sets' PyrLK of the next step (caller's stream)
@@ -352,6 +353,7 @@ int release(tbdk_tbd* t)
     if (t->la_s) (void)hipStreamSynchronize(t->la_s);
     if (t->la_done) (void)hipEventDestroy(t->la_done);
     if (t->la_ready) (void)hipEventDestroy(t->la_ready);
+    if (t->lk_issued) (void)hipEventDestroy(t->lk_issued);
     if (t->la_s && t->own_la) (void)hipStreamDestroy(t->la_s);
     if (t->eig_done) (void)hipEventDestroy(t->eig_done);
     if (t->side && t->own_side) (void)hipStreamDestroy(t->side);
@@ -528,6 +530,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fit_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->lk_issued, hipEventDisableTiming);
     // the look-ahead PyrLK at the lowest priority (on gfx950 the range is
     // normal..high, so this is the default; a high-priority caller stream for
     // the critical PyrLK measured no difference either)
@@ -830,7 +833,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // eigenvalue kernel
     auto launch_la = [&](int n, bool eig, tbdk_pyr& A, tbdk_pyr& B) -> int {
         hipStream_t ls = t->la_s;
-        hipError_t e = wait_if_pending(ls, t->la_ready);
+        hipError_t e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
         if (e == hipSuccess && eig) e = wait_if_pending(ls, t->eig_done);
         if (e == hipSuccess && !t->zc)
             e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
@@ -893,14 +896,24 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
     }
     tbdk_pyr& Pnext = Pprev;  // the look-ahead pyramid replaces the previous frame's
-    auto enqueue_next_pyr = [&]() -> int {
+    // side (ctx option tbd_la_pyr_side): built on the look-ahead stream behind
+    // this step's PyrLK launches (lk_issued; they read the buffer it
+    // overwrites), beside the fit, so the look-ahead PyrLK that follows it on
+    // that stream needs no cross-stream edge
+    auto enqueue_next_pyr = [&](bool side) -> int {
+        hipStream_t ps = s;
+        if (side) {
+            ps = t->la_s;
+            const hipError_t e = hipStreamWaitEvent(ps, t->lk_issued, 0);
+            if (e != hipSuccess) return map_status(e);
+        }
         t->la_frame = next;
         t->la_pitch = next_pitch;
-        t->la_stream = s;
+        t->la_stream = ps;
         t->la_pyr = true;
-        const int r = tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, s);
+        const int r = tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, ps);
         if (r != TBDK_OK) return r;
-        return map_status(hipEventRecord(t->la_ready, s));  // the next frame's pyramid (and this fit) done
+        return map_status(hipEventRecord(t->la_ready, ps));  // the next frame's pyramid (and this fit) done
     };
     if (run_klt) {
         if (nB > 0) {
@@ -923,6 +936,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         hipError_t e = hipSuccess;  // zero-copy without a look-ahead wait sets it nowhere below
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
             e = wait_if_pending(s, t->la_done);
+            if (e != hipSuccess) return map_status(e);
+        }
+        const bool pyr_side = next && t->ctx->opt_tbd_la_pyr_side;
+        if (pyr_side) {
+            e = hipEventRecord(t->lk_issued, s);
             if (e != hipSuccess) return map_status(e);
         }
         const bool by_flag = t->fit_flag && nents > 0;
@@ -950,7 +968,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e == hipSuccess && !by_flag) e = hipEventRecord(t->fit_done, s);
         if (e != hipSuccess) return map_status(e);
         if (next) {  // runs on the device while this step waits for the fit and tracks
-            rc = enqueue_next_pyr();
+            rc = enqueue_next_pyr(pyr_side);
             if (rc != TBDK_OK) return rc;
         }
         if (early_order == 2) {
@@ -1043,7 +1061,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             SUB_MARK(0);
             if (ns > 0) {
                 hipStream_t ls = t->la_s;
-                e = wait_if_pending(ls, t->la_ready);
+                e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
                 if (e == hipSuccess && !t->zc)
                     e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
                 if (e != hipSuccess) return map_status(e);
@@ -1080,7 +1098,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (next && early_launched && ne > 0 && (ela >= 2 || (ela == 1 && frame_id % c.redetect_every == 0))) {
             for (int q = 0; q < ne; ++q) t->h_ers[q] = erow0 + q;
             hipStream_t ls = t->la_s;
-            e = wait_if_pending(ls, t->la_ready);
+            e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
             if (e == hipSuccess) e = wait_if_pending(ls, t->early_done);
             if (e == hipSuccess && !t->zc)
                 e = hipMemcpyAsync(t->d_ers, t->h_ers, sizeof(int32_t) * ne, hipMemcpyHostToDevice, ls);
@@ -1109,7 +1127,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 hipError_t e = wait_if_pending(s, t->la_done);
                 if (e != hipSuccess) return map_status(e);
             }
-            rc = enqueue_next_pyr();
+            rc = enqueue_next_pyr(false);
             if (rc != TBDK_OK) return rc;
         }
     }

@@ -273,9 +273,10 @@ def test_tbd_fit_flag_matches_event(gpu):
 
 def test_tbd_deferred_lookahead_matches(gpu):
     """The look-ahead PyrLK of the unchanged sets launched by the next step
-    right after its critical PyrLK (ctx option tbd_la_defer) gives the same
-    frames as launched at the end of its own step, through tbdk_tbd_run and
-    per-frame steps with and without an announced next frame."""
+    right after its critical PyrLK (ctx option tbd_la_defer), and the
+    look-ahead pyramid built on the look-ahead stream (tbd_la_pyr_side), give
+    the same frames as the defaults, through tbdk_tbd_run and per-frame steps
+    with and without an announced next frame."""
     from opencv_amd import klt, tbd
 
     W, H, N, F = 960, 540, 40, 16
@@ -284,8 +285,9 @@ def test_tbd_deferred_lookahead_matches(gpu):
     c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=4)
     res = []
     try:
-        for d in (0, 1):
+        for d, side in ((0, 0), (1, 0), (0, 1), (1, 1)):
             gpu.set_option("tbd_la_defer", d)
+            gpu.set_option("tbd_la_pyr_side", side)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
             stepped = tbd.TbdLoop(c, ctx=gpu)
@@ -296,7 +298,9 @@ def test_tbd_deferred_lookahead_matches(gpu):
             res.append(([_mkey(m) for m in ms], loop.tracks(), mt, stepped.tracks()))
     finally:
         gpu.set_option("tbd_la_defer", 0)
-    assert res[0] == res[1]
+        gpu.set_option("tbd_la_pyr_side", 1)  # the default
+    for r in res[1:]:
+        assert r == res[0]
     assert res[0][0] == res[0][2]
     assert sum(m[7] for m in res[0][0]) > 0
 
