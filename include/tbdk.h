@@ -193,10 +193,13 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_fit_wgpub" (0/1, default 1): with the fit flag, each fit workgroup
  *       publishes its tracks' results with one system-scope release (wave 0
  *       stores them), not one release per wave (results equal).
- *   "tbd_la_pyr_side" (0/1, default 1): the TBD loop builds the look-ahead
- *       pyramid on its look-ahead stream (behind the step's PyrLK launches,
- *       beside the fit) instead of on the caller's stream behind the fit, so
- *       the look-ahead PyrLK that follows it needs no cross-stream edge
+ *   "tbd_la_pyr_side" (0/1/2, default 2): where the TBD loop builds the
+ *       look-ahead pyramid: 0 on the caller's stream behind the fit; 1 on its
+ *       look-ahead stream behind the step's PyrLK launches, beside the fit; 2 on
+ *       the look-ahead stream right after the step's critical PyrLK launch,
+ *       behind only the caller's work before the step (the loop keeps three
+ *       pyramids, so the one it overwrites is two frames old and no longer
+ *       read). The look-ahead PyrLK that follows it needs no cross-stream edge
  *       (results equal).
  *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
  *       sets is launched by the next step right after its critical PyrLK

@@ -218,7 +218,8 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_la_pyr_side") == 0) {
-        ctx->opt_tbd_la_pyr_side = value != 0;
+        if (value < 0 || value > 2) return TBDK_EINVAL;
+        ctx->opt_tbd_la_pyr_side = (int)value;
         return TBDK_OK;
     }
     if (std::strcmp(name, "tbd_la_defer") == 0) {

@@ -197,8 +197,12 @@ using namespace tbdk;
 struct tbdk_tbd {
     tbdk_ctx* ctx = nullptr;
     tbdk_tbd_config cfg;
-    tbdk_pyr pyr[2];
+    // three pyramids in rotation: this frame's (cur), the previous frame's and
+    // the look-ahead frame's, so the look-ahead build never overwrites a
+    // pyramid this step's PyrLK still reads
+    tbdk_pyr pyr[3];
     int cur = 0;
+    bool last_fit = false;  // the previous step ran PyrLK and synced on its fit
     bool have_prev = false;
     tbd::Tracker* tracker = nullptr;
     tbdk_trajectories* traj = nullptr;  // caller-owned; records per-object tracking results
@@ -224,6 +228,7 @@ struct tbdk_tbd {
     hipEvent_t fit_done = nullptr;   // this frame's predictions are on the host
     hipEvent_t la_ready = nullptr;   // look-ahead pyramid complete (recorded on the step's stream)
     hipEvent_t lk_issued = nullptr;  // tbd_la_pyr_side: this step's PyrLK launches (on the step's stream) done
+    hipEvent_t step_begin = nullptr; // tbd_la_pyr_side 2: the caller's work on the step's stream before the step
     hipEvent_t la_done = nullptr;    // look-ahead PyrLK complete (recorded on la_s)
     // the look-ahead PyrLK runs on its own stream behind the GFTT eigenvalue
     // kernel, so the refreshed sets' PyrLK of the next step (caller's stream)
@@ -354,10 +359,11 @@ int release(tbdk_tbd* t)
     if (t->la_done) (void)hipEventDestroy(t->la_done);
     if (t->la_ready) (void)hipEventDestroy(t->la_ready);
     if (t->lk_issued) (void)hipEventDestroy(t->lk_issued);
+    if (t->step_begin) (void)hipEventDestroy(t->step_begin);
     if (t->la_s && t->own_la) (void)hipStreamDestroy(t->la_s);
     if (t->eig_done) (void)hipEventDestroy(t->eig_done);
     if (t->side && t->own_side) (void)hipStreamDestroy(t->side);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if (t->pyr[i].storage) tbdk_pyr_destroy(t->ctx, &t->pyr[i]);
     if (t->pyr_ready) (void)hipEventDestroy(t->pyr_ready);
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
@@ -438,7 +444,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->cfg = *cfg;
     std::memset(t->pyr, 0, sizeof(t->pyr));
     int rc = TBDK_OK;
-    for (int i = 0; i < 2 && rc == TBDK_OK; ++i)
+    for (int i = 0; i < 3 && rc == TBDK_OK; ++i)
         // levels only: PyrLK derives the window's Scharr values itself, so the
         // build writes no derivative planes (ctx option tbd_pyr_derivs = 1: with
         // the planes, for A/B runs; same results)
@@ -531,6 +537,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->lk_issued, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->step_begin, hipEventDisableTiming);
     // the look-ahead PyrLK at the lowest priority (on gfx950 the range is
     // normal..high, so this is the default; a high-priority caller stream for
     // the critical PyrLK measured no difference either)
@@ -654,7 +661,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     double launch_us = 0.0;
     const tbdk_tbd_config& c = t->cfg;
     tbdk_pyr& P = t->pyr[t->cur];
-    tbdk_pyr& Pprev = t->pyr[t->cur ^ 1];
+    tbdk_pyr& Pprev = t->pyr[(t->cur + 2) % 3];
     (void)hipSetDevice(t->ctx->device);
     int rc = TBDK_OK;
 
@@ -673,6 +680,13 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
     }
     t->la_pyr = t->la_lk = false;
+    // tbd_la_pyr_side 2 (the look-ahead pyramid enqueued right after this
+    // step's critical PyrLK): mark the caller's work on s before this step
+    const bool early_pyr = next && t->ctx->opt_tbd_la_pyr_side == 2 && t->last_fit;
+    if (early_pyr) {
+        const hipError_t e = hipEventRecord(t->step_begin, s);
+        if (e != hipSuccess) return map_status(e);
+    }
     if (!la_valid) {
         rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, s);
         if (rc != TBDK_OK) return rc;
@@ -817,6 +831,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     std::vector<tbd::Track>& tracks = t->tracker->getTracks();
     int nents = 0, klt_points = 0, klt_pred = 0, lk_points = 0, nA = 0, nB = 0;
     bool merged = false;  // the unchanged and refreshed sets in one PyrLK launch
+    bool pyr_enqueued = false;  // the look-ahead pyramid already enqueued (tbd_la_pyr_side 2)
     int64_t lk_iters = 0;
     t->preds.clear();
     const bool run_klt = c.use_klt && t->have_prev && !tracks.empty();
@@ -895,16 +910,18 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         hipError_t e = wait_if_pending(s, t->post_done);
         if (e != hipSuccess) return map_status(e);
     }
-    tbdk_pyr& Pnext = Pprev;  // the look-ahead pyramid replaces the previous frame's
+    tbdk_pyr& Pnext = t->pyr[(t->cur + 1) % 3];  // the look-ahead pyramid: two frames back's buffer
     // side (ctx option tbd_la_pyr_side): built on the look-ahead stream behind
     // this step's PyrLK launches (lk_issued; they read the buffer it
     // overwrites), beside the fit, so the look-ahead PyrLK that follows it on
     // that stream needs no cross-stream edge
-    auto enqueue_next_pyr = [&](bool side) -> int {
+    auto enqueue_next_pyr = [&](bool side, bool wait = true) -> int {
         hipStream_t ps = s;
         if (side) {
             ps = t->la_s;
-            const hipError_t e = hipStreamWaitEvent(ps, t->lk_issued, 0);
+            // without the wait for this step's PyrLK: behind the caller's work
+            // on its stream before this step (the next frame's upload, say)
+            const hipError_t e = wait ? hipStreamWaitEvent(ps, t->lk_issued, 0) : wait_if_pending(ps, t->step_begin);
             if (e != hipSuccess) return map_status(e);
         }
         t->la_frame = next;
@@ -928,6 +945,15 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = launch_la(la_defer, t->la_defer_eig, Pprev, P);
             if (rc != TBDK_OK) return rc;
         }
+        // tbd_la_pyr_side 2: the look-ahead pyramid now, on the look-ahead
+        // stream with no wait: its buffer held the pyramid of two frames back,
+        // whose last readers (the previous step's PyrLK, the GFTT before it)
+        // completed before the previous step's fit, which the host synced on
+        if (early_pyr) {
+            rc = enqueue_next_pyr(true, false);
+            if (rc != TBDK_OK) return rc;
+            pyr_enqueued = true;
+        }
         STEP_MARK(3);
         if (early_order == 1) {
             rc = launch_early_gftt();
@@ -938,7 +964,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             e = wait_if_pending(s, t->la_done);
             if (e != hipSuccess) return map_status(e);
         }
-        const bool pyr_side = next && t->ctx->opt_tbd_la_pyr_side;
+        const bool pyr_side = next && !pyr_enqueued && t->ctx->opt_tbd_la_pyr_side;
         if (pyr_side) {
             e = hipEventRecord(t->lk_issued, s);
             if (e != hipSuccess) return map_status(e);
@@ -967,7 +993,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (!t->zc) e = hipMemcpyAsync(t->h_fit, t->d_fit, sizeof(FitOut) * nents, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && !by_flag) e = hipEventRecord(t->fit_done, s);
         if (e != hipSuccess) return map_status(e);
-        if (next) {  // runs on the device while this step waits for the fit and tracks
+        if (next && !pyr_enqueued) {  // runs on the device while this step waits for the fit and tracks
             rc = enqueue_next_pyr(pyr_side);
             if (rc != TBDK_OK) return rc;
         }
@@ -1264,7 +1290,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     }
     for (int sl : t->spec_list) t->spec_member[(size_t)sl] = 0;
     t->spec_list.clear();
-    t->cur ^= 1;
+    t->cur = (t->cur + 1) % 3;
+    t->last_fit = run_klt && synced;
     t->eb ^= 1;
     t->have_prev = true;
 

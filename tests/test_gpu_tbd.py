@@ -285,7 +285,7 @@ def test_tbd_deferred_lookahead_matches(gpu):
     c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=4)
     res = []
     try:
-        for d, side in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        for d, side in ((0, 0), (1, 0), (0, 1), (1, 1), (0, 2), (1, 2)):
             gpu.set_option("tbd_la_defer", d)
             gpu.set_option("tbd_la_pyr_side", side)
             loop = tbd.TbdLoop(c, ctx=gpu)
@@ -298,7 +298,7 @@ def test_tbd_deferred_lookahead_matches(gpu):
             res.append(([_mkey(m) for m in ms], loop.tracks(), mt, stepped.tracks()))
     finally:
         gpu.set_option("tbd_la_defer", 0)
-        gpu.set_option("tbd_la_pyr_side", 1)  # the default
+        gpu.set_option("tbd_la_pyr_side", 2)  # the default
     for r in res[1:]:
         assert r == res[0]
     assert res[0][0] == res[0][2]
