@@ -125,9 +125,10 @@ def ktrace_grid_us(frags, pick: str = "max_grid"):
     kernel and grid from the newest committed profiles/rNN_ktrace_grid.json
     (tools/ktrace_by_grid.py over the profiled bench run): for each kernel name
     fragment the entry of the largest grid (pick "max_grid": the 4K leg's
-    launches) or of the most dispatches (pick "most": the loop's); (sum of
-    their mean durations in us, [(kernel, grid, dispatches, avg_us)], source)
-    or (None, None, None)."""
+    launches) or of the most dispatches (pick "most": the loop's, which since
+    round 5 run beside the critical PyrLK, so their durations include that
+    overlap); (sum of their mean durations in us, [(kernel, grid, dispatches,
+    avg_us)], source) or (None, None, None)."""
     d, files = _pmc_summaries("_ktrace_grid.json")
     if not files:
         return None, None, None

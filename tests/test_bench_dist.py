@@ -308,4 +308,7 @@ def test_loop_traffic_fields_from_committed_loop_summary():
     us, used, gsrc = bench.ktrace_grid_us(["pyr_build_kernel", "pyr_down_padded_kernel"], pick="max_grid")
     assert us is not None and gsrc.endswith("_ktrace_grid.json") and len(used) == 2
     us1, used1, _ = bench.ktrace_grid_us(["pyr_build_kernel", "pyr_down_padded_kernel"], pick="most")
-    assert us1 is not None and us1 < us  # the loop's 1080p grids take less time than the 4K leg's
+    # the loop's 1080p grids (fewer threads than the 4K leg's); since round 5 the loop
+    # builds its look-ahead pyramid beside the critical PyrLK, so their durations
+    # include that overlap and are not compared with the 4K leg's
+    assert us1 is not None and us1 > 0 and all(u[1] < g[1] for u, g in zip(used1, used))
