@@ -201,6 +201,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       pyramids, so the one it overwrites is two frames old and no longer
  *       read). The look-ahead PyrLK that follows it needs no cross-stream edge
  *       (results equal).
+ *   "tbd_post_direct" (0/1, default 1): after a step that runs no post-tracker
+ *       GFTT, the next step's refreshed-set PyrLK waits for the early GFTT's
+ *       completion directly rather than through the post-tracker stream's
+ *       event (not with tbd_early_order 0; results equal).
  *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
  *       sets is launched by the next step right after its critical PyrLK
  *       instead of at the end of its own step (results equal; A/B runs).

@@ -222,6 +222,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_la_pyr_side = (int)value;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_post_direct") == 0) {
+        ctx->opt_tbd_post_direct = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_la_defer") == 0) {
         ctx->opt_tbd_la_defer = value != 0;
         return TBDK_OK;

@@ -221,6 +221,9 @@ struct tbdk_tbd {
     // caller's stream waits for `post_done` before its LK launch
     hipStream_t side = nullptr;
     hipEvent_t post_done = nullptr;
+    // what the next step's refreshed-set PyrLK waits for: post_done, or (ctx
+    // option tbd_post_direct, no post-tracker GFTT) the early GFTT's own event
+    hipEvent_t post_wait = nullptr;
     // look-ahead (tbdk_tbd_step_ahead): the next frame's pyramid, enqueued
     // behind this frame's fit (built while the host tracks), and the next
     // frame's PyrLK of the point sets this step leaves unchanged, enqueued
@@ -888,7 +891,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         // post-tracker work; when that work is already complete (the first frame
         // of a run, steps without look-ahead) both kinds of sets wait for nothing
         // and one launch of nA + nB sets replaces two back-to-back ones
-        merged = nA > 0 && nB > 0 && hipEventQuery(t->post_done) == hipSuccess;
+        merged = nA > 0 && nB > 0 && (!t->post_wait || hipEventQuery(t->post_wait) == hipSuccess);
         if (nA > 0 && !merged) {
             rc = lk_internal(t->ctx, &Pprev, &P, reinterpret_cast<const float*>(t->slot_pts),
                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
@@ -907,7 +910,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     STEP_MARK(2);
     std::fill(t->refreshed.begin(), t->refreshed.end(), 0);
     {  // the previous step's early and post-tracker GFTT (their rows) before the refreshed sets
-        hipError_t e = wait_if_pending(s, t->post_done);
+        hipError_t e = t->post_wait ? wait_if_pending(s, t->post_wait) : hipSuccess;
         if (e != hipSuccess) return map_status(e);
     }
     tbdk_pyr& Pnext = t->pyr[(t->cur + 1) % 3];  // the look-ahead pyramid: two frames back's buffer
@@ -1233,7 +1236,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // PyrLK of the point sets this leaves unchanged is enqueued after it (the
     // look-ahead PyrLK): the GFTT heads the next frame's critical path, so it is
     // queued first and the PyrLK fills the device around it.
-    if (early_launched) {
+    // tbd_post_direct: with no post-tracker GFTT the next step waits for the
+    // early GFTT's event itself (no side-stream wait and marker on the host's
+    // way to that step; not with early order 0, whose next early GFTT would
+    // re-record that event before the wait)
+    const bool post_direct = nroi == 0 && early_launched && t->ctx->opt_tbd_post_direct && early_order != 0;
+    if (early_launched && !post_direct) {
         hipError_t e = wait_if_pending(t->side, t->early_done);
         if (e != hipSuccess) return map_status(e);
     }
@@ -1254,9 +1262,12 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // post_done also after an early GFTT none of whose ROIs was used: the next
     // step's fit sync then orders that GFTT's table upload before the staging
     // table is rewritten (two steps later)
-    if (nroi > 0 || early_launched) {
+    if (post_direct) {
+        t->post_wait = t->early_done;
+    } else if (nroi > 0 || early_launched) {
         hipError_t e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
+        t->post_wait = t->post_done;
     }
     STEP_MARK(10);
     // ---- look-ahead: PyrLK of the next frame for every live track whose point
@@ -1467,6 +1478,7 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
     std::vector<int32_t> counts(4 * (size_t)t->cfg.max_tracks);  // slots and GFTT rows
     (void)hipSetDevice(t->ctx->device);
     hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work (behind the early GFTT) runs on `side`
+    if (e == hipSuccess && t->early_s) e = hipStreamSynchronize(t->early_s);  // the early GFTT rows (tbd_post_direct)
     if (e == hipSuccess) e = hipMemcpy(counts.data(), t->slot_counts, sizeof(int32_t) * counts.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return map_status(e);
     int k = 0;

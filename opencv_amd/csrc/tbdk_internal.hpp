@@ -95,6 +95,7 @@ struct tbdk_ctx {
     int opt_gftt_inline = 1;     // tbdk_ctx_set_option("gftt_inline"): GFTT ROI tables in the kernel arguments
     int opt_tbd_fit_wgpub = 1;   // tbdk_ctx_set_option("tbd_fit_wgpub"): one system-scope release per fit workgroup
     int opt_tbd_la_pyr_side = 2;  // tbdk_ctx_set_option("tbd_la_pyr_side"): where the look-ahead pyramid is built
+    int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch

@@ -285,9 +285,10 @@ def test_tbd_deferred_lookahead_matches(gpu):
     c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=4)
     res = []
     try:
-        for d, side in ((0, 0), (1, 0), (0, 1), (1, 1), (0, 2), (1, 2)):
+        for d, side, pd in ((0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 1), (0, 2, 1), (1, 2, 1), (0, 2, 0)):
             gpu.set_option("tbd_la_defer", d)
             gpu.set_option("tbd_la_pyr_side", side)
+            gpu.set_option("tbd_post_direct", pd)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
             stepped = tbd.TbdLoop(c, ctx=gpu)
@@ -299,6 +300,7 @@ def test_tbd_deferred_lookahead_matches(gpu):
     finally:
         gpu.set_option("tbd_la_defer", 0)
         gpu.set_option("tbd_la_pyr_side", 2)  # the default
+        gpu.set_option("tbd_post_direct", 1)
     for r in res[1:]:
         assert r == res[0]
     assert res[0][0] == res[0][2]
