@@ -779,6 +779,93 @@ def rank_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, n: int, script: str = None, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N rank
+    processes of this same script, one per GPU (WORLD_SIZE = N, RANK =
+    LOCAL_RANK = i, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT), as
+    torch.distributed.run would.  This process makes no GPU call and execs
+    nothing: the ranks are children, rank 0's stdout (the one JSON line) is
+    relayed, the others' stdout is dropped, stderr is inherited.  When a rank
+    fails the others are ended (their exact PIDs) and its exit code returned,
+    so a failure cannot leave the rest waiting in a barrier.  Returns the exit
+    code (0 when every rank exited 0)."""
+    import subprocess
+    import threading
+
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+
+    def relay():
+        for ln in procs[0].stdout:
+            lines.append(ln)
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(poll_s)
+    th.join(timeout=30)
+    if rc == 0 and sum(1 for ln in lines if ln.lstrip().startswith("{")) != 1:
+        print(f"bench.py: rank 0 printed {len(lines)} stdout lines, expected one JSON line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def check_world(gpus: int, world: int) -> None:
+    """--gpus N must agree with the launcher's WORLD_SIZE (torchrun sets it):
+    a mismatch would print a line whose n_gpus is not what was asked for."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (the launcher started {world} ranks); "
+                         "run `bench.py --gpus N` alone (it starts N ranks itself) or under torchrun "
+                         "with --nproc-per-node equal to --gpus")
+
+
+def gather_seeds(seed: int, world: int):
+    """Every rank's sequence seed on every rank (gloo; outside the timed region),
+    for the line: the replicas ran seeds s..s+N-1."""
+    if world <= 1:
+        return [seed]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, seed)
+    return out
+
+
 _T0 = time.perf_counter()
 
 
@@ -873,6 +960,7 @@ def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_le
 
     progress("rendering the sequence", rank)
     measure.prepare(args.seed + rank)
+    seeds = gather_seeds(args.seed + rank, world)
     progress("warm-up", rank)
     measure.warmup(args.warmup)
     if world > 1:
@@ -896,6 +984,7 @@ def run_contract(args, world: int, rank: int, measure, sync, dist_device, cpu_le
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        "rank_seeds": seeds,
     }
     progress(f"timed region: {line['value']} frames/s", rank)
     if cpu_leg is not None and rank == 0 and world == 1:
@@ -1203,6 +1292,45 @@ def pmc_bytes(kernel_substrs):
     return None
 
 
+class RehearsalMeasure:
+    """Stands in for TbdMeasure in `--rehearse` runs (no GPU): records its
+    seed, sleeps `ms` per step."""
+
+    def __init__(self, ms: float):
+        self.ms, self.seed = ms, None
+
+    def prepare(self, seed: int):
+        self.seed = seed
+
+    def warmup(self, w: int):
+        time.sleep(self.ms * w / 1000.0)
+
+    def timed(self, k: int):
+        time.sleep(self.ms * k / 1000.0)
+        return [None] * k
+
+
+def rehearse(args, world: int, rank: int):
+    """The contract (rank group, seeds, barriers, max-over-ranks time, one line
+    on rank 0) with RehearsalMeasure instead of the GPU loop; rank r is
+    (1 + r) times slower, so the job time is the last rank's."""
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = RehearsalMeasure(args.rehearse * (1 + rank))
+    line, _ = run_contract(args, world, rank, m, lambda: None, "cpu", cpu_leg=None)
+    line.update({"dtype": "u8", "data": "rehearsal (no GPU work: each step sleeps)",
+                 "config": {"workload": "bench.py --rehearse", "parallelism": f"replicas x{world}"}})
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return line
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1267,7 +1395,18 @@ def main(argv=None):
     ap.add_argument("--hog-width", type=int, default=1920)
     ap.add_argument("--hog-height", type=int, default=1080)
     ap.add_argument("--hog-frames", type=int, default=60)
+    ap.add_argument("--rehearse", type=float, default=None, metavar="MS_PER_STEP",
+                    help="rehearse the multi-rank contract with no GPU: every step of rank r sleeps "
+                         "MS_PER_STEP x (1 + r) ms (tests/test_bench_dist.py); the line says data: rehearsal")
     args = ap.parse_args(argv)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process starts the N ranks itself (before any GPU call)
+        raise SystemExit(spawn_ranks(argv, args.gpus))
+    world, rank, local = rank_env()
+    check_world(args.gpus, world)
+    if args.rehearse is not None:
+        return rehearse(args, world, rank)
     if args.no_secondary:
         args.no_step_api = args.no_h2d = args.no_kitti = args.no_farneback = args.no_f16 = args.no_hog = True
         args.no_dense = True
@@ -1275,7 +1414,6 @@ def main(argv=None):
         args.no_copy_peak = True
         args.repeats = 0
 
-    world, rank, local = rank_env()
     full_affinity = os.sched_getaffinity(0)
     pin = {"pinned": False, "reason": "--no-pin"} if args.no_pin else pin_rank(local)  # before any GPU call
 

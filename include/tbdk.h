@@ -220,7 +220,7 @@ int tbdk_ctx_device(const tbdk_ctx* ctx);
  * enable != 0 starts recording (clears previous records). */
 int tbdk_timing_enable(tbdk_ctx* ctx, int enable);
 /* Synchronises the recorded events and returns, for kernel `name`
- * ("pyr_build", "lk_sparse", ...), the number of launches and the summed
+ * ("pyr_build", "lk_sparse", "lk_dense" (tbdk_lk_dense), ...), the number of launches and the summed
  * device milliseconds. */
 int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 /* Restrict recording to the comma-separated kernel names in `names` (NULL or
@@ -779,6 +779,13 @@ int tbdk_app_default_args(tbdk_app_args* args);
 int tbdk_app_run(const tbdk_app_args* args, tbdk_app_result* result);
 
 int tbdk_tbd_default_config(int width, int height, tbdk_tbd_config* cfg);
+/* Loops on one context share the context's three side streams (post-tracker
+ * GFTT, look-ahead PyrLK, early GFTT), created by its first loop: loops
+ * stepped concurrently from different host threads on one context serialise
+ * their off-critical work on them, and tbdk_tbd_destroy / tbdk_tbd_tracks
+ * synchronise those streams, so they also wait for the other loops' work.
+ * Use one context per concurrently stepped loop (the bench runs one loop per
+ * GPU and process), and destroy every loop before its context. */
 int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out);
 int tbdk_tbd_destroy(tbdk_tbd* tbd);
 /* One frame through the loop.  frame: device u8 (width x height, pitch);

@@ -12,8 +12,11 @@
 #include <vector>
 namespace tbdk {
 
-// K -> int; the capacity (a power of two) must exceed the largest number of
-// live entries (the loop sizes it to 4x its track capacity)
+// K -> int; the capacity is a power of two, sized by the loop to 4x its
+// track capacity.  An insert that would fill more than half of it doubles the
+// table first (a rehash: pointers from find() do not survive an insert), so a
+// load the sizing did not foresee costs a rehash instead of a probe that
+// never meets an empty slot.
 template <class K>
 class FlatMap {
 public:
@@ -36,6 +39,7 @@ public:
     // emplace semantics: false (value untouched) when k is present
     bool insert(K k, int v)
     {
+        reserve_one();
         size_t i = home(k);
         for (; used_[i]; i = (i + 1) & mask_)
             if (keys_[i] == k) return false;
@@ -47,6 +51,7 @@ public:
     }
     void set(K k, int v)
     {
+        reserve_one();
         size_t i = home(k);
         for (; used_[i]; i = (i + 1) & mask_)
             if (keys_[i] == k) {
@@ -88,6 +93,29 @@ public:
     size_t capacity() const { return mask_ + 1; }
 
 private:
+    void reserve_one()
+    {
+        if (2 * (size_ + 1) <= mask_ + 1) return;
+        std::vector<K> ok;
+        std::vector<int> ov;
+        std::vector<uint8_t> ou;
+        ok.swap(keys_);
+        ov.swap(vals_);
+        ou.swap(used_);
+        const size_t cap = 2 * ok.size();
+        keys_.assign(cap, K());
+        vals_.assign(cap, 0);
+        used_.assign(cap, 0);
+        mask_ = cap - 1;
+        for (size_t j = 0; j < ok.size(); ++j) {
+            if (!ou[j]) continue;
+            size_t i = home(ok[j]);
+            while (used_[i]) i = (i + 1) & mask_;
+            keys_[i] = ok[j];
+            vals_[i] = ov[j];
+            used_[i] = 1;
+        }
+    }
     size_t home(K k) const
     {
         uint64_t x = (uint64_t)k;

@@ -620,7 +620,7 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
         a.flow_pitch = dense->flow_pitch;
         a.dstatus = dense->status;
         a.dstatus_pitch = dense->status_pitch;
-        int rec = timing_begin(ctx, "lk_sparse", s);
+        int rec = timing_begin(ctx, "lk_dense", s);
         hipError_t e = launch_lk_multi_dense(a, s);
         timing_end(ctx, rec, s);
         return map_err(e);

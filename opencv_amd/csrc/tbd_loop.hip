@@ -168,6 +168,15 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
         // stores (each release writes the XCD's L2 back)
         if (flag && !wg_pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
+    // wg_pub: every wave waits until its own global stores (compacted slot
+    // points, slot count) are acknowledged by the L2 before the workgroup
+    // barrier, so wave 0's single system-scope release after it (an L2
+    // write-back of every dirty line) covers all eight waves' stores.  Without
+    // this wait a wave's stores could still be in flight when the release runs:
+    // the barrier orders the waves at workgroup scope only.  The look-ahead
+    // PyrLK on another stream reads them once the host sees the flag, with no
+    // kernel boundary in between.
+    if (flag && wg_pub) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     if (flag) {
         // publish: after the workgroup's barrier one thread counts the
         // workgroup's results at system scope; the last workgroup resets the

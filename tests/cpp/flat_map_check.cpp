@@ -47,8 +47,32 @@ static int check(unsigned seed, K span, size_t live_max)
     return 0;
 }
 
+// a table sized for far fewer entries than it receives grows instead of
+// probing forever: 16 slots, 5000 live keys, then erase them all
+static int check_growth()
+{
+    tbdk::FlatMap<unsigned> fm(16);
+    for (unsigned k = 0; k < 5000; ++k) {
+        if (!fm.insert(k * 7919u, (int)k)) return 6;
+        fm.set(k * 7919u + 1u, -(int)k);
+    }
+    if (fm.size() != 10000 || fm.capacity() < 20000) return 7;
+    for (unsigned k = 0; k < 5000; ++k) {
+        const int* p = fm.find(k * 7919u);
+        const int* q = fm.find(k * 7919u + 1u);
+        if (!p || *p != (int)k || !q || *q != -(int)k) return 8;
+    }
+    for (unsigned k = 0; k < 5000; ++k)
+        if (!fm.erase(k * 7919u) || !fm.erase(k * 7919u + 1u)) return 9;
+    return fm.size() == 0 && !fm.find(7919u) ? 0 : 10;
+}
+
 int main()
 {
+    if (const int g = check_growth()) {
+        std::printf("FAIL growth code %d\n", g);
+        return 1;
+    }
     for (unsigned s = 1; s <= 4; ++s) {
         int r = check<unsigned>(s, 600u, 256);  // track ids, dense collisions
         if (!r) r = check<unsigned long long>(s + 10, 1ull << 40, 1024);  // box keys, sparse

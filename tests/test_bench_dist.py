@@ -312,3 +312,82 @@ def test_loop_traffic_fields_from_committed_loop_summary():
     # builds its look-ahead pyramid beside the critical PyrLK, so their durations
     # include that overlap and are not compared with the 4K leg's
     assert us1 is not None and us1 > 0 and all(u[1] < g[1] for u, g in zip(used1, used))
+
+
+def _json_lines(out):
+    import json
+
+    return [json.loads(ln) for ln in out.splitlines() if ln.lstrip().startswith("{")]
+
+
+def test_main_gpus_2_starts_two_ranks(monkeypatch, capsys):
+    """`bench.py --gpus 2` with no launcher starts two rank
+    processes itself (gloo group, no GPU in --rehearse mode) and relays rank
+    0's single line: n_gpus 2, seeds s and s+1, value = the steps of both
+    ranks / the slower rank's time."""
+    import pytest
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "2", "--steps", "10", "--warmup", "2", "--seed", "500", "--rehearse", "10"])
+    assert e.value.code == 0
+    lines = _json_lines(capsys.readouterr().out)
+    assert len(lines) == 1
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["rank_seeds"] == [500, 501] and ln["steps"] == 10
+    el = ln["ms_per_step"] * 10 / 1000.0
+    assert el >= 0.2  # rank 1 sleeps 2 x 10 ms per step
+    assert abs(ln["value"] - 2 * 10 / el) < 0.01 * ln["value"]
+    assert ln["data"].startswith("rehearsal")
+
+
+def test_gpus_world_size_mismatch_fails(monkeypatch):
+    import pytest
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "1", "--rehearse", "1"])
+    assert e.value.code and "WORLD_SIZE=2" in str(e.value.code)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "4", "--rehearse", "1"])
+    assert e.value.code and "--gpus 4" in str(e.value.code)
+
+
+def test_spawn_ranks_ends_the_job_when_a_rank_fails(tmp_path):
+    """A rank that fails ends the job with its exit code; the rank still
+    running (here: sleeping, as one waiting in a barrier would) is ended."""
+    import time
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    s = tmp_path / "r.py"
+    s.write_text("import os, sys, time\n"
+                 "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
+                 "time.sleep(600)\n")
+    t0 = time.time()
+    assert bench.spawn_ranks([], 2, script=str(s)) == 3
+    assert time.time() - t0 < 60
+
+
+def test_torchrun_gpus_2_matches_launcher(tmp_path):
+    """The driver's N > 1 form: torch.distributed.run --nproc-per-node 2 ...
+    bench.py --gpus 2 (WORLD_SIZE from the launcher, no self-spawn)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",
+                        "--rehearse", "5"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and len(lines[0]["rank_seeds"]) == 2

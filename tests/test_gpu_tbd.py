@@ -252,7 +252,11 @@ def test_tbd_zero_copy_matches_copies(gpu):
 
 def test_tbd_fit_flag_matches_event(gpu):
     """Fit completion published by the fit kernel's system-scope flag (default)
-    and by an event behind the fit give the same frames."""
+    and by an event behind the fit give the same frames; with the flag, one
+    release per fit workgroup (tbd_fit_wgpub 1, the default: every wave's
+    stores acknowledged before the barrier) and one per wave (0) agree too,
+    with and without the look-ahead pyramid on the look-ahead stream (where
+    the speculative PyrLK has no stream edge to the fit)."""
     from opencv_amd import klt, tbd
 
     W, H, N, F = 960, 540, 32, 12
@@ -261,14 +265,19 @@ def test_tbd_fit_flag_matches_event(gpu):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
     res = []
     try:
-        for fl in (1, 0):
+        for fl, wg, side in ((1, 1, 2), (0, 1, 2), (1, 0, 2), (1, 1, 0), (1, 0, 0)):
             gpu.set_option("tbd_fit_flag", fl)
+            gpu.set_option("tbd_fit_wgpub", wg)
+            gpu.set_option("tbd_la_pyr_side", side)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
             res.append(([_mkey(m) for m in ms], loop.tracks()))
     finally:
         gpu.set_option("tbd_fit_flag", 1)
-    assert res[0] == res[1]
+        gpu.set_option("tbd_fit_wgpub", 1)
+        gpu.set_option("tbd_la_pyr_side", 2)
+    for r in res[1:]:
+        assert r == res[0]
 
 
 def test_tbd_deferred_lookahead_matches(gpu):
