@@ -183,9 +183,14 @@ __device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p,
 // threshold-independent half of the reference's threshold + 3x3 dilate test)
 // into lm.  S0 = the SUM the walk started from; Scap = the SUM before row
 // ycap (the next segment's fresh-start row); S = the SUM after the last row.
+// Compact (GfttArgs::compact): no eigenvalue plane; with each row's
+// local-maximum ballot, the values of its set lanes only, in lane order, at the
+// start of the strip row's own columns (column ccol + rank of the lane's bit),
+// which is all gftt_select reads when quality <= 1 (see there).
+template <bool compact>
 __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, uint64_t* __restrict__ lm,
                                             int w, int ep, int y0, int y1, int ys, int ye, int ycap, bool fresh,
-                                            double (&S)[3], double (&S0)[3], double (&Scap)[3], int& best)
+                                            double (&S)[3], double (&S0)[3], double (&Scap)[3], int& best, int ccol)
 {
     const int H = g.H;
     auto pix = [&](int yy) { return eig_ld(g, refl(yy, H)); };
@@ -242,7 +247,8 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
         const float t = aa - cc;
         const float e = (aa + cc) - sqrtf(bb * bb + t * t);
         if (ST || store) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), rE, eoff == kDrop ? kDrop : eoff + (uint32_t)(y * ep * 4), 0, 0);
+            if constexpr (!compact)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), rE, eoff == kDrop ? kDrop : eoff + (uint32_t)(y * ep * 4), 0, 0);
             const int kk = fkey(e);
             best = (g.out_lane && kk > best) ? kk : best;
         }
@@ -251,10 +257,17 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
             m = fmaxf(m, fmaxf(from_left(e2), from_right(e2)));
             m = fmaxf(m, fmaxf(from_left(e1), from_right(e1)));
             m = fmaxf(m, fmaxf(from_left(e), from_right(e)));
-            const uint64_t bal = __ballot(x_in && e1 >= m);
+            const bool lmax = x_in && e1 >= m;
+            const uint64_t bal = __ballot(lmax);
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 bv = {(unsigned)bal, (unsigned)(bal >> 32)};
             __builtin_amdgcn_raw_buffer_store_b64(bv, rL, lane == 0 ? (uint32_t)((y - 1) * 8) : kDrop, 0, 0);
+            if constexpr (compact) {  // row y - 1's candidates, packed in lane order
+                const uint32_t rk =
+                    __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e1), rE,
+                                                      lmax ? (uint32_t)(((y - 1) * ep + ccol + (int)rk) * 4) : kDrop, 0, 0);
+            }
         }
         e2 = e1;
         e1 = e;
@@ -339,6 +352,8 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     // local-maximum words of this strip (ROIs of at least 3x3; never written otherwise)
     uint64_t* lm = a.lmax + R.moff + (size_t)strip * H;
     const bool has_lm = R.w >= 3 && H >= 3;
+    const bool compact = a.compact != 0;
+    const int ccol = strip * kGfttStrip;  // the strip's first output column
 
     const int L = (H + kEigWaves - 1) / kEigWaves;  // own rows per segment
     const int y0 = wv * L, y1 = min(H, y0 + L);
@@ -366,7 +381,12 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     };
     GFTT_ESTAMP(0);
     if (live) {
-        eig_segment(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0, Scap, best);
+        if (compact)
+            eig_segment<true>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0,
+                              Scap, best, ccol);
+        else
+            eig_segment<false>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0,
+                               Scap, best, ccol);
         if (ycap >= 0) {
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -394,7 +414,12 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         __syncthreads();  // s_cap is rewritten below
         if (wv >= bad && live) {
             best = INT_MIN;
-            eig_segment(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S, S0, Scap, best);
+            if (compact)
+                eig_segment<true>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S,
+                                  S0, Scap, best, ccol);
+            else
+                eig_segment<false>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S,
+                                   S0, Scap, best, ccol);
             if (ycap >= 0) {
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -896,6 +921,9 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                 if (y < 1 || y > R.h - 2) continue;
                 uint64_t word = wi == tid ? word0 : a.lmax[R.moff + wi];
                 const float* Er = Ep + (size_t)y * gftt_epitch(R.w) + st * kGfttStrip - kGfttHalo;
+                // compact: the word's values packed in bit order at the strip row's first columns
+                const float* Ec = Er + kGfttHalo;
+                int rk = 0;
                 while (word) {  // up to 8 value loads in flight per round
                     int xs[8];
                     float vs[8];
@@ -905,7 +933,7 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                         if (word) {
                             xs[u] = __builtin_ctzll(word);
                             word &= word - 1ull;
-                            vs[u] = Er[xs[u]];
+                            vs[u] = a.compact ? Ec[rk++] : Er[xs[u]];
                         }
                     }
 #pragma unroll
@@ -917,7 +945,9 @@ __global__ __launch_bounds__(kSelThreads) void gftt_select_kernel(GfttArgs a)
                     }
                 }
             }
-        } else {
+        } else if (!a.compact) {
+            // (compact mode runs with quality <= 1 only: thr = max * q >= max when
+            // max <= 0, so no value exceeds thr and the ROI has no candidate)
             const int iw = R.w - 2, n = iw * (R.h - 2), ep = gftt_epitch(R.w);
             for (int p = tid; p < n; p += kSelThreads) {
                 const int y = p / iw + 1, x = p - (y - 1) * iw + 1;

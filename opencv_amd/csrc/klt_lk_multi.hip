@@ -87,13 +87,15 @@ __device__ __forceinline__ uint32_t seg_total(uint32_t scanned, int e4, int s4)
 // 31 wide), exact as a modulo-2^32 difference of plain scans, and its int ->
 // float conversion is the same single rounding.
 template <int N>
-__device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N])
+__device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N], bool* split = nullptr)
 {
     static_assert(N >= 1 && N <= 3, "three 11-bit fields per packed scan");
     bool big = false;
 #pragma unroll
     for (int k = 0; k < N; ++k) big |= (uint32_t)v[k] + (1u << 26) >= (1u << 27);
-    if (__builtin_amdgcn_ballot_w64(big) == 0) {  // wave-uniform
+    const bool slow = __builtin_amdgcn_ballot_w64(big) != 0;  // wave-uniform
+    if (split) *split = slow;
+    if (!slow) {
         uint32_t sv[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) sv[k] = (uint32_t)v[k];
@@ -202,8 +204,12 @@ constexpr int kMultiWaves = TBDK_LK_MULTI_WAVES;
 // the launch's point-list key, Newton steps | reloads << 16 | max iters << 32,
 // then 16 u32 phase stamps (ticks after start): per level L, [4L] its start,
 // [4L+1] the setup's G sums done, [4L+2] the first J window loaded (the probe
-// waits for it there), [4L+3] its Newton steps done; [12] the error pass done.
-// Not in the product library.
+// waits for it there), [4L+3] its Newton steps done; [12] the error pass done;
+// [13] the point's coordinates arrived (start: the wave's first instruction),
+// [14] the first level's source rows arrived (FLY; the probe waits for them
+// there), [15] its window terms done (before the G sums); bits 48.. of the
+// steps word: the levels whose G sums took seg_sum_exact's split path.  Not in
+// the product library.
 #ifdef TBDK_LK_TRACE
 __device__ unsigned long long* g_lk_trace;
 __device__ unsigned int g_lk_trace_cap;
@@ -246,12 +252,44 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     const int k = lane == 0 ? P : (lane - 1) / WW;
     const int x = k < P ? lane - 1 - k * WW : 0;
     const int wave = xcd_swizzle(blockIdx.x, gridDim.x) * kMultiWaves + (threadIdx.x >> 6);
-    const int i = k >= P ? -1 : DENSE ? (wave * P + k < a.n ? wave * P + k : -1) : seg_point(a, wave * P + k);
+    // the point's index in a segmented list (seg_point) and its coordinates: the
+    // segment's count and the point are loaded together, the point speculatively
+    // (index s * stride + j lies inside segment s's stride-sized row of the
+    // loop's point buffers whether or not j < count), so a wave's start pays one
+    // memory round trip before its first level's rows, not two
+#ifdef TBDK_LK_TRACE
+    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();  // the wave's first instruction
+#endif
+    int i = -1;
+    float p0x = 0.f, p0y = 0.f;
+    if constexpr (DENSE) {
+        i = k < P && wave * P + k < a.n ? wave * P + k : -1;
+    } else {
+        const int kk = wave * P + k;
+        if (k < P && kk < a.n) {
+            if (!a.seg_counts) {
+                i = kk;
+                p0x = a.prev_pts[2 * i];
+                p0y = a.prev_pts[2 * i + 1];
+            } else {
+                const int seg = kk / a.seg_stride, j = kk - seg * a.seg_stride;
+                const int s = a.seg_ninl > 0 ? (int)a.seg_inl[seg] : a.seg_list ? a.seg_list[seg] : seg;
+                const int cand = s * a.seg_stride + j;
+                const int cnt = a.seg_counts[s];
+                const float cx = a.prev_pts[2 * cand], cy = a.prev_pts[2 * cand + 1];
+                if (j < cnt) {
+                    i = cand;
+                    p0x = cx;
+                    p0y = cy;
+                }
+            }
+        }
+    }
     const bool valid = i >= 0;
     if (!any_lane(valid)) return;  // wave-uniform
 #ifdef TBDK_LK_TRACE
-    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
     int tr_steps = 0, tr_reloads = 0;
+    unsigned tr_gsplit = 0;  // levels whose G sums took seg_sum_exact's split path
     auto tr_stamp = [&](int idx) {
         const unsigned r = a.trace_base + (unsigned)wave;
         const unsigned d = (unsigned)(__builtin_amdgcn_s_memrealtime() - tr_t0);
@@ -260,6 +298,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #else
     auto tr_stamp = [](int) {};
 #endif
+#ifdef TBDK_LK_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the point's coordinates have arrived
+    tr_stamp(13);
+#endif
     const int e4 = 4 * (k * WW + WW), s4 = 4 * (k * WW);  // last lane of the point, lane before its first
     const int rnd9 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 5 - 1));
     const int rnd14 = __builtin_amdgcn_readfirstlane(1 << (W_BITS1 - 1));
@@ -267,8 +309,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     const float FLT_SCALE = 1.f / (1 << 20);
     const float halfx = (WW - 1) * 0.5f, halfy = (WH - 1) * 0.5f;
     const int gy = DENSE && valid ? i / a.dense_w : 0, gx = DENSE && valid ? i - gy * a.dense_w : 0;  // DENSE: the pixel
-    const float p0x = DENSE ? (float)gx : valid ? a.prev_pts[2 * i] : 0.f;
-    const float p0y = DENSE ? (float)gy : valid ? a.prev_pts[2 * i + 1] : 0.f;
+    if constexpr (DENSE) {
+        p0x = (float)gx;
+        p0y = (float)gy;
+    }
     float outx = 0.f, outy = 0.f;
     if ((a.flags & TBDK_OPTFLOW_USE_INITIAL_FLOW) && valid) {
         outx = a.next_pts[2 * i];
@@ -397,6 +441,10 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 uint32_t u[WH + 3];
 #pragma unroll
                 for (int r = 0; r < WH + 3; ++r) u[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);
+#ifdef TBDK_LK_TRACE
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the level's source rows have arrived
+                if (level == a.max_level) tr_stamp(14);
+#endif
                 // Outside the level the derivative planes hold BORDER_CONSTANT 0
                 // (lkpyramid.cpp:1357).  A zero derivative contributes nothing to the
                 // bilinear sums, so the rule is applied to the derivative weights:
@@ -507,9 +555,20 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #pragma unroll
                 for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(ipk[q]));
             }
+#ifdef TBDK_LK_TRACE
+            __builtin_amdgcn_sched_barrier(0);
+            if (level == a.max_level) tr_stamp(15);  // the first level's window terms done (before the G sums)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             if (k >= P) acc[0] = acc[1] = acc[2] = 0;
             float s[3];
+#ifdef TBDK_LK_TRACE
+            bool tr_split = false;
+            seg_sum_exact<3>(acc, e4, s4, s, &tr_split);
+            tr_gsplit |= tr_split ? 1u << level : 0u;
+#else
             seg_sum_exact<3>(acc, e4, s4, s);
+#endif
             tr_stamp(4 * level + 1);
             // J columns at the first Newton position, loaded after the G sums (with
             // the loads in flight during the sums the kernel needs 148 VGPRs, 3
@@ -721,7 +780,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                                       : (unsigned long long)(uintptr_t)(a.seg_list ? (const void*)a.seg_list
                                                                                    : (const void*)a.prev_pts);
                 o[5] = (unsigned)tr_steps | ((unsigned long long)(unsigned)tr_reloads << 16) |
-                       ((unsigned long long)(unsigned)mx << 32);
+                       ((unsigned long long)(unsigned)mx << 32) | ((unsigned long long)tr_gsplit << 48);
             }
         }
     }

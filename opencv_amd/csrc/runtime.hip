@@ -43,7 +43,8 @@ static bool timing_selected(const std::string& only, const char* name)
 
 int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
 {
-    if (!ctx->timing) return -1;
+    if (!ctx->timing.load(std::memory_order_relaxed)) return -1;
+    std::lock_guard<std::mutex> lk(ctx->timing_mu);
     if (!ctx->timing_only.empty() && !timing_selected(ctx->timing_only, name)) return -1;
     int64_t* calls = nullptr;
     for (auto& c : ctx->timing_calls)
@@ -66,7 +67,12 @@ int timing_begin(tbdk_ctx* ctx, const char* name, hipStream_t s)
 void timing_end(tbdk_ctx* ctx, int rec, hipStream_t s)
 {
     if (rec < 0) return;
-    (void)hipEventRecord(ctx->recs[rec].end, s);
+    hipEvent_t end;
+    {
+        std::lock_guard<std::mutex> lk(ctx->timing_mu);
+        end = ctx->recs[rec].end;
+    }
+    (void)hipEventRecord(end, s);
 }
 
 static int map_err(hipError_t e)
@@ -138,6 +144,7 @@ int tbdk_timing_enable(tbdk_ctx* ctx, int enable)
 {
     if (!ctx) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
+    std::lock_guard<std::mutex> lk(ctx->timing_mu);
     for (auto& r : ctx->recs) {
         ctx->free_events.push_back(r.begin);
         ctx->free_events.push_back(r.end);
@@ -230,6 +237,14 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_la_defer = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "gftt_compact") == 0) {
+        ctx->opt_gftt_compact = value != 0;
+        return TBDK_OK;
+    }
+    if (std::strcmp(name, "tbd_async_la") == 0) {
+        ctx->opt_tbd_async_la = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "gftt_inline") == 0) {
         ctx->opt_gftt_inline = value != 0;
         return TBDK_OK;
@@ -275,6 +290,7 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
 int tbdk_timing_select(tbdk_ctx* ctx, const char* names)
 {
     if (!ctx) return TBDK_EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->timing_mu);
     ctx->timing_only.clear();
     if (names && *names) {
         ctx->timing_only = ",";
@@ -289,6 +305,7 @@ int tbdk_timing_query(tbdk_ctx* ctx, const char* name, int64_t* launches, double
 {
     if (!ctx || !name) return TBDK_EINVAL;
     DeviceGuard g(ctx->device);
+    std::lock_guard<std::mutex> lk(ctx->timing_mu);
     int64_t cnt = 0;
     double tot = 0.0;
     for (auto& r : ctx->recs) {
@@ -310,6 +327,7 @@ int tbdk_timing_calls(tbdk_ctx* ctx, const char* name, int64_t* calls)
 {
     if (!ctx || !name || !calls) return TBDK_EINVAL;
     *calls = 0;
+    std::lock_guard<std::mutex> lk(ctx->timing_mu);
     for (auto& c : ctx->timing_calls)
         if (c.first == name) *calls = c.second;
     return TBDK_OK;
@@ -792,6 +810,7 @@ int gftt_launch(tbdk_ctx* ctx, GfttScratch& sc, const uint8_t* img, int pitch, c
     a.corner_stride = corner_stride ? corner_stride : p->max_corners;
     a.counts = counts;
     a.eig_redo = ctx->opt_gftt_eig_redo;
+    a.compact = ctx->opt_gftt_compact && p->quality_level <= 1.0 && !gftt_generic(p) ? 1 : 0;
     a.ninl = 0;
     if (h_rois && ctx->opt_gftt_inline && plan.nroi <= kGfttInline) {  // the table into the kernel arguments
         bool fits = true;

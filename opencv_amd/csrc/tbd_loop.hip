@@ -27,13 +27,16 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <new>
 #include <queue>
+#include <thread>
 #include <vector>
 
 #include "box_fit.hpp"
@@ -199,12 +202,98 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
     }
 }
 
+// The loop's launch worker (ctx option tbd_async_la): a host thread that issues
+// the look-ahead PyrLK launches (the speculative one after the fit sync, the
+// post-tracker one at the end of the step) while the loop's own thread goes on
+// with the tracker step and the next frame.  Those launches feed no result back
+// to the host within the step, so each is a job handed over in FIFO order; the
+// loop drains the queue (waits for every posted job) before any host call that
+// depends on what a job enqueued: a wait on la_done, a launch on the look-ahead
+// stream, the end of a public call.  A HIP launch costs 2.4-3.4 us of host time
+//  and the speculative block ~6-14 us, all of it on the frame's
+// host chain between the fit and the next critical PyrLK launch.
+class LaunchWorker {
+public:
+    explicit LaunchWorker(int device) : device_(device), th_([this] { run(); }) {}
+    ~LaunchWorker()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    // queue f (runs on the worker, in posting order)
+    void post(std::function<int()> f)
+    {
+        while (head_.load(std::memory_order_relaxed) - tail_.load(std::memory_order_acquire) >= kJobs)
+            __builtin_ia32_pause();
+        jobs_[head_.load(std::memory_order_relaxed) % kJobs] = std::move(f);
+        head_.fetch_add(1, std::memory_order_seq_cst);  // seq_cst pair with run()'s sleeping_ / head_
+        if (sleeping_.load(std::memory_order_seq_cst)) {
+            std::lock_guard<std::mutex> lk(mu_);
+            cv_.notify_one();
+        }
+    }
+    // wait until every posted job has run; the first error since the last drain
+    int drain()
+    {
+        while (tail_.load(std::memory_order_acquire) != head_.load(std::memory_order_relaxed)) __builtin_ia32_pause();
+        return err_.exchange(TBDK_OK);
+    }
+
+private:
+    static constexpr unsigned kJobs = 8;
+    static constexpr double kSpinUs = 1000.0;  // spin this long for the next job, then sleep
+    void run()
+    {
+        (void)hipSetDevice(device_);
+        using clk = std::chrono::steady_clock;
+        auto idle0 = clk::now();
+        for (;;) {
+            const unsigned tl = tail_.load(std::memory_order_relaxed);
+            if (head_.load(std::memory_order_acquire) != tl) {
+                const int r = jobs_[tl % kJobs]();
+                jobs_[tl % kJobs] = nullptr;
+                if (r != TBDK_OK) {
+                    int ok = TBDK_OK;
+                    err_.compare_exchange_strong(ok, r);
+                }
+                tail_.store(tl + 1, std::memory_order_release);
+                idle0 = clk::now();
+                continue;
+            }
+            if (std::chrono::duration<double, std::micro>(clk::now() - idle0).count() < kSpinUs) {
+                for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+                continue;
+            }
+            std::unique_lock<std::mutex> lk(mu_);
+            sleeping_.store(true, std::memory_order_seq_cst);
+            cv_.wait(lk, [&] { return stop_ || head_.load(std::memory_order_seq_cst) != tail_.load(std::memory_order_relaxed); });
+            sleeping_.store(false, std::memory_order_relaxed);
+            if (stop_ && head_.load(std::memory_order_acquire) == tail_.load(std::memory_order_relaxed)) return;
+            idle0 = clk::now();
+        }
+    }
+    int device_;
+    std::function<int()> jobs_[kJobs];
+    std::atomic<unsigned> head_{0}, tail_{0};
+    std::atomic<int> err_{TBDK_OK};
+    std::atomic<bool> sleeping_{false};
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+    std::thread th_;  // last: started once the members above exist
+};
+
 }  // namespace tbdk
 
 using namespace tbdk;
 
 struct tbdk_tbd {
     tbdk_ctx* ctx = nullptr;
+    LaunchWorker* worker = nullptr;  // ctx option tbd_async_la (read by tbdk_tbd_create)
     tbdk_tbd_config cfg;
     // three pyramids in rotation: this frame's (cur), the previous frame's and
     // the look-ahead frame's, so the look-ahead build never overwrites a
@@ -361,9 +450,26 @@ inline uint64_t box_key(int x, int y, int w, int h)
            (uint64_t)(uint16_t)h;
 }
 
+// the launch worker's queue drained (a no-op without the worker): the first
+// error of a posted job, else TBDK_OK
+inline int drain(tbdk_tbd* t) { return t->worker ? t->worker->drain() : TBDK_OK; }
+
+// run f now, or (launch worker) post it
+inline int run_or_post(tbdk_tbd* t, std::function<int()> f)
+{
+    if (!t->worker) return f();
+    t->worker->post(std::move(f));
+    return TBDK_OK;
+}
+
 int release(tbdk_tbd* t)
 {
     if (!t) return TBDK_OK;
+    if (t->worker) {  // every posted launch issued before the streams are synchronised
+        (void)t->worker->drain();
+        delete t->worker;
+        t->worker = nullptr;
+    }
     if (t->side) (void)hipStreamSynchronize(t->side);
     if (t->post_done) (void)hipEventDestroy(t->post_done);
     if (t->fit_done) (void)hipEventDestroy(t->fit_done);
@@ -592,6 +698,13 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->slot_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
     t->npts_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
     t->erow_of = FlatMap<uint64_t>(4 * (size_t)cfg->max_tracks);
+    if (ctx->opt_tbd_async_la) {
+        t->worker = new (std::nothrow) LaunchWorker(ctx->device);
+        if (!t->worker) {
+            release(t);
+            return TBDK_ENOMEM;
+        }
+    }
     rc = gftt_reserve(t->gftt, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc == TBDK_OK) rc = gftt_reserve(t->gftt2, ctx->device, cfg->max_tracks, (int64_t)cfg->width * cfg->height * 2);
     if (rc != TBDK_OK) {
@@ -688,6 +801,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
     }
     if (had_la_lk && !la_valid) {  // discarded: it may still read the pyramid about to be rebuilt
+        rc = drain(t);
+        if (rc != TBDK_OK) return rc;
         hipError_t e = wait_if_pending(s, t->la_done);
         if (e != hipSuccess) return map_status(e);
     }
@@ -858,18 +973,25 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // the look-ahead PyrLK of the n unchanged sets in h_la, pyramid A -> B, on
     // la_s behind the look-ahead pyramid and (eig) the post-tracker GFTT's
     // eigenvalue kernel
+    // (launch worker: posted; h_la, la_ready and eig_done are rewritten only
+    // after a drain)
     auto launch_la = [&](int n, bool eig, tbdk_pyr& A, tbdk_pyr& B) -> int {
-        hipStream_t ls = t->la_s;
-        hipError_t e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
-        if (e == hipSuccess && eig) e = wait_if_pending(ls, t->eig_done);
-        if (e == hipSuccess && !t->zc)
-            e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
-        if (e != hipSuccess) return map_status(e);
-        const int r = lk_internal(t->ctx, &A, &B, reinterpret_cast<const float*>(t->slot_pts),
-                                  reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                  n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la, nullptr, t->h_la);
-        if (r != TBDK_OK) return r;
-        return map_status(hipEventRecord(t->la_done, ls));
+        const bool wait_ready = t->la_stream != t->la_s;
+        tbdk_pyr* pa = &A;
+        tbdk_pyr* pb = &B;
+        return run_or_post(t, [t, n, eig, wait_ready, lp, pa, pb]() -> int {
+            hipStream_t ls = t->la_s;
+            hipError_t e = wait_ready ? wait_if_pending(ls, t->la_ready) : hipSuccess;
+            if (e == hipSuccess && eig) e = wait_if_pending(ls, t->eig_done);
+            if (e == hipSuccess && !t->zc)
+                e = hipMemcpyAsync(t->d_la, t->h_la, sizeof(int32_t) * n, hipMemcpyHostToDevice, ls);
+            if (e != hipSuccess) return map_status(e);
+            const int r = lk_internal(t->ctx, pa, pb, reinterpret_cast<const float*>(t->slot_pts),
+                                      reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
+                                      n * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_la, nullptr, t->h_la);
+            if (r != TBDK_OK) return r;
+            return map_status(hipEventRecord(t->la_done, ls));
+        });
     };
     // the previous step's deferred look-ahead PyrLK (ctx option tbd_la_defer),
     // launched below once this step's critical PyrLK is; dropped with the look-ahead
@@ -928,6 +1050,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // overwrites), beside the fit, so the look-ahead PyrLK that follows it on
     // that stream needs no cross-stream edge
     auto enqueue_next_pyr = [&](bool side, bool wait = true) -> int {
+        // the posted look-ahead launches first (they read la_ready; in stream
+        // order on la_s ahead of this build, as without the worker)
+        const int dr = drain(t);
+        if (dr != TBDK_OK) return dr;
         hipStream_t ps = s;
         if (side) {
             ps = t->la_s;
@@ -973,6 +1099,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         hipError_t e = hipSuccess;  // zero-copy without a look-ahead wait sets it nowhere below
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
+            rc = drain(t);
+            if (rc != TBDK_OK) return rc;
             e = wait_if_pending(s, t->la_done);
             if (e != hipSuccess) return map_status(e);
         }
@@ -1081,6 +1209,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         // host tracks; the post-tracker phase adds the unchanged sets it missed
         if (next && t->ctx->opt_tbd_spec_la && frame_id % c.redetect_every != 0) {
             SUB_START();
+            rc = drain(t);  // h_spec is rewritten below
+            if (rc != TBDK_OK) return rc;
             int ns = 0;
             k = 0;
             for (const auto& tr : tracks) {
@@ -1098,19 +1228,24 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             }
             SUB_MARK(0);
             if (ns > 0) {
-                hipStream_t ls = t->la_s;
-                e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
-                if (e == hipSuccess && !t->zc)
-                    e = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
-                if (e != hipSuccess) return map_status(e);
-                SUB_MARK(1);
-                rc = lk_internal(t->ctx, &P, &Pnext, reinterpret_cast<const float*>(t->slot_pts),
-                                 reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr, t->slot_iters,
-                                 ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls, t->d_spec, nullptr, t->h_spec);
+                // (launch worker: posted, so the tracker step below starts now)
+                const bool wait_ready = t->la_stream != t->la_s;
+                tbdk_pyr* pa = &P;
+                tbdk_pyr* pb = &Pnext;
+                rc = run_or_post(t, [t, ns, wait_ready, lp, pa, pb]() -> int {
+                    hipStream_t ls = t->la_s;
+                    hipError_t e2 = wait_ready ? wait_if_pending(ls, t->la_ready) : hipSuccess;
+                    if (e2 == hipSuccess && !t->zc)
+                        e2 = hipMemcpyAsync(t->d_spec, t->h_spec, sizeof(int32_t) * ns, hipMemcpyHostToDevice, ls);
+                    if (e2 != hipSuccess) return map_status(e2);
+                    const int r = lk_internal(t->ctx, pa, pb, reinterpret_cast<const float*>(t->slot_pts),
+                                              reinterpret_cast<float*>(t->slot_next), t->slot_status, nullptr,
+                                              t->slot_iters, ns * kSlotPts, &lp, t->slot_counts, kSlotPts, ls,
+                                              t->d_spec, nullptr, t->h_spec);
+                    if (r != TBDK_OK) return r;
+                    return map_status(hipEventRecord(t->la_done, ls));
+                });
                 if (rc != TBDK_OK) return rc;
-                SUB_MARK(2);
-                e = hipEventRecord(t->la_done, ls);
-                if (e != hipSuccess) return map_status(e);
                 SUB_MARK(3);
                 for (int q = 0; q < ns; ++q) {
                     t->spec_member[(size_t)t->h_spec[q]] = 1;
@@ -1134,6 +1269,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         const int ela = t->ctx->opt_tbd_early_la;
         const int ne = (int)t->erois.size();
         if (next && early_launched && ne > 0 && (ela >= 2 || (ela == 1 && frame_id % c.redetect_every == 0))) {
+            rc = drain(t);  // la_s and la_done from this thread below
+            if (rc != TBDK_OK) return rc;
             for (int q = 0; q < ne; ++q) t->h_ers[q] = erow0 + q;
             hipStream_t ls = t->la_s;
             e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
@@ -1162,6 +1299,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             // the next pyramid is rebuilt over the previous frame's, which the
             // previous step's look-ahead PyrLK (on la_s) may still be reading
             if (had_la_lk) {
+                rc = drain(t);
+                if (rc != TBDK_OK) return rc;
                 hipError_t e = wait_if_pending(s, t->la_done);
                 if (e != hipSuccess) return map_status(e);
             }
@@ -1353,6 +1492,14 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     return TBDK_OK;
 }
 
+// every public call returns with all of its work enqueued (the launch worker's
+// queue drained): the caller may synchronise its streams or the device
+int finish(tbdk_tbd* t, int rc)
+{
+    const int d = t ? drain(t) : TBDK_OK;
+    return rc != TBDK_OK ? rc : d;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1382,15 +1529,16 @@ int tbdk_probe_step_profile(double* out, int cap)
 int tbdk_tbd_step(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
                   int ndets, tbdk_frame_metrics* metrics, void* stream)
 {
-    return step_impl(t, frame, pitch, frame_id, dets, ndets, nullptr, 0, metrics, static_cast<hipStream_t>(stream));
+    return finish(t, step_impl(t, frame, pitch, frame_id, dets, ndets, nullptr, 0, metrics,
+                               static_cast<hipStream_t>(stream)));
 }
 
 int tbdk_tbd_step_ahead(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets,
                         int ndets, const uint8_t* next_frame, int next_pitch, tbdk_frame_metrics* metrics,
                         void* stream)
 {
-    return step_impl(t, frame, pitch, frame_id, dets, ndets, next_frame, next_pitch, metrics,
-                     static_cast<hipStream_t>(stream));
+    return finish(t, step_impl(t, frame, pitch, frame_id, dets, ndets, next_frame, next_pitch, metrics,
+                               static_cast<hipStream_t>(stream)));
 }
 
 int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,
@@ -1406,9 +1554,9 @@ int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first
         int rc = step_impl(t, frames[i], pitch, first_frame_id + i, dets ? dets + det_offsets[i] : nullptr,
                            det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr,
                            static_cast<hipStream_t>(stream));
-        if (rc != TBDK_OK) return rc;
+        if (rc != TBDK_OK) return finish(t, rc);
     }
-    return TBDK_OK;
+    return finish(t, TBDK_OK);
 }
 
 int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,
@@ -1461,11 +1609,11 @@ int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int 
         int rc = step_impl(t, t->ring[i % 3], t->ring_pitch, first_frame_id + i,
                            dets ? dets + det_offsets[i] : nullptr, det_offsets[i + 1] - det_offsets[i], next,
                            t->ring_pitch, metrics ? metrics + i : nullptr, s);
-        if (rc != TBDK_OK) return rc;
+        if (rc != TBDK_OK) return finish(t, rc);
         e = hipEventRecord(t->freed[i % 3], s);
-        if (e != hipSuccess) return map_status(e);
+        if (e != hipSuccess) return finish(t, map_status(e));
     }
-    return TBDK_OK;
+    return finish(t, TBDK_OK);
 }
 
 int tbdk_tbd_predictions(const tbdk_tbd* t, tbdk_prediction* out, int cap, int* n)
@@ -1485,6 +1633,7 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
     if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
     const auto& tracks = t->tracker->getTracks();
     std::vector<int32_t> counts(4 * (size_t)t->cfg.max_tracks);  // slots and GFTT rows
+    if (const int d = drain(t)) return d;
     (void)hipSetDevice(t->ctx->device);
     hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work (behind the early GFTT) runs on `side`
     if (e == hipSuccess && t->early_s) e = hipStreamSynchronize(t->early_s);  // the early GFTT rows (tbd_post_direct)

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -71,7 +72,10 @@ struct HogScratch;  // hog.hip
 
 struct tbdk_ctx {
     int device = 0;
-    bool timing = false;
+    std::atomic<bool> timing{false};
+    // guards the timing state below (timing_only, timing_calls, recs,
+    // free_events): a TBD loop's launch worker records launches too
+    std::mutex timing_mu;
     int opt_gftt_eig_redo = 0;  // tbdk_ctx_set_option("gftt_eig_redo")
     int opt_pyr_xcd = 1;       // tbdk_ctx_set_option("pyr_xcd"): pyramid roles' row bands per XCD
     int opt_pyr_rows = 1;      // tbdk_ctx_set_option("pyr_rows"): rows per thread of the two-role u8 build (1, 2, 4)
@@ -97,6 +101,8 @@ struct tbdk_ctx {
     int opt_tbd_la_pyr_side = 2;  // tbdk_ctx_set_option("tbd_la_pyr_side"): where the look-ahead pyramid is built
     int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
+    int opt_gftt_compact = 1;    // tbdk_ctx_set_option("gftt_compact"): GFTT writes only its candidates' values
+    int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
     std::vector<std::pair<std::string, int64_t>> timing_calls;  // selected launches per name (sampled or not)
@@ -314,6 +320,10 @@ struct GfttArgs {
     int corner_stride;
     int32_t* counts;  // nroi (-1: candidate overflow)
     int eig_redo;     // test option: walk every eig strip segment in sequence
+    // != 0: no eigenvalue plane; per strip row only its local maxima's values,
+    // packed in lane order at the row's first columns (ctx option gftt_compact;
+    // only with quality <= 1, where a ROI whose max is <= 0 has no candidate)
+    int compact;
     // > 0: the ROI table is inl[0, nroi) instead of rois (ctx option gftt_inline):
     // the TBD loop's tables live in pinned host memory, where the eigenvalue
     // kernel's binary search over them is a chain of host-link round trips

@@ -412,3 +412,45 @@ def test_tbd_lookahead_then_no_tracks(gpu):
     gap = [f for f in range(11, 26) if nt[f - 1] > 0 and nt[f] == 0]
     assert gap, f"no step ended with every track deleted: {nt}"  # the no-track step follows it
     assert nt[-1] > 0 and sum(m[7] for m in base[0][27:]) > 0  # tracking resumed after the gap
+
+
+def test_tbd_async_launch_worker_matches(gpu):
+    """The look-ahead PyrLK launches issued by the loop's launch worker thread
+    (ctx option tbd_async_la, read at loop creation) and by the loop's own
+    thread give the same frames, through tbdk_tbd_run and per-frame steps with
+    and without an announced next frame, with and without the deferred
+    look-ahead; with timing events on, the worker's launches are recorded
+    beside the loop thread's (the context's timing state is shared)."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 40, 16
+    frames, gt = klt.synth_render(13, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
+    res = []
+    try:
+        for asy, d in ((0, 0), (1, 0), (1, 1)):
+            gpu.set_option("tbd_async_la", asy)
+            gpu.set_option("tbd_la_defer", d)
+            gpu.timing_select(["lk_sparse"])
+            gpu.timing_enable(True)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            n_lk, _ = gpu.timing_query("lk_sparse")
+            gpu.timing_enable(False)
+            gpu.timing_select(None)
+            stepped = tbd.TbdLoop(c, ctx=gpu)
+            mt = []
+            for f in range(F):
+                nxt = frames[f + 1] if f + 1 < F and f % 3 != 2 else None
+                mt.append(_mkey(stepped.step(frames[f], f, dets[f], next_frame=nxt)))
+            res.append(([_mkey(m) for m in ms], loop.tracks(), mt, stepped.tracks(), n_lk))
+            del loop, stepped
+    finally:
+        gpu.set_option("tbd_async_la", 0)
+        gpu.set_option("tbd_la_defer", 0)
+        gpu.timing_enable(False)
+        gpu.timing_select(None)
+    for r in res[1:]:
+        assert r[:4] == res[0][:4]
+    assert res[0][4] > F and res[1][4] == res[0][4]  # every PyrLK launch timed, the worker's included
