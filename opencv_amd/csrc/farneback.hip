@@ -644,8 +644,43 @@ __device__ __forceinline__ void fb_finish(const FbIterArgs& a, int x, int y, con
 
 // LDS slot of strip lane l: one pad double every 4, so the horizontal runs
 // (thread q reads lanes 4q..4q+3+2m) hit distinct banks
+//
+// TBDK_FB_W64 (round 6): the horizontal windows read as 8-byte pairs
+// (ds_read_b64: twice the bytes per LDS cycle of ds_read_b32); the windows
+// start at even columns, so the row is unpadded, and rows (channel, batch
+// row) are kFbStrip + 2 floats apart — an odd number of 8-byte banks — so the
+// 32 lanes of a read group, 16 distinct windows of one row or the tail of one
+// row and the head of the next, hit distinct banks (tools/r06_fb_lds.sh)
+#ifndef TBDK_FB_W64
+#define TBDK_FB_W64 1
+#endif
+#if TBDK_FB_W64
+__device__ __forceinline__ int fb_slot(int l) { return l; }
+constexpr int kFbSlots = kFbStrip + 2;
+#else
 __device__ __forceinline__ int fb_slot(int l) { return l + (l >> 2); }
 constexpr int kFbSlots = kFbStrip + kFbStrip / 4;
+#endif
+// the window values row[l0 .. l0 + NW) (l0 and NW even under TBDK_FB_W64)
+template <int NW>
+__device__ __forceinline__ void fb_window(const float* row, int l0, float (&win)[NW])
+{
+#if TBDK_FB_W64
+    static_assert(NW % 2 == 0, "8-byte pairs");
+#pragma unroll
+    for (int i = 0; i < NW; i += 2) {
+        // volatile: one ds_read_b64 per pair (the load merger otherwise pairs
+        // them into ds_read2_b64, which moves 128 B per LDS cycle, as b32 does)
+        typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+        const uint64_t p = *(lds_u64*)(row + min(l0 + i, kFbStrip - 2));
+        win[i] = __uint_as_float((uint32_t)p);
+        win[i + 1] = __uint_as_float((uint32_t)(p >> 32));
+    }
+#else
+#pragma unroll
+    for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(l0 + i, kFbStrip - 1))];
+#endif
+}
 
 // horizontal window + 2x2 solve of one batch row: thread task -> (row r, TK
 // consecutive output columns starting at strip offset o0).  Box sums restart at
@@ -674,8 +709,7 @@ __device__ __forceinline__ void fb_hsums(const FbIterArgs& a, const float (*vb)[
             // optflowgf.cpp:548-553: sum = v[x]*k0; sum += k[i]*(v[x-i] + v[x+i])
             constexpr int NW = TK + 2 * M;
             float win[NW];
-#pragma unroll
-            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(o0 + i, kFbStrip - 1))];
+            fb_window<NW>(row, o0, win);
 #pragma unroll
             for (int k = 0; k < TK; ++k) {
                 float s = win[k + M] * a.gk[0];
@@ -688,8 +722,7 @@ __device__ __forceinline__ void fb_hsums(const FbIterArgs& a, const float (*vb)[
             // out(c) = (out(c-1) + v[c+2m]) - v[c-1]
             constexpr int NW = 4 + 2 * M;
             float win[NW];
-#pragma unroll
-            for (int i = 0; i < NW; ++i) win[i] = row[fb_slot(min(g0 + i, kFbStrip - 1))];
+            fb_window<NW>(row, g0, win);
             float sacc = win[0];
 #pragma unroll
             for (int i = 1; i <= 2 * M; ++i) sacc += win[i];
@@ -830,7 +863,7 @@ __global__ __launch_bounds__(kFbThreads, (kFbRB == 8 ? (M <= 6 && !GAUSS ? 2 : 1
     constexpr int RR = kFbRB + 2 * M;     // M ring rows
     constexpr int VC = 4;                 // centres per thread in the vertical pass
     __shared__ float mr[5 * RR * kFbStrip];
-    __shared__ float vb[kFbRB][5][kFbSlots];
+    __shared__ __attribute__((aligned(16))) float vb[kFbRB][5][kFbSlots];
 
     const int tid = threadIdx.x;
     const int col = tid & (kFbStrip - 1), half = tid >> 7;

@@ -197,3 +197,23 @@ def test_gftt_params_rejected(gpu):
     for kw in ({"blockSize": 0}, {"blockSize": 64}, {"harrisK": float("nan")}):
         with pytest.raises(_lib.TbdkError):
             klt.GoodFeaturesToTrackDetector(10, 0.01, 0.0, **kw).detect_rois(img, [(0, 0, 20, 20)])
+
+
+@pytest.mark.parametrize("compact", [0, 1])
+@pytest.mark.parametrize("maxc,q,md", [(256, 0.01, 3.0), (500, 0.001, 0.0), (64, 1.0, 2.0), (40, 1.5, 1.0)])
+def test_gftt_compact_and_dense_candidates(gpu, compact, maxc, q, md):
+    """GFTT with the eigenvalue plane (ctx option gftt_compact = 0) and with
+    only its local maxima's values written (1, the default; used for quality
+    <= 1, the dense plane above it): the same corner lists as the oracle,
+    including the basketball frame's edge and degenerate ROIs and quality 1
+    (the bound of the compact mode's no-candidate rule for ROIs whose max <= 0)."""
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "basketball_pair.npz"))
+    img = d["a"]
+    rois = [(0, 0, 160, 120), (600, 440, 40, 40), (0, 0, 3, 3), (5, 5, 2, 50), (300, 200, 77, 33), (0, 0, 640, 480),
+            (250, 250, 57, 121), (10, 400, 113, 80)]
+    gpu.set_option("gftt_compact", compact)
+    try:
+        c, n = detect(gpu, img, rois, maxc, q, md)
+    finally:
+        gpu.set_option("gftt_compact", 1)
+    check(img, rois, c, n, maxc, q, md)
