@@ -120,6 +120,23 @@ def pmc_traffic(kernel_substr: str, suffix: str = "_pmc_loop.json"):
     return None, None
 
 
+def ktrace_loop_avg_us(kernel: str):
+    """Mean rocprofv3 kernel-trace duration (us) of `kernel` over the contract's
+    loop only: the newest committed profiles/rNN_kernel_stats_loop.csv
+    (tools/profile_round.sh: `rocprofv3 --kernel-trace --stats -- bench.py
+    --no-secondary --no-cpu-baseline`, configs[2]'s launches only; the full
+    rNN_kernel_stats.csv also averages the KITTI, bounds-at-frame, fp16 and dense
+    legs' launches of the same kernel).  (avg_us, calls, source) or (None, None, None)."""
+    import csv
+
+    d, files = _pmc_summaries("_kernel_stats_loop.csv")
+    for f in reversed(files):
+        for row in csv.DictReader(open(os.path.join(d, f))):
+            if row["Name"].startswith(kernel):
+                return float(row["AverageNs"]) / 1000.0, int(row["Calls"]), f
+    return None, None, None
+
+
 def ktrace_grid_us(frags, pick: str = "max_grid"):
     """Kernel-trace durations (rocprofv3's GPU start / end: no launch cost) per
     kernel and grid from the newest committed profiles/rNN_ktrace_grid.json
@@ -1549,6 +1566,7 @@ def main(argv=None):
         traffic, traffic_src = pmc_traffic(f"lk_multi_kernel<{args.win}, {args.win}, true>")
     if traffic is None:
         traffic, traffic_src = pmc_traffic(f"lk_strip_kernel<{args.win}, {args.win}>")
+    kt_loop = ktrace_loop_avg_us(f"void tbdk::lk_multi_kernel<{args.win}, {args.win}, true, false>")
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic, "kernel": "lk_sparse",
                 "traffic_source": traffic_src,
@@ -1568,6 +1586,10 @@ def main(argv=None):
                 "frac_sampled": (round(flops_per_launch / (lk["avg_us"] * 1e-6) / 1e12 / PEAK_F32_TFLOPS, 4)
                                  if lk["avg_us"] else None),
                 "avg_us_every_launch": lk_every,
+                "avg_us_kernel_trace_loop": kt_loop[0], "kernel_trace_loop_calls": kt_loop[1],
+                "kernel_trace_loop_source": kt_loop[2],
+                "frac_kernel_trace_loop": (round(flops_per_launch / (kt_loop[0] * 1e-6) / 1e12 / PEAK_F32_TFLOPS, 4)
+                                           if kt_loop[0] else None),
                 "frac_every_launch": (round(flops_per_launch / (lk_every * 1e-6) / 1e12 / PEAK_F32_TFLOPS, 4)
                                       if lk_every else None),
                 "flops_per_launch": flops_per_launch,

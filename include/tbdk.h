@@ -208,6 +208,14 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
  *       sets is launched by the next step right after its critical PyrLK
  *       instead of at the end of its own step (results equal; A/B runs).
+ *   "gftt_compact" (0/1, default 1): GFTT with quality <= 1 (blockSize 3,
+ *       min-eigenvalue) writes no eigenvalue plane, only its local maxima's
+ *       values per strip row (corner lists equal; quality > 1, Harris and other
+ *       block sizes keep the plane).
+ *   "tbd_async_la" (0/1, default 0; taken by tbdk_tbd_create): the TBD loop's
+ *       look-ahead PyrLK launches are issued by a worker thread of the loop
+ *       (one more host thread per loop, spinning between frames; results equal;
+ *       A/B runs).
  *   "timing_every" (>= 1, default 1): HIP events on a pseudo-random 1/N of the
  *       launches of each kernel selected for timing: launch i (counted per
  *       kernel name from tbdk_timing_enable) is timed iff splitmix64(i) % N == 0

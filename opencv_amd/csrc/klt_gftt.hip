@@ -125,8 +125,11 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
 // by the "gftt_eig_redo" option in the tests) the segments are walked again one
 // after another, each from its predecessor's final SUM: the reference's
 // sequential order.
+// 4 since round 6: 256-thread workgroups find CU room beside the loop's PyrLK
+// waves sooner (loop +1 % over 8 rounds with the compact candidates; standalone
+// the 8-segment walk is faster, 19.5 against 23.6 us for 76 ROIs)
 #ifndef TBDK_GFTT_EIG_WAVES
-#define TBDK_GFTT_EIG_WAVES 8
+#define TBDK_GFTT_EIG_WAVES 4
 #endif
 constexpr int kEigWaves = TBDK_GFTT_EIG_WAVES;  // row segments (waves) per strip
 constexpr int kEigPref = 8;   // pixel rows in flight per wave

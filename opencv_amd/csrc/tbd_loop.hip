@@ -114,7 +114,9 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
         const size_t base = (size_t)E.slot * kSlotPts, rb = (size_t)row * kSlotPts;
         int m = 0, it = 0;
         // every chunk's loads first (one memory round trip for the wave, not one
-        // per chunk of 64 points), then the ballot compaction in point order
+        // per chunk of 64 points), issued together with the count's (the row's
+        // whole capacity is read and masked by the count afterwards), then the
+        // ballot compaction in point order
         constexpr int kChunks = kSlotPts / 64;
         uint8_t stv[kChunks];
         int itv[kChunks];
@@ -122,11 +124,17 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) {
             const int j = c * 64 + lane;
-            const bool in = j < cnt;
-            stv[c] = in ? slot_status[rb + j] : (uint8_t)0;
-            itv[c] = in ? slot_iters[rb + j] : 0;
-            pv[c] = in ? slot_pts[rb + j] : make_float2(0.f, 0.f);
-            nv[c] = in ? slot_next[rb + j] : make_float2(0.f, 0.f);
+            stv[c] = slot_status[rb + j];
+            itv[c] = slot_iters[rb + j];
+            pv[c] = slot_pts[rb + j];
+            nv[c] = slot_next[rb + j];
+        }
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) {
+            if (c * 64 + lane >= cnt) {
+                stv[c] = 0;
+                itv[c] = 0;
+            }
         }
 #pragma unroll
         for (int c = 0; c < kChunks; ++c) {
@@ -192,9 +200,16 @@ __global__ __launch_bounds__(64 * kFitWaves) void tbd_fit_kernel(const FitEntry*
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         }
         if (threadIdx.x == 0) {
+            // the workgroup's results were released above (system scope: wave 0's
+            // fence, or every wave's own); the count itself is relaxed, and the
+            // last workgroup's acquire fence pairs with those release fences
+            // (fence-fence synchronisation through the count's release sequence)
+            // before its release store of the flag, which the host acquires
+            if (!wg_pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the waves' releases, cumulated by the barrier
             const unsigned prev =
-                __hip_atomic_fetch_add(fit_cnt, (unsigned)nin, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(fit_cnt, (unsigned)nin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (prev + (unsigned)nin == (unsigned)nents) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 *fit_cnt = 0u;
                 __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }

@@ -67,7 +67,7 @@ def summarize(rec, label=""):
     span = en.max()
     steps = (rec[:, 5] & 0xFFFF).astype(np.int64)
     rel = ((rec[:, 5] >> 16) & 0xFFFF).astype(np.int64)
-    mit = (rec[:, 5] >> 32).astype(np.int64)
+    mit = ((rec[:, 5] >> 32) & 0xFFFF).astype(np.int64)
     ends = np.sort(en)
     q = lambda f: ends[min(len(ends) - 1, int(f * len(ends)))]
     simd = (rec[:, 2] & 0xFFFFFFFF).astype(np.int64)

@@ -3,6 +3,8 @@
 #   profiles/<tag>_kernel_stats.csv : rocprofv3 --kernel-trace --stats of the default bench.py
 #   profiles/<tag>_bench.json       : that run's bench line
 #   profiles/<tag>_ktrace_grid.json : that run's kernel-trace durations per (kernel, grid size) (tools/ktrace_by_grid.py)
+#   profiles/<tag>_kernel_stats_loop.csv : --kernel-trace --stats of bench.py --no-secondary (configs[2]'s loop only:
+#                                     the roofline's frac_kernel_trace_loop)
 #   profiles/<tag>_pmc_loop.json    : FETCH_SIZE / WRITE_SIZE of the contract's legs only (bench.py --no-secondary:
 #                                     the 1080p x 128 loop), separate --pmc passes -- the loop kernels' traffic fields
 #   profiles/<tag>_pmc.json         : FETCH_SIZE / WRITE_SIZE, separate --pmc passes (bench.py --steps 60, reduced
@@ -19,6 +21,7 @@ if [ "${1:-}" = "--collect" ]; then
     cp "$out/pmc.json" "profiles/${tag}_pmc.json"
     cp "$out/pmc_loop.json" "profiles/${tag}_pmc_loop.json"
     cp "$out/ktrace_grid.json" "profiles/${tag}_ktrace_grid.json"
+    cp "$out"/stats_loop/kt_kernel_stats.csv "profiles/${tag}_kernel_stats_loop.csv"
     exit 0
 fi
 tag=$1
@@ -28,6 +31,9 @@ timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/
 python3 "$root/tools/ktrace_by_grid.py" "$out/stats/kt_kernel_trace.csv" "$out/ktrace_grid.json" \
     "rocprofv3 --kernel-trace --stats of the default bench.py (this round's kernel_stats run): per (kernel, grid) GPU durations" \
     > /dev/null
+# the contract's loop alone (bench.py --no-secondary): kernel-trace durations of configs[2]'s launches only
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_loop" -o kt \
+    -- python3 "$root/bench.py" --no-secondary --no-cpu-baseline > "$out/bench_loop.json" 2> "$out/bench_loop.err"
 for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$out/loop_$c" -o pmc \
         -- python3 "$root/bench.py" --no-secondary --no-cpu-baseline > "$out/loop_$c.json" 2> "$out/loop_$c.err"
