@@ -241,10 +241,6 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_gftt_compact = value != 0;
         return TBDK_OK;
     }
-    if (std::strcmp(name, "tbd_early_after_lk") == 0) {
-        ctx->opt_tbd_early_after_lk = value != 0;
-        return TBDK_OK;
-    }
     if (std::strcmp(name, "tbd_async_la") == 0) {
         ctx->opt_tbd_async_la = value != 0;
         return TBDK_OK;

@@ -344,7 +344,6 @@ struct tbdk_tbd {
     hipEvent_t fit_done = nullptr;   // this frame's predictions are on the host
     hipEvent_t la_ready = nullptr;   // look-ahead pyramid complete (recorded on the step's stream)
     hipEvent_t lk_issued = nullptr;  // tbd_la_pyr_side: this step's PyrLK launches (on the step's stream) done
-    hipEvent_t lk_crit = nullptr;    // tbd_early_after_lk: this step's critical PyrLK done (on the step's stream)
     hipEvent_t step_begin = nullptr; // tbd_la_pyr_side 2: the caller's work on the step's stream before the step
     hipEvent_t la_done = nullptr;    // look-ahead PyrLK complete (recorded on la_s)
     // the look-ahead PyrLK runs on its own stream behind the GFTT eigenvalue
@@ -493,7 +492,6 @@ int release(tbdk_tbd* t)
     if (t->la_done) (void)hipEventDestroy(t->la_done);
     if (t->la_ready) (void)hipEventDestroy(t->la_ready);
     if (t->lk_issued) (void)hipEventDestroy(t->lk_issued);
-    if (t->lk_crit) (void)hipEventDestroy(t->lk_crit);
     if (t->step_begin) (void)hipEventDestroy(t->step_begin);
     if (t->la_s && t->own_la) (void)hipStreamDestroy(t->la_s);
     if (t->eig_done) (void)hipEventDestroy(t->eig_done);
@@ -672,7 +670,6 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->la_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->lk_issued, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->lk_crit, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->step_begin, hipEventDisableTiming);
     // the look-ahead PyrLK at the lowest priority (on gfx950 the range is
     // normal..high, so this is the default; a high-priority caller stream for
@@ -1112,14 +1109,6 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         }
         STEP_MARK(3);
         if (early_order == 1) {
-            // ctx option tbd_early_after_lk: the early GFTT (needed only after the
-            // tracker step) starts when the critical PyrLK has finished, so the
-            // two do not share the CUs
-            if (t->ctx->opt_tbd_early_after_lk && nB > 0) {
-                hipError_t e2 = hipEventRecord(t->lk_crit, s);
-                if (e2 == hipSuccess) e2 = hipStreamWaitEvent(t->early_s, t->lk_crit, 0);
-                if (e2 != hipSuccess) return map_status(e2);
-            }
             rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
         }

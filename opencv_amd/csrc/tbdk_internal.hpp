@@ -102,7 +102,6 @@ struct tbdk_ctx {
     int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
     int opt_gftt_compact = 1;    // tbdk_ctx_set_option("gftt_compact"): GFTT writes only its candidates' values
-    int opt_tbd_early_after_lk = 0;  // tbdk_ctx_set_option("tbd_early_after_lk"): early GFTT behind the critical PyrLK
     int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch

@@ -455,23 +455,3 @@ def test_tbd_async_launch_worker_matches(gpu):
         assert r[:4] == res[0][:4]
     assert res[0][4] > F and res[1][4] == res[0][4]  # every PyrLK launch timed, the worker's included
 
-
-def test_tbd_early_gftt_after_critical_lk_matches(gpu):
-    """The early GFTT held back until the step's critical PyrLK has finished
-    (ctx option tbd_early_after_lk) gives the same frames as the default."""
-    from opencv_amd import klt, tbd
-
-    W, H, N, F = 960, 540, 40, 14
-    frames, gt = klt.synth_render(14, W, H, N, 0, F, ctx=gpu)
-    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
-    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
-    res = []
-    try:
-        for opt in (0, 1):
-            gpu.set_option("tbd_early_after_lk", opt)
-            loop = tbd.TbdLoop(c, ctx=gpu)
-            ms = loop.run(frames, 0, dets)
-            res.append(([_mkey(m) for m in ms], loop.tracks(), sum(m.early_gftt for m in ms)))
-    finally:
-        gpu.set_option("tbd_early_after_lk", 0)
-    assert res[0] == res[1] and res[0][2] > F
