@@ -59,17 +59,19 @@ def pyr_bytes(w: int, h: int, nlevels: int) -> int:
     return sum(sizes[i] + sizes[i + 1] for i in range(nlevels - 1))
 
 
-def pyr_build_bytes(w: int, h: int, nlevels: int, pad: int = 32) -> int:
-    """The bytes a levels-only build must move (the loop's pyramids): the frame
-    read once, every padded level written (reflect-101 frame included), and each
-    level from 2 on reading its interior predecessor (level 1 is made from the
-    frame itself).  B_pyr above leaves out the padded level-0 copy."""
+def pyr_build_bytes(w: int, h: int, nlevels: int, pad: int = 32, copy_l0: bool = True) -> int:
+    """The bytes a levels-only build must move: the frame read once, every
+    padded level written (reflect-101 frame included), and each level from 2 on
+    reading its interior predecessor (level 1 is made from the frame itself).
+    copy_l0 False: the TBD loop's build inside tbdk_tbd_run since round 6 (ctx
+    option tbd_borrow_l0), where level 0 is the frame itself and no padded copy
+    is written.  B_pyr above leaves out the padded level-0 copy as well."""
     sizes, padded = [], []
     for _ in range(nlevels):
         sizes.append(w * h)
         padded.append((w + 2 * pad) * (h + 2 * pad))
         w, h = (w + 1) // 2, (h + 1) // 2
-    return sizes[0] + sum(padded) + sum(sizes[1:nlevels - 1])
+    return sizes[0] + sum(padded[0 if copy_l0 else 1:]) + sum(sizes[1:nlevels - 1])
 
 
 def max_over_ranks(value: float, world: int, device=None) -> float:
@@ -1596,7 +1598,8 @@ def main(argv=None):
                 "mean_points_per_launch": lk_pts / max(1, lk["launches"]),
                 "mean_iters_per_point": lk_it / max(1, lk_pts)}
     pb = pyr_bytes(args.width, args.height, nlev)
-    pbb = pyr_build_bytes(args.width, args.height, nlev)
+    borrow = "tbd_borrow_l0=1" in [kv.replace(" ", "") for kv in args.ctx_option] and not args.pyr_derivs
+    pbb = pyr_build_bytes(args.width, args.height, nlev, copy_l0=not borrow)
     pyr = kstats.get("pyr_build", kstats_aside.get("pyr_build", nolaunch))
     pyr_gbs = pbb / (pyr["avg_us"] * 1e-6) / 1e9 if pyr["launches"] else 0.0
     cnt = pmc_bytes(PYR_KERNELS)
@@ -1613,10 +1616,12 @@ def main(argv=None):
                 "traffic_fetch_x2": (cnt["fetch_x2"] + cnt["write"]) if cnt else None,
                 "traffic_over_algorithmic": round((cnt["fetch_raw"] + cnt["write"]) / pbb, 3) if cnt else None,
                 "traffic_kernels": cnt["kernels"] if cnt else None, "traffic_source": cnt["source"] if cnt else None,
-                "note": "achieved = the levels-only build's algorithmic bytes (frame read once, every padded level "
-                        "written, levels >= 2 reading their predecessor; bytes_per_launch) / the build's HIP-event "
-                        "time (both launches); b_pyr_survey = SURVEY §8d's B_pyr (no level-0 copy); traffic = "
-                        "FETCH_SIZE + WRITE_SIZE per build from the committed PMC summary (4-byte loads: no x2)"}
+                "level0": "the frame itself (tbd_borrow_l0: no padded copy)" if borrow else "padded copy",
+                "note": "achieved = the loop's build's algorithmic bytes (frame read once, every padded level "
+                        "written -- from level 1 on when level 0 is the frame itself --, levels >= 2 reading their "
+                        "predecessor; bytes_per_launch) / the build's HIP-event time (its launches); b_pyr_survey = "
+                        "SURVEY §8d's B_pyr (no level-0 copy); traffic = FETCH_SIZE + WRITE_SIZE per build from the "
+                        "committed PMC summary (4-byte loads: no x2)"}
     # north_star's "HBM-read roofline on pyramid+PyrLK": SURVEY §8d bytes B_pyr + B_lk + N*21,
     # with B_lk at its upper bound (2 full pyramids), over the two stages' summed time
     w_, h_, lv_bytes = args.width, args.height, 0

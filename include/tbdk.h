@@ -212,6 +212,15 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       min-eigenvalue) writes no eigenvalue plane, only its local maxima's
  *       values per strip row (corner lists equal; quality > 1, Harris and other
  *       block sizes keep the plane).
+ *   "tbd_borrow_l0" (0/1, default 0): inside tbdk_tbd_run the loop's pyramids
+ *       take the caller's frames as level 0 (no padded copy; PyrLK reads
+ *       windows across a frame's edge by reflect-101 coordinates, the values
+ *       the copy holds); when the call returns the last frame's level 0 has
+ *       been copied into the loop's own buffer and the caller's stream waits
+ *       for the last read of a frame, so the frames may be reused once that
+ *       stream is synchronised (results equal; PyrLK measured slower reading
+ *       the frames than the loop's reused buffers, so off by default).
+ *       tbdk_tbd_step / _step_ahead / _run_host always copy.
  *   "tbd_async_la" (0/1, default 0; taken by tbdk_tbd_create): the TBD loop's
  *       look-ahead PyrLK launches are issued by a worker thread of the loop
  *       (one more host thread per loop, spinning between frames; results equal;

@@ -363,15 +363,32 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         uint32_t w0, w1;
         bilinear_weights(prevx - ipx, prevy - ipy, w0, w1);
 
+        uint32_t jp[WH + 1];
         const int hp = L.h + 2 * L.ipad;
-        const __amdgpu_buffer_rsrc_t rI = make_rsrc(L.I, L.ipitch * hp + 256);
+        // an unpadded level (pad 0: the TBD loop's level 0, the frame itself) is
+        // bounded exactly; padded levels carry 256 bytes of over-read room
+        const __amdgpu_buffer_rsrc_t rI = make_rsrc(L.I, L.ipitch * hp + (L.ipad ? 256 : 0));
         const __amdgpu_buffer_rsrc_t rD = make_rsrc(L.D, L.dpitch * (L.h + 2 * L.dpad) + 256);
-        const __amdgpu_buffer_rsrc_t rJ = make_rsrc(L.J, L.jpitch * (L.h + 2 * L.jpad) + 256);
+        const __amdgpu_buffer_rsrc_t rJ = make_rsrc(L.J, L.jpitch * (L.h + 2 * L.jpad) + (L.jpad ? 256 : 0));
+        // the J window rows jy0 .. jy0 + WH at columns jx0 + x, jx0 + x + 1 into jp;
+        // on an unpadded level a wave with a window across the edge takes the
+        // reflect-101 path (wave-uniform)
+        auto load_j = [&](bool on, int jx0, int jy0) {
+            if (L.jpad == 0 &&
+                any_lane(on && (jx0 + x < 0 || jx0 + x + 1 >= L.w || jy0 < 0 || jy0 + WH >= L.h))) {
+#pragma unroll
+                for (int r = 0; r <= WH; ++r)
+                    jp[r] = on ? load_pair_refl(rJ, L.jpitch, L.w, L.h, jy0 + r, jx0 + x) : 0u;
+                return;
+            }
+            const uint32_t joff = on ? (uint32_t)((jy0 + L.jpad) * L.jpitch + jx0 + x + L.jpad) : 0u;
+#pragma unroll
+            for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+        };
 
         nextx -= halfx;
         nexty -= halfy;
         int pinx = (int)floorf(nextx), piny = (int)floorf(nexty);
-        uint32_t jp[WH + 1];
 
         // ---- per row: ic = round - I x32 * 2^9, so that the J bilinear sum
         // started from ic and shifted right by 9 is diff = J x32 - I x32 itself
@@ -439,8 +456,16 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 // reference's row / column reflection.
                 const uint32_t ioff = act ? (uint32_t)((ipy - 1 + L.ipad) * L.ipitch + ipx + x - 1 + L.ipad) : 0u;
                 uint32_t u[WH + 3];
+                if (L.ipad == 0 &&
+                    any_lane(act && (ipx + x - 1 < 0 || ipx + x + 2 >= L.w || ipy - 1 < 0 || ipy + WH + 1 >= L.h))) {
 #pragma unroll
-                for (int r = 0; r < WH + 3; ++r) u[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);
+                    for (int r = 0; r < WH + 3; ++r)
+                        u[r] = act ? load4_refl(rI, L.ipitch, L.w, L.h, ipy - 1 + r, ipx + x - 1) : 0u;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < WH + 3; ++r)
+                        u[r] = __builtin_amdgcn_raw_buffer_load_b32(rI, ioff, r * L.ipitch, 0);
+                }
 #ifdef TBDK_LK_TRACE
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the level's source rows have arrived
                 if (level == a.max_level) tr_stamp(14);
@@ -575,9 +600,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
             // waves per SIMD; this way 116, 4 waves)
             {
                 const bool jin = act && !(pinx < -WW || pinx >= L.w || piny < -WH || piny >= L.h);
-                const uint32_t joff = jin ? (uint32_t)((piny + L.jpad) * L.jpitch + pinx + x + L.jpad) : 0u;
-#pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+                load_j(jin, pinx, piny);
 #ifdef TBDK_LK_TRACE
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -625,9 +648,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #ifdef TBDK_LK_TRACE
                 ++tr_reloads;
 #endif
-                const uint32_t joff = act ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
-#pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+                load_j(act, inx, iny);
                 pinx = inx;
                 piny = iny;
             }
@@ -726,9 +747,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                     }
                 }
                 bilinear_weights(npx - inx, npy - iny, w0, w1);
-                const uint32_t joff = want ? (uint32_t)((iny + L.jpad) * L.jpitch + inx + x + L.jpad) : 0u;
-#pragma unroll
-                for (int r = 0; r <= WH; ++r) jp[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+                load_j(want, inx, iny);
                 int e = 0;
 #pragma unroll
                 for (int q = 0; q < NP; ++q) {

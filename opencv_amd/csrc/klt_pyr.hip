@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kRoleThreads) void pyr_build_kernel(PyrRolesArgs a)
 
 // levels 0 and 1 of pyr from the frame in one launch
 static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_pyr& pyr, hipStream_t s, int rows_a,
-                                    int rows_b, int xcd)
+                                    int rows_b, int xcd, bool skip_l0)
 {
     PyrRolesArgs a;
     const tbdk_level& S = pyr.lv[0];
@@ -388,6 +388,7 @@ static hipError_t launch_pyr_fuse01(const uint8_t* src, int spitch, const tbdk_p
     a.rb = rows_b;
     a.nAr = blocks((long)a.wa4 * ((S.height + 2 * S.pad + a.ra - 1) / a.ra));
     a.nA = xcd ? (a.nAr + 7) & ~7 : a.nAr;
+    if (skip_l0) a.nA = a.nAr = 0;  // level 0 is the frame itself: role B only
     a.nB = blocks((long)a.wb4 * ((D1.height + 2 * D1.pad + a.rb - 1) / a.rb));
     a.xcd = xcd;
     hipLaunchKernelGGL(pyr_build_kernel, dim3(a.nA + a.nB), dim3(kRoleThreads), 0, s, a);
@@ -720,15 +721,20 @@ static hipError_t launch_pyr_fused(const uint8_t* src, int spitch, const tbdk_py
 // every level of a u8 pyramid from the frame: levels 0 and 1 in one launch
 // (fuse), or one launch per level
 hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, int xcd,
-                             hipStream_t s)
+                             hipStream_t s, bool skip_l0)
 {
     hipError_t e;
     int level = 1;
-    if (fuse >= 2 && pyr_fused_ok(pyr)) {
+    if (skip_l0) {  // the two-role launch without its copy role (levels >= 2 from level 1 as usual)
+        if (pyr.nlevels < 2) return hipSuccess;
+        rows = rows < 1 ? 1 : rows > kRowsA ? kRowsA : rows;
+        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1, xcd, true);
+        level = 2;
+    } else if (fuse >= 2 && pyr_fused_ok(pyr)) {
         e = launch_pyr_fused(img, pitch, pyr, s, &level);
     } else if (fuse && pyr.nlevels >= 2) {
         rows = rows < 1 ? 1 : rows > kRowsA ? kRowsA : rows;
-        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1, xcd);
+        e = launch_pyr_fuse01(img, pitch, pyr, s, rows, rows > 1 ? 2 : 1, xcd, false);
         level = 2;
     } else {
         e = launch_pad_copy(img, pitch, pyr.lv[0], s);

@@ -83,6 +83,37 @@ __device__ __forceinline__ uint32_t load_pair_u8_ua(__amdgpu_buffer_rsrc_t rs, u
     return __builtin_amdgcn_perm(v, v, 0x0C010C00u);
 }
 
+// ---- unpadded levels (the TBD loop's level 0 read straight from the frame):
+// windows that cross the level's edge take reflect-101 coordinates per byte,
+// the values the padded copy (lkpyramid.cpp:726-740) holds there
+
+// reflect-101 of c into [0, n), for -n < c < 2n - 1
+__device__ __forceinline__ int refl101(int c, int n)
+{
+    c = c < 0 ? -c : c;
+    return c >= n ? 2 * (n - 1) - c : c;
+}
+
+// pixels col .. col + 3 of `row` as one dword (byte k = pixel col + k)
+__device__ __forceinline__ uint32_t load4_refl(__amdgpu_buffer_rsrc_t rs, int pitch, int w, int h, int row, int col)
+{
+    const int yo = refl101(row, h) * pitch;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(yo + refl101(col + k, w)), 0, 0) << (8 * k);
+    return v;
+}
+
+// (pixel col, pixel col + 1) of `row` as an int16 pair, as load_pair_u8_ua
+__device__ __forceinline__ uint32_t load_pair_refl(__amdgpu_buffer_rsrc_t rs, int pitch, int w, int h, int row, int col)
+{
+    const int yo = refl101(row, h) * pitch;
+    const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(yo + refl101(col, w)), 0, 0);
+    const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(yo + refl101(col + 1, w)), 0, 0);
+    return a | (b << 16);
+}
+
 // v_perm selector picking bytes (off & 3) and (off & 3) + 1 of the 8 loaded
 // bytes, zero-extended to two int16
 __device__ __forceinline__ uint32_t pair_sel(uint32_t off)

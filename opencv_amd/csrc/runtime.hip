@@ -241,6 +241,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_gftt_compact = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_borrow_l0") == 0) {
+        ctx->opt_tbd_borrow_l0 = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_async_la") == 0) {
         ctx->opt_tbd_async_la = value != 0;
         return TBDK_OK;
@@ -470,6 +474,38 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     return map_err(e);
 }
 
+}  // extern "C"
+
+int tbdk::pyr_build_borrowed(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, hipStream_t s)
+{
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pyr->cn > 1 || pyr->depth != TBDK_DEPTH_8U ||
+        !(pyr->flags & TBDK_PYR_NO_DERIVS) || pitch < pyr->lv[0].width || !ctx->opt_pyr_fuse)
+        return TBDK_EINVAL;
+    DeviceGuard g(ctx->device);
+    pyr->lv[0].data = const_cast<uint8_t*>(img);
+    pyr->lv[0].pitch = pitch;
+    pyr->lv[0].pad = 0;
+    pyr->flags |= kPyrL0Borrowed;
+    int rec = timing_begin(ctx, "pyr_build", s);
+    const hipError_t e = launch_pyr_levels(img, pitch, *pyr, ctx->opt_pyr_fuse, ctx->opt_pyr_rows, ctx->opt_pyr_xcd, s,
+                                           true);
+    timing_end(ctx, rec, s);
+    return map_err(e);
+}
+
+int tbdk::pyr_restore_l0(tbdk_ctx* ctx, tbdk_pyr* pyr, const tbdk_level& own_l0, hipStream_t s)
+{
+    if (!ctx || !pyr) return TBDK_EINVAL;
+    if (!(pyr->flags & kPyrL0Borrowed)) return TBDK_OK;
+    DeviceGuard g(ctx->device);
+    const hipError_t e = launch_pad_copy(pyr->lv[0].data, pyr->lv[0].pitch, own_l0, s);
+    pyr->lv[0] = own_l0;
+    pyr->flags &= ~kPyrL0Borrowed;
+    return map_err(e);
+}
+
+extern "C" {
+
 int tbdk_pyr_build_f16(tbdk_ctx* ctx, const uint16_t* img, int pitch, tbdk_pyr* pyr, void* stream)
 {
     if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pyr->depth != TBDK_DEPTH_16F || pitch < 2 * pyr->lv[0].width ||
@@ -588,8 +624,16 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
         const tbdk_level& I = prev->lv[l];
         const tbdk_level& J = next->lv[l];
         if (I.width != J.width || I.height != J.height) return TBDK_EINVAL;
-        if (I.pad < pad_needed || J.pad < pad_needed) return TBDK_EINVAL;
+        // a borrowed level 0 (the TBD loop's; pad 0) is read with reflect-101
+        // coordinates at its edges by the several-points-per-wave kernel only
+        const bool bI = l == 0 && (prev->flags & kPyrL0Borrowed) && I.pad == 0;
+        const bool bJ = l == 0 && (next->flags & kPyrL0Borrowed) && J.pad == 0;
+        if ((I.pad < pad_needed && !bI) || (J.pad < pad_needed && !bJ)) return TBDK_EINVAL;
         const tbdk_level& D = prev->dv[l];
+        const int impl_eff = p->impl ? p->impl : ctx->opt_lk_impl;
+        if ((bI || bJ) && (dense || cn > 1 || f16 || D.data || !lk_multi_supported(p->win_w, p->win_h) ||
+                           (impl_eff != 0 && impl_eff != 3)))
+            return TBDK_EINVAL;
         a.lv[l] = LkLevel{I.data, J.data, D.data, I.width, I.height, I.pitch, J.pitch, I.pad, J.pad, D.pitch, D.pad};
     }
     a.max_level = max_level;

@@ -314,6 +314,11 @@ struct tbdk_tbd {
     // the look-ahead frame's, so the look-ahead build never overwrites a
     // pyramid this step's PyrLK still reads
     tbdk_pyr pyr[3];
+    // each pyramid's own level-0 buffer; inside tbdk_tbd_run (ctx option
+    // tbd_borrow_l0) level 0 is the caller's frame itself, whose pointer stays
+    // valid for the whole call, and the padded copy is not made
+    tbdk_level own_l0[3];
+    bool borrow = false;
     int cur = 0;
     bool last_fit = false;  // the previous step ran PyrLK and synced on its fit
     bool have_prev = false;
@@ -477,6 +482,47 @@ inline int run_or_post(tbdk_tbd* t, std::function<int()> f)
     return TBDK_OK;
 }
 
+// a frame's pyramid into P: borrowed level 0 inside tbdk_tbd_run (levels 1..
+// only), else the padded copy (a pyramid that was borrowed gets its own level
+// 0 buffer back first)
+int build_pyr(tbdk_tbd* t, const uint8_t* img, int pitch, tbdk_pyr& P, hipStream_t s)
+{
+    const int i = (int)(&P - t->pyr);
+    if (t->borrow) return pyr_build_borrowed(t->ctx, img, pitch, &P, s);
+    if (P.flags & kPyrL0Borrowed) {
+        P.lv[0] = t->own_l0[i];
+        P.flags &= ~kPyrL0Borrowed;
+    }
+    return tbdk_pyr_build(t->ctx, img, pitch, &P, s);
+}
+
+// the end of a borrowing tbdk_tbd_run: the pyramid the next step reads as its
+// previous frame's gets its level 0 copied into its own buffer (the caller's
+// frame may go away after the call); the others only point at their own
+// buffers again (each is rebuilt before it is read)
+int end_borrow(tbdk_tbd* t, hipStream_t s)
+{
+    if (!t->borrow) return TBDK_OK;
+    t->borrow = false;
+    int rc = TBDK_OK;
+    for (int i = 0; i < 3; ++i) {
+        tbdk_pyr& P = t->pyr[i];
+        if (!(P.flags & kPyrL0Borrowed)) continue;
+        if (i == (t->cur + 2) % 3 && t->have_prev) {
+            const int r = pyr_restore_l0(t->ctx, &P, t->own_l0[i], s);
+            if (rc == TBDK_OK) rc = r;
+        } else {
+            P.lv[0] = t->own_l0[i];
+            P.flags &= ~kPyrL0Borrowed;
+        }
+    }
+    // the last step's GFTT (early / post-tracker streams) still reads a frame:
+    // the caller's stream waits for it, so synchronising that stream covers
+    // every read of the caller's frames
+    if (rc == TBDK_OK && t->post_wait) rc = map_status(wait_if_pending(s, t->post_wait));
+    return rc;
+}
+
 int release(tbdk_tbd* t)
 {
     if (!t) return TBDK_OK;
@@ -588,6 +634,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         release(t);
         return rc;
     }
+    for (int i = 0; i < 3; ++i) t->own_l0[i] = t->pyr[i].lv[0];
     const size_t S = (size_t)cfg->max_tracks;
     hipError_t e = hipSuccess;
     auto dm = [&](void** p, size_t bytes) {
@@ -830,7 +877,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (e != hipSuccess) return map_status(e);
     }
     if (!la_valid) {
-        rc = tbdk_pyr_build(t->ctx, frame, pitch, &P, s);
+        rc = build_pyr(t, frame, pitch, P, s);
         if (rc != TBDK_OK) return rc;
         hipError_t e = hipEventRecord(t->pyr_ready, s);
         if (e != hipSuccess) return map_status(e);
@@ -1081,7 +1128,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         t->la_pitch = next_pitch;
         t->la_stream = ps;
         t->la_pyr = true;
-        const int r = tbdk_pyr_build(t->ctx, next, next_pitch, &Pnext, ps);
+        const int r = build_pyr(t, next, next_pitch, Pnext, ps);
         if (r != TBDK_OK) return r;
         return map_status(hipEventRecord(t->la_ready, ps));  // the next frame's pyramid (and this fit) done
     };
@@ -1564,14 +1611,24 @@ int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first
     for (int i = 0; i < nframes; ++i)
         if (!frames[i] || det_offsets[i + 1] < det_offsets[i] || det_offsets[i] < 0) return TBDK_EINVAL;
     if (nframes > 0 && det_offsets[nframes] > det_offsets[0] && !dets) return TBDK_EINVAL;
+    // ctx option tbd_borrow_l0: the frames stay valid for the whole call, so
+    // their pyramids take them as level 0 (derivative-plane pyramids excepted)
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    t->borrow = t->ctx->opt_tbd_borrow_l0 && !t->ctx->opt_tbd_pyr_derivs && t->ctx->opt_pyr_fuse &&
+                t->cfg.width >= 2 * (t->cfg.win + 2) && t->cfg.height >= 2 * (t->cfg.win + 2);
     for (int i = 0; i < nframes; ++i) {
         const uint8_t* next = i + 1 < nframes ? frames[i + 1] : nullptr;
         int rc = step_impl(t, frames[i], pitch, first_frame_id + i, dets ? dets + det_offsets[i] : nullptr,
-                           det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr,
-                           static_cast<hipStream_t>(stream));
-        if (rc != TBDK_OK) return finish(t, rc);
+                           det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr, s);
+        if (rc != TBDK_OK) {
+            (void)finish(t, TBDK_OK);
+            (void)end_borrow(t, s);
+            return rc;
+        }
     }
-    return finish(t, TBDK_OK);
+    const int rc = finish(t, TBDK_OK);
+    const int rb = end_borrow(t, s);
+    return rc != TBDK_OK ? rc : rb;
 }
 
 int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,

@@ -102,6 +102,7 @@ struct tbdk_ctx {
     int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
     int opt_gftt_compact = 1;    // tbdk_ctx_set_option("gftt_compact"): GFTT writes only its candidates' values
+    int opt_tbd_borrow_l0 = 0;   // tbdk_ctx_set_option("tbd_borrow_l0"): tbdk_tbd_run's pyramids take the frame as level 0 (A/B)
     int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
@@ -149,8 +150,22 @@ hipError_t launch_pyr_down_plain(const uint8_t* src, int w, int h, int spitch, u
 // Scharr derivative planes (interior only; the zero frame is written once at allocation)
 hipError_t launch_scharr_levels(const tbdk_pyr& pyr, hipStream_t s);
 // every u8 level of pyr from the frame (fused launches where the levels allow)
+// skip_l0: levels 1.. only, level 0 being the frame itself (pyr.lv[0] already
+// points at it, pad 0; the two-role launch with no copy role)
 hipError_t launch_pyr_levels(const uint8_t* img, int pitch, const tbdk_pyr& pyr, int fuse, int rows, int xcd,
-                             hipStream_t s);
+                             hipStream_t s, bool skip_l0 = false);
+// tbdk_pyr.flags bit (internal): level 0 is borrowed -- lv[0] is the caller's
+// frame (pad 0), built by pyr_build_borrowed for the TBD loop; only the
+// several-points-per-wave PyrLK kernel reads such a level (reflect-101 at its
+// edges by coordinates)
+constexpr int32_t kPyrL0Borrowed = 1 << 30;
+// the u8 levels-only pyramid of a frame with level 0 borrowed from the frame
+// (no padded copy); own_l0: the pyramid's own level-0 buffer, restored by
+// pyr_restore_l0
+int pyr_build_borrowed(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, hipStream_t s);
+// a borrowed pyramid's level 0 copied into its own padded buffer (own_l0) and
+// made its level 0 again
+int pyr_restore_l0(tbdk_ctx* ctx, tbdk_pyr* pyr, const tbdk_level& own_l0, hipStream_t s);
 // the fp16 pyramid (klt_f16.hip): level 0 from a u8 (img_f16 = 0) or fp16 frame,
 // the fp16 pyrDown levels and the fp16 derivative pairs
 hipError_t launch_pyr_build_f16(const uint8_t* img, int pitch, int img_f16, const tbdk_pyr& pyr, hipStream_t s);

@@ -300,8 +300,10 @@ def test_loop_traffic_fields_from_committed_loop_summary():
     p = bench.pmc_bytes(["pyr_build_kernel", "pyr_down_padded_kernel"])
     assert p is not None and p["source"].endswith("_pmc_loop.json")
     alg = bench.pyr_build_bytes(1920, 1080, 3)
-    ratio = (p["fetch_raw"] + p["write"]) / alg
-    assert 0.85 < ratio < 1.1, ratio
+    # the summary's build: with the padded level-0 copy (rounds 4-5, early round 6) or with the
+    # frame itself as level 0 (tbd_borrow_l0, round 6)
+    ratios = [(p["fetch_raw"] + p["write"]) / a for a in (alg, bench.pyr_build_bytes(1920, 1080, 3, copy_l0=False))]
+    assert any(0.85 < r < 1.1 for r in ratios), ratios
     lk, src = bench.pmc_traffic("lk_multi_kernel<21, 21, true, false>")  # the name bench.main looks up
     assert src is not None and src.endswith("_pmc_loop.json")
     assert 0 < lk < 2 * alg

@@ -455,3 +455,31 @@ def test_tbd_async_launch_worker_matches(gpu):
         assert r[:4] == res[0][:4]
     assert res[0][4] > F and res[1][4] == res[0][4]  # every PyrLK launch timed, the worker's included
 
+
+
+def test_tbd_run_borrowed_level0_matches_copy(gpu):
+    """tbdk_tbd_run's pyramids taking the caller's frame as level 0 (ctx option
+    tbd_borrow_l0, A/B: no padded copy; PyrLK reads windows across the
+    frame's edge by reflect-101 coordinates) give the same frames as the padded
+    copy, including across consecutive run calls (the last frame's level 0 is
+    copied into the loop's own buffer when a call ends) and a per-frame step
+    after them; a small frame with many objects puts windows on every edge."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 320, 240, 48, 18
+    frames, gt = klt.synth_render(15, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=W, bounds_ymax=H, redetect_every=4)
+    res = []
+    try:
+        for b in (0, 1):
+            gpu.set_option("tbd_borrow_l0", b)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = list(loop.run(frames[:7], 0, dets[:7]))
+            ms += list(loop.run(frames[7:F - 1], 7, dets[7:F - 1]))
+            ms.append(loop.step(frames[F - 1], F - 1, dets[F - 1]))
+            res.append(([_mkey(m) for m in ms], loop.tracks(), sum(m.lk_points for m in ms)))
+            del loop
+    finally:
+        gpu.set_option("tbd_borrow_l0", 0)
+    assert res[0] == res[1] and res[0][2] > 0
