@@ -130,6 +130,11 @@ int tbdk_ctx_destroy(tbdk_ctx* ctx);
  *       kernel derives the window's Scharr values from the u8 level even when
  *       the pyramid has derivative planes (it always does without them;
  *       results equal).
+ *   "lk_solo" (0..100, default 4): the several-points-per-wave PyrLK kernel
+ *       runs a wave's last stepping point on all the wave's lanes (its window
+ *       rows split over the lane groups) once the wave's other points have
+ *       stopped, from Newton step lk_solo of the level on (0: never; padded
+ *       levels only; results equal).
  *   "lk_impl" (0..3): the PyrLK kernel taken when tbdk_lk_params.impl is 0
  *       (the TBD loop's setting): 0 auto, else as tbdk_lk_params.impl
  *       (results equal).

@@ -132,7 +132,12 @@ __device__ __forceinline__ SobelRow sobel_row(float s0, float s1, float s2, floa
 #define TBDK_GFTT_EIG_WAVES 4
 #endif
 constexpr int kEigWaves = TBDK_GFTT_EIG_WAVES;  // row segments (waves) per strip
-constexpr int kEigPref = 8;   // pixel rows in flight per wave
+constexpr int kEigPref = 8;   // pixel rows in flight per wave (the eigenvalue-plane kernel)
+// ... in the compact-candidate kernel: 4 keeps it at <= 128 VGPRs (8: 148),
+// so its waves fit where one of the loop's PyrLK waves (121) has ended
+#ifndef TBDK_GFTT_EIG_PREF_C
+#define TBDK_GFTT_EIG_PREF_C 4
+#endif
 #ifndef TBDK_GFTT_WALK_PRIO
 #define TBDK_GFTT_WALK_PRIO 3  // s_setprio of gftt_select's walking wave
 #endif
@@ -190,7 +195,7 @@ __device__ __forceinline__ void eig_rowsums(const EigLane& g, const SobelRow& p,
 // local-maximum ballot, the values of its set lanes only, in lane order, at the
 // start of the strip row's own columns (column ccol + rank of the lane's bit),
 // which is all gftt_select reads when quality <= 1 (see there).
-template <bool compact>
+template <bool compact, int PREF = compact ? TBDK_GFTT_EIG_PREF_C : kEigPref>
 __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict__ E, uint64_t* __restrict__ lm,
                                             int w, int ep, int y0, int y1, int ys, int ye, int ycap, bool fresh,
                                             double (&S)[3], double (&S0)[3], double (&Scap)[3], int& best, int ccol)
@@ -291,24 +296,27 @@ __device__ __forceinline__ void eig_segment(const EigLane& g, float* __restrict_
     int sb = min(min(y1, H - 1), ye);
     if (ycap >= 0) sb = min(sb, ycap);
     int y = ys;
-    if (sb - sa >= kEigPref) {
+    if (sb - sa >= PREF) {
         for (; y < sa; ++y) generic(y);
-        float nxt[kEigPref];
+        float nxt[PREF];
 #pragma unroll
-        for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(y + 2 + j);
-        for (; y + kEigPref <= sb; y += kEigPref) {
-            float cur[kEigPref];
+        for (int j = 0; j < PREF; ++j) nxt[j] = pix_fwd(y + 2 + j);
+        for (; y + PREF <= sb; y += PREF) {
+            float cur[PREF];
 #pragma unroll
-            for (int j = 0; j < kEigPref; ++j) cur[j] = nxt[j];
+            for (int j = 0; j < PREF; ++j) cur[j] = nxt[j];
 #pragma unroll
-            for (int j = 0; j < kEigPref; ++j) nxt[j] = pix_fwd(min(y + kEigPref + 2 + j, H));  // in flight
+            for (int j = 0; j < PREF; ++j) nxt[j] = pix_fwd(min(y + PREF + 2 + j, H));  // in flight
 #pragma unroll
-            for (int j = 0; j < kEigPref; ++j) row(std::true_type{}, y + j, cur[j], true, true, true);
+            for (int j = 0; j < PREF; ++j) row(std::true_type{}, y + j, cur[j], true, true, true);
         }
     }
     for (; y < ye; ++y) generic(y);
 }
 
+// compact (GfttArgs::compact, see eig_segment): one instantiation per mode,
+// so each has its own register budget
+template <bool compact>
 __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
 {
     __shared__ double s_cap[kEigWaves][3][64];
@@ -355,7 +363,6 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     // local-maximum words of this strip (ROIs of at least 3x3; never written otherwise)
     uint64_t* lm = a.lmax + R.moff + (size_t)strip * H;
     const bool has_lm = R.w >= 3 && H >= 3;
-    const bool compact = a.compact != 0;
     const int ccol = strip * kGfttStrip;  // the strip's first output column
 
     const int L = (H + kEigWaves - 1) / kEigWaves;  // own rows per segment
@@ -384,12 +391,8 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
     };
     GFTT_ESTAMP(0);
     if (live) {
-        if (compact)
-            eig_segment<true>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0,
-                              Scap, best, ccol);
-        else
-            eig_segment<false>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0,
-                               Scap, best, ccol);
+        eig_segment<compact>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, true, S, S0,
+                             Scap, best, ccol);
         if (ycap >= 0) {
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -417,12 +420,8 @@ __global__ __launch_bounds__(64 * kEigWaves) void gftt_eig_kernel(GfttArgs a)
         __syncthreads();  // s_cap is rewritten below
         if (wv >= bad && live) {
             best = INT_MIN;
-            if (compact)
-                eig_segment<true>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S,
-                                  S0, Scap, best, ccol);
-            else
-                eig_segment<false>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S,
-                                   S0, Scap, best, ccol);
+            eig_segment<compact>(g, E, has_lm ? lm : nullptr, R.w, gftt_epitch(R.w), y0, y1, ys, ye, ycap, false, S,
+                                 S0, Scap, best, ccol);
             if (ycap >= 0) {
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) s_cap[wv][ch][lane] = Scap[ch];
@@ -1190,13 +1189,15 @@ void gftt_plan(GfttArgs& a, int max_area)
 
 hipError_t launch_gftt_eig(const GfttArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
+    if (a.compact) hipLaunchKernelGGL(gftt_eig_kernel<true>, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
+    else hipLaunchKernelGGL(gftt_eig_kernel<false>, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_gftt(const GfttArgs& a, hipStream_t s, hipEvent_t after_eig)
 {
-    hipLaunchKernelGGL(gftt_eig_kernel, dim3(a.ncblk), dim3(64 * kEigWaves), 0, s, a);
+    const hipError_t e0 = launch_gftt_eig(a, s);
+    if (e0 != hipSuccess) return e0;
     if (after_eig) {
         const hipError_t e = hipEventRecord(after_eig, s);
         if (e != hipSuccess) return e;

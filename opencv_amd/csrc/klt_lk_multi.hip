@@ -82,17 +82,21 @@ __device__ __forceinline__ uint32_t seg_total(uint32_t scanned, int e4, int s4)
 // exact int64 sum of the other kernels.  e4 / s4: byte addresses of the point's
 // last lane and of the lane before its first.
 //
-// Fast path, taken by the whole wave when every partial lies in (-2^26, 2^26):
-// a point's total is then below 31 * 2^26 < 2^31 in magnitude (windows up to
-// 31 wide), exact as a modulo-2^32 difference of plain scans, and its int ->
-// float conversion is the same single rounding.
-template <int N>
+// Fast path, taken by the whole wave when every partial lies in (-2^FB, 2^FB):
+// a point's total is then below 31 * 2^26 < 2^31 in magnitude (FB 26: windows
+// up to 31 wide), or 63 * 2^25 (FB 25: a point spread over all 63 lanes, the
+// one-point steps below), exact as a modulo-2^32 difference of plain scans, and
+// its int -> float conversion is the same single rounding.  The split path
+// holds for segments of up to 63 lanes (lo totals below 63 * 2^26 < 2^32, hi
+// totals in [-16 * 63, 15 * 63], inside an 11-bit field).
+template <int N, int FB = 26>
 __device__ __forceinline__ void seg_sum_exact(const int (&v)[N], int e4, int s4, float (&out)[N], bool* split = nullptr)
 {
     static_assert(N >= 1 && N <= 3, "three 11-bit fields per packed scan");
+    static_assert(FB <= 26, "hi parts are v >> 26");
     bool big = false;
 #pragma unroll
-    for (int k = 0; k < N; ++k) big |= (uint32_t)v[k] + (1u << 26) >= (1u << 27);
+    for (int k = 0; k < N; ++k) big |= (uint32_t)v[k] + (1u << FB) >= (2u << FB);
     const bool slow = __builtin_amdgcn_ballot_w64(big) != 0;  // wave-uniform
     if (split) *split = slow;
     if (!slow) {
@@ -243,6 +247,7 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
     constexpr int IM = FLY ? TBDK_LK_IPACK_FLY : TBDK_LK_IPACK;
     constexpr bool IPACK = IM == 1, ILIN = IM == 2;
     constexpr bool GL = TBDK_LK_GLDS != 0;
+    constexpr bool kSoloOk = P >= 2 && !GL && !ILIN;  // one-point steps (LkArgs::solo_min)
     // GL: this wave's (Ix, Iy) row pairs, [row pair][lane] (8 B per lane: b64 accesses)
     __shared__ uint2 sg[GL ? NP * kMultiWaves : 1][64];
     const int lane = threadIdx.x & 63;
@@ -622,6 +627,136 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
         D = 1.f / D;
 
         float pdx = 0.f, pdy = 0.f;
+        // The remaining Newton steps of point ks, the wave's only active one, from
+        // step j on (the stepping of the loop below, the same integers and float
+        // operations): its window's rows are dealt to the P lane groups, group g
+        // holding row pairs [g*NPG, (g+1)*NPG) of every column (the I terms and
+        // the interpolated Ix / Iy pairs moved over by ds_bpermute from the
+        // point's own lanes, the J rows loaded per group), so a step costs each
+        // lane NPG row pairs instead of NP; the per-point values are broadcast
+        // from the point's first lane and the result goes back to its lanes.
+        auto solo_steps = [&](int ks, int j) {
+            constexpr int NPG = (NP + P - 1) / P;  // row pairs per lane group
+            constexpr int RG = 2 * NPG;            // window rows per lane group
+            const int sl = 1 + ks * WW;            // the point's first lane
+            const int src = k < P ? 4 * (sl + x) : 0;  // this lane's column of the point (bpermute address)
+            const int g = k < P ? k : 0;
+            uint32_t gx2[NPG], gy2[NPG], ip2[IPACK ? NPG : 1];
+            int ic2[IM == 0 ? RG : 1];
+#pragma unroll
+            for (int t = 0; t < NPG; ++t) gx2[t] = gy2[t] = 0u;
+            if constexpr (IPACK) {
+#pragma unroll
+                for (int t = 0; t < NPG; ++t) ip2[t] = 0u;
+            }
+            if constexpr (IM == 0) {
+#pragma unroll
+                for (int t = 0; t < RG; ++t) ic2[t] = 0;
+            }
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const uint32_t tx = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gxk[q]);
+                const uint32_t ty = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gyk[q]);
+                gx2[q % NPG] = g == q / NPG ? tx : gx2[q % NPG];
+                gy2[q % NPG] = g == q / NPG ? ty : gy2[q % NPG];
+                if constexpr (IPACK) {
+                    const uint32_t ti = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ipk[q]);
+                    ip2[q % NPG] = g == q / NPG ? ti : ip2[q % NPG];
+                }
+            }
+            if constexpr (IM == 0) {
+#pragma unroll
+                for (int r = 0; r < WH; ++r) {
+                    const int ti = __builtin_amdgcn_ds_bpermute(src, ic[r]);
+                    ic2[r % RG] = g == r / RG ? ti : ic2[r % RG];
+                }
+            }
+            if (k >= P) {  // lane 0 (and lanes past the last point) add nothing
+#pragma unroll
+                for (int t = 0; t < NPG; ++t) gx2[t] = gy2[t] = 0u;
+            }
+            auto bc = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), sl)); };
+            float snx = bc(nextx), sny = bc(nexty), sox = bc(outx), soy = bc(outy), spdx = bc(pdx), spdy = bc(pdy);
+            const float sA11 = bc(A11), sA12 = bc(A12), sA22 = bc(A22), sD = bc(D);
+            // rows rbase .. rbase + RG of the window at J origin (jx0, jy0) of a padded
+            // level (an unpadded one takes no one-point steps); rows past the window
+            // (the last group) feed only pairs whose Ix / Iy halves are zero, and a
+            // row past the level's buffer reads 0
+            const int rbase = g * RG;
+            uint32_t jp2[RG + 1];
+            auto load_j2 = [&](int jx0, int jy0) {
+                const uint32_t joff = (uint32_t)((jy0 + rbase + L.jpad) * L.jpitch + jx0 + x + L.jpad);
+#pragma unroll
+                for (int r = 0; r <= RG; ++r) jp2[r] = load_pair_u8_ua(rJ, joff, r * L.jpitch);
+            };
+            int qx = INT_MIN, qy = 0, snit = 0;
+            bool sout = false;
+            for (; j < a.max_count; ++j) {
+                const int inx = (int)floorf(snx), iny = (int)floorf(sny);
+                if (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h) {
+                    sout = true;
+                    break;
+                }
+                ++snit;
+#ifdef TBDK_LK_TRACE
+                ++tr_steps;
+#endif
+                if (inx != qx || iny != qy) {
+#ifdef TBDK_LK_TRACE
+                    ++tr_reloads;
+#endif
+                    load_j2(inx, iny);
+                    qx = inx;
+                    qy = iny;
+                }
+                uint32_t v0, v1;
+                bilinear_weights(snx - inx, sny - iny, v0, v1);
+                int b[2] = {0, 0};
+#pragma unroll
+                for (int t = 0; t < NPG; ++t) {
+                    uint32_t d;
+                    if constexpr (IPACK) {
+                        const uint32_t jv = pack_diff(bilin_s<0>(jp2[2 * t], jp2[2 * t + 1], v0, v1, rnd9),
+                                                      bilin_s<0>(jp2[2 * t + 1], jp2[2 * t + 2], v0, v1, rnd9));
+                        d = as_u32(as_s16x2(jv) - as_s16x2(ip2[t]));
+                    } else {
+                        d = pack_diff(bilin_c(jp2[2 * t], jp2[2 * t + 1], v0, v1, ic2[2 * t]),
+                                      bilin_c(jp2[2 * t + 1], jp2[2 * t + 2], v0, v1, ic2[2 * t + 1]));
+                    }
+                    b[0] = sdot2(d, gx2[t], b[0]);
+                    b[1] = sdot2(d, gy2[t], b[1]);
+                }
+                float fb[2];
+                seg_sum_exact<2, 25>(b, 4 * (P * WW), 0, fb);  // lanes 1 .. P*WW (lane 0 adds 0)
+                const float fb1 = fb[0] * FLT_SCALE;
+                const float fb2 = fb[1] * FLT_SCALE;
+                const float ddx = (sA12 * fb2 - sA22 * fb1) * sD;
+                const float ddy = (sA12 * fb1 - sA11 * fb2) * sD;
+                snx += ddx;
+                sny += ddy;
+                sox = snx + halfx;
+                soy = sny + halfy;
+                if ((double)ddx * ddx + (double)ddy * ddy <= a.eps2) break;
+                if (j > 0 && (double)fabsf(ddx + spdx) < 0.01 && (double)fabsf(ddy + spdy) < 0.01) {
+                    sox -= ddx * 0.5f;
+                    soy -= ddy * 0.5f;
+                    break;
+                }
+                spdx = ddx;
+                spdy = ddy;
+            }
+            if (k == ks) {
+                outx = sox;
+                outy = soy;
+#ifdef TBDK_LK_PROBE_ITERS_LV
+                nit += snit << (8 * level);
+#else
+                nit += snit;
+#endif
+                if (sout && level == 0) status = 0;
+            }
+            act = false;
+        };
         for (int j = 0; j < a.max_count; ++j) {
             if (!any_lane(act)) break;
 #ifdef TBDK_LK_TRACE
@@ -630,12 +765,28 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
 #if TBDK_LK_PRIO_STEPS > 0
             if (++wsteps == TBDK_LK_PRIO_STEPS) __builtin_amdgcn_s_setprio(3);
 #endif
+            if constexpr (kSoloOk) {
+                // one point left stepping (LkArgs::solo_min): its remaining steps
+                // on all the wave's lanes, the window rows split over the P lane
+                // groups (solo_steps); then the level's Newton phase is over
+                if (a.solo_min > 0 && j >= a.solo_min && L.jpad > 0) {
+                    const uint64_t heads = __builtin_amdgcn_ballot_w64(act && x == 0 && k < P);
+                    if (__builtin_popcountll(heads) == 1) {
+                        solo_steps((__builtin_ctzll(heads) - 1) / WW, j);
+                        break;
+                    }
+                }
+            }
             const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
             if (act && (inx < -WW || inx >= L.w || iny < -WH || iny >= L.h)) {
                 if (level == 0) status = 0;
                 act = false;
             }
+#ifdef TBDK_LK_PROBE_ITERS_LV  // probe builds: the Newton steps per level, 8 bits each (level L at bit 8L)
+            nit += act ? 1 << (8 * level) : 0;
+#else
             nit += act ? 1 : 0;
+#endif
             const bool moved = act && (inx != pinx || iny != piny);
 #ifdef TBDK_LK_PROBE_RELOADS  // tuning builds: 1 always reloads, 2 counts reloads into iters, 3 never reloads
 #if TBDK_LK_PROBE_RELOADS == 2

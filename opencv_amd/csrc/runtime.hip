@@ -283,6 +283,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_lk_seg_inline = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "lk_solo") == 0) {
+        if (value < 0 || value > 100) return TBDK_EINVAL;
+        ctx->opt_lk_solo = (int)value;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "lk_impl") == 0) {  // kernel used when tbdk_lk_params.impl is 0 (auto)
         if (value < 0 || value > 3) return TBDK_EINVAL;
         ctx->opt_lk_impl = (int)value;
@@ -664,6 +669,7 @@ int tbdk::lk_internal(tbdk_ctx* ctx, const tbdk_pyr* prev, const tbdk_pyr* next,
             a.seg_list = nullptr;
         }
     }
+    a.solo_min = ctx->opt_lk_solo;
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     bool have_d = true;

@@ -80,6 +80,7 @@ struct tbdk_ctx {
     int opt_pyr_xcd = 1;       // tbdk_ctx_set_option("pyr_xcd"): pyramid roles' row bands per XCD
     int opt_pyr_rows = 1;      // tbdk_ctx_set_option("pyr_rows"): rows per thread of the two-role u8 build (1, 2, 4)
     int opt_pyr_fuse = 1;      // tbdk_ctx_set_option("pyr_fuse"): 1 the two-role launch + one per level, 2 levels 0-2 in one tiled launch (slower, A/B), 0 one launch per level
+    int opt_lk_solo = 4;       // tbdk_ctx_set_option("lk_solo"): LkArgs::solo_min of the lk_multi launches
     int opt_lk_scharr_fly = 0; // tbdk_ctx_set_option("lk_scharr_fly"): lk_multi derives Ix/Iy itself
     int opt_lk_impl = 0;        // tbdk_ctx_set_option("lk_impl"): PyrLK kernel under impl 0
     int opt_lk_seg_inline = 1;  // tbdk_ctx_set_option("lk_seg_inline"): segment lists in the kernel arguments
@@ -220,6 +221,10 @@ struct LkArgs {
     // the TBD loop's lists live in pinned host memory (zero-copy), where every
     // wave's first load would be a round trip over the host link
     uint16_t seg_inl[kSegInline];
+    // lk_multi: a wave whose other points have stopped runs its last point's
+    // remaining Newton steps on all its lanes from step solo_min on (0: never;
+    // ctx option lk_solo)
+    int solo_min;
 #ifdef TBDK_LK_TRACE
     unsigned trace_base;  // probe builds: first trace record of this launch (klt_lk_multi.hip)
 #endif

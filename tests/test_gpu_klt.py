@@ -326,6 +326,64 @@ def test_lk_1080p_full_size(gpu, impl):
     assert_tolerance(g, sse, ex=ex)
 
 
+@pytest.mark.parametrize("solo", [1, 3])
+def test_lk_one_point_steps_bit_exact(gpu, solo):
+    """ctx option lk_solo: a wave whose other points have stopped runs its last
+    point's remaining Newton steps from step `solo` on with the window's rows
+    split over all its lanes; next_pts / status / err / iteration counts equal
+    the exact-order oracle for windows 7..31 (1..9 points per wave), the
+    lo/hi-split sums, the edge points and flags, levels-only (Scharr on the fly)
+    and derivative-plane pyramids"""
+    K = klt()
+    gpu.set_option("lk_solo", solo)
+    try:
+        fr, _ = O.synth(20261015, 640, 480, 32, 0, 2)
+        pts = grid_points(480, 640, 6, 2)
+        g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, impl=3)
+        assert_exact(g, ex)
+        fr, _ = O.synth(77, 320, 240, 12, 3, 2)
+        pts = grid_points(240, 320, 7, 0) + np.float32([0.37, 0.61])
+        for win, maxlev in (((7, 7), 2), ((13, 13), 3), ((21, 21), 3), ((31, 31), 2)):
+            g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, win, maxlev, 30, impl=3)
+            assert_exact(g, ex)
+        fr, _ = O.synth(9, 200, 150, 6, 0, 2)
+        pts = np.array([[-100, -100], [1e4, 5], [0, 0], [199.9, 149.9], [-21.0, 50.0], [-20.5, 3.0], [210.0, 160.0],
+                        [100.5, 75.5], [3.2, 147.9], [-10.0, -10.0], [219.0, 169.0], [-31.0, 80.0]], np.float32)
+        for flags, init in ((0, None), (8, None), (4, pts + np.float32([1.5, -0.5]))):
+            g, ex, _ = run_pair(gpu, fr[0], fr[1], pts, flags=flags, init=init, impl=3)
+            assert_exact(g, ex)
+        rng = np.random.default_rng(5)
+        a = (rng.integers(0, 2, (120, 160)) * 255).astype(np.uint8).repeat(2, 0).repeat(2, 1)
+        b = np.roll(a, (1, -2), (0, 1))
+        b[rng.random(b.shape) < 0.1] ^= 255
+        pts = grid_points(240, 320, 9, 0) + np.float32([0.43, 0.27])
+        for win, maxlev in (((21, 21), 2), ((31, 31), 1)):
+            g, ex, _ = run_pair(gpu, a, b, pts, win, maxlev, 30, impl=3)
+            assert_exact(g, ex)
+        # levels-only pyramids (the TBD loop's instance) against the planes instance
+        fr, _ = K.synth_render(52, 640, 480, 24, 0, 2, ctx=gpu)
+        pts = np.random.default_rng(21).uniform([-12, -12], [652, 492], (3000, 2)).astype(np.float32)
+        lk = K.SparsePyrLKOpticalFlow((21, 21), 2, 30)
+        out = []
+        for d in (True, False):
+            Pa = K.build_pyramid(fr[0], (21, 21), 2, ctx=gpu, derivs=d)
+            Pb = K.build_pyramid(fr[1], (21, 21), 2, ctx=gpu, derivs=d)
+            r = lk.calc(Pa, Pb, to_dev(pts), want_iters=True)
+            torch.cuda.synchronize()
+            out.append([r.next_pts.cpu().numpy(), r.status.cpu().numpy(), r.err.cpu().numpy(), r.iters.cpu().numpy()])
+        gpu.set_option("lk_solo", 0)
+        Pa = K.build_pyramid(fr[0], (21, 21), 2, ctx=gpu, derivs=False)
+        Pb = K.build_pyramid(fr[1], (21, 21), 2, ctx=gpu, derivs=False)
+        r = lk.calc(Pa, Pb, to_dev(pts), want_iters=True)
+        torch.cuda.synchronize()
+        base = [r.next_pts.cpu().numpy(), r.status.cpu().numpy(), r.err.cpu().numpy(), r.iters.cpu().numpy()]
+        for o in out:
+            for u, v in zip(o, base):
+                assert np.array_equal(u, v)
+    finally:
+        gpu.set_option("lk_solo", 4)
+
+
 def _sample_hash(i):
     """splitmix64(i): the library times launch i iff this % timing_every == 0"""
     M = (1 << 64) - 1

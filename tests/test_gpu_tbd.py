@@ -483,3 +483,30 @@ def test_tbd_run_borrowed_level0_matches_copy(gpu):
     finally:
         gpu.set_option("tbd_borrow_l0", 0)
     assert res[0] == res[1] and res[0][2] > 0
+
+
+def test_tbd_run_one_point_steps_match(gpu):
+    """ctx option lk_solo (a wave's last stepping point on all its lanes) inside
+    the frame loop: the same per-frame metrics (PyrLK iteration totals included)
+    and tracks as without it, through tbdk_tbd_run and per-frame steps."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 40, 16
+    frames, gt = klt.synth_render(29, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=4)
+    res = []
+    try:
+        for solo in (0, 2, 5):
+            gpu.set_option("lk_solo", solo)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            stepped = tbd.TbdLoop(c, ctx=gpu)
+            mt = [_mkey(stepped.step(frames[f], f, dets[f])) for f in range(F)]
+            res.append(([_mkey(m) for m in ms], [m.lk_iters for m in ms], loop.tracks(), mt, stepped.tracks()))
+            del loop, stepped
+    finally:
+        gpu.set_option("lk_solo", 4)
+    assert sum(res[0][1]) > 0
+    for r in res[1:]:
+        assert r == res[0]

@@ -45,3 +45,10 @@ def test_streaming_kernels_use_no_lds(res):
 def test_loop_pyrlk_fits_four_waves_per_simd(res):
     k = [k for k in res if "lk_multi_kernelILi21ELi21ELb1E" in k]
     assert len(k) == 1 and res[k[0]]["vgpr_count"] <= 128, res.get(k[0] if k else None)
+
+
+def test_compact_gftt_eig_fits_beside_one_pyrlk_wave(res):
+    """the loop's GFTT eigenvalue kernel (compact candidates) stays at <= 128
+    VGPRs, so its waves fit a SIMD slot one ending PyrLK wave frees"""
+    k = [k for k in res if "gftt_eig_kernelILb1E" in k]
+    assert len(k) == 1 and res[k[0]]["vgpr_count"] <= 128, res.get(k[0] if k else None)
