@@ -178,11 +178,12 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       system-scope flag in pinned memory that the host polls, instead of an
  *       event recorded behind the fit (whose marker held the next frame's
  *       pyramid back; results equal).
- *   "tbd_early_order" (0/1/2, default 1): where a step launches its early
- *       GFTT: 0 first, 1 after the critical refreshed-set PyrLK (its host
- *       setup no longer delays that launch, and the PyrLK waves are dispatched
- *       ahead of the GFTT's), 2 after the fit and the next frame's pyramid,
- *       before the host waits for the fit (results equal).
+ *   "tbd_early_order" (0/1/2, default 0): where a step launches its early
+ *       GFTT (and, tbd_gftt_ahead, the next frame's): 0 first, 1 after the
+ *       critical refreshed-set PyrLK (its host setup no longer delays that
+ *       launch, and the PyrLK waves are dispatched ahead of the GFTT's), 2 after
+ *       the fit and the next frame's pyramid, before the host waits for the fit
+ *       (results equal).
  *   "tbd_early_prio" (0/1, default 0; taken by tbdk_tbd_create): the early
  *       GFTT's stream at the lowest (0) or highest (1) priority (results equal).
  *   "tbd_pyr_derivs" (0/1, default 0; taken by tbdk_tbd_create): the loop's
@@ -209,7 +210,7 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *   "tbd_post_direct" (0/1, default 1): after a step that runs no post-tracker
  *       GFTT, the next step's refreshed-set PyrLK waits for the early GFTT's
  *       completion directly rather than through the post-tracker stream's
- *       event (not with tbd_early_order 0; results equal).
+ *       event (results equal).
  *   "tbd_la_defer" (0/1, default 0): the look-ahead PyrLK of the unchanged
  *       sets is launched by the next step right after its critical PyrLK
  *       instead of at the end of its own step (results equal; A/B runs).
@@ -217,6 +218,13 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       min-eigenvalue) writes no eigenvalue plane, only its local maxima's
  *       values per strip row (corner lists equal; quality > 1, Harris and other
  *       block sizes keep the plane).
+ *   "tbd_gftt_ahead" (0/1, default 1): inside tbdk_tbd_run each step also
+ *       launches the NEXT frame's early GFTT over its new-track ROIs (that
+ *       frame's detections beyond the bounds filter), over the caller's next
+ *       frame, so the refreshed-set PyrLK of the step after it does not wait for
+ *       a GFTT launched only one step earlier; the step of that frame launches
+ *       just the ROIs it misses (re-detection guesses).  The caller's stream
+ *       waits for that work before the call returns (results equal).
  *   "tbd_borrow_l0" (0/1, default 0): inside tbdk_tbd_run the loop's pyramids
  *       take the caller's frames as level 0 (no padded copy; PyrLK reads
  *       windows across a frame's edge by reflect-101 coordinates, the values

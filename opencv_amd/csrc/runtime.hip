@@ -283,6 +283,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_lk_seg_inline = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_gftt_ahead") == 0) {
+        ctx->opt_tbd_gftt_ahead = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "lk_solo") == 0) {
         if (value < 0 || value > 100) return TBDK_EINVAL;
         ctx->opt_lk_solo = (int)value;

@@ -47,6 +47,8 @@
 namespace tbdk {
 
 constexpr int kSlotPts = 256;  // corner capacity per track
+constexpr int kEarlySets = 3;  // early GFTT row sets (this step's, the next frame's ahead, the previous step's)
+constexpr int kRowSets = 2 + kEarlySets;  // rows of the slot arrays, in units of max_tracks (see tbdk_tbd::src_row)
 
 struct FitEntry {
     int slot;
@@ -396,19 +398,33 @@ struct tbdk_tbd {
     GfttRoi* h_tab = nullptr;
     // GFTT rows: the corner sets of refreshed tracks stay where GFTT writes them
     // and are tracked from there; the next fit compacts the tracked points into
-    // the slot.  Rows of the slot arrays: [0, S) slots, [S, 3S) the early GFTT's
-    // rows (two sets by step parity eb, see early_s), [3S, 4S) the post-tracker
-    // GFTT's rows.  src_row[slot] = the refreshed set's row until the next fit.
+    // the slot.  Rows of the slot arrays: [0, S) slots, [S, 4S) the early GFTT's
+    // rows (three sets by step, eb: this step's, eb + 1 the next frame's GFTT
+    // launched ahead, eb + 2 the previous step's, read by this step's PyrLK and
+    // fit), [4S, 5S) the post-tracker GFTT's rows.  src_row[slot] = the
+    // refreshed set's row until the next fit.
     std::vector<int> src_row;
     std::vector<int> src_list;
-    // early GFTT (see the top of the file): ROI tables double-buffered by step
-    // parity (pinned; a table is rewritten two steps later, after a fit sync
-    // that orders its upload), device table, corner rows and counts
-    GfttRoi* h_etab[2] = {nullptr, nullptr};
+    // early GFTT (see the top of the file): ROI tables by row set (pinned; a
+    // table is rewritten three steps later, after fit syncs that order its
+    // upload), device table, corner rows and counts
+    GfttRoi* h_etab[kEarlySets] = {nullptr, nullptr, nullptr};
     GfttRoi* d_etab = nullptr;
     int eb = 0;  // early-row set of this step
     std::vector<tbdk_roi> erois;                  // this step's early ROIs
     FlatMap<uint64_t> erow_of;                    // ROI box -> early corner row
+    // the next frame's early GFTT launched ahead by tbdk_tbd_run (ctx option
+    // tbd_gftt_ahead): the new-track ROIs of that frame's detections, in row set
+    // eb + 1, over the caller's frame; the step of that frame takes them over
+    // and launches only the ROIs they miss (re-detection guesses)
+    int ahead_id = INT_MIN;
+    const uint8_t* ahead_frame = nullptr;
+    int ahead_pitch = 0;
+    int ahead_set = -1;                           // row set of an ahead launch not yet taken over
+    bool ahead_any = false;                       // an ahead launch in this tbdk_tbd_run call
+    hipEvent_t ahead_tail = nullptr;              // tbdk_tbd_run's end: the early stream's work on its frames
+    std::vector<tbdk_roi> ahead_rois;
+    FlatMap<uint64_t> ahead_row_of;
     std::vector<int> det_order;                   // scratch: detections by left edge
     GfttScratch gftt;   // the early GFTT's (early_s); the loop's own, not the context's
     GfttScratch gftt2;  // the post-tracker GFTT's (side), so the next step's early GFTT need not wait for it
@@ -429,7 +445,7 @@ struct tbdk_tbd {
     int fit_tag = 0;
     hipStream_t early_s = nullptr;                // lowest priority: off the critical path
     bool own_side = false, own_la = false, own_early = false;  // created here, not the context's
-    hipEvent_t early_done = nullptr;
+    hipEvent_t early_done[kEarlySets] = {nullptr, nullptr, nullptr};  // per row set: its last GFTT launch done
     // host bookkeeping; slots are handed out lowest-first so the LK launch
     // covers only [0, max live slot] x 256 points
     std::priority_queue<int, std::vector<int>, std::greater<int>> free_slots;
@@ -547,7 +563,9 @@ int release(tbdk_tbd* t)
     if (t->pyr_ready) (void)hipEventDestroy(t->pyr_ready);
     if (t->early_s) (void)hipStreamSynchronize(t->early_s);
     if (t->early_s && t->own_early) (void)hipStreamDestroy(t->early_s);
-    if (t->early_done) (void)hipEventDestroy(t->early_done);
+    for (hipEvent_t& ev : t->early_done)
+        if (ev) (void)hipEventDestroy(ev);
+    if (t->ahead_tail) (void)hipEventDestroy(t->ahead_tail);
     gftt_scratch_free(t->gftt);
     gftt_scratch_free(t->gftt2);
     if (t->up_s) (void)hipStreamSynchronize(t->up_s);
@@ -653,11 +671,11 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
         else dm(d, bytes);
     };
     // 4 S rows: the slots, two sets of early GFTT rows, the post-tracker GFTT rows
-    dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * 4 * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * 4 * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_status), 4 * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * 4 * S * kSlotPts);
-    dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * 4 * S);
+    dm(reinterpret_cast<void**>(&t->slot_pts), sizeof(float2) * kRowSets * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_next), sizeof(float2) * kRowSets * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_status), kRowSets * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_iters), sizeof(int32_t) * kRowSets * S * kSlotPts);
+    dm(reinterpret_cast<void**>(&t->slot_counts), sizeof(int32_t) * kRowSets * S);
     const size_t pre_bytes = (sizeof(FitEntry) + sizeof(int32_t)) * S;
     hm(&t->h_pre, pre_bytes);
     hm(reinterpret_cast<void**>(&t->h_fit), sizeof(FitOut) * S);
@@ -665,15 +683,16 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     hm(reinterpret_cast<void**>(&t->h_la), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_spec), sizeof(int32_t) * S);
     hm(reinterpret_cast<void**>(&t->h_ers), sizeof(int32_t) * S);
-    hm(reinterpret_cast<void**>(&t->h_etab[0]), 2 * sizeof(GfttRoi) * S);
-    if (t->h_etab[0]) t->h_etab[1] = t->h_etab[0] + S;
+    hm(reinterpret_cast<void**>(&t->h_etab[0]), kEarlySets * sizeof(GfttRoi) * S);
+    for (int k = 1; k < kEarlySets; ++k)
+        if (t->h_etab[0]) t->h_etab[k] = t->h_etab[0] + (size_t)k * S;
     sm(&t->d_pre, t->h_pre, pre_bytes);
     sm(reinterpret_cast<void**>(&t->d_fit), t->h_fit, sizeof(FitOut) * S);
     sm(reinterpret_cast<void**>(&t->d_tab), t->h_tab, sizeof(GfttRoi) * S);
     sm(reinterpret_cast<void**>(&t->d_la), t->h_la, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_spec), t->h_spec, sizeof(int32_t) * S);
     sm(reinterpret_cast<void**>(&t->d_ers), t->h_ers, sizeof(int32_t) * S);
-    sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], 2 * sizeof(GfttRoi) * S);
+    sm(reinterpret_cast<void**>(&t->d_etab), t->h_etab[0], kEarlySets * sizeof(GfttRoi) * S);
     t->fit_flag = t->zc && ctx->opt_tbd_fit_flag != 0;
     if (t->fit_flag) {
         hm(reinterpret_cast<void**>(&t->h_flag), 64);
@@ -690,7 +709,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->refreshed.assign((size_t)S, 0);
     t->la_member.assign((size_t)S, 0);
     t->spec_member.assign((size_t)S, 0);
-    t->ers_row.assign((size_t)4 * S, 0);
+    t->ers_row.assign((size_t)kRowSets * S, 0);
     t->b_list.assign((size_t)S, 0);
     t->src_row.assign((size_t)S, -1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->pyr_ready, hipEventDisableTiming);
@@ -734,7 +753,9 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
                                         ctx->opt_tbd_early_prio ? prio_greatest : prio_least);
         if (e == hipSuccess) t->own_early = true;
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->early_done, hipEventDisableTiming);
+    for (hipEvent_t& ev : t->early_done)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ahead_tail, hipEventDisableTiming);
     if (e != hipSuccess) {
         release(t);
         return map_status(e);
@@ -760,6 +781,7 @@ int tbdk_tbd_create(tbdk_ctx* ctx, const tbdk_tbd_config* cfg, tbdk_tbd** out)
     t->slot_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
     t->npts_of = FlatMap<unsigned>(4 * (size_t)cfg->max_tracks);
     t->erow_of = FlatMap<uint64_t>(4 * (size_t)cfg->max_tracks);
+    t->ahead_row_of = FlatMap<uint64_t>(4 * (size_t)cfg->max_tracks);
     if (ctx->opt_tbd_async_la) {
         t->worker = new (std::nothrow) LaunchWorker(ctx->device);
         if (!t->worker) {
@@ -831,7 +853,8 @@ long g_sub_n = 0;
 // while the host tracker runs), and its PyrLK of the unchanged point sets
 // behind the post-tracker GFTT; the next step skips what was done.
 int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const tbdk_detection* dets, int ndets,
-              const uint8_t* next, int next_pitch, tbdk_frame_metrics* metrics, hipStream_t s)
+              const uint8_t* next, int next_pitch, tbdk_frame_metrics* metrics, hipStream_t s,
+              const tbdk_detection* next_dets = nullptr, int next_ndets = -1)
 {
     if (!t || !frame || ndets < 0 || (ndets > 0 && !dets) || pitch < t->cfg.width ||
         (next && next_pitch < t->cfg.width))
@@ -901,13 +924,48 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // PyrLK and fit); the
     // post-tracker phase takes its corners for every refreshed set whose box
     // equals one of these ROIs.
-    t->erois.clear();
-    t->erow_of.clear();
     const int S = c.max_tracks;
-    const int erow0 = S * (1 + t->eb);  // this step's early GFTT rows (the previous step's: the other set)
-    bool early_launched = false;
+    const int erow0 = S * (1 + t->eb);  // this step's early GFTT rows (see tbdk_tbd::src_row)
+    // the ROIs the previous step launched ahead for this frame (tbd_gftt_ahead):
+    // this step's early ROIs start with them, in their rows
+    const bool ahead_in = t->ahead_id == frame_id && t->ahead_frame == frame && t->ahead_pitch == pitch;
+    if (ahead_in) {
+        std::swap(t->erois, t->ahead_rois);
+        std::swap(t->erow_of, t->ahead_row_of);
+    } else {
+        t->erois.clear();
+        t->erow_of.clear();
+        if (t->ahead_set == t->eb) {  // launched for another frame: it may still read this set's pinned table
+            const hipError_t e = hipEventSynchronize(t->early_done[t->eb]);
+            if (e != hipSuccess) return map_status(e);
+        }
+    }
+    t->ahead_id = INT_MIN;
+    t->ahead_set = -1;
+    bool early_launched = ahead_in && !t->erois.empty();
+    // one launch of the early GFTT over rois[0, n) into row set `set` from row
+    // `row0` on, over the image at img (the pinned table at h_etab[set] + tab0)
+    auto early_launch = [&](const tbdk_roi* rois, int n, int set, int tab0, const uint8_t* img, int ipitch) -> int {
+        GfttPlan eplan;
+        GfttRoi* htab = t->h_etab[set] + tab0;
+        int rc2 = gftt_prepare(rois, n, c.width, c.height, &gp, htab, &eplan);
+        if (rc2 != TBDK_OK) return rc2;
+        hipStream_t es = t->early_s;  // ordered at the top of the step
+        const GfttRoi* dtab = t->zc ? t->d_etab + (htab - t->h_etab[0]) : t->d_etab;
+        if (!t->zc) {
+            hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * n, hipMemcpyHostToDevice, es);
+            if (e != hipSuccess) return map_status(e);
+        }
+        const int row0 = S * (1 + set) + tab0;
+        rc2 = gftt_launch(t->ctx, t->gftt, img, ipitch, dtab, eplan, &gp,
+                          reinterpret_cast<float*>(t->slot_pts + (size_t)row0 * kSlotPts), t->slot_counts + row0, es,
+                          nullptr, kSlotPts, htab);
+        if (rc2 != TBDK_OK) return rc2;
+        return map_status(hipEventRecord(t->early_done[set], es));
+    };
     auto launch_early_gftt = [&]() -> int {
         if (!c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
+        const size_t n0 = t->erois.size();  // taken over from the ahead launch
         const bool all_new = t->tracker->getTracks().empty();
         for (int i = 0; i < ndets && (int)t->erois.size() < c.max_tracks; ++i) {
             const tbdk_detection& d = dets[i];
@@ -969,26 +1027,42 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
                 t->erois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
             }
         }
-        if (!t->erois.empty()) {
-            GfttPlan eplan;
-            GfttRoi* htab = t->h_etab[t->eb];
-            int rc2 = gftt_prepare(t->erois.data(), (int)t->erois.size(), c.width, c.height, &gp, htab, &eplan);
-            if (rc2 != TBDK_OK) return rc2;
-            hipStream_t es = t->early_s;  // ordered at the top of the step
-            const GfttRoi* dtab = t->zc ? t->d_etab + (htab - t->h_etab[0]) : t->d_etab;
-            if (!t->zc) {
-                hipError_t e = hipMemcpyAsync(t->d_etab, htab, sizeof(GfttRoi) * t->erois.size(),
-                                              hipMemcpyHostToDevice, es);
-                if (e != hipSuccess) return map_status(e);
-            }
+        if (t->erois.size() > n0) {  // the ROIs no ahead launch covered
             const tbdk_level& L0 = P.lv[0];
-            rc2 = gftt_launch(t->ctx, t->gftt, L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch, dtab, eplan, &gp,
-                              reinterpret_cast<float*>(t->slot_pts + (size_t)erow0 * kSlotPts), t->slot_counts + erow0,
-                              es, nullptr, kSlotPts, htab);
-            if (rc2 != TBDK_OK) return rc2;
-            const hipError_t e = hipEventRecord(t->early_done, es);
-            if (e != hipSuccess) return map_status(e);
+            const int r2 = early_launch(t->erois.data() + n0, (int)(t->erois.size() - n0), t->eb, (int)n0,
+                                        L0.data + (size_t)L0.pad * L0.pitch + L0.pad, L0.pitch);
+            if (r2 != TBDK_OK) return r2;
             early_launched = true;
+        }
+        // the next frame's new-track ROIs (its detections beyond the bounds
+        // filter, as above), launched ahead over the caller's next frame into
+        // the next row set: that frame's step takes them over, so its
+        // refreshed-set PyrLK no longer waits for a GFTT launched one step
+        // before it (tbdk_tbd_run knows the next frame's detections)
+        if (next && next_dets && next_ndets > 0 && t->ctx->opt_tbd_gftt_ahead && !all_new) {
+            const int nb = (t->eb + 1) % kEarlySets;
+            t->ahead_rois.clear();
+            t->ahead_row_of.clear();
+            for (int i = 0; i < next_ndets && (int)t->ahead_rois.size() < c.max_tracks; ++i) {
+                const tbdk_detection& d = next_dets[i];
+                const bool beyond = d.x >= c.bounds_xmax || d.y >= c.bounds_ymax || d.x + d.width < c.bounds_xmin ||
+                                    d.y + d.height < c.bounds_ymin;
+                if (!beyond) continue;
+                const int x0 = std::max(d.x, 0), y0 = std::max(d.y, 0);
+                const int x1 = std::min(d.x + d.width, c.width), y1 = std::min(d.y + d.height, c.height);
+                if (x1 - x0 < 3 || y1 - y0 < 3) continue;
+                if (!t->ahead_row_of.insert(box_key(x0, y0, x1 - x0, y1 - y0), (int)t->ahead_rois.size())) continue;
+                t->ahead_rois.push_back(tbdk_roi{x0, y0, x1 - x0, y1 - y0});
+            }
+            if (!t->ahead_rois.empty()) {
+                const int r2 = early_launch(t->ahead_rois.data(), (int)t->ahead_rois.size(), nb, 0, next, next_pitch);
+                if (r2 != TBDK_OK) return r2;
+                t->ahead_id = frame_id + 1;
+                t->ahead_frame = next;
+                t->ahead_pitch = next_pitch;
+                t->ahead_set = nb;
+                t->ahead_any = true;
+            }
         }
         return TBDK_OK;
     };
@@ -1336,7 +1410,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             for (int q = 0; q < ne; ++q) t->h_ers[q] = erow0 + q;
             hipStream_t ls = t->la_s;
             e = t->la_stream == ls ? hipSuccess : wait_if_pending(ls, t->la_ready);
-            if (e == hipSuccess) e = wait_if_pending(ls, t->early_done);
+            if (e == hipSuccess) e = wait_if_pending(ls, t->early_done[t->eb]);
             if (e == hipSuccess && !t->zc)
                 e = hipMemcpyAsync(t->d_ers, t->h_ers, sizeof(int32_t) * ne, hipMemcpyHostToDevice, ls);
             if (e != hipSuccess) return map_status(e);
@@ -1403,7 +1477,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // row of the post-tracker GFTT below), tracked from there by the next step
     t->rois.clear();
     int nroi = 0, nearly = 0;
-    const int prow0 = 3 * S;  // the post-tracker GFTT's rows
+    const int prow0 = (1 + kEarlySets) * S;  // the post-tracker GFTT's rows
     if (c.use_klt) {
         for (const auto& tr : t->tracker->getTracks()) {
             const int* it = t->slot_of.find(tr.id);
@@ -1448,11 +1522,11 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // queued first and the PyrLK fills the device around it.
     // tbd_post_direct: with no post-tracker GFTT the next step waits for the
     // early GFTT's event itself (no side-stream wait and marker on the host's
-    // way to that step; not with early order 0, whose next early GFTT would
-    // re-record that event before the wait)
-    const bool post_direct = nroi == 0 && early_launched && t->ctx->opt_tbd_post_direct && early_order != 0;
+    // way to that step; each early row set has its own event, so the next
+    // step's early launches, whatever their order, re-record other sets' events)
+    const bool post_direct = nroi == 0 && early_launched && t->ctx->opt_tbd_post_direct;
     if (early_launched && !post_direct) {
-        hipError_t e = wait_if_pending(t->side, t->early_done);
+        hipError_t e = wait_if_pending(t->side, t->early_done[t->eb]);
         if (e != hipSuccess) return map_status(e);
     }
     if (nroi > 0) {
@@ -1473,7 +1547,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // step's fit sync then orders that GFTT's table upload before the staging
     // table is rewritten (two steps later)
     if (post_direct) {
-        t->post_wait = t->early_done;
+        t->post_wait = t->early_done[t->eb];
     } else if (nroi > 0 || early_launched) {
         hipError_t e = hipEventRecord(t->post_done, t->side);
         if (e != hipSuccess) return map_status(e);
@@ -1513,7 +1587,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     t->spec_list.clear();
     t->cur = (t->cur + 1) % 3;
     t->last_fit = run_klt && synced;
-    t->eb ^= 1;
+    t->eb = (t->eb + 1) % kEarlySets;
     t->have_prev = true;
 
     STEP_MARK(11);
@@ -1616,19 +1690,32 @@ int tbdk_tbd_run(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first
     hipStream_t s = static_cast<hipStream_t>(stream);
     t->borrow = t->ctx->opt_tbd_borrow_l0 && !t->ctx->opt_tbd_pyr_derivs && t->ctx->opt_pyr_fuse &&
                 t->cfg.width >= 2 * (t->cfg.win + 2) && t->cfg.height >= 2 * (t->cfg.win + 2);
+    t->ahead_any = false;
+    // the caller's stream after the early GFTT work launched ahead over its frames
+    auto end_ahead = [&]() -> int {
+        if (!t->ahead_any) return TBDK_OK;
+        t->ahead_any = false;
+        hipError_t e = hipEventRecord(t->ahead_tail, t->early_s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, t->ahead_tail, 0);
+        return map_status(e);
+    };
     for (int i = 0; i < nframes; ++i) {
         const uint8_t* next = i + 1 < nframes ? frames[i + 1] : nullptr;
+        const bool nd = next && dets;
         int rc = step_impl(t, frames[i], pitch, first_frame_id + i, dets ? dets + det_offsets[i] : nullptr,
-                           det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr, s);
+                           det_offsets[i + 1] - det_offsets[i], next, pitch, metrics ? metrics + i : nullptr, s,
+                           nd ? dets + det_offsets[i + 1] : nullptr, nd ? det_offsets[i + 2] - det_offsets[i + 1] : -1);
         if (rc != TBDK_OK) {
             (void)finish(t, TBDK_OK);
+            (void)end_ahead();
             (void)end_borrow(t, s);
             return rc;
         }
     }
     const int rc = finish(t, TBDK_OK);
+    const int ra = end_ahead();
     const int rb = end_borrow(t, s);
-    return rc != TBDK_OK ? rc : rb;
+    return rc != TBDK_OK ? rc : ra != TBDK_OK ? ra : rb;
 }
 
 int tbdk_tbd_run_host(tbdk_tbd* t, const uint8_t* const* frames, int pitch, int first_frame_id,
@@ -1704,7 +1791,7 @@ int tbdk_tbd_tracks(tbdk_tbd* t, tbdk_track_info* out, int cap, int* n)
 {
     if (!t || !n || cap < 0 || (cap > 0 && !out)) return TBDK_EINVAL;
     const auto& tracks = t->tracker->getTracks();
-    std::vector<int32_t> counts(4 * (size_t)t->cfg.max_tracks);  // slots and GFTT rows
+    std::vector<int32_t> counts(kRowSets * (size_t)t->cfg.max_tracks);  // slots and GFTT rows
     if (const int d = drain(t)) return d;
     (void)hipSetDevice(t->ctx->device);
     hipError_t e = hipStreamSynchronize(t->side);  // post-tracker work (behind the early GFTT) runs on `side`

@@ -92,7 +92,7 @@ struct tbdk_ctx {
     int opt_tbd_spec_la = 1;     // tbdk_ctx_set_option("tbd_spec_lookahead")
     int opt_tbd_zero_copy = 1;   // tbdk_ctx_set_option("tbd_zero_copy"), read by tbdk_tbd_create
     int opt_tbd_fit_flag = 1;    // tbdk_ctx_set_option("tbd_fit_flag"), read by tbdk_tbd_create
-    int opt_tbd_early_order = 1;  // tbdk_ctx_set_option("tbd_early_order"): where the early GFTT is launched in a step (round 5: 1)
+    int opt_tbd_early_order = 0;  // tbdk_ctx_set_option("tbd_early_order"): where the early GFTT is launched in a step (round 6: 0)
     int opt_tbd_early_prio = 0;  // tbdk_ctx_set_option("tbd_early_prio"), read by tbdk_tbd_create
     int opt_tbd_early_la = 1;    // tbdk_ctx_set_option("tbd_early_la"): look-ahead PyrLK of early GFTT rows
     int opt_tbd_pyr_derivs = 0;  // tbdk_ctx_set_option("tbd_pyr_derivs"): loop pyramids with Scharr planes (A/B)
@@ -103,6 +103,7 @@ struct tbdk_ctx {
     int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
     int opt_gftt_compact = 1;    // tbdk_ctx_set_option("gftt_compact"): GFTT writes only its candidates' values
+    int opt_tbd_gftt_ahead = 1;  // tbdk_ctx_set_option("tbd_gftt_ahead"): tbdk_tbd_run's early GFTT a frame ahead
     int opt_tbd_borrow_l0 = 0;   // tbdk_ctx_set_option("tbd_borrow_l0"): tbdk_tbd_run's pyramids take the frame as level 0 (A/B)
     int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)

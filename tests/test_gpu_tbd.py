@@ -217,7 +217,7 @@ def test_tbd_early_gftt_matches_post_tracker_gftt(gpu, api):
         gpu.set_option("tbd_early_gftt", 2)
         gpu.set_option("tbd_spec_lookahead", 1)
         gpu.set_option("tbd_early_la", 1)
-        gpu.set_option("tbd_early_order", 1)  # the default
+        gpu.set_option("tbd_early_order", 0)  # the default
         gpu.set_option("tbd_early_prio", 0)
     base = res[0, 0, 0, 0, 0]
     for key, r in res.items():
@@ -510,3 +510,38 @@ def test_tbd_run_one_point_steps_match(gpu):
     assert sum(res[0][1]) > 0
     for r in res[1:]:
         assert r == res[0]
+
+
+def test_tbd_run_gftt_ahead_matches(gpu):
+    """ctx option tbd_gftt_ahead (tbdk_tbd_run launches the next frame's
+    new-track GFTT one step ahead, over the caller's next frame): the same
+    per-frame metrics and tracks as without it and as per-frame steps, with the
+    bounds quirk (every frame starts new tracks beyond the filter), frequent
+    re-detections, and a run split by a per-frame step (each run's last step
+    has no next frame, so no launch is left ahead across calls)."""
+    from opencv_amd import klt, tbd
+
+    W, H, N, F = 960, 540, 40, 18
+    frames, gt = klt.synth_render(41, W, H, N, 0, F, ctx=gpu)
+    dets = [tbd.detections_from_gt(gt[f].numpy()) for f in range(F)]
+    c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
+    res = []
+    try:
+        for ahead in (0, 1):
+            gpu.set_option("tbd_gftt_ahead", ahead)
+            loop = tbd.TbdLoop(c, ctx=gpu)
+            ms = loop.run(frames, 0, dets)
+            split = tbd.TbdLoop(c, ctx=gpu)
+            mt = list(split.run(frames[:7], 0, dets[:7]))
+            mt.append(split.step(frames[7], 7, dets[7]))
+            mt += list(split.run(frames[8:], 8, dets[8:]))
+            res.append(([_mkey(m) for m in ms], loop.tracks(), [_mkey(m) for m in mt], split.tracks()))
+            del loop, split
+    finally:
+        gpu.set_option("tbd_gftt_ahead", 1)
+    stepped = tbd.TbdLoop(c, ctx=gpu)
+    ref = [_mkey(stepped.step(frames[f], f, dets[f])) for f in range(F)]
+    assert sum(k[10] for k in ref) > F  # re-detections / new tracks every frame
+    for r in res:
+        assert r[0] == ref and r[2] == ref
+        assert r[1] == stepped.tracks() and r[3] == stepped.tracks()
