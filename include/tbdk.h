@@ -225,6 +225,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       a GFTT launched only one step earlier; the step of that frame launches
  *       just the ROIs it misses (re-detection guesses).  The caller's stream
  *       waits for that work before the call returns (results equal).
+ *   "tbd_ahead_at" (0/1/2, default 0): where a step launches that ahead GFTT:
+ *       0 with its own early GFTT, 1 after its critical PyrLK, 2 just before
+ *       the host waits for the fit (never before the step's own early GFTT;
+ *       results equal).
  *   "tbd_borrow_l0" (0/1, default 0): inside tbdk_tbd_run the loop's pyramids
  *       take the caller's frames as level 0 (no padded copy; PyrLK reads
  *       windows across a frame's edge by reflect-101 coordinates, the values

@@ -283,6 +283,11 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_lk_seg_inline = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_ahead_at") == 0) {
+        if (value < 0 || value > 2) return TBDK_EINVAL;
+        ctx->opt_tbd_ahead_at = (int)value;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_gftt_ahead") == 0) {
         ctx->opt_tbd_gftt_ahead = value != 0;
         return TBDK_OK;

@@ -1034,11 +1034,21 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             if (r2 != TBDK_OK) return r2;
             early_launched = true;
         }
-        // the next frame's new-track ROIs (its detections beyond the bounds
-        // filter, as above), launched ahead over the caller's next frame into
-        // the next row set: that frame's step takes them over, so its
-        // refreshed-set PyrLK no longer waits for a GFTT launched one step
-        // before it (tbdk_tbd_run knows the next frame's detections)
+        return TBDK_OK;
+    };
+    // the next frame's new-track ROIs (its detections beyond the bounds filter,
+    // as above), launched ahead over the caller's next frame into the next row
+    // set: that frame's step takes them over, so its refreshed-set PyrLK no
+    // longer waits for a GFTT launched one step before it (tbdk_tbd_run knows
+    // the next frame's detections).  Where (ctx option tbd_ahead_at): 0 right
+    // after this step's early launch, 1 after the critical PyrLK launch, 2 just
+    // before the host waits for the fit (its host work off the frame's chain)
+    bool ahead_done = false;
+    auto launch_gftt_ahead = [&](int at) -> int {
+        if (ahead_done || at < t->ctx->opt_tbd_ahead_at) return TBDK_OK;
+        ahead_done = true;
+        if (!c.use_klt || !t->ctx->opt_tbd_early_gftt) return TBDK_OK;
+        const bool all_new = t->tracker->getTracks().empty();
         if (next && next_dets && next_ndets > 0 && t->ctx->opt_tbd_gftt_ahead && !all_new) {
             const int nb = (t->eb + 1) % kEarlySets;
             t->ahead_rois.clear();
@@ -1074,6 +1084,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     const int early_order = t->ctx->opt_tbd_early_order;
     if (early_order == 0) {
         rc = launch_early_gftt();
+        if (rc == TBDK_OK) rc = launch_gftt_ahead(0);
         if (rc != TBDK_OK) return rc;
     }
     STEP_MARK(1);
@@ -1233,6 +1244,10 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
         }
+        if (early_order <= 1) {
+            rc = launch_gftt_ahead(1);
+            if (rc != TBDK_OK) return rc;
+        }
         hipError_t e = hipSuccess;  // zero-copy without a look-ahead wait sets it nowhere below
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
             rc = drain(t);
@@ -1277,6 +1292,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
         }
+        rc = launch_gftt_ahead(2);
+        if (rc != TBDK_OK) return rc;
         auto ts0 = clk::now();
         STEP_MARK(4);
         launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
@@ -1431,6 +1448,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
             rc = launch_early_gftt();
             if (rc != TBDK_OK) return rc;
         }
+        rc = launch_gftt_ahead(2);
+        if (rc != TBDK_OK) return rc;
         if (next) {
             // the next pyramid is rebuilt over the previous frame's, which the
             // previous step's look-ahead PyrLK (on la_s) may still be reading

@@ -103,6 +103,7 @@ struct tbdk_ctx {
     int opt_tbd_post_direct = 1;  // tbdk_ctx_set_option("tbd_post_direct"): next step waits for the early GFTT itself
     int opt_tbd_la_defer = 0;    // tbdk_ctx_set_option("tbd_la_defer"): look-ahead PyrLK launched by the next step
     int opt_gftt_compact = 1;    // tbdk_ctx_set_option("gftt_compact"): GFTT writes only its candidates' values
+    int opt_tbd_ahead_at = 0;    // tbdk_ctx_set_option("tbd_ahead_at"): where a step launches the ahead GFTT (0..2)
     int opt_tbd_gftt_ahead = 1;  // tbdk_ctx_set_option("tbd_gftt_ahead"): tbdk_tbd_run's early GFTT a frame ahead
     int opt_tbd_borrow_l0 = 0;   // tbdk_ctx_set_option("tbd_borrow_l0"): tbdk_tbd_run's pyramids take the frame as level 0 (A/B)
     int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)

@@ -527,8 +527,9 @@ def test_tbd_run_gftt_ahead_matches(gpu):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
     res = []
     try:
-        for ahead in (0, 1):
+        for ahead, at in ((0, 2), (1, 0), (1, 1), (1, 2)):
             gpu.set_option("tbd_gftt_ahead", ahead)
+            gpu.set_option("tbd_ahead_at", at)  # where the step launches it
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
             split = tbd.TbdLoop(c, ctx=gpu)
@@ -539,6 +540,7 @@ def test_tbd_run_gftt_ahead_matches(gpu):
             del loop, split
     finally:
         gpu.set_option("tbd_gftt_ahead", 1)
+        gpu.set_option("tbd_ahead_at", 0)
     stepped = tbd.TbdLoop(c, ctx=gpu)
     ref = [_mkey(stepped.step(frames[f], f, dets[f])) for f in range(F)]
     assert sum(k[10] for k in ref) > F  # re-detections / new tracks every frame
