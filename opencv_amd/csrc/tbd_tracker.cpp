@@ -230,6 +230,45 @@ TBDK_SOLVER_CLONES static unsigned zero_row(double* __restrict row, const double
     return cnt;
 }
 
+// the zero test of the reduced cost (equalsZero, tbd.hpp:178-181) on an entry
+// stored as `value - colMin` (step 2's subtraction, :563-578)
+static inline bool zero_after(double value, double colMin)
+{
+    const double v = value - colMin;
+    return std::fabs(v) < 0.00000001;
+}
+
+// zero bits of one row's default entries: bit c = zero_after(a, colMin[c])
+TBDK_SOLVER_CLONES static void zero_bits_uniform(double a, const double* __restrict colMin, unsigned n,
+                                                 uint64_t* __restrict bits)
+{
+    for (unsigned w = 0; w * 64 < n; ++w) {
+        const unsigned c0 = w * 64, c1 = std::min(n, c0 + 64);
+        uint64_t m = 0;
+        for (unsigned c = c0; c < c1; ++c) m |= (uint64_t)(std::fabs(a - colMin[c]) < 0.00000001) << (c - c0);
+        bits[w] = m;
+    }
+}
+
+// first index of sorted a[0..n) whose value is >= key (std::lower_bound), with
+// conditional moves instead of branches
+static inline unsigned lower_bound_cmov(const int* a, unsigned n, long key)
+{
+    const int* base = a;
+    while (n > 1) {
+        const unsigned half = n / 2;
+        base = ((long)base[half - 1] < key) ? base + half : base;
+        n -= half;
+    }
+    return (unsigned)(base - a) + (unsigned)(n == 1 && (long)*base < key);
+}
+
+static inline void set_bit(uint64_t* bits, unsigned c, bool v)
+{
+    const uint64_t b = (uint64_t)1 << (c & 63);
+    bits[c >> 6] = v ? (bits[c >> 6] | b) : (bits[c >> 6] & ~b);
+}
+
 // calculateCostMatrix + solveAssignmentProblem + classifyAssignments
 // (tbd.cpp:333-891) on a flat n x n matrix.  The reference's operation order
 // on every matrix entry is kept (row minima, column minima, the step-4
@@ -238,6 +277,22 @@ TBDK_SOLVER_CLONES static unsigned zero_row(double* __restrict row, const double
 // minima are accumulated row by row (same r order per column), the zero
 // pattern and its row/column counts are rebuilt in one pass, and the
 // "row assigned to column c" lookup of the cover step is an inverse map.
+//
+// The first round does not build the matrix.  A track row holds three kinds of
+// entries: the detections its predicted box overlaps (a handful, found by an
+// x-sorted sweep), 1.0 for every other detection (computeBoundingBoxOverlap
+// returns exactly 0.0 for disjoint boxes) and the padding; a padding row is
+// padding throughout.  After step 1 every entry of a kind is the same double
+// (`1.0 - m`, `pad - m`), so each column's minimum is the smallest such value
+// among the rows without an overlap in that column, or an overlap entry, and
+// an entry's zero test is `fabs(value - colMin[c]) < 1e-8` on the same two
+// doubles the dense pass subtracts.  The zero pattern is kept as one bit per
+// entry, the step-2 assignment (:585-714) scans bits.  Only when that round
+// leaves rows unassigned (about 2 % of the bench's frames) is the matrix built,
+// entry by entry with the same operations, and the dense rounds continue with
+// step 3.  Minima use the reference's `(v < m) ? v : m` step, whose result does
+// not depend on the order of the values when no -0.0 can occur (a padding
+// value that is not in (0, huge) takes the dense path).
 void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& assignments,
                               std::vector<unsigned>& unassignedTracks, std::vector<unsigned>& unassignedDetections)
 {
@@ -245,120 +300,311 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
     const unsigned n = std::max(nT, nD);
     const double huge = 10000000.0;
     const double pad = args.costOfNonAssignment * 2;
-    cost.resize((size_t)n * n);
-    detX0.resize(nD); detY0.resize(nD); detX1.resize(nD); detY1.resize(nD); detArea.resize(nD);
+    detKey.resize(nD);
     detOrder.resize(nD);
     int maxW = 0;
-    for (unsigned j = 0; j < nD; ++j) {
-        const Rect& b = dets[j].bbox;
-        detX0[j] = b.x; detY0[j] = b.y; detX1[j] = b.x + b.width; detY1[j] = b.y + b.height;
-        detArea[j] = b.area();
-        detOrder[j] = j;
-        maxW = std::max(maxW, b.width);
+    for (unsigned j = 0; j < nD; ++j) {  // (x0, index) packed in one ordered key
+        detKey[j] = ((uint64_t)((uint32_t)dets[j].bbox.x ^ 0x80000000u) << 32) | j;
+        maxW = std::max(maxW, dets[j].bbox.width);
     }
     // detections by left edge: a track row only visits the detections whose x-range
     // can touch its box; all others are strictly separated, where the reference's
     // computeBoundingBoxOverlap returns exactly 0.0 (cost exactly 1.0)
-    std::sort(detOrder.begin(), detOrder.end(), [&](unsigned a, unsigned b) { return detX0[a] < detX0[b]; });
-    sortedX0.resize(nD);
-    for (unsigned k = 0; k < nD; ++k) sortedX0[k] = detX0[detOrder[k]];
+    std::sort(detKey.begin(), detKey.end());
+    for (unsigned k = 0; k < nD; ++k) detOrder[k] = (unsigned)detKey[k];
+    sortedX0.resize(nD); sortedX1.resize(nD); sortedY0.resize(nD); sortedY1.resize(nD); sortedArea.resize(nD);
+    for (unsigned k = 0; k < nD; ++k) {
+        const Rect& b = dets[detOrder[k]].bbox;
+        sortedX0[k] = b.x; sortedX1[k] = b.x + b.width; sortedY0[k] = b.y; sortedY1[k] = b.y + b.height;
+        sortedArea[k] = b.area();
+    }
     assignmentPerRow.assign(n, n);
     if (n == 0) return;
-    colMin.assign(n, huge);
-    // calculateCostMatrix (:333-351) fused with step 1, the row minima (:494-516),
-    // and step 2's column minima
-    for (unsigned r = 0; r < n; ++r) {
-        double* row = &cost[(size_t)r * n];
-        unsigned c0 = 0;
-        if (r < nT) {
-            const Rect& p = tracks[r].predPosition;
-            const int px0 = p.x, py0 = p.y, px1 = p.x + p.width, py1 = p.y + p.height, pa = p.area();
-            for (unsigned j = 0; j < nD; ++j) row[j] = 1.0;
-            const unsigned lb = (unsigned)(std::lower_bound(sortedX0.begin(), sortedX0.end(), px0 - maxW) -
-                                           sortedX0.begin());
-            const unsigned ub = (unsigned)(std::upper_bound(sortedX0.begin(), sortedX0.end(), px1) - sortedX0.begin());
-            for (unsigned k = lb; k < ub; ++k) {
-                const unsigned j = detOrder[k];
-                if (detX0[j] > px1 || detX1[j] < px0 || detY0[j] > py1 || detY1[j] < py0) continue;
-                const int xl = std::max(px0, detX0[j]), xr = std::min(px1, detX1[j]);
-                const int yt = std::max(py0, detY0[j]), yb = std::min(py1, detY1[j]);
-                if (xr < xl || yb < yt) continue;  // (:1094-1097) -> 0.0
-                const double inter = (double)(xr - xl) * (double)(yb - yt);
-                const double uni = (double)(pa + detArea[j]) - inter;
-                row[j] = 1.0 - inter / uni;
-            }
-            c0 = nD;
+    // calculateCostMatrix (:333-351): the overlap entries of every track row
+    exStart.resize(nT + 1);
+    exCol.clear();
+    exVal.clear();
+    cand.resize(nD);
+    for (unsigned r = 0; r < nT; ++r) {
+        exStart[r] = (unsigned)exCol.size();
+        const Rect& p = tracks[r].predPosition;
+        const int px0 = p.x, py0 = p.y, px1 = p.x + p.width, py1 = p.y + p.height, pa = p.area();
+        const unsigned lb = lower_bound_cmov(sortedX0.data(), nD, (long)px0 - maxW);
+        const unsigned ub = lower_bound_cmov(sortedX0.data(), nD, (long)px1 + 1);  // the first x0 > px1
+        // boxes that touch or overlap (computeBoundingBoxOverlap's xright >= xleft and
+        // ybottom >= ytop, :1094-1097), gathered without branches
+        unsigned nc = 0;
+        for (unsigned k = lb; k < ub; ++k) {
+            cand[nc] = k;
+            nc += (unsigned)((sortedX1[k] >= px0) & (sortedY0[k] <= py1) & (sortedY1[k] >= py0));
         }
-        for (unsigned c = c0; c < n; ++c) row[c] = pad;
-        sub_row_min_and_colmin(row, n, row_min(row, n, huge), colMin.data());
+        for (unsigned i = 0; i < nc; ++i) {
+            const unsigned k = cand[i];
+            const int xl = std::max(px0, sortedX0[k]), xr = std::min(px1, sortedX1[k]);
+            const int yt = std::max(py0, sortedY0[k]), yb = std::min(py1, sortedY1[k]);
+            const double inter = (double)(xr - xl) * (double)(yb - yt);
+            const double uni = (double)(pa + sortedArea[k]) - inter;
+            exCol.push_back(detOrder[k]);
+            exVal.push_back(1.0 - inter / uni);
+        }
     }
-    {
-        // the column minima's subtraction is fused into the first round's zero pass
-        zero.resize((size_t)n * n);
-        rowZeros.resize(n);
-        colZeros.resize(n);
-        colLast.resize(n);
-        colRow.resize(n);
-        rowA.resize(n);
-        colA.resize(n);
-        rowM.resize(n);
-        colM.resize(n);
-        bool first = true;
-        while (true) {  // (:585-887)
-            std::fill(colZeros.begin(), colZeros.end(), 0u);
-            for (unsigned r = 0; r < n; ++r)
-                rowZeros[r] = zero_row(&cost[(size_t)r * n], first ? colMin.data() : nullptr, n, &zero[(size_t)r * n],
-                                       colZeros.data(), colLast.data(), r);
-            first = false;
-            std::fill(rowA.begin(), rowA.end(), 0);
-            std::fill(colA.begin(), colA.end(), 0);
-            std::fill(colRow.begin(), colRow.end(), n);
-            unsigned numAssigned = 0;
-            assignmentPerRow.assign(n, n);
-            auto assign = [&](unsigned r, unsigned c) {
-                rowA[r] = colA[c] = 1;
-                assignmentPerRow[r] = c;
-                colRow[c] = r;
-                numAssigned++;
-            };
-            bool made = true;
-            while (made) {
-                made = false;
-                // rows with exactly one zero (:607-636)
+    exStart[nT] = (unsigned)exCol.size();
+
+    rowZeros.resize(n);
+    colZeros.resize(n);
+    colLast.resize(n);
+    colRow.resize(n);
+    rowA.assign(n, 0);
+    colA.assign(n, 0);
+    rowM.resize(n);
+    colM.resize(n);
+    colRow.assign(n, n);
+    unsigned numAssigned = 0;
+    lastRounds = 1;
+    auto assign = [&](unsigned r, unsigned c) {
+        rowA[r] = colA[c] = 1;
+        assignmentPerRow[r] = c;
+        colRow[c] = r;
+        numAssigned++;
+    };
+
+    const bool sparse = !denseSolver && pad > 0.0 && pad < huge;
+    bool dense_zero_pass = true;  // the dense loop starts with step 2's zero pattern
+    if (sparse) {
+        // step 1 (:494-516): every row's minimum over its value kinds
+        rowMinV.resize(nT);
+        rowDef.resize(nT);
+        rowPadV.resize(nT);
+        exValR.resize(exVal.size());
+        for (unsigned r = 0; r < nT; ++r) {
+            double m = huge;
+            if (exStart[r + 1] - exStart[r] < nD) m = (1.0 < m) ? 1.0 : m;
+            for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k) m = (exVal[k] < m) ? exVal[k] : m;
+            if (n > nD) m = (pad < m) ? pad : m;
+            rowMinV[r] = m;
+            rowDef[r] = 1.0 - m;
+            rowPadV[r] = pad - m;
+            for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k) exValR[k] = exVal[k] - m;
+        }
+        const double padRowV = pad - ((pad < huge) ? pad : huge);  // rows nT..n-1
+        // step 2's column minima (:539-561)
+        colExStart.assign(nD + 1, 0);
+        for (unsigned k = 0; k < exCol.size(); ++k) colExStart[exCol[k] + 1]++;
+        for (unsigned c = 0; c < nD; ++c) colExStart[c + 1] += colExStart[c];
+        colExRow.resize(exCol.size());
+        colExVal.resize(exCol.size());
+        colFill.assign(colExStart.begin(), colExStart.end() - 1);
+        for (unsigned r = 0; r < nT; ++r)
+            for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k) {
+                const unsigned at = colFill[exCol[k]]++;
+                colExRow[at] = r;
+                colExVal[at] = exValR[k];
+            }
+        defOrder.resize(nT);
+        for (unsigned r = 0; r < nT; ++r) defOrder[r] = r;
+        if (!(nT < n && padRowV == 0.0))
+            std::sort(defOrder.begin(), defOrder.end(), [&](unsigned a, unsigned b) { return rowDef[a] < rowDef[b]; });
+        colMin.assign(n, huge);
+        // with padding rows (value pad - pad = +0.0) and every other entry >= +0.0
+        // (v - m with m the row's minimum), every column's minimum is +0.0
+        const bool zeroMins = nT < n && padRowV == 0.0;
+        if (zeroMins) std::fill(colMin.begin(), colMin.begin() + nD, 0.0);
+        for (unsigned c = 0; !zeroMins && c < nD; ++c) {
+            double cm = huge;
+            const unsigned e0 = colExStart[c], e1 = colExStart[c + 1];
+            for (unsigned r : defOrder) {  // the smallest 1.0 - m of the rows with a 1.0 entry here
+                bool ex = false;
+                for (unsigned k = e0; k < e1; ++k) ex |= colExRow[k] == r;
+                if (!ex) {
+                    cm = (rowDef[r] < cm) ? rowDef[r] : cm;
+                    break;
+                }
+            }
+            for (unsigned k = e0; k < e1; ++k) cm = (colExVal[k] < cm) ? colExVal[k] : cm;
+            if (nT < n) cm = (padRowV < cm) ? padRowV : cm;
+            colMin[c] = cm;
+        }
+        double cmPad = huge;  // columns nD..n-1 (track rows only: nT == n)
+        if (n > nD)
+            for (unsigned r = 0; r < nT; ++r) cmPad = (rowPadV[r] < cmPad) ? rowPadV[r] : cmPad;
+        for (unsigned c = nD; c < n; ++c) colMin[c] = cmPad;
+        double cmLo = huge, cmHi = -huge;
+        for (unsigned c = 0; c < nD; ++c) {
+            cmLo = std::min(cmLo, colMin[c]);
+            cmHi = std::max(cmHi, colMin[c]);
+        }
+        // the zero pattern after the column minima, one bit per entry
+        const unsigned W = (n + 63) / 64;
+        zbits.assign((size_t)n * W, 0);
+        if (nT < n) {  // padding rows: one pattern
+            zero_bits_uniform(padRowV, colMin.data(), n, &zbits[(size_t)nT * W]);
+            for (unsigned r = nT + 1; r < n; ++r)
+                std::memcpy(&zbits[(size_t)r * W], &zbits[(size_t)nT * W], W * sizeof(uint64_t));
+        }
+        for (unsigned r = 0; r < nT; ++r) {
+            uint64_t* b = &zbits[(size_t)r * W];
+            const double a = rowDef[r];
+            // no 1.0 entry can be a zero when a is 1e-8 or more away from every column minimum
+            if (nD && !(a - cmHi >= 0.00000001) && !(a - cmLo <= -0.00000001))
+                zero_bits_uniform(a, colMin.data(), nD, b);
+            for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k)
+                set_bit(b, exCol[k], zero_after(exValR[k], colMin[exCol[k]]));
+            if (n > nD && zero_after(rowPadV[r], cmPad))
+                for (unsigned c = nD; c < n; ++c) set_bit(b, c, true);
+        }
+        std::fill(colZeros.begin(), colZeros.end(), 0u);
+        for (unsigned r = 0; r < std::min(n, nT + 1); ++r) {  // track rows, then the first padding row
+            const uint64_t* b = &zbits[(size_t)r * W];
+            const unsigned reps = r < nT ? 1 : n - nT, last = r < nT ? r : n - 1;
+            unsigned cnt = 0;
+            for (unsigned w = 0; w < W; ++w)
+                for (uint64_t m = b[w]; m; m &= m - 1) {
+                    const unsigned c = w * 64 + (unsigned)__builtin_ctzll(m);
+                    colZeros[c] += reps;
+                    colLast[c] = last;
+                    cnt++;
+                }
+            rowZeros[r] = cnt;
+        }
+        for (unsigned r = nT + 1; r < n; ++r) rowZeros[r] = rowZeros[nT];
+        // step 2's assignment (:585-714) on the bits
+        colAbits.assign(W, 0);
+        auto assign_b = [&](unsigned r, unsigned c) {
+            assign(r, c);
+            colAbits[c >> 6] |= (uint64_t)1 << (c & 63);
+        };
+        bool made = true;
+        while (made) {
+            made = false;
+            for (unsigned r = 0; r < n; ++r) {  // rows with exactly one zero (:607-636)
+                if (rowA[r] || rowZeros[r] != 1) continue;
+                const uint64_t* b = &zbits[(size_t)r * W];
+                unsigned w = 0;
+                while (!b[w]) ++w;
+                const unsigned c = w * 64 + (unsigned)__builtin_ctzll(b[w]);
+                if (!colA[c]) {
+                    assign_b(r, c);
+                    made = true;
+                }
+            }
+            for (unsigned c = 0; c < n; ++c) {  // columns with exactly one zero (:639-668)
+                if (colA[c] || colZeros[c] != 1) continue;
+                const unsigned r = colLast[c];
+                if (!rowA[r]) {
+                    assign_b(r, c);
+                    made = true;
+                }
+            }
+            if (!made) {  // first free zero of every unassigned row (:672-714)
                 for (unsigned r = 0; r < n; ++r) {
-                    if (rowA[r] || rowZeros[r] != 1) continue;
-                    const uint8_t* z = &zero[(size_t)r * n];
-                    unsigned c = 0;
-                    while (!z[c]) ++c;
-                    if (!colA[c]) {
-                        assign(r, c);
-                        made = true;
+                    if (rowA[r]) continue;
+                    const uint64_t* b = &zbits[(size_t)r * W];
+                    for (unsigned w = 0; w < W; ++w) {
+                        const uint64_t m = b[w] & ~colAbits[w];
+                        if (m) {
+                            assign_b(r, w * 64 + (unsigned)__builtin_ctzll(m));
+                            made = true;
+                            break;
+                        }
                     }
                 }
-                // columns with exactly one zero (:639-668)
+            }
+        }
+        if (numAssigned < n) {
+            // the dense rounds continue from step 3: the matrix and zero pattern as
+            // the dense first round leaves them (each entry `(raw - m) - colMin[c]`)
+            cost.resize((size_t)n * n);
+            zero.resize((size_t)n * n);
+            for (unsigned r = 0; r < n; ++r) {
+                double* row = &cost[(size_t)r * n];
+                if (r < nT) {
+                    for (unsigned c = 0; c < nD; ++c) row[c] = rowDef[r];
+                    for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k) row[exCol[k]] = exValR[k];
+                    for (unsigned c = nD; c < n; ++c) row[c] = rowPadV[r];
+                } else {
+                    for (unsigned c = 0; c < n; ++c) row[c] = padRowV;
+                }
+                const uint64_t* b = &zbits[(size_t)r * W];
                 for (unsigned c = 0; c < n; ++c) {
-                    if (colA[c] || colZeros[c] != 1) continue;
-                    const unsigned r = colLast[c];
-                    if (!rowA[r]) {
-                        assign(r, c);
-                        made = true;
-                    }
+                    row[c] -= colMin[c];
+                    zero[(size_t)r * n + c] = (uint8_t)((b[c >> 6] >> (c & 63)) & 1);
                 }
-                // otherwise: first free zero of every unassigned row (:672-714)
-                if (!made) {
+            }
+            dense_zero_pass = false;
+        }
+    } else {
+        // the dense first round: calculateCostMatrix fused with step 1, the row
+        // minima (:494-516), and step 2's column minima
+        cost.resize((size_t)n * n);
+        zero.resize((size_t)n * n);
+        colMin.assign(n, huge);
+        for (unsigned r = 0; r < n; ++r) {
+            double* row = &cost[(size_t)r * n];
+            unsigned c0 = 0;
+            if (r < nT) {
+                for (unsigned j = 0; j < nD; ++j) row[j] = 1.0;
+                for (unsigned k = exStart[r]; k < exStart[r + 1]; ++k) row[exCol[k]] = exVal[k];
+                c0 = nD;
+            }
+            for (unsigned c = c0; c < n; ++c) row[c] = pad;
+            sub_row_min_and_colmin(row, n, row_min(row, n, huge), colMin.data());
+        }
+    }
+    if (numAssigned < n) {
+        // the column minima's subtraction is fused into the dense first round's zero pass
+        bool first = dense_zero_pass;
+        while (true) {  // (:585-887)
+            if (dense_zero_pass) {
+                std::fill(colZeros.begin(), colZeros.end(), 0u);
+                for (unsigned r = 0; r < n; ++r)
+                    rowZeros[r] = zero_row(&cost[(size_t)r * n], first ? colMin.data() : nullptr, n,
+                                           &zero[(size_t)r * n], colZeros.data(), colLast.data(), r);
+                first = false;
+                std::fill(rowA.begin(), rowA.end(), 0);
+                std::fill(colA.begin(), colA.end(), 0);
+                std::fill(colRow.begin(), colRow.end(), n);
+                numAssigned = 0;
+                assignmentPerRow.assign(n, n);
+                bool made = true;
+                while (made) {
+                    made = false;
+                    // rows with exactly one zero (:607-636)
                     for (unsigned r = 0; r < n; ++r) {
-                        if (rowA[r]) continue;
+                        if (rowA[r] || rowZeros[r] != 1) continue;
                         const uint8_t* z = &zero[(size_t)r * n];
-                        for (unsigned c = 0; c < n; ++c) {
-                            if (z[c] && !colA[c]) {
-                                assign(r, c);
-                                made = true;
-                                break;
+                        unsigned c = 0;
+                        while (!z[c]) ++c;
+                        if (!colA[c]) {
+                            assign(r, c);
+                            made = true;
+                        }
+                    }
+                    // columns with exactly one zero (:639-668)
+                    for (unsigned c = 0; c < n; ++c) {
+                        if (colA[c] || colZeros[c] != 1) continue;
+                        const unsigned r = colLast[c];
+                        if (!rowA[r]) {
+                            assign(r, c);
+                            made = true;
+                        }
+                    }
+                    // otherwise: first free zero of every unassigned row (:672-714)
+                    if (!made) {
+                        for (unsigned r = 0; r < n; ++r) {
+                            if (rowA[r]) continue;
+                            const uint8_t* z = &zero[(size_t)r * n];
+                            for (unsigned c = 0; c < n; ++c) {
+                                if (z[c] && !colA[c]) {
+                                    assign(r, c);
+                                    made = true;
+                                    break;
+                                }
                             }
                         }
                     }
                 }
             }
+            dense_zero_pass = true;
             if (numAssigned == n) break;
             // step 3: cover zeros (:735-829)
             for (unsigned r = 0; r < n; ++r) rowM[r] = !rowA[r];
@@ -383,6 +629,7 @@ void Tracker::solveAssignment(std::vector<Detection>& dets, std::vector<int>& as
                 if (!rowM[r]) allMarked = false;
             if (allMarked) break;
             // step 4 (:853-886): covered rows are the unmarked ones, covered columns the marked ones
+            lastRounds++;
             double mu = huge;
             for (unsigned r = 0; r < n; ++r) {
                 if (!rowM[r]) continue;

@@ -145,6 +145,9 @@ public:
     void setTracks(const std::vector<Track>& t) { tracks = t; }  // tbd.cpp:187-190
     // the rand() the new tracks' colours are drawn from (null: not drawn)
     void setRand(CRand* r) { rng = r; }
+    // solve every frame on the dense cost matrix (the first round too); the
+    // default solves the first round on the entries' value kinds (same result)
+    void setDenseSolver(bool on) { denseSolver = on; }
 
     // Tracker::performTrackingStep (tbd.cpp:210-286).  preds (may be null)
     // override the motion model for the tracks they name.
@@ -160,11 +163,13 @@ public:
     std::vector<unsigned> createdIds;  // tracks created this step
     std::vector<unsigned> deletedIds;  // tracks removed this step (filtered or lost)
     std::vector<int> lastAssignments;  // per track (after filtering), -1 unassigned
+    unsigned lastRounds = 0;           // solver rounds of the last step (step 4 runs between rounds)
 
 private:
     TbdArgs args;
     CRand* rng = nullptr;
     unsigned nextTrackId = 0;
+    bool denseSolver = false;
     std::vector<Track> tracks;
     std::vector<double> cost;  // flat n x n cost matrix
     std::vector<unsigned> assignmentPerRow;
@@ -174,7 +179,14 @@ private:
     std::vector<double> colMin;
     std::vector<char> rowA, colA, rowM, colM;
     std::vector<int> predIndex;
-    std::vector<int> detX0, detY0, detX1, detY1, detArea, sortedX0;
+    std::vector<uint64_t> detKey;
+    std::vector<int> sortedX0, sortedX1, sortedY0, sortedY1, sortedArea;
+    std::vector<unsigned> cand;
+    // first-round solver scratch: overlap entries per track row and per column,
+    // row minima and value kinds, the zero pattern as bits
+    std::vector<unsigned> exStart, exCol, colExStart, colExRow, colFill, defOrder;
+    std::vector<double> exVal, exValR, colExVal, rowMinV, rowDef, rowPadV;
+    std::vector<uint64_t> zbits, colAbits;
 
     void predictNewLocationsOfTracks(int frame_id, const Prediction* preds, int npreds);
     void filterTracksOutOfBounds(int xmin, int xmax, int ymin, int ymax);

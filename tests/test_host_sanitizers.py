@@ -50,3 +50,20 @@ def test_flat_map_matches_unordered_map_under_asan_ubsan(tmp_path):
                            os.path.join(ROOT, "tests", "cpp", "flat_map_check.cpp"), "-o", exe])
     p = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and "flat_map ok" in p.stdout, p.stdout + p.stderr
+
+
+def test_tracker_first_round_solver_matches_dense_under_asan_ubsan(tmp_path):
+    """The tracker's first assignment round solved on the cost entries' value
+    kinds (tbd_tracker.cpp, the default) against the same tracker solving every
+    round on the dense matrix (Tracker::setDenseSolver), frame by frame over 64
+    scenarios (ties, duplicates, dropouts, clutter, zero-size boxes, padding
+    values below 1, at 1 and outside (0, 1e7)); at least one frame must reach
+    the dense rounds after the first.  Host-built with ASan + UBSan."""
+    exe = str(tmp_path / "tracker_solver_check")
+    csrc = os.path.join(ROOT, "opencv_amd", "csrc")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=undefined", "-I", csrc,
+                           os.path.join(ROOT, "tests", "cpp", "tracker_solver_check.cpp"),
+                           os.path.join(csrc, "tbd_tracker.cpp"), "-o", exe])
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "tracker solver ok" in p.stdout, p.stdout + p.stderr
