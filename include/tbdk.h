@@ -238,6 +238,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value);
  *       stream is synchronised (results equal; PyrLK measured slower reading
  *       the frames than the loop's reused buffers, so off by default).
  *       tbdk_tbd_step / _step_ahead / _run_host always copy.
+ *   "tbd_fit_gate" (0/1, default 1): the TBD loop's host waits (polling) for
+ *       the look-ahead PyrLK's completion event and then launches the fit on
+ *       the step's stream behind the step's own PyrLK, instead of enqueuing a
+ *       cross-stream wait in front of the fit (results equal; A/B runs).
  *   "tbd_async_la" (0/1, default 0; taken by tbdk_tbd_create): the TBD loop's
  *       look-ahead PyrLK launches are issued by a worker thread of the loop
  *       (one more host thread per loop, spinning between frames; results equal;

@@ -233,6 +233,10 @@ int tbdk_ctx_set_option(tbdk_ctx* ctx, const char* name, int64_t value)
         ctx->opt_tbd_post_direct = value != 0;
         return TBDK_OK;
     }
+    if (std::strcmp(name, "tbd_fit_gate") == 0) {
+        ctx->opt_tbd_fit_gate = value != 0;
+        return TBDK_OK;
+    }
     if (std::strcmp(name, "tbd_la_defer") == 0) {
         ctx->opt_tbd_la_defer = value != 0;
         return TBDK_OK;

@@ -1095,7 +1095,7 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
     // rewritten after this step's sync, which orders every
     // earlier upload.  So this frame's pyramid / LK / fit queue up behind the
     // previous GFTT.
-    double wait_us = 0.0;
+    double wait_us = 0.0, gate_us = 0.0;  // gate: the host's wait before the fit launch (tbd_fit_gate)
     bool synced = false;  // has this step waited for the stream (see above)?
 
     // ---- KLT propagation of every live track.  Slots whose point set the previous
@@ -1252,8 +1252,26 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (la_lk) {  // the fit reads the look-ahead PyrLK's results
             rc = drain(t);
             if (rc != TBDK_OK) return rc;
-            e = wait_if_pending(s, t->la_done);
-            if (e != hipSuccess) return map_status(e);
+            if (t->ctx->opt_tbd_fit_gate) {
+                // ctx option tbd_fit_gate: the host waits for the look-ahead PyrLK
+                // and then launches the fit behind this step's PyrLK on the same
+                // stream, with no cross-queue barrier packet between them (the
+                // packet cost ~15 us after the PyrLK ended, on the critical chain;
+                // the look-ahead launch usually ends well before this one)
+                const auto tg0 = clk::now();
+                while ((e = hipEventQuery(t->la_done)) == hipErrorNotReady) {
+                    for (int p = 0; p < 16; ++p) __builtin_ia32_pause();
+                    if (std::chrono::duration<double, std::micro>(clk::now() - tg0).count() > 2000.0) {
+                        e = hipEventSynchronize(t->la_done);  // not the per-frame case
+                        break;
+                    }
+                }
+                if (e != hipSuccess) return map_status(e);
+                gate_us = std::chrono::duration<double, std::micro>(clk::now() - tg0).count();
+            } else {
+                e = wait_if_pending(s, t->la_done);
+                if (e != hipSuccess) return map_status(e);
+            }
         }
         const bool pyr_side = next && !pyr_enqueued && t->ctx->opt_tbd_la_pyr_side;
         if (pyr_side) {
@@ -1296,7 +1314,8 @@ int step_impl(tbdk_tbd* t, const uint8_t* frame, int pitch, int frame_id, const 
         if (rc != TBDK_OK) return rc;
         auto ts0 = clk::now();
         STEP_MARK(4);
-        launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count();
+        launch_us = std::chrono::duration<double, std::micro>(ts0 - t_step0).count() - gate_us;
+        wait_us += gate_us;
         // the one host wait of the frame, on the critical path: poll instead of
         // a blocking synchronize (its wake-up latency is part of every frame).
         // The poll pauses between queries (the core's sibling thread keeps its

@@ -106,6 +106,7 @@ struct tbdk_ctx {
     int opt_tbd_ahead_at = 0;    // tbdk_ctx_set_option("tbd_ahead_at"): where a step launches the ahead GFTT (0..2)
     int opt_tbd_gftt_ahead = 1;  // tbdk_ctx_set_option("tbd_gftt_ahead"): tbdk_tbd_run's early GFTT a frame ahead
     int opt_tbd_borrow_l0 = 0;   // tbdk_ctx_set_option("tbd_borrow_l0"): tbdk_tbd_run's pyramids take the frame as level 0 (A/B)
+    int opt_tbd_fit_gate = 1;    // tbdk_ctx_set_option("tbd_fit_gate"): the host launches the fit once the look-ahead PyrLK is done
     int opt_tbd_async_la = 0;    // tbdk_ctx_set_option("tbd_async_la"): look-ahead launches by a worker thread (read by tbdk_tbd_create)
     std::string timing_only;  // ",name,name," filter of tbdk_timing_select ("" = all)
     int timing_every = 1;     // tbdk_ctx_set_option("timing_every"): events on every Nth selected launch
