@@ -157,7 +157,11 @@ def ktrace_grid_us(frags, pick: str = "max_grid"):
         c = [e for e in ents if frag in e["kernel"]]
         if not c:
             return None, None, None
-        e = max(c, key=(lambda e: e["grid"]) if pick == "max_grid" else (lambda e: e["dispatches"]))
+        if pick.startswith("dispatches:"):  # the entry of a leg with its own dispatch count
+            c = [e for e in c if e["dispatches"] == int(pick.split(":")[1])]
+            if not c:
+                return None, None, None
+        e = max(c, key=(lambda e: e["grid"]) if pick != "most" else (lambda e: e["dispatches"]))
         tot += e["avg_us"]
         used.append((e["kernel"], e["grid"], e["dispatches"], e["avg_us"]))
     return round(tot, 3), used, files[-1]
@@ -1261,8 +1265,43 @@ def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
     cp = copy_rate_at(ctx, b)
     tr, tr2, src = pmc_pyr_traffic("u8", [("pyr_build_kernel", 1), ("pyr_down_padded_kernel", 1)])
     kt_us, kt_used, kt_src = ktrace_grid_us(("pyr_build_kernel", "pyr_down_padded_kernel"), "max_grid")
+    # the borrowed build (tbdk_pyr_build_borrowed: level 0 is the frame, no padded
+    # copy; the reference GPU class's pyramid): 180 timed + 10 warm-up builds, so
+    # that its kernel-trace entries are told apart by their dispatch count
+    PB = klt.Pyramid(ctx, W, H, ml, (21, 21), derivs=False)
+    fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
+    for i in range(10):
+        PB.build_borrowed(fr[i & 1])
+    torch.cuda.synchronize()
+    ctx.timing_select(["pyr_build"])
+    ctx.timing_enable(True)
+    for i in range(180):
+        PB.build_borrowed(fr[i & 1])
+    torch.cuda.synchronize()
+    cb, msb = ctx.timing_query("pyr_build")
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    del fr, PB
+    usb = msb / cb * 1000.0
+    bb = pyr_build_bytes(W, H, ml + 1, copy_l0=False)
+    gbsb = bb / (usb * 1e-6) / 1e9
+    # (its level-2 launch has the padded build's grid: one kernel-trace entry for both)
+    ktb_us, ktb_used, ktb_src = ktrace_grid_us(("pyr_build_kernel",), "dispatches:190")
+    ktd_us, ktd_used, _ = ktrace_grid_us(("pyr_down_padded_kernel",), "max_grid")
+    if ktb_us is not None and ktd_us is not None:
+        ktb_us, ktb_used = round(ktb_us + ktd_us, 3), ktb_used + ktd_used
+    else:
+        ktb_us = ktb_used = ktb_src = None
+    borrowed = {"achieved": round(gbsb, 1), "frac": round(gbsb / PEAK_HBM_GBS, 4), "bytes_per_launch": bb,
+                "avg_us": round(usb, 2), "builds": cb, "kernel_trace_us": ktb_us, "kernel_trace_launches": ktb_used,
+                "kernel_trace_source": ktb_src,
+                "frac_kernel_trace": round(bb / (ktb_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4) if ktb_us else None,
+                "kernel": "tbdk_pyr_build_borrowed (levels 1-2 from the frame; level 0 is the frame itself)",
+                "note": "algorithmic bytes: the frame read once, levels 1.. written padded, level 2 reading level 1 "
+                        "(no level-0 copy: cudaoptflow/src/pyrlk.cpp:144-145)"}
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": b, "avg_us": round(us, 2), "builds": c,
+            "borrowed_level0": borrowed,
             "traffic": tr, "traffic_fetch_x2": tr2, "traffic_source": src,
             "traffic_over_algorithmic": round(tr / b, 3) if tr else None,
             "size_matched_copy": cp, "frac_size_matched_copy": round(gbs / cp["gbs"], 4),

@@ -292,6 +292,17 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
  * TBD loop's pyramids are of this kind. */
 int tbdk_pyr_create_levels(tbdk_ctx* ctx, int width, int height, int max_level, int win_w, int win_h,
                            tbdk_pyr* pyr);
+/* Levels 1.. of a levels-only u8 pyramid (tbdk_pyr_create_levels) from the
+ * device frame `img`, which becomes level 0 itself: no padded copy, as the
+ * pyramid of cv::cuda::SparsePyrLKOpticalFlow, whose level 0 is the input
+ * GpuMat (cudaoptflow/src/pyrlk.cpp:144-145).  tbdk_lk_sparse (its
+ * several-points-per-wave kernel: impl 0 or 3, 1 channel, window width <= 31)
+ * reads that level with buildOpticalFlowPyramid's reflect-101 border
+ * (lkpyramid.cpp:726-740) by coordinates, with the same results as the padded
+ * copy; other kernels return TBDK_EINVAL.  The frame must stay valid and
+ * unchanged while the pyramid is read; the next tbdk_pyr_build gives the
+ * pyramid its own level 0 again.  Levels are as tbdk_pyr_build's, bit for bit. */
+int tbdk_pyr_build_borrowed(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream);
 
 /* Multi-channel frames (cv::cuda::SparsePyrLKOpticalFlow takes 1, 3 or 4
  * channels, cudaoptflow/src/pyrlk.cpp:140-142,197-205; the CPU

@@ -205,6 +205,7 @@ SIGNATURES = {
     "tbdk_pyr_build_f16": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_destroy": (C.c_int, [C.c_void_p, C.POINTER(Pyr)]),
     "tbdk_pyr_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
+    "tbdk_pyr_build_borrowed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(Pyr), C.c_void_p]),
     "tbdk_pyr_download": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int, C.c_int]),
     "tbdk_pyr_download_deriv": (C.c_int, [C.c_void_p, C.POINTER(Pyr), C.c_int, C.c_void_p, C.c_int]),
     "tbdk_pyr_down_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,

@@ -470,6 +470,13 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     const int cn = pyr && pyr->cn > 1 ? pyr->cn : 1;
     if (!ctx || !img || !pyr || pyr->nlevels <= 0 || pitch < pyr->lv[0].width * cn) return TBDK_EINVAL;
     if (cn > 1 && pyr->depth == TBDK_DEPTH_16F) return TBDK_EINVAL;
+    if (pyr->flags & kPyrL0Borrowed) {  // a borrowed level 0 (tbdk_pyr_build_borrowed): the own buffer again
+        tbdk_level& L = pyr->lv[0];
+        L.pad = level_pad(pyr->win_w, pyr->win_h);
+        L.pitch = align_up(L.width + 2 * L.pad, 256);  // u8 levels only (pyr_create's layout)
+        L.data = static_cast<uint8_t*>(pyr->storage);
+        pyr->flags &= ~kPyrL0Borrowed;
+    }
     DeviceGuard g(ctx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rec = timing_begin(ctx, "pyr_build", s);
@@ -490,6 +497,19 @@ int tbdk_pyr_build(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, 
     }
     timing_end(ctx, rec, s);
     return map_err(e);
+}
+
+int tbdk_pyr_build_borrowed(tbdk_ctx* ctx, const uint8_t* img, int pitch, tbdk_pyr* pyr, void* stream)
+{
+    if (!ctx || !img || !pyr || pyr->nlevels <= 0 || !pyr->storage) return TBDK_EINVAL;
+    if (pyr->flags & kPyrL0Borrowed) {  // borrowing already: its own level 0 descriptor first
+        tbdk_level& L = pyr->lv[0];
+        L.pad = level_pad(pyr->win_w, pyr->win_h);
+        L.pitch = align_up(L.width + 2 * L.pad, 256);
+        L.data = static_cast<uint8_t*>(pyr->storage);
+        pyr->flags &= ~kPyrL0Borrowed;
+    }
+    return tbdk::pyr_build_borrowed(ctx, img, pitch, pyr, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -170,6 +170,22 @@ class Pyramid:
                                                    C.byref(self.pyr), _stream_ptr(stream)), "tbdk_pyr_build")
         return self
 
+    def build_borrowed(self, img: torch.Tensor, stream=None) -> "Pyramid":
+        """Levels-only u8 pyramid whose level 0 is `img` itself (no padded copy;
+        tbdk_pyr_build_borrowed, the reference GPU class's pyramid,
+        cudaoptflow/src/pyrlk.cpp:144-145).  `img` must stay alive and unchanged
+        while the pyramid is read; the pyramid keeps a reference to it."""
+        if self.dtype != torch.uint8 or self.channels != 1:
+            raise _lib.TbdkError("borrowed level 0: u8 single-channel levels-only pyramids")
+        if img.dim() != 2 or not img.is_cuda or img.dtype != torch.uint8 or img.shape[0] != self.height or \
+                img.shape[1] != self.width or img.stride(1) != 1:
+            raise _lib.TbdkError("Pyramid.build_borrowed expects a 2-D uint8 device tensor of the pyramid's size")
+        _lib.check(self.ctx.lib.tbdk_pyr_build_borrowed(self.ctx.handle, C.c_void_p(img.data_ptr()),
+                                                        int(img.stride(0)), C.byref(self.pyr), _stream_ptr(stream)),
+                   "tbdk_pyr_build_borrowed")
+        self._borrowed = img
+        return self
+
     def level(self, i: int, with_border: bool = False):
         """Host copy of level i as a (H, W) numpy array, uint8 or float16 (test / download helper)."""
         import numpy as np

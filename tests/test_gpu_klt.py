@@ -154,6 +154,77 @@ def test_pyramid_fuse_modes_bit_exact(gpu, shape, maxlev, win):
         gpu.set_option("pyr_xcd", 1)
 
 
+@pytest.mark.parametrize("shape,maxlev,win", [((1080, 1920), 2, 21), ((2160, 3840), 2, 21), ((1081, 1923), 3, 21),
+                                             ((137, 261), 2, 21), ((61, 93), 4, 7), ((375, 1242), 3, 15)])
+def test_pyramid_borrowed_level0_bit_exact(gpu, shape, maxlev, win):
+    """tbdk_pyr_build_borrowed: level 0 is the frame itself (pad 0, the frame's
+    pitch), levels 1.. bit-exact with the oracle's padded levels; a following
+    tbdk_pyr_build gives the pyramid its own padded level 0 again, and a
+    borrowed build after that borrows again"""
+    K = klt()
+    rng = np.random.default_rng(sum(shape) + win)
+    imgs = [rng.integers(0, 256, shape, dtype=np.uint8) for _ in range(2)]
+    frames = [to_dev(i) for i in imgs]
+    P = K.Pyramid(gpu, shape[1], shape[0], maxlev, (win, win), derivs=False)
+    own = P.pyr.lv[0].data
+    for k, op in enumerate(("borrow", "build", "borrow")):
+        img = imgs[k & 1]
+        if op == "borrow":
+            P.build_borrowed(frames[k & 1])
+        else:
+            P.build(frames[k & 1])
+        torch.cuda.synchronize()
+        L0 = P.pyr.lv[0]
+        if op == "borrow":
+            assert L0.data == frames[k & 1].data_ptr() and L0.pad == 0 and L0.pitch == shape[1]
+        else:
+            assert L0.data == own and L0.pad > 0
+        R = O.Pyramid(img, (win, win), maxlev, pad=P.pyr.lv[1].pad)
+        assert P.nlevels == R.nlevels
+        assert np.array_equal(P.level(0), img)
+        for lvl in range(1, P.nlevels):
+            assert np.array_equal(P.level(lvl, True), R.level(lvl, True)), f"{op} level {lvl}"
+        if op == "build":
+            assert np.array_equal(P.level(0, True), R.level(0, True))
+
+
+@pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])
+def test_lk_borrowed_level0_equals_padded(gpu, win, maxlev):
+    """PyrLK (the several-points-per-wave kernel) on pyramids whose level 0 is
+    the frame itself (tbdk_pyr_build_borrowed: reflect-101 taps by coordinates
+    where a window crosses the frame edge) equals PyrLK on the padded pyramids
+    bit for bit, windows over the edges and points outside the frame included,
+    with and without the minimum-eigenvalue error; other kernels refuse the
+    borrowed level"""
+    K = klt()
+    fr, _ = K.synth_render(57 + win, 640, 480, 24, 0, 2, ctx=gpu)
+    rng = np.random.default_rng(win + maxlev)
+    pts = np.concatenate([rng.uniform([-12, -12], [652, 492], (3000, 2)),
+                          np.array([[0, 0], [639, 479], [0.5, 240], [639.75, 10.25], [320, 0], [320, 479.5]])])
+    pts = to_dev(pts.astype(np.float32))
+    for flags8 in (False, True):
+        lk = K.SparsePyrLKOpticalFlow((win, win), maxlev, 30, getMinEigenVals=flags8, impl=3)
+        out = []
+        for borrow in (False, True):
+            Pa = K.Pyramid(gpu, 640, 480, maxlev, (win, win), derivs=False)
+            Pb = K.Pyramid(gpu, 640, 480, maxlev, (win, win), derivs=False)
+            if borrow:
+                Pa.build_borrowed(fr[0])
+                Pb.build_borrowed(fr[1])
+            else:
+                Pa.build(fr[0])
+                Pb.build(fr[1])
+            r = lk.calc(Pa, Pb, pts, want_iters=True)
+            torch.cuda.synchronize()
+            out.append([r.next_pts.cpu().numpy(), r.status.cpu().numpy(), r.err.cpu().numpy(), r.iters.cpu().numpy()])
+        for a, b in zip(*out):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), f"flags8 {flags8}"
+        assert out[0][1].mean() > 0.5
+    lk1 = K.SparsePyrLKOpticalFlow((win, win), maxlev, 30, impl=1)
+    with pytest.raises(Exception):
+        lk1.calc(Pa, Pb, pts)
+
+
 @pytest.mark.parametrize("win,maxlev", [(21, 2), (21, 3), (7, 3), (31, 2), (15, 4)])
 def test_lk_levels_only_equals_derivative_planes(gpu, win, maxlev):
     """PyrLK on levels-only pyramids (the window's Scharr values derived in the
