@@ -884,17 +884,27 @@ __global__ TBDK_MULTI_BOUNDS void lk_multi_kernel(LkArgs a)
                 // sets live at once this block set the kernel's register peak)
                 uint32_t ipr[ILIN ? NP : 1];
                 if constexpr (ILIN) {
-                    uint32_t iw0, iw1, ir[WH + 1];
+                    uint32_t iw0, iw1;
                     bilinear_weights(prevx - ipx, prevy - ipy, iw0, iw1);
+                    // an unpadded level: reflect-101 when a window crosses its edge
+                    const bool irefl = L.ipad == 0 && any_lane(want && (ipx + x < 0 || ipx + x + 1 >= L.w ||
+                                                                        ipy < 0 || ipy + WH >= L.h));
                     const uint32_t ioff = want ? (uint32_t)((ipy + L.ipad) * L.ipitch + ipx + x + L.ipad) : 0u;
-#pragma unroll
-                    for (int r = 0; r <= WH; ++r) ir[r] = load_pair_u8_ua(rI, ioff, r * L.ipitch);
+                    auto irow = [&](int r) -> uint32_t {
+                        if (irefl) return want ? load_pair_refl(rI, L.ipitch, L.w, L.h, ipy + r, ipx + x) : 0u;
+                        return load_pair_u8_ua(rI, ioff, r * L.ipitch);
+                    };
+                    // row by row (two rows live), packed by row pairs
+                    uint32_t ra = irow(0);
 #pragma unroll
                     for (int q = 0; q < NP; ++q) {
                         const int r = 2 * q;
-                        ipr[q] = pack_shr<W_BITS1 - 5>(bilin_s<0>(ir[r], ir[r + 1], iw0, iw1, rnd9),
-                                                        r + 1 < WH ? bilin_s<0>(ir[r + 1], ir[r + 2], iw0, iw1, rnd9) : 0);
+                        const uint32_t rb = irow(r + 1);
+                        const uint32_t rc = r + 2 <= WH ? irow(r + 2) : 0u;
+                        ipr[q] = pack_shr<W_BITS1 - 5>(bilin_s<0>(ra, rb, iw0, iw1, rnd9),
+                                                        r + 1 < WH ? bilin_s<0>(rb, rc, iw0, iw1, rnd9) : 0);
                         asm volatile("" : "+v"(ipr[q]));
+                        ra = rc;
                     }
                 }
                 bilinear_weights(npx - inx, npy - iny, w0, w1);
