@@ -256,7 +256,9 @@ def test_tbd_fit_flag_matches_event(gpu):
     release per fit workgroup (tbd_fit_wgpub 1, the default: every wave's
     stores acknowledged before the barrier) and one per wave (0) agree too,
     with and without the look-ahead pyramid on the look-ahead stream (where
-    the speculative PyrLK has no stream edge to the fit)."""
+    the speculative PyrLK has no stream edge to the fit), and with
+    the fit launched by the host after the look-ahead PyrLK's event (tbd_fit_gate
+    1, the default) or behind a stream wait on it (0)."""
     from opencv_amd import klt, tbd
 
     W, H, N, F = 960, 540, 32, 12
@@ -265,10 +267,12 @@ def test_tbd_fit_flag_matches_event(gpu):
     c = tbd.default_config(W, H, bounds_xmax=640, bounds_ymax=360, redetect_every=3)
     res = []
     try:
-        for fl, wg, side in ((1, 1, 2), (0, 1, 2), (1, 0, 2), (1, 1, 0), (1, 0, 0)):
+        for fl, wg, side, gate in ((1, 1, 2, 1), (0, 1, 2, 1), (1, 0, 2, 1), (1, 1, 0, 1), (1, 0, 0, 1),
+                                   (1, 1, 2, 0), (0, 1, 2, 0), (1, 1, 0, 0)):
             gpu.set_option("tbd_fit_flag", fl)
             gpu.set_option("tbd_fit_wgpub", wg)
             gpu.set_option("tbd_la_pyr_side", side)
+            gpu.set_option("tbd_fit_gate", gate)
             loop = tbd.TbdLoop(c, ctx=gpu)
             ms = loop.run(frames, 0, dets)
             res.append(([_mkey(m) for m in ms], loop.tracks()))
@@ -276,6 +280,7 @@ def test_tbd_fit_flag_matches_event(gpu):
         gpu.set_option("tbd_fit_flag", 1)
         gpu.set_option("tbd_fit_wgpub", 1)
         gpu.set_option("tbd_la_pyr_side", 2)
+        gpu.set_option("tbd_fit_gate", 1)
     for r in res[1:]:
         assert r == res[0]
 
