@@ -978,6 +978,11 @@ def init_rank_group(world: int, rank: int, local: int) -> None:
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if os.environ.get("TBDK_BENCH_SHARE_GPU") == "1":
+            # rehearsal of the N-rank path on a box with fewer GPUs than ranks:
+            # ranks share the GPUs round-robin (the throughput is then not a
+            # scaling figure; device_count() does not initialise the GPU)
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:

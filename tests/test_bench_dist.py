@@ -49,7 +49,7 @@ def test_replica_timing_world_size_2():
     assert all(abs(r[2] - 480 * 2 / 2.0) < 1e-12 for r in res)  # frames of all ranks / max time
 
 
-def _group_worker(rank, world, port, q):
+def _group_worker(rank, world, port, q, share=False):
     import torch
     import torch.distributed as dist
 
@@ -57,6 +57,9 @@ def _group_worker(rank, world, port, q):
     import bench
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if share:  # the one-GPU rehearsal switch: ranks wrap onto the devices there are
+        os.environ["TBDK_BENCH_SHARE_GPU"] = "1"
+        torch.cuda.device_count = lambda: 1
     dev = []
     torch.cuda.set_device = lambda d: dev.append(d)  # no GPU here; record the selection
     bench.init_rank_group(world, rank, rank)
@@ -86,6 +89,24 @@ def test_rank_group_is_host_only_world_size_2():
     assert [r[1] for r in res] == ["gloo", "gloo"]
     assert [r[2] for r in res] == [[0], [1]]
     assert [r[3] for r in res] == [4.0, 4.0]
+
+
+def test_rank_group_shared_gpu_rehearsal():
+    """TBDK_BENCH_SHARE_GPU=1 (rehearsing the N-rank bench on a box with fewer
+    GPUs than ranks): rank i selects GPU i mod device_count; the group is the
+    same gloo group.  Without the switch each rank keeps its own GPU (above)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, 2, port, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == ["gloo", "gloo"]
+    assert [r[2] for r in res] == [[0], [0]]
 
 
 def test_bench_creates_no_rccl_group():
