@@ -1317,6 +1317,48 @@ def pyramid_4k_leg(ctx, dev, builds: int = 200) -> dict:
                     "build's HIP-event time (events on the launch stream around its launches)"}
 
 
+def standalone_pyr(ctx, W: int, H: int, builds: int = 200) -> dict:
+    """The loop's levels-only u8 build (3 levels, win 21) of a W x H frame on an
+    otherwise idle GPU: HIP events around every build (mean over `builds`,
+    alternating two frames), beside the uncontended kernel-trace durations of
+    the same build from the committed rocprofv3 summary of
+    tools/probe_pyr_build.py (profiles/rNN_pyr_probe_ktrace.json, per grid)."""
+    import torch
+    from opencv_amd import klt
+
+    fr, _ = klt.synth_render(7, W, H, 64, 0, 2, ctx=ctx)
+    P = klt.Pyramid(ctx, W, H, 2, (21, 21), derivs=False)
+    for i in range(10):
+        P.build(fr[i & 1])
+    torch.cuda.synchronize()
+    ctx.timing_select(["pyr_build"])
+    ctx.timing_enable(True)
+    for i in range(builds):
+        P.build(fr[i & 1])
+    torch.cuda.synchronize()
+    c, ms = ctx.timing_query("pyr_build")
+    ctx.timing_enable(False)
+    ctx.timing_select(None)
+    del fr, P
+    out = {"avg_us": round(ms / c * 1000.0, 2), "builds": c, "kernel_trace_us": None, "kernel_trace_source": None}
+    d, files = _pmc_summaries("_pyr_probe_ktrace.json")
+    if files:
+        ents = json.load(open(os.path.join(d, files[-1])))["entries"]
+        sel = PYR_PROBE_GRIDS.get((W, H))
+        if sel:
+            us = [e["avg_us"] for e in ents for k, g in sel if k in e["kernel"] and e["grid"] == g]
+            if len(us) == len(sel):
+                out.update(kernel_trace_us=round(sum(us), 3), kernel_trace_source=files[-1],
+                           kernel_trace_launches=[list(x) for x in sel])
+    return out
+
+
+# the levels-only build's launches (kernel, grid size) per frame size, as
+# tools/ktrace_by_grid.py keys them (two-role launch with the copy role, level 2)
+PYR_PROBE_GRIDS = {(1920, 1080): (("pyr_build_kernel", 297984), ("pyr_down_padded_kernel", 85504)),
+                   (3840, 2160): (("pyr_build_kernel", 1110272), ("pyr_down_padded_kernel", 154624))}
+
+
 def kitti_leg(args, ctx, dev, world: int, rank: int):
     """BASELINE configs[3]: KITTI-shaped 1242x375 sequences, one per GPU (seed
     s + rank, sequences s..s+7 at 8 GPUs), 128 objects, the full loop; frames of
@@ -1649,6 +1691,8 @@ def main(argv=None):
     cnt = pmc_bytes(PYR_KERNELS)
     cp_pyr = copy_rate_at(ctx, pbb) if not args.no_copy_peak else None
     kt_us, kt_used, kt_src = ktrace_grid_us(("pyr_build_kernel", "pyr_down_padded_kernel"), "most")
+    # the same build uncontended (the loop's runs beside the critical PyrLK since round 5)
+    sa_pyr = standalone_pyr(ctx, args.width, args.height) if not args.no_pyr4k else None
     roof_pyr = {"bound": "hbm", "achieved": round(pyr_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(pyr_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": pbb, "b_pyr_survey": pb,
                 "size_matched_copy": cp_pyr,
@@ -1661,6 +1705,9 @@ def main(argv=None):
                 "traffic_over_algorithmic": round((cnt["fetch_raw"] + cnt["write"]) / pbb, 3) if cnt else None,
                 "traffic_kernels": cnt["kernels"] if cnt else None, "traffic_source": cnt["source"] if cnt else None,
                 "level0": "the frame itself (tbd_borrow_l0: no padded copy)" if borrow else "padded copy",
+                "standalone": sa_pyr,
+                "frac_standalone": round(pyr_build_bytes(args.width, args.height, nlev) / (sa_pyr["avg_us"] * 1e-6)
+                                         / 1e9 / PEAK_HBM_GBS, 4) if sa_pyr else None,
                 "note": "achieved = the loop's build's algorithmic bytes (frame read once, every padded level "
                         "written -- from level 1 on when level 0 is the frame itself --, levels >= 2 reading their "
                         "predecessor; bytes_per_launch) / the build's HIP-event time (its launches); b_pyr_survey = "
