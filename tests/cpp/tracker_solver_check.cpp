@@ -5,7 +5,7 @@
 // duplicated and clustered boxes (ties, several zeros per row and column,
 // step-3/step-4 rounds), dropouts (padding columns), clutter (padding rows),
 // zero-size boxes (0/0 costs), touching boxes and padding values below 1,
-// at 1 and outside (0, 1e7) (the dense path).
+// at 1 and outside (0, 1e7) (the dense path), frames without detections.
 // Build: g++ -std=c++17 -I opencv_amd/csrc tests/cpp/tracker_solver_check.cpp opencv_amd/csrc/tbd_tracker.cpp
 #include <cmath>
 #include <cstdint>
@@ -87,6 +87,7 @@ int main()
                 d.bbox = Rect(U(-20, W), U(-20, H), U(0, 80), U(0, 80));
                 dets.push_back(d);
             }
+            if (scen % 4 == 3 && f % 7 == 6) dets.clear();  // a frame without detections (padding columns only)
             std::vector<Detection> d2 = dets;
             fast.performTrackingStep(dets, f);
             dense.performTrackingStep(d2, f);
